@@ -1,0 +1,222 @@
+// torch bindings of the pddl HIP kernels (module `_pddl_native`).
+//
+// Every op launches on the caller's current HIP stream and raises on a bad shape or a
+// launch error; the Python layer (pddl.ops) never silently falls back to eager PyTorch on
+// a GPU tensor.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/util/Optional.h>
+
+#include "kernels/kernels.h"
+
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+#define PCHECK(cond, msg) TORCH_CHECK(cond, "pddl: ", msg)
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void ok(const char* err, const char* what) { TORCH_CHECK(err == nullptr, "pddl ", what, ": ", err ? err : ""); }
+
+const uint16_t* bfp(const Tensor& t) {
+  PCHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16, "expected a bf16 GPU tensor");
+  return reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+uint16_t* bfpm(const Tensor& t) { return const_cast<uint16_t*>(bfp(t)); }
+const uint16_t* obfp(const OptT& t) { return t.has_value() ? bfp(*t) : nullptr; }
+float* f32p(const Tensor& t) {
+  PCHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32, "expected an fp32 GPU tensor");
+  return t.data_ptr<float>();
+}
+const float* of32p(const OptT& t) { return t.has_value() ? f32p(*t) : nullptr; }
+// Row stride of a row-major [..., C] view (innermost dim contiguous).
+int ld(const Tensor& t) {
+  PCHECK(t.stride(-1) == 1, "innermost dim must be contiguous");
+  return t.dim() >= 2 ? (int)t.stride(-2) : (int)t.size(-1);
+}
+int old(const OptT& t) { return t.has_value() ? ld(*t) : 0; }
+
+// Generic implicit-GEMM (conv forward / dgrad / fp32 dense).
+void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
+           int64_t Ho, int64_t Wo, Tensor b, int64_t mode, OptT scale, OptT shift, OptT res, OptT mask, OptT add,
+           Tensor out, int64_t relu, OptT out2, int64_t relu2, int64_t n_split, int64_t up2, int64_t Hf,
+           int64_t Wf) {
+  pddl::IgemmParams p{};
+  PCHECK(a1.is_contiguous(), "A source must be contiguous NHWC");
+  p.a1 = bfp(a1);
+  p.C1 = (int)a1.size(-1);
+  p.N = (int)a1.size(0);
+  p.H = (int)H; p.W = (int)W;
+  PCHECK(a1.numel() == (int64_t)p.N * H * W * p.C1, "A source numel does not match N*H*W*C");
+  p.R = (int)R; p.S = (int)S; p.stride = (int)stride; p.pad = (int)pad;
+  p.Ho = (int)Ho; p.Wo = (int)Wo; p.M = p.N * (int)Ho * (int)Wo;
+  p.K1 = (int)(R * S * p.C1);
+  p.K = p.K1;
+  if (a2.has_value()) {
+    PCHECK(a2->is_contiguous() && a2->size(0) == a1.size(0), "second A source shape");
+    p.a2 = bfp(*a2);
+    p.C2 = (int)a2->size(-1);
+    PCHECK(a2->numel() == (int64_t)p.N * H * W * p.C2, "second A source numel");
+    p.K += (int)(R * S * p.C2);
+  }
+  PCHECK(b.dim() == 2 && b.size(1) >= p.K, "B must be [Nn][>=K]");
+  p.b = bfp(b); p.ldb = ld(b); p.Nn = (int)b.size(0);
+  p.mode = (int)mode;
+  if (mode != pddl::EPI_DGRAD) {
+    PCHECK(scale.has_value() && shift.has_value(), "forward epilogue needs scale and shift");
+    PCHECK(scale->numel() >= p.Nn && shift->numel() >= p.Nn, "scale/shift too short");
+  }
+  p.scale = of32p(scale); p.shift = of32p(shift);
+  p.res = obfp(res); p.ld_res = old(res);
+  p.mask = obfp(mask); p.ld_mask = old(mask);
+  p.add = obfp(add); p.ld_add = old(add);
+  if (mode == pddl::EPI_F32) p.out = f32p(out); else p.out = bfpm(out);
+  p.ldo = ld(out);
+  p.relu = (int)relu;
+  if (out2.has_value()) { p.out2 = bfpm(*out2); p.ldo2 = ld(*out2); }
+  p.relu2 = (int)relu2; p.n_split = (int)n_split;
+  p.up2 = (int)up2; p.Hf = (int)Hf; p.Wf = (int)Wf;
+  const int64_t rows_out = up2 ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
+  PCHECK(out.numel() / std::max<int64_t>(1, out.size(-1)) >= (out2.has_value() ? p.M : rows_out) ||
+             out.dim() >= 2,
+         "output too small");
+  ok(pddl::igemm_launch(p, cur_stream()), "igemm");
+}
+
+void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Ho,
+           int64_t Wo, Tensor g, OptT g2, int64_t co_split, Tensor dw, int64_t K, int64_t splits) {
+  pddl::WgradParams p{};
+  PCHECK(x.is_contiguous() && g.stride(-1) == 1, "wgrad operand layout");
+  p.x = bfp(x); p.N = (int)x.size(0); p.H = (int)H; p.W = (int)W; p.C = (int)x.size(-1);
+  p.ldx = p.C;
+  p.R = (int)R; p.S = (int)S; p.stride = (int)stride; p.pad = (int)pad; p.Ho = (int)Ho; p.Wo = (int)Wo;
+  p.M = p.N * (int)Ho * (int)Wo;
+  p.g = bfp(g); p.ldg = ld(g);
+  PCHECK(g.numel() / g.size(-1) == p.M || g.dim() == 2, "gradient rows != N*Ho*Wo");
+  if (g2.has_value()) { p.g2 = bfp(*g2); p.ldg2 = ld(*g2); p.co_split = (int)co_split; }
+  p.Cout = (int)dw.size(0); p.K = (int)K;
+  p.dw = f32p(dw); p.ld_dw = ld(dw);
+  PCHECK(dw.size(1) >= K, "dw too narrow");
+  p.splits = (int)splits;
+  ok(pddl::wgrad_launch(p, cur_stream()), "wgrad");
+}
+
+void stem_im2col(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_t oy, int64_t ox, Tensor out) {
+  pddl::StemParams p{};
+  PCHECK(in.is_cuda() && in.is_contiguous() && in.dim() == 4 && in.size(3) == 3, "stem input must be [B,H,W,3]");
+  PCHECK(in.scalar_type() == torch::kUInt8 || in.scalar_type() == torch::kFloat32, "stem input uint8 or fp32");
+  p.in = in.data_ptr(); p.in_u8 = in.scalar_type() == torch::kUInt8;
+  p.B = (int)in.size(0); p.Hin = (int)in.size(1); p.Win = (int)in.size(2);
+  p.Hc = (int)Hc; p.Wc = (int)Wc; p.mode = (int)mode; p.oy = (int)oy; p.ox = (int)ox;
+  if (flip.has_value()) {
+    PCHECK(flip->scalar_type() == torch::kUInt8 && flip->numel() == p.B, "flip flags [B] uint8");
+    p.flip = flip->data_ptr<uint8_t>();
+  }
+  p.scale = 1.f / 255.f;
+  p.Ho = (int)((Hc + 6 - 7) / 2 + 1); p.Wo = (int)((Wc + 6 - 7) / 2 + 1);
+  p.out = bfpm(out); p.ldo = ld(out);
+  PCHECK(out.numel() >= (int64_t)p.B * p.Ho * p.Wo * p.ldo, "stem output too small");
+  ok(pddl::stem_im2col_launch(p, cur_stream()), "stem_im2col");
+}
+
+void maxpool_fwd(Tensor x, Tensor y, Tensor idx) {
+  PCHECK(x.is_contiguous() && y.is_contiguous() && idx.is_contiguous() && idx.scalar_type() == torch::kUInt8,
+         "maxpool layouts");
+  ok(pddl::maxpool_fwd_launch(bfp(x), bfpm(y), idx.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1),
+                              (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), cur_stream()),
+     "maxpool_fwd");
+}
+void maxpool_bwd(Tensor gy, Tensor idx, OptT xmask, Tensor gx) {
+  ok(pddl::maxpool_bwd_launch(bfp(gy), idx.data_ptr<uint8_t>(), obfp(xmask), bfpm(gx), (int)gx.size(0),
+                              (int)gx.size(1), (int)gx.size(2), (int)gx.size(3), (int)gy.size(1), (int)gy.size(2),
+                              cur_stream()),
+     "maxpool_bwd");
+}
+void gap_fwd(Tensor x, Tensor y) {
+  ok(pddl::gap_fwd_launch(bfp(x), bfpm(y), (int)x.size(0), (int)(x.size(1) * x.size(2)), (int)x.size(3),
+                          cur_stream()),
+     "gap_fwd");
+}
+void gap_bwd(Tensor gp, Tensor ymask, Tensor g) {
+  ok(pddl::gap_bwd_launch(bfp(gp), ld(gp), bfp(ymask), bfpm(g), (int)g.size(0), (int)(g.size(1) * g.size(2)),
+                          (int)g.size(3), cur_stream()),
+     "gap_bwd");
+}
+void colsum(Tensor g, int64_t C, Tensor out) {
+  const int ldg = ld(g);
+  const int64_t M = g.numel() / g.size(-1);
+  ok(pddl::colsum_launch(bfp(g), (int)M, (int)C, ldg, f32p(out), cur_stream()), "colsum");
+}
+void softmax_xent(Tensor logits, Tensor labels, int64_t ncls, double gscale, Tensor dlogits, Tensor loss_sum,
+                  Tensor correct) {
+  PCHECK(labels.scalar_type() == torch::kInt64 && labels.is_cuda(), "labels int64 GPU");
+  ok(pddl::softmax_xent_launch(f32p(logits), ld(logits), labels.data_ptr<int64_t>(), (int)logits.size(0),
+                               (int)ncls, (float)gscale, bfpm(dlogits), ld(dlogits), f32p(loss_sum),
+                               f32p(correct), cur_stream()),
+     "softmax_xent");
+}
+void prep(Tensor params, Tensor table, int64_t nlayers, int64_t max_elems, Tensor wbf, Tensor scale, Tensor shift,
+          double eps) {
+  PCHECK(table.is_cuda() && table.scalar_type() == torch::kUInt8, "prep table");
+  PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::PrepLayer), "prep table size");
+  ok(pddl::prep_launch(f32p(params), reinterpret_cast<const pddl::PrepLayer*>(table.data_ptr()), (int)nlayers,
+                       (int)max_elems, bfpm(wbf), f32p(scale), f32p(shift), (float)eps, cur_stream()),
+     "prep");
+}
+void wgrad_finalize(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor scale, Tensor dgamma_raw) {
+  PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::FinLayer), "finalize table size");
+  ok(pddl::wgrad_finalize_launch(f32p(params), f32p(grads), reinterpret_cast<const pddl::FinLayer*>(table.data_ptr()),
+                                 (int)nlayers, f32p(scale), f32p(dgamma_raw), cur_stream()),
+     "wgrad_finalize");
+}
+void bn_grad(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor colsum, Tensor dgamma_raw,
+             Tensor scale, double eps) {
+  PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::BnGradLayer), "bn_grad table size");
+  ok(pddl::bn_grad_launch(f32p(params), f32p(grads), reinterpret_cast<const pddl::BnGradLayer*>(table.data_ptr()),
+                          (int)nlayers, f32p(colsum), f32p(dgamma_raw), f32p(scale), (float)eps, cur_stream()),
+     "bn_grad");
+}
+void adam(Tensor p, Tensor g, Tensor m, Tensor v, double lr_t, double b1, double b2, double eps, double gscale) {
+  ok(pddl::adam_launch(f32p(p), f32p(g), f32p(m), f32p(v), p.numel(), (float)lr_t, (float)b1, (float)b2, (float)eps,
+                       (float)gscale, cur_stream()),
+     "adam");
+}
+void sgd(Tensor p, Tensor g, Tensor mom, double lr, double momentum, double wd, bool nesterov, double gscale) {
+  ok(pddl::sgd_launch(f32p(p), f32p(g), f32p(mom), p.numel(), (float)lr, (float)momentum, (float)wd,
+                      nesterov ? 1 : 0, (float)gscale, cur_stream()),
+     "sgd");
+}
+void scale_(Tensor x, double a) { ok(pddl::scale_launch(f32p(x), x.numel(), (float)a, cur_stream()), "scale"); }
+void cast_bf16(Tensor x, Tensor y) { ok(pddl::cast_bf16_launch(f32p(x), bfpm(y), x.numel(), cur_stream()), "cast"); }
+void cast_f32(Tensor x, Tensor y) { ok(pddl::cast_f32_launch(bfp(x), f32p(y), x.numel(), cur_stream()), "cast"); }
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "pddl MI355X (gfx950) HIP kernels";
+  m.def("igemm", &igemm);
+  m.def("wgrad", &wgrad);
+  m.def("stem_im2col", &stem_im2col);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("gap_fwd", &gap_fwd);
+  m.def("gap_bwd", &gap_bwd);
+  m.def("colsum", &colsum);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("prep", &prep);
+  m.def("wgrad_finalize", &wgrad_finalize);
+  m.def("bn_grad", &bn_grad);
+  m.def("adam", &adam);
+  m.def("sgd", &sgd);
+  m.def("scale_", &scale_);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("cast_f32", &cast_f32);
+  m.attr("PREP_LAYER_BYTES") = (int)sizeof(pddl::PrepLayer);
+  m.attr("FIN_LAYER_BYTES") = (int)sizeof(pddl::FinLayer);
+  m.attr("BNGRAD_LAYER_BYTES") = (int)sizeof(pddl::BnGradLayer);
+  m.attr("EPI_FWD") = (int)pddl::EPI_FWD;
+  m.attr("EPI_DGRAD") = (int)pddl::EPI_DGRAD;
+  m.attr("EPI_F32") = (int)pddl::EPI_F32;
+}

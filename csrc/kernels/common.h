@@ -1,0 +1,69 @@
+// Shared device helpers for the CDNA4 (gfx950 / MI355X) kernels of pddl.
+//
+// Storage convention: bf16 tensors are raw `uint16_t` buffers (torch.bfloat16
+// bit pattern); every kernel computes in fp32 and rounds once on store.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pddl {
+
+typedef uint16_t bf16_t;
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// Round-to-nearest-even via the hardware convert (keeps NaN a NaN; see
+// MI355X_MICROARCH.md "Correctness boundaries").
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+// 64 bytes of zeros: the source of every out-of-bounds LDS-DMA lane (padding
+// rows of the implicit-GEMM gather, tile overhang).  LDS-DMA cannot write a
+// literal, so invalid lanes read from here instead.  One copy per translation
+// unit (no relocatable device code needed).
+static __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
+
+__host__ __device__ __forceinline__ long lmin(long a, long b) { return a < b ? a : b; }
+
+// Bijective XCD-aware remap of the linear workgroup id (cdna_hip_programming
+// §5 "XCD swizzle must be bijective"): consecutive logical tiles land on the
+// same XCD so blocks sharing an operand panel share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = b & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (b >> 3);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace pddl

@@ -1,0 +1,432 @@
+#include "hip/hip_runtime.h"
+// Memory-bound kernels around the implicit-GEMM convs (gfx950):
+//   * stem_im2col  : Rescaling(1/255) -> RandomCrop/resize -> RandomFlip -> ZeroPadding2D(3)
+//                    -> 7x7/s2 im2col rows, in one pass (reference imagenet-resnet50.py:53-55
+//                    and the Keras ResNet50 stem)
+//   * maxpool      : ZeroPadding2D(1) + MaxPooling2D(3, 2) forward (argmax byte) and backward
+//                    (gather form, fused with the ReLU mask of conv1's output)  (N6)
+//   * gap          : GlobalAveragePooling2D forward / backward (+ ReLU mask)   (N7)
+//   * colsum       : per-channel sum of a gradient (BN beta / conv-bias grads)
+//   * softmax_xent : softmax + sparse categorical cross-entropy + accuracy, fwd+bwd fused (N9)
+//   * prep / wgrad_finalize / bn_grad : frozen-BN folding and per-channel parameter grads (N4)
+// Every kernel moves 16 bytes per lane (8 x bf16) where the layout allows (Guideline 13).
+#include "common.h"
+#include "kernels.h"
+
+namespace pddl {
+
+// ------------------------------------------------------------------------------ stem
+__device__ __forceinline__ float stem_pix(const StemParams& p, int b, int y, int x, int c) {
+  if (p.flip && p.flip[b]) x = p.Wc - 1 - x;
+  auto fetch = [&](int yy, int xx) -> float {
+    const long idx = (((long)b * p.Hin + yy) * p.Win + xx) * 3 + c;
+    return p.in_u8 ? (float)reinterpret_cast<const uint8_t*>(p.in)[idx]
+                   : reinterpret_cast<const float*>(p.in)[idx];
+  };
+  float v;
+  if (p.mode == 0) {
+    v = fetch(y, x);
+  } else if (p.mode == 2) {
+    v = fetch(y + p.oy, x + p.ox);
+  } else {  // bilinear, half-pixel centers (tf.image.resize / keras smart_resize)
+    const float sy = (y + 0.5f) * ((float)p.Hin / p.Hc) - 0.5f;
+    const float sx = (x + 0.5f) * ((float)p.Win / p.Wc) - 0.5f;
+    const float fy = floorf(sy), fx = floorf(sx);
+    const int y0 = max((int)fy, 0), x0 = max((int)fx, 0);
+    const int y1 = min((int)ceilf(sy), p.Hin - 1), x1 = min((int)ceilf(sx), p.Win - 1);
+    const float ly = sy - fy, lx = sx - fx;
+    const float top = fetch(y0, x0) + (fetch(y0, x1) - fetch(y0, x0)) * lx;
+    const float bot = fetch(y1, x0) + (fetch(y1, x1) - fetch(y1, x0)) * lx;
+    v = top + (bot - top) * ly;
+  }
+  return v * p.scale;
+}
+
+__global__ void stem_im2col_kernel(StemParams p, long nchunks) {
+  const int cpr = p.ldo / 8;  // 16-byte chunks per row
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nchunks; q += (long)gridDim.x * blockDim.x) {
+    const long row = q / cpr;
+    const int ck = (int)(q - row * cpr);
+    const int b = (int)(row / (p.Ho * p.Wo));
+    const int rem = (int)(row - (long)b * p.Ho * p.Wo);
+    const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = ck * 8 + e;
+      float val = 0.f;
+      if (k < 147) {
+        const int r = k / 21, rm = k - r * 21, s = rm / 3, c = rm - s * 3;
+        const int y = 2 * ho - 3 + r, x = 2 * wo - 3 + s;
+        if (y >= 0 && y < p.Hc && x >= 0 && x < p.Wc) val = stem_pix(p, b, y, x, c);
+      }
+      v[e] = val;
+    }
+    *reinterpret_cast<uint4*>(p.out + row * p.ldo + ck * 8) = pack8(v);
+  }
+}
+
+const char* stem_im2col_launch(const StemParams& p, hipStream_t s) {
+  if (p.ldo % 8 || p.ldo < 152) return "stem: ldo must be >= 152 and a multiple of 8";
+  const long nchunks = (long)p.B * p.Ho * p.Wo * (p.ldo / 8);
+  const int grid = (int)lmin((nchunks + 255) / 256, 65536);
+  hipLaunchKernelGGL(stem_im2col_kernel, dim3(grid), dim3(256), 0, s, p, nchunks);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// --------------------------------------------------------------------------- maxpool
+// Window of output (ho, wo) covers input rows 2ho-1 .. 2ho+1 (ZeroPadding2D(1) then 3x3/s2
+// valid).  Padded taps are real zeros (as in Keras); the first maximum in scan order wins.
+__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                                   int B, int H, int W, int C, int Ho, int Wo) {
+  const int cg = C / 8;
+  const long total = (long)B * Ho * Wo * cg;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(t % cg);
+    const long pix = t / cg;
+    const int wo = (int)(pix % Wo);
+    const long t2 = pix / Wo;
+    const int ho = (int)(t2 % Ho), b = (int)(t2 / Ho);
+    float best[8]; uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int hi = 2 * ho - 1 + r, wi = 2 * wo - 1 + s;
+        float v[8];
+        if (hi >= 0 && hi < H && wi >= 0 && wi < W) {
+          unpack8(*reinterpret_cast<const uint4*>(x + (((long)b * H + hi) * W + wi) * C + g * 8), v);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; bi[e] = (uint8_t)(r * 3 + s); }
+      }
+    const long o = pix * C + g * 8;
+    *reinterpret_cast<uint4*>(y + o) = pack8(best);
+    uint2 pk;
+    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = pk;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
+                                   const bf16_t* __restrict__ xmask, bf16_t* __restrict__ gx,
+                                   int B, int H, int W, int C, int Ho, int Wo) {
+  const int cg = C / 8;
+  const long total = (long)B * H * W * cg;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(t % cg);
+    const long pix = t / cg;
+    const int w = (int)(pix % W);
+    const long t2 = pix / W;
+    const int h = (int)(t2 % H), b = (int)(t2 / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int hp = h + 1, wp = w + 1;  // padded coordinates
+    const int ho_lo = max(0, (hp - 1) / 2), ho_hi = min(Ho - 1, hp / 2);
+    const int wo_lo = max(0, (wp - 1) / 2), wo_hi = min(Wo - 1, wp / 2);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int r = hp - 2 * ho;
+      if (r < 0 || r > 2) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int s = wp - 2 * wo;
+        if (s < 0 || s > 2) continue;
+        const long o = (((long)b * Ho + ho) * Wo + wo) * C + g * 8;
+        const uint2 pk = *reinterpret_cast<const uint2*>(idx + o);
+        float gv[8];
+        unpack8(*reinterpret_cast<const uint4*>(gy + o), gv);
+        const uint8_t want = (uint8_t)(r * 3 + s);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t word = e < 4 ? pk.x : pk.y;
+          const uint8_t id = (word >> (8 * (e & 3))) & 0xff;
+          if (id == want) acc[e] += gv[e];
+        }
+      }
+    }
+    const long o = pix * C + g * 8;
+    if (xmask) {
+      float mv[8];
+      unpack8(*reinterpret_cast<const uint4*>(xmask + o), mv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = mv[e] > 0.f ? acc[e] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(gx + o) = pack8(acc);
+  }
+}
+
+static int grid_for(long n) { return (int)lmin((n + 255) / 256, 8192); }
+
+const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, int B, int H, int W, int C, int Ho,
+                               int Wo, hipStream_t s) {
+  if (C % 8) return "maxpool: C % 8";
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)B * Ho * Wo * C / 8)), dim3(256), 0, s, x, y, idx, B,
+                     H, W, C, Ho, Wo);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uint16_t* xmask, uint16_t* gx, int B,
+                               int H, int W, int C, int Ho, int Wo, hipStream_t s) {
+  if (C % 8) return "maxpool: C % 8";
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long)B * H * W * C / 8)), dim3(256), 0, s, gy, idx, xmask,
+                     gx, B, H, W, C, Ho, Wo);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ------------------------------------------------------------------------------- GAP
+__global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B, int HW, int C) {
+  const int cg = C / 8;
+  const long total = (long)B * cg;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(t % cg), b = (int)(t / cg);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < HW; ++i) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + ((long)b * HW + i) * C + g * 8), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+    const float inv = 1.f / HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    *reinterpret_cast<uint4*>(y + (long)b * C + g * 8) = pack8(acc);
+  }
+}
+__global__ void gap_bwd_kernel(const bf16_t* __restrict__ gp, int ldgp, const bf16_t* __restrict__ ymask,
+                               bf16_t* __restrict__ g, int B, int HW, int C) {
+  const int cg = C / 8;
+  const long total = (long)B * HW * cg;
+  const float inv = 1.f / HW;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int gg = (int)(t % cg);
+    const long row = t / cg;
+    const int b = (int)(row / HW);
+    float v[8], mv[8];
+    unpack8(*reinterpret_cast<const uint4*>(gp + (long)b * ldgp + gg * 8), v);
+    unpack8(*reinterpret_cast<const uint4*>(ymask + row * C + gg * 8), mv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = mv[e] > 0.f ? v[e] * inv : 0.f;
+    *reinterpret_cast<uint4*>(g + row * C + gg * 8) = pack8(v);
+  }
+}
+const char* gap_fwd_launch(const uint16_t* x, uint16_t* y, int B, int HW, int C, hipStream_t s) {
+  if (C % 8) return "gap: C % 8";
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(grid_for((long)B * C / 8)), dim3(256), 0, s, x, y, B, HW, C);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+const char* gap_bwd_launch(const uint16_t* gp, int ldgp, const uint16_t* ymask, uint16_t* g, int B, int HW, int C,
+                           hipStream_t s) {
+  if (C % 8 || ldgp % 8) return "gap: C % 8";
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)B * HW * C / 8)), dim3(256), 0, s, gp, ldgp, ymask, g, B,
+                     HW, C);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ---------------------------------------------------------------------------- colsum
+// out[c] += sum_m g[m, c].  Block = 256 threads = CG column groups (8 columns each) x RL row
+// lanes; registers accumulate, LDS folds the row lanes, one atomic per column per block.
+__global__ void colsum_kernel(const bf16_t* __restrict__ g, int M, int C, int ldg, int rows_per_block,
+                              float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int G = C / 8;
+  const int CG = G < 32 ? G : 32;
+  const int RL = 256 / CG;
+  const int t = threadIdx.x;
+  const int cgi = t % CG, rl = t / CG;
+  const int colg = blockIdx.x * CG + cgi;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (colg < G && rl < RL) {
+    for (int r = r0 + rl; r < r1; r += RL) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(g + (long)r * ldg + colg * 8), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[t * 8 + e] = acc[e];
+  __syncthreads();
+  if (t < CG * 8) {
+    const int cg2 = t / 8, e = t % 8;
+    float s = 0.f;
+    for (int l = 0; l < RL; ++l) s += red[((l * CG) + cg2) * 8 + e];
+    const int col = (blockIdx.x * CG + cg2) * 8 + e;
+    if (col < C) unsafeAtomicAdd(out + col, s);
+  }
+}
+const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, hipStream_t s) {
+  if (C % 8 || ldg % 8) return "colsum: C % 8";
+  const int G = C / 8, CG = G < 32 ? G : 32;
+  const int gx = (G + CG - 1) / CG;
+  int rpb = 512;
+  int gy = (M + rpb - 1) / rpb;
+  if ((long)gx * gy > 4096) { gy = (4096 + gx - 1) / gx; rpb = (M + gy - 1) / gy; gy = (M + rpb - 1) / rpb; }
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, s, g, M, C, ldg, rpb, out);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ---------------------------------------------------------------------- softmax-xent
+// One wave per example.  loss += logsumexp - logit[label]; dlogits = (softmax - onehot)*gscale
+// written as bf16 into [B][ldd] (columns >= ncls zeroed: they are the K padding of the head
+// dgrad); correct += (first argmax == label).
+__global__ void softmax_xent_kernel(const float* __restrict__ logits, int ldl, const int64_t* __restrict__ labels,
+                                    int B, int ncls, float gscale, bf16_t* __restrict__ dl, int ldd,
+                                    float* __restrict__ loss_sum, float* __restrict__ correct) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* row = logits + (long)b * ldl;
+  float mx = -INFINITY; int amax = 0x7fffffff;
+  for (int j = lane; j < ncls; j += 64) {
+    const float v = row[j];
+    if (v > mx) { mx = v; amax = j; }
+  }
+  // wave argmax (first index among equal maxima)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(amax, o, 64);
+    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+  }
+  float se = 0.f;
+  for (int j = lane; j < ncls; j += 64) se += __expf(row[j] - mx);
+  se = warp_sum(se);
+  const int lab = (int)labels[b];
+  const float inv = 1.f / se;
+  for (int j = lane; j < ldd; j += 64) {
+    float d = 0.f;
+    if (j < ncls) d = (__expf(row[j] - mx) * inv - (j == lab ? 1.f : 0.f)) * gscale;
+    dl[(long)b * ldd + j] = f2bf(d);
+  }
+  if (lane == 0) {
+    const float lse = mx + __logf(se);
+    unsafeAtomicAdd(loss_sum, lse - row[lab]);
+    unsafeAtomicAdd(correct, amax == lab ? 1.f : 0.f);
+  }
+}
+const char* softmax_xent_launch(const float* logits, int ldl, const int64_t* labels, int B, int ncls, float gscale,
+                                uint16_t* dlogits, int ldd, float* loss_sum, float* correct, hipStream_t s) {
+  if (ldd < ncls) return "softmax_xent: ldd < ncls";
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3((B + 3) / 4), dim3(256), 0, s, logits, ldl, labels, B, ncls, gscale,
+                     dlogits, ldd, loss_sum, correct);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ----------------------------------------------------------------------------- prep
+// After each optimizer step: fp32 master -> bf16 forward weights [cout][kpad] (zero padded),
+// bf16 dgrad weights W'[c][R-1-r][S-1-s][co] = a[co] * W[co][r][s][c], and the folded
+// frozen-BN affine a = gamma / sqrt(var + eps), b = (bias - mean) * a + beta.
+__global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __restrict__ L, uint16_t* __restrict__ wbf,
+                            float* __restrict__ scale, float* __restrict__ shift, float eps) {
+  const PrepLayer l = L[blockIdx.y];
+  const int RSC = l.R * l.S * l.cin;
+  auto fold = [&](int co, float* a_out, float* b_out) {
+    const float g = l.gamma_off >= 0 ? prm[l.gamma_off + co] : 1.f;
+    const float var = l.var_off >= 0 ? prm[l.var_off + co] : 1.f - eps;
+    const float mu = l.mean_off >= 0 ? prm[l.mean_off + co] : 0.f;
+    const float be = l.beta_off >= 0 ? prm[l.beta_off + co] : 0.f;
+    const float bi = l.bias_off >= 0 ? prm[l.bias_off + co] : 0.f;
+    const float a = (l.gamma_off >= 0 || l.var_off >= 0) ? g * rsqrtf(var + eps) : 1.f;
+    *a_out = a;
+    *b_out = (bi - mu) * a + be;
+  };
+  const long nf = (long)l.cout * l.kpad;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nf; e += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(e / l.kpad), k = (int)(e - (long)co * l.kpad);
+    const float w = k < RSC ? prm[l.w_off + (long)co * RSC + k] : 0.f;
+    wbf[l.wf_off + e] = f2bf(w);
+    if (l.wd_off >= 0 && k < RSC) {
+      float a, b;
+      fold(co, &a, &b);
+      const int rs = k / l.cin, c = k - rs * l.cin;
+      const int r = rs / l.S, s = rs - r * l.S;
+      const long d = (((long)c * l.R + (l.R - 1 - r)) * l.S + (l.S - 1 - s)) * l.cout_pad + co;
+      wbf[l.wd_off + d] = f2bf(a * w);
+    }
+    if (k == 0) {
+      float a, b;
+      fold(co, &a, &b);
+      scale[l.ch_off + co] = a;
+      shift[l.ch_off + co] = b;
+    }
+  }
+}
+const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems, uint16_t* wbf,
+                        float* scale, float* shift, float eps, hipStream_t s) {
+  int gx = (max_elems + 255) / 256;
+  if (gx > 256) gx = 256;
+  hipLaunchKernelGGL(prep_kernel, dim3(gx, nlayers), dim3(256), 0, s, params, layers_dev, wbf, scale, shift, eps);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// --------------------------------------------------------------------- wgrad finalize
+__global__ void wgrad_finalize_kernel(const float* __restrict__ prm, float* __restrict__ grads,
+                                      const FinLayer* __restrict__ L, const float* __restrict__ scale,
+                                      float* __restrict__ dgamma_raw) {
+  __shared__ float red[4];
+  const FinLayer l = L[blockIdx.y];
+  const int co = blockIdx.x;
+  if (co >= l.cout) return;
+  const float* w = prm + l.w_off + (long)co * l.k;
+  float* dw = grads + l.w_off + (long)co * l.k;
+  const float a = l.ch_off >= 0 ? scale[l.ch_off + co] : 1.f;
+  float dot = 0.f;
+  for (int k = threadIdx.x; k < l.k; k += blockDim.x) {
+    const float d = dw[k];
+    dot += w[k] * d;
+    dw[k] = d * a;
+  }
+  dot = warp_sum(dot);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dot;
+  __syncthreads();
+  if (threadIdx.x == 0 && l.dg_off >= 0) dgamma_raw[l.dg_off + co] = red[0] + red[1] + red[2] + red[3];
+}
+const char* wgrad_finalize_launch(const float* params, float* grads, const FinLayer* layers_dev, int nlayers,
+                                  const float* scale, float* dgamma_raw, hipStream_t s) {
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(2048, nlayers), dim3(256), 0, s, params, grads, layers_dev, scale,
+                     dgamma_raw);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// --------------------------------------------------------------------------- bn grads
+__global__ void bn_grad_kernel(const float* __restrict__ prm, float* __restrict__ grads,
+                               const BnGradLayer* __restrict__ L, const float* __restrict__ colsum,
+                               const float* __restrict__ dgr, const float* __restrict__ scale, float eps) {
+  const BnGradLayer l = L[blockIdx.y];
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < l.cout; c += gridDim.x * blockDim.x) {
+    const float sg = colsum[l.colsum_off + c];
+    const float a = l.ch_off >= 0 ? scale[l.ch_off + c] : 1.f;
+    if (l.bias_off >= 0) grads[l.bias_off + c] = a * sg;
+    if (l.beta_off >= 0) grads[l.beta_off + c] = sg;
+    if (l.gamma_off >= 0) {
+      const float mu = prm[l.mean_off + c], var = prm[l.var_off + c];
+      const float bi = l.bias_off >= 0 ? prm[l.bias_off + c] : 0.f;
+      grads[l.gamma_off + c] = (dgr[l.dg_off + c] + (bi - mu) * sg) * rsqrtf(var + eps);
+    }
+  }
+}
+const char* bn_grad_launch(const float* params, float* grads, const BnGradLayer* layers_dev, int nlayers,
+                           const float* colsum, const float* dgamma_raw, const float* scale, float eps,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(bn_grad_kernel, dim3(8, nlayers), dim3(256), 0, s, params, grads, layers_dev, colsum, dgamma_raw,
+                     scale, eps);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+}  // namespace pddl

@@ -1,0 +1,113 @@
+// Host-visible parameter blocks and launchers of the pddl HIP kernels.
+// This header is included by the kernel translation units and by the torch bindings;
+// it deliberately has no torch dependency so the .hip files compile in seconds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pddl {
+
+enum EpiMode { EPI_FWD = 0, EPI_DGRAD = 1, EPI_F32 = 2 };
+
+struct IgemmParams {
+  // A operand: NHWC bf16 tensor(s), gathered as im2col rows.
+  const uint16_t* a1; int C1;      // first source, channels (multiple of 64)
+  const uint16_t* a2; int C2;      // optional second source (concatenated along K)
+  int N, H, W;                     // input dims shared by both sources
+  int R, S, stride, pad;
+  int Ho, Wo, M;                   // GEMM rows = N * Ho * Wo
+  int K1, K;                       // K1 = R*S*C1, K = K1 + R*S*C2
+  // B operand: [Nn][ldb] bf16, K contiguous.
+  const uint16_t* b; int ldb; int Nn;
+  // epilogue
+  int mode;
+  const float* scale; const float* shift;           // per output column (FWD / F32)
+  const uint16_t* res; int ld_res;                  // FWD residual (added before act)
+  const uint16_t* mask; int ld_mask;                // DGRAD: multiply by (mask > 0)
+  const uint16_t* add; int ld_add;                  // DGRAD: added before the mask
+  void* out; int ldo; int relu;
+  void* out2; int ldo2; int relu2; int n_split;     // FWD: columns >= n_split -> out2
+  int up2; int Hf, Wf;                              // DGRAD: scatter to a 2x finer grid
+};
+const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
+
+struct WgradParams {
+  const uint16_t* x; int N, H, W, C;   // conv input, NHWC (or [M][ldx] rows for 1x1/s1)
+  int ldx;
+  int R, S, stride, pad, Ho, Wo, M;
+  const uint16_t* g; int ldg;          // output gradient [M][ldg]
+  const uint16_t* g2; int ldg2; int co_split;  // optional second gradient for rows >= co_split
+  int Cout, K;                         // dW is [Cout][K]
+  float* dw; int ld_dw;                // fp32, accumulated with atomics
+  int splits;                          // split of M across workgroups (0 = auto)
+};
+const char* wgrad_launch(const WgradParams& p, hipStream_t stream);
+
+// ---- elementwise / reduction kernels (eltwise.hip) ----
+struct StemParams {
+  const void* in; int in_u8;          // [B, Hin, Win, 3] uint8 or fp32 (0..255)
+  int B, Hin, Win;
+  int Hc, Wc;                         // preprocessed (cropped / resized) size
+  int mode;                           // 0 identity, 1 bilinear resize, 2 crop at (oy, ox)
+  int oy, ox;
+  const uint8_t* flip;                // per-image horizontal flip flags (nullable)
+  float scale;                        // Rescaling(1/255)
+  uint16_t* out; int Ho, Wo, ldo;     // im2col rows [B*Ho*Wo][ldo], k = (r*7+s)*3+c, zero padded
+};
+const char* stem_im2col_launch(const StemParams& p, hipStream_t s);
+
+const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, int B, int H, int W, int C,
+                               int Ho, int Wo, hipStream_t s);
+const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uint16_t* xmask, uint16_t* gx,
+                               int B, int H, int W, int C, int Ho, int Wo, hipStream_t s);
+const char* gap_fwd_launch(const uint16_t* x, uint16_t* y, int B, int HW, int C, hipStream_t s);
+const char* gap_bwd_launch(const uint16_t* gp, int ldgp, const uint16_t* ymask, uint16_t* g, int B, int HW, int C,
+                           hipStream_t s);
+const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, hipStream_t s);
+const char* softmax_xent_launch(const float* logits, int ldl, const int64_t* labels, int B, int ncls,
+                                float gscale, uint16_t* dlogits, int ldd, float* loss_sum, float* correct,
+                                hipStream_t s);
+
+// Per-layer parameter preparation after every optimizer step (one launch for all layers).
+struct PrepLayer {
+  int w_off;          // offset of the fp32 kernel [Cout][R][S][Cin] in the flat param buffer
+  int cout, R, S, cin;
+  int kpad;           // forward bf16 row length (>= R*S*cin, multiple of 64)
+  long wf_off;        // offset (elements) of the forward bf16 weights
+  long wd_off;        // offset of the dgrad bf16 weights [cin][R][S][cout_pad] (-1: none)
+  int cout_pad;
+  int bias_off, gamma_off, beta_off, mean_off, var_off;   // -1 when absent
+  int ch_off;         // offset of this layer's folded scale/shift (per output channel)
+};
+const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems,
+                        uint16_t* wbf, float* scale, float* shift, float eps, hipStream_t s);
+
+// dW finalize: dgamma_raw[c] = sum_k W[c,k] * dWraw[c,k]; dW[c,k] *= a[c] (in place).
+struct FinLayer {
+  int w_off; int cout; int k;   // flat offsets of W (params) / dW (grads), rows x k
+  int ch_off;                   // folded scale index
+  int dg_off;                   // output offset for dgamma_raw (per channel, -1: none)
+};
+const char* wgrad_finalize_launch(const float* params, float* grads, const FinLayer* layers_dev, int nlayers,
+                                  const float* scale, float* dgamma_raw, hipStream_t s);
+
+// Per-channel BN/bias grads from column sums and dgamma_raw.
+struct BnGradLayer {
+  int cout, ch_off;
+  int bias_off, gamma_off, beta_off, mean_off, var_off;   // -1 when absent (grads written into `grads`)
+  int colsum_off, dg_off;
+};
+const char* bn_grad_launch(const float* params, float* grads, const BnGradLayer* layers_dev, int nlayers,
+                           const float* colsum, const float* dgamma_raw, const float* scale, float eps,
+                           hipStream_t s);
+
+// ---- optimizers (optim.hip) ----
+const char* adam_launch(float* p, const float* g, float* m, float* v, long n, float lr_t, float b1, float b2,
+                        float eps, float gscale, hipStream_t s);
+const char* sgd_launch(float* p, const float* g, float* mom, long n, float lr, float momentum, float wd,
+                       int nesterov, float gscale, hipStream_t s);
+const char* scale_launch(float* x, long n, float a, hipStream_t s);
+const char* cast_bf16_launch(const float* x, uint16_t* y, long n, hipStream_t s);
+const char* cast_f32_launch(const uint16_t* x, float* y, long n, hipStream_t s);
+
+}  // namespace pddl

@@ -1,0 +1,207 @@
+// Weight-gradient of the implicit-GEMM convolution on MFMA (gfx950).
+//
+//   dW[co, k] += sum_m g[m, co] * im2col(x)[m, k]        (k = (r, s, c), c fastest)
+//
+// Reference parity: the backward-filter half of every Keras Conv2D / Dense weight update
+// (ResourceApplyAdam consumes these, imagenet-resnet50.py:62); SURVEY.md §2.4 N3.
+//
+// Both operands are row-major along the reduction axis m in NHWC memory (g is [M][Cout],
+// x rows are [M][K]), which is the "TN" GEMM case.  Instead of transposing in memory, the
+// tiles are staged lane-linearly into LDS as [m][col] by 16-byte LDS-DMA and read with the
+// gfx950 transposing LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10): one
+// read gives a lane 4 consecutive m for one column, two reads give the 8-deep k fragment of
+// a 16x16x32 bf16 MFMA operand.
+//
+// The reduction over M = N*Ho*Wo (up to 800k rows) is split across workgroups; partial
+// tiles go through LDS and are added with row-contiguous (256 B per wave instruction)
+// no-return fp32 atomics into the flat fp32 gradient buffer (MI355X_MICROARCH.md "Global
+// float atomics": ~1.3 TB/s chip-wide, so splits are sized to keep atomic bytes small).
+#include "common.h"
+#include "kernels.h"
+
+namespace pddl {
+
+// Bank-conflict swizzle for the [m][128 x bf16] (256-byte row) images: the 8 rows a
+// 32-lane half of ds_read_b64_tr_b16 touches get distinct even chunk XORs, so the 16
+// 16-byte chunks they read cover all 64 banks exactly once.
+__device__ __forceinline__ int tr_swz(int row) { return ((row & 3) | ((row >> 1) & 4)) << 1; }
+
+template <bool FAST>
+__global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split) {
+  constexpr int TILE_BYTES = 64 * 256;        // 64 m-rows x 128 bf16
+  constexpr int STAGE = 2 * TILE_BYTES;       // G tile + X tile
+  constexpr int EPI_LD = 68;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tco = (p.Cout + 127) / 128, tk = (p.K + 127) / 128, ntiles = tco * tk;
+  const int splits = (p.M + m_per_split - 1) / m_per_split;
+  const int wg = xcd_remap(blockIdx.x, ntiles * splits);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int co0 = (tile % tco) * 128, k0 = (tile / tco) * 128;
+  const int mbeg = split * m_per_split;
+  const int mend = min(p.M, mbeg + m_per_split);
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
+  const int HoWo = p.Ho * p.Wo;
+
+  // (r, s, c0) of the two 64-column halves of this k tile (generic path only).
+  int hr[2], hs[2], hc[2]; bool hv[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kk = k0 + h * 64;
+    hv[h] = kk < p.K;
+    const int rs = kk / p.C; hc[h] = kk - rs * p.C; hr[h] = rs / p.S; hs[h] = rs - hr[h] * p.S;
+  }
+
+  // Loader lane geometry: piece i of wave w covers rows (w*4+i)*4 .. +3, 16 chunks per row.
+  const int lrow = lane >> 4, lpos = lane & 15;
+
+  auto load_tile = [&](int mb, int buf) {
+    char* gb = smem + buf * STAGE;
+    char* xb = gb + TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wave * 4 + i) * 4 + lrow;
+      const int chunk = lpos ^ tr_swz(row);
+      const int m = mb + row;
+      const bool mok = m < mend;
+      // gradient operand
+      const int co = co0 + chunk * 8;
+      const bf16_t* gs = zero;
+      if (mok && co < p.Cout) {
+        if (p.g2 && co >= p.co_split) gs = p.g2 + (long)m * p.ldg2 + (co - p.co_split);
+        else gs = p.g + (long)m * p.ldg + co;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)gs, LDS_PTR(gb + (wave * 4 + i) * 1024), 16, 0, 0);
+      // input operand
+      const bf16_t* xs = zero;
+      if (FAST) {
+        const int kc = k0 + chunk * 8;
+        if (mok && kc < p.K) xs = p.x + (long)m * p.ldx + kc;
+      } else {
+        const int h = chunk >> 3;
+        const int r = h ? hr[1] : hr[0], s = h ? hs[1] : hs[0], c = h ? hc[1] : hc[0];
+        const bool v = h ? hv[1] : hv[0];
+        if (mok && v) {
+          const int n = m / HoWo, rem = m - n * HoWo;
+          const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+          const int hi = ho * p.stride - p.pad + r, wi = wo * p.stride - p.pad + s;
+          if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+            xs = p.x + ((long)((n * p.H + hi) * p.W + wi) * p.C + c + (chunk & 7) * 8);
+        }
+      }
+      __builtin_amdgcn_global_load_lds((const void*)xs, LDS_PTR(xb + (wave * 4 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // Fragment-read lane geometry (T10): group G = lane>>4 reads rows 8G + 4h + q, q = (lane&15)>>2,
+  // columns 4p..4p+3, p = lane&3.
+  const int G = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int nit = (mend - mbeg + 63) / 64;
+  if (nit > 0) {
+    load_tile(mbeg, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
+    const char* gb = smem + cur * STAGE;
+    const char* xb = gb + TILE_BYTES;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      int roff[2], rsw[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int row = kh * 32 + 8 * G + 4 * h2 + q;
+        roff[h2] = row * 256 + (pp & 1) * 8;
+        rsw[h2] = tr_swz(row);
+      }
+      v8bf af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ch = wm * 8 + i * 2 + (pp >> 1);
+        v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) v4bf*)(gb + roff[0] + ((ch ^ rsw[0]) << 4)));
+        v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) v4bf*)(gb + roff[1] + ((ch ^ rsw[1]) << 4)));
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = wn * 8 + j * 2 + (pp >> 1);
+        v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) v4bf*)(xb + roff[0] + ((ch ^ rsw[0]) << 4)));
+        v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) v4bf*)(xb + roff[1] + ((ch ^ rsw[1]) << 4)));
+        bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (nit == 0) return;
+
+  // Epilogue: per-wave 32x64 fp32 staging, then one 256-byte atomic row per instruction.
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
+  const int kcol = k0 + wn * 64 + lane;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          stage[(i2 * 16 + (lane >> 4) * 4 + jj) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 2 + i2][j][jj];
+    __syncthreads();
+    if (kcol < p.K) {
+      for (int r = 0; r < 32; ++r) {
+        const int co = co0 + wm * 64 + pass * 32 + r;
+        if (co < p.Cout) unsafeAtomicAdd(p.dw + (long)co * p.ld_dw + kcol, stage[r * EPI_LD + lane]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
+  WgradParams p = pin;
+  const bool fast = (p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0);
+  if (!fast && p.C % 64) return "wgrad: C must be a multiple of 64 for the gather path";
+  if (p.Cout % 8 || p.ldg % 8 || (fast && p.ldx % 8)) return "wgrad: Cout / ldg / ldx must be multiples of 8";
+  if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "wgrad: empty problem";
+  if (!fast && (long)p.N * p.H * p.W * p.C >= (1L << 31)) return "wgrad: input too large";
+  const int ntiles = ((p.Cout + 127) / 128) * ((p.K + 127) / 128);
+  int splits = p.splits;
+  if (splits <= 0) {
+    splits = (2048 + ntiles - 1) / ntiles;
+    const int maxs = (p.M + 255) / 256;  // at least 4 iterations per workgroup
+    if (splits > maxs) splits = maxs;
+    if (splits < 1) splits = 1;
+  }
+  int mps = (p.M + splits - 1) / splits;
+  mps = (mps + 63) / 64 * 64;
+  splits = (p.M + mps - 1) / mps;
+  const int nwg = ntiles * splits;
+  if (fast)
+    hipLaunchKernelGGL(wgrad_kernel<true>, dim3(nwg), dim3(256), 0, stream, p, mps);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<false>, dim3(nwg), dim3(256), 0, stream, p, mps);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+}  // namespace pddl
