@@ -1,0 +1,391 @@
+"""HIP execution engine for ResNet-50 on MI355X: explicit forward/backward schedule.
+
+No autograd tape on the GPU path.  The whole training step is a fixed sequence of native
+kernel launches over preallocated NHWC bf16 activation buffers (sized once for the batch),
+with fp32 master parameters, gradients and optimizer state in flat buffers:
+
+  forward  : stem_im2col (preprocess fused) -> igemm(stem) -> maxpool -> 16 bottleneck
+             blocks (3 or 4 igemm launches each; frozen BN + bias + residual + ReLU folded
+             into epilogues; conv1 and the projection conv0 share one launch) -> GAP ->
+             igemm(dense, fp32) -> softmax-xent (fwd+bwd fused)
+  backward : per layer wgrad (fp32 atomics into the flat gradient buffer) + colsum +
+             dgrad igemm whose epilogue applies the ReLU mask of the layer below and adds
+             the residual gradient; conv1+conv0 dgrad is ONE GEMM over a K-concatenation;
+             then wgrad_finalize (dW *= BN scale, dgamma partials) and bn_grad (per-channel).
+  buckets  : `bucket_cb(i)` fires as soon as gradient bucket i (a contiguous slice of the
+             flat buffer) has been fully produced on the compute stream, so a DP strategy
+             can all-reduce it while backward continues.
+
+Reference parity: the Keras graph of imagenet-resnet50.py:51-67 (see models/reference.py
+for the fp32 oracle and tests/test_gpu_engine.py for the parity checks).
+"""
+from __future__ import annotations
+
+import struct
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from ..ops.native import require_native
+from .resnet50 import BN_EPS, ParamLayout
+
+_PREP_FMT = "<6i2q7i4x"
+_FIN_FMT = "<5i"
+_BNG_FMT = "<9i"
+
+
+def _ceil(a, b):
+    return (a + b - 1) // b * b
+
+
+class HipEngine:
+    def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
+                 device="cuda", bn_mode: str = "frozen", num_classes: int = 1000):
+        if bn_mode != "frozen":
+            raise NotImplementedError("HipEngine: bn_mode='train' runs on the TorchEngine path for now")
+        self.N = require_native()
+        self.L = layout
+        self.device = torch.device(device)
+        self.batch = batch
+        self.crop = crop
+        self.image_size = image_size
+        self.num_classes = num_classes
+        self.ncls_pad = _ceil(num_classes, 64)
+        assert struct.calcsize(_PREP_FMT) == self.N.PREP_LAYER_BYTES
+        assert struct.calcsize(_FIN_FMT) == self.N.FIN_LAYER_BYTES
+        assert struct.calcsize(_BNG_FMT) == self.N.BNGRAD_LAYER_BYTES
+        dev = self.device
+        L = layout
+        self.params = torch.zeros(L.total, dtype=torch.float32, device=dev)
+        # ---- per-channel bookkeeping (folded scale / shift, colsum, dgamma partials)
+        self.ch: Dict[str, int] = {}
+        off = 0
+        for c in L.convs:
+            self.ch[c.name] = off
+            off += c.cout
+        self.ch["dense"] = off
+        off += _ceil(num_classes, 8)
+        self.nch = _ceil(off, 64)
+        # ---- one zeroed-per-step workspace: grads | colsum | dgamma_raw | stats
+        n_tr = L.n_trainable
+        self.ws = torch.zeros(n_tr + 2 * self.nch + 64, dtype=torch.float32, device=dev)
+        self.grads = self.ws[:n_tr]
+        self.colsum = self.ws[n_tr:n_tr + self.nch]
+        self.dgr = self.ws[n_tr + self.nch:n_tr + 2 * self.nch]
+        self.stats = self.ws[n_tr + 2 * self.nch:n_tr + 2 * self.nch + 2]
+        self.scale = torch.ones(self.nch, dtype=torch.float32, device=dev)
+        self.shift = torch.zeros(self.nch, dtype=torch.float32, device=dev)
+        self._build_weight_tables()
+        self._alloc_acts(batch)
+
+    # ------------------------------------------------------------------ tables
+    def _build_weight_tables(self):
+        L = self.L
+        wf: Dict[str, int] = {}
+        off = 0
+        for c in L.convs:
+            kpad = _ceil(c.k * c.k * c.cin, 64)
+            wf[c.name] = off
+            off += c.cout * kpad
+        wf["dense"] = off
+        off += self.num_classes * 2048
+        # dgrad weights: [cin][R][S][ld]; a projection block's conv1 and conv0 share rows
+        wd: Dict[str, int] = {}
+        wd_ld: Dict[str, int] = {}
+        for b in L.blocks:
+            if b.proj:
+                c1, c0 = b.convs["1"], b.convs["0"]
+                ld = c1.cout + c0.cout
+                wd[c1.name], wd[c0.name] = off, off + c1.cout
+                wd_ld[c1.name] = wd_ld[c0.name] = ld
+                off += c1.cin * ld
+            else:
+                c1 = b.convs["1"]
+                wd[c1.name], wd_ld[c1.name] = off, c1.cout
+                off += c1.cin * c1.cout
+            for k in ("2", "3"):
+                c = b.convs[k]
+                wd[c.name], wd_ld[c.name] = off, c.cout
+                off += c.cin * c.k * c.k * c.cout
+        wd["dense"], wd_ld["dense"] = off, self.ncls_pad
+        off += 2048 * self.ncls_pad
+        self.wbf = torch.zeros(off, dtype=torch.bfloat16, device=self.device)
+        self.wf, self.wd, self.wd_ld = wf, wd, wd_ld
+        # prep table
+        rows = []
+        max_el = 0
+        for c in L.convs + ["dense"]:
+            if c == "dense":
+                name, cout, R, cin = "dense", self.num_classes, 1, 2048
+                kpad = 2048
+                bias, gam, bet, mu, var = L.off("dense", "bias"), -1, -1, -1, -1
+                wd_off, ld = wd["dense"], wd_ld["dense"]
+            else:
+                name, cout, R, cin = c.name, c.cout, c.k, c.cin
+                kpad = _ceil(R * R * cin, 64)
+                bias = L.off(c.name, "bias")
+                gam, bet = L.off(c.bn, "gamma"), L.off(c.bn, "beta")
+                mu, var = L.off(c.bn, "moving_mean"), L.off(c.bn, "moving_variance")
+                wd_off, ld = wd.get(c.name, -1), wd_ld.get(c.name, 0)
+            rows.append(struct.pack(_PREP_FMT, L.off(name, "kernel"), cout, R, R, cin, kpad, wf[name], wd_off, ld,
+                                    bias, gam, bet, mu, var, self.ch[name]))
+            max_el = max(max_el, cout * kpad)
+        self._prep_tab = self._dev_table(rows)
+        self._prep_n = len(rows)
+        self._prep_max = max_el
+        # finalize table rows per layer, bn-grad table
+        self._fin_rows: Dict[str, bytes] = {}
+        for c in L.convs:
+            self._fin_rows[c.name] = struct.pack(_FIN_FMT, L.off(c.name, "kernel"), c.cout, c.k * c.k * c.cin,
+                                                 self.ch[c.name], self.ch[c.name])
+        self._fin_tabs: Dict[str, torch.Tensor] = {}
+        for b in L.blocks:
+            keys = ["3", "2", "1", "0"] if b.proj else ["3", "2", "1"]
+            self._fin_tabs[b.name] = self._dev_table([self._fin_rows[b.convs[k].name] for k in keys])
+        self._fin_tabs["stem"] = self._dev_table([self._fin_rows[L.stem.name]])
+        bg = []
+        for c in L.convs:
+            cs = self.ch[c.name]
+            for b in L.blocks:   # conv0 of a projection block shares conv3's gradient
+                if b.proj and b.convs["0"].name == c.name:
+                    cs = self.ch[b.convs["3"].name]
+            bg.append(struct.pack(_BNG_FMT, c.cout, self.ch[c.name], L.off(c.name, "bias"), L.off(c.bn, "gamma"),
+                                  L.off(c.bn, "beta"), L.off(c.bn, "moving_mean"), L.off(c.bn, "moving_variance"),
+                                  cs, self.ch[c.name]))
+        bg.append(struct.pack(_BNG_FMT, self.num_classes, self.ch["dense"], L.off("dense", "bias"), -1, -1, -1, -1,
+                              self.ch["dense"], -1))
+        self._bng_tab = self._dev_table(bg)
+        self._bng_n = len(bg)
+
+    def _dev_table(self, rows: List[bytes]) -> torch.Tensor:
+        buf = bytearray(b"".join(rows))
+        return torch.frombuffer(buf, dtype=torch.uint8).clone().to(self.device)
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc_acts(self, B):
+        L, dev = self.L, self.device
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        crop = self.crop
+        H1 = (crop + 6 - 7) // 2 + 1
+        H2 = (H1 + 2 - 3) // 2 + 1
+        self.H1, self.H2 = H1, H2
+        self.stem_col = torch.empty(B, H1, H1, 192, **bf)
+        self.c1 = torch.empty(B, H1, H1, 64, **bf)
+        self.pool = torch.empty(B, H2, H2, 64, **bf)
+        self.pidx = torch.empty(B, H2, H2, 64, dtype=torch.uint8, device=dev)
+        self.acts: Dict[str, Dict[str, torch.Tensor]] = {}
+        H = H2
+        inner = 0
+        outer = B * H1 * H1 * 64
+        self.geo = {}
+        for b in L.blocks:
+            f = b.filters
+            Ho = (H - 1) // b.stride + 1
+            a = {"y1": torch.empty(B, Ho, Ho, f, **bf), "y2": torch.empty(B, Ho, Ho, f, **bf),
+                 "out": torch.empty(B, Ho, Ho, 4 * f, **bf)}
+            if b.proj:
+                a["sc"] = torch.empty(B, Ho, Ho, 4 * f, **bf)
+            self.acts[b.name] = a
+            self.geo[b.name] = (H, Ho)
+            inner = max(inner, B * Ho * Ho * f)
+            outer = max(outer, B * H * H * b.cin, B * Ho * Ho * 4 * f)
+            H = Ho
+        self.H5 = H
+        self.gbuf = [torch.empty(outer, **bf), torch.empty(outer, **bf)]
+        self.g1buf = torch.empty(inner, **bf)
+        self.g2buf = torch.empty(inner, **bf)
+        self.pooled = torch.empty(B, 2048, **bf)
+        self.logits = torch.empty(B, self.num_classes, dtype=torch.float32, device=dev)
+        self.dlogits = torch.zeros(B, self.ncls_pad, **bf)
+        self.dpooled = torch.empty(B, 2048, **bf)
+        self.labels_dev = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.cap = B
+
+    # ------------------------------------------------------------------ params
+    def init(self, seed=0):
+        self.L.init_params(self.params, seed)
+        self.after_update()
+
+    def after_update(self):
+        """Refresh bf16 forward / dgrad weights and folded BN affine from the fp32 master."""
+        self.N.prep(self.params, self._prep_tab, self._prep_n, self._prep_max, self.wbf, self.scale, self.shift,
+                    BN_EPS)
+
+    def _wf(self, name, rows, k):
+        o = self.wf[name]
+        return self.wbf[o:o + rows * k].view(rows, k)
+
+    def _wdv(self, name, cin, k):
+        o = self.wd[name]
+        return self.wbf[o:o + cin * k].view(cin, k)
+
+    def _gview(self, name, rows, k):
+        o = self.L.off(name, "kernel")
+        return self.grads[o:o + rows * k].view(rows, k)
+
+    # ------------------------------------------------------------------ forward
+    def _stem_mode(self, training, crop_offset):
+        if self.crop == self.image_size:
+            return 0, 0, 0
+        if self.crop > self.image_size or not training:
+            return 1, 0, 0
+        return 2, crop_offset[0], crop_offset[1]
+
+    def _forward(self, images, B, training, flip, crop_offset):
+        N, L = self.N, self.L
+        mode, oy, ox = self._stem_mode(training, crop_offset)
+        col = self.stem_col[:B]
+        N.stem_im2col(images, flip if training else None, mode, self.crop, self.crop, oy, ox, col)
+        H1, H2 = self.H1, self.H2
+        s = L.stem
+        c1 = self.c1[:B]
+        N.igemm(col, None, H1, H1, 1, 1, 1, 0, H1, H1, self._wf(s.name, 64, 192), 0,
+                self.scale[self.ch[s.name]:], self.shift[self.ch[s.name]:], None, None, None, c1, 1,
+                None, 0, 0, 0, 0, 0)
+        pool = self.pool[:B]
+        N.maxpool_fwd(c1, pool, self.pidx[:B])
+        x = pool
+        for b in L.blocks:
+            a = self.acts[b.name]
+            H, Ho = self.geo[b.name]
+            f, cin = b.filters, b.cin
+            y1, y2, out = a["y1"][:B], a["y2"][:B], a["out"][:B]
+            c1n = b.convs["1"].name
+            ch1 = self.ch[c1n]
+            if b.proj:
+                N.igemm(x, None, H, H, 1, 1, b.stride, 0, Ho, Ho, self._wf(c1n, 5 * f, cin), 0,
+                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, a["sc"][:B], 0, f, 0, 0, 0)
+                res = a["sc"][:B]
+            else:
+                N.igemm(x, None, H, H, 1, 1, 1, 0, Ho, Ho, self._wf(c1n, f, cin), 0,
+                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, None, 0, 0, 0, 0, 0)
+                res = x
+            c2 = b.convs["2"].name
+            N.igemm(y1, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wf(c2, f, 9 * f), 0,
+                    self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0, 0, 0)
+            c3 = b.convs["3"].name
+            N.igemm(y2, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(c3, 4 * f, f), 0,
+                    self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 0, 0, 0)
+            x = out
+        pooled = self.pooled[:B]
+        H5 = self.H5
+        N.gap_fwd(x, pooled)
+        logits = self.logits[:B]
+        chd = self.ch["dense"]
+        N.igemm(pooled.view(B, 1, 1, 2048), None, 1, 1, 1, 1, 1, 0, 1, 1, self._wf("dense", self.num_classes, 2048), 2,
+                self.scale[chd:], self.shift[chd:], None, None, None, logits, 0, None, 0, 0, 0, 0, 0)
+        return x
+
+    def _labels(self, labels, B):
+        lab = self.labels_dev[:B]
+        lab.copy_(labels, non_blocking=True)
+        return lab
+
+    # ------------------------------------------------------------------ train step
+    def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0),
+                         bucket_cb: Optional[Callable[[int], None]] = None, buckets=None):
+        N, L = self.N, self.L
+        B = images.shape[0]
+        assert B <= self.cap, "batch larger than the engine's buffers"
+        self.ws.zero_()
+        lab = self._labels(labels, B)
+        x5 = self._forward(images, B, True, flip, crop_offset)
+        logits = self.logits[:B]
+        dl = self.dlogits[:B]
+        N.softmax_xent(logits, lab, self.num_classes, float(gscale), dl, self.stats[0:1], self.stats[1:2])
+
+        # bucket readiness tracking (kernels region is filled in layout order)
+        bks = buckets if buckets is not None else []
+        nb = [0]
+
+        def done_upto(off):
+            while bucket_cb is not None and nb[0] < len(bks) - 1 and bks[nb[0]][1] <= off:
+                bucket_cb(nb[0])
+                nb[0] += 1
+
+        # ---- head
+        pooled = self.pooled[:B]
+        chd = self.ch["dense"]
+        N.wgrad(pooled.view(B, 1, 1, 2048), 1, 1, 1, 1, 1, 0, 1, 1, dl, None, 0,
+                self._gview("dense", self.num_classes, 2048), 2048, 0)
+        N.colsum(dl, self.num_classes, self.colsum[chd:])
+        dpooled = self.dpooled[:B]
+        N.igemm(dl.view(B, 1, 1, self.ncls_pad), None, 1, 1, 1, 1, 1, 0, 1, 1,
+                self._wdv("dense", 2048, self.ncls_pad), 1, None, None, None, None, None, dpooled, 0,
+                None, 0, 0, 0, 0, 0)
+        e = L.entry("dense", "kernel")
+        done_upto(e.offset + e.size)
+        cur = 0
+        H5 = self.H5
+        gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
+        N.gap_bwd(dpooled, x5, gout)
+        # ---- blocks
+        blocks = L.blocks
+        for bi in range(len(blocks) - 1, -1, -1):
+            b = blocks[bi]
+            a = self.acts[b.name]
+            H, Ho = self.geo[b.name]
+            f, cin = b.filters, b.cin
+            x_in = self.acts[blocks[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
+            mask_in = x_in if bi > 0 else None
+            y1, y2 = a["y1"][:B], a["y2"][:B]
+            gout = self.gbuf[cur][: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
+            c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
+            # conv3
+            N.colsum(gout, 4 * f, self.colsum[self.ch[c3n]:])
+            N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)
+            g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2, None,
+                    g2, 0, None, 0, 0, 0, 0, 0)
+            # conv2 (3x3)
+            N.colsum(g2, f, self.colsum[self.ch[c2n]:])
+            N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
+            g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1, None,
+                    g1, 0, None, 0, 0, 0, 0, 0)
+            # conv1 (+ conv0)
+            N.colsum(g1, f, self.colsum[self.ch[c1n]:])
+            nxt = 1 - cur
+            gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+            if b.proj:
+                N.wgrad(x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0)
+                N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
+                N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, 5 * f), 1, None, None, None,
+                        mask_in, None, gx, 0, None, 0, 0, 1 if b.stride == 2 else 0, H, H)
+                last = L.entry(b.convs["0"].name, "kernel")
+            else:
+                N.wgrad(x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0)
+                N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
+                N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, f), 1, None, None, None,
+                        mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0)
+                last = L.entry(c1n, "kernel")
+            done_upto(last.offset + last.size)
+            cur = nxt
+        # ---- stem
+        H1, H2 = self.H1, self.H2
+        gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
+        gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
+        N.maxpool_bwd(gpool, self.pidx[:B], self.c1[:B], gc1)
+        s = L.stem
+        N.colsum(gc1, 64, self.colsum[self.ch[s.name]:])
+        N.wgrad(self.stem_col[:B], H1, H1, 1, 1, 1, 0, H1, H1, gc1, None, 0, self._gview(s.name, 64, 147), 147, 0)
+        N.wgrad_finalize(self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)
+        done_upto(L.kernels_end)
+        N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
+        if bucket_cb is not None:
+            while nb[0] < len(bks):
+                bucket_cb(nb[0])
+                nb[0] += 1
+        return self.stats
+
+    @torch.no_grad()
+    def evaluate(self, images, labels):
+        B = images.shape[0]
+        assert B <= self.cap
+        self.stats.zero_()
+        lab = self._labels(labels, B)
+        self._forward(images, B, False, None, (0, 0))
+        N = self.N
+        N.softmax_xent(self.logits[:B], lab, self.num_classes, 0.0, self.dlogits[:B], self.stats[0:1],
+                       self.stats[1:2])
+        return self.stats

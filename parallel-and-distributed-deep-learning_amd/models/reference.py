@@ -1,0 +1,149 @@
+"""PyTorch fp32 reference of the reference model (numerics oracle + CPU execution path).
+
+Implements exactly the Keras graph of imagenet-resnet50.py:51-61 with plain PyTorch ops
+and autograd, reading parameters as views of the flat layout (models/resnet50.py):
+Rescaling(1/255) -> RandomCrop (resize when the crop exceeds the input, Q1; random crop
+otherwise, Q2) -> RandomFlip("horizontal") -> ResNet50 v1 with BN in inference mode (Q3,
+`training=False`) or batch statistics (`bn_mode="train"`) -> GAP -> Dense -> softmax
+cross-entropy.  The GPU engine's kernels are tested against this module.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .resnet50 import BN_EPS, BN_MOMENTUM, ParamLayout
+
+
+def preprocess(images: torch.Tensor, crop: int, training: bool, flip: Optional[torch.Tensor] = None,
+               crop_offset=(0, 0)) -> torch.Tensor:
+    """[B,H,W,3] uint8/float (0..255) -> NCHW float32 in [0,1] at crop x crop."""
+    x = images.float().permute(0, 3, 1, 2) * (1.0 / 255.0)
+    H, W = x.shape[-2:]
+    if crop > H or crop > W or (not training and crop != H):
+        x = F.interpolate(x, size=(crop, crop), mode="bilinear", align_corners=False, antialias=False)
+    elif crop < H:
+        oy, ox = crop_offset
+        x = x[:, :, oy:oy + crop, ox:ox + crop]
+    if training and flip is not None:
+        f = flip.to(torch.bool).to(x.device)
+        x = torch.where(f.view(-1, 1, 1, 1), x.flip(-1), x)
+    return x
+
+
+class ReferenceResNet50:
+    """Functional ResNet-50 over a flat parameter buffer (fp32, any device)."""
+
+    def __init__(self, layout: ParamLayout, bn_mode: str = "frozen"):
+        self.L = layout
+        self.bn_mode = bn_mode
+        self.stats = None   # flat buffer holding the BN moving statistics (non-trainable)
+
+    def _w(self, params, layer, kind):
+        if kind in ("moving_mean", "moving_variance") and self.stats is not None:
+            return self.L.view(self.stats, layer, kind)
+        return self.L.view(params, layer, kind)
+
+    def _conv(self, params, x, c, pad_explicit=False):
+        w = self._w(params, c.name, "kernel").permute(0, 3, 1, 2)
+        b = self._w(params, c.name, "bias")
+        pad = 0 if pad_explicit else c.pad
+        return F.conv2d(x, w, b, stride=c.stride, padding=pad)
+
+    def _bn(self, params, x, c, training):
+        g = self._w(params, c.bn, "gamma")
+        be = self._w(params, c.bn, "beta")
+        mu = self._w(params, c.bn, "moving_mean")
+        var = self._w(params, c.bn, "moving_variance")
+        if self.bn_mode == "train" and training:
+            bm = x.mean(dim=(0, 2, 3))
+            bv = x.var(dim=(0, 2, 3), unbiased=False)
+            with torch.no_grad():
+                n = x.numel() / x.shape[1]
+                mu.mul_(BN_MOMENTUM).add_((1 - BN_MOMENTUM) * bm.detach())
+                var.mul_(BN_MOMENTUM).add_((1 - BN_MOMENTUM) * bv.detach() * n / max(n - 1, 1))
+            mu_, var_ = bm, bv
+        else:
+            mu_, var_ = mu.detach(), var.detach()
+        inv = torch.rsqrt(var_ + BN_EPS)
+        return (x - mu_.view(1, -1, 1, 1)) * (g * inv).view(1, -1, 1, 1) + be.view(1, -1, 1, 1)
+
+    def features(self, params, x, training=True):
+        L = self.L
+        s = L.stem
+        x = F.pad(x, (3, 3, 3, 3))
+        x = F.relu(self._bn(params, self._conv(params, x, s, pad_explicit=True), s, training))
+        x = F.pad(x, (1, 1, 1, 1))
+        x = F.max_pool2d(x, 3, 2)
+        for b in L.blocks:
+            c = b.convs
+            if b.proj:
+                sc = self._bn(params, self._conv(params, x, c["0"]), c["0"], training)
+            else:
+                sc = x
+            y = F.relu(self._bn(params, self._conv(params, x, c["1"]), c["1"], training))
+            y = F.relu(self._bn(params, self._conv(params, y, c["2"]), c["2"], training))
+            y = self._bn(params, self._conv(params, y, c["3"]), c["3"], training)
+            x = F.relu(y + sc)
+        return x.mean(dim=(2, 3))
+
+    def logits(self, params, x, training=True):
+        f = self.features(params, x, training)
+        return f @ self._w(params, "dense", "kernel").t() + self._w(params, "dense", "bias")
+
+
+class TorchEngine:
+    """CPU (or any-device fp32) execution engine with the same interface as the HIP engine.
+
+    Parameters are views of one flat fp32 buffer; `.grad` of each view is a view of the
+    flat gradient buffer, so autograd accumulates straight into the bucketed layout.
+    """
+
+    def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, device="cpu", bn_mode="frozen",
+                 num_classes: int = 1000):
+        self.L = layout
+        self.device = torch.device(device)
+        self.batch = batch
+        self.crop = crop
+        self.params = torch.zeros(layout.total, dtype=torch.float32, device=self.device)
+        self.grads = torch.zeros(layout.n_trainable, dtype=torch.float32, device=self.device)
+        self.model = ReferenceResNet50(layout, bn_mode)
+        self.num_classes = num_classes
+        self._leaf = None
+
+    def init(self, seed=0):
+        self.L.init_params(self.params, seed)
+        self.after_update()
+
+    def after_update(self):
+        pass
+
+    def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0), bucket_cb=None):
+        # leaf over the trainable prefix; BN statistics are read (and, in train mode,
+        # updated in place) straight from the flat buffer
+        p = self.params[: self.L.n_trainable].detach().requires_grad_(True)
+        self.model.stats = self.params
+        x = preprocess(images.to(self.device), self.crop, True, flip, crop_offset)
+        logits = self.model.logits(p, x, training=True)
+        lab = labels.to(self.device)
+        loss_sum = F.cross_entropy(logits, lab, reduction="sum")
+        (loss_sum * gscale).backward()
+        with torch.no_grad():
+            self.grads.copy_(p.grad)
+            correct = (logits.argmax(1) == lab).sum().float()
+            stats = torch.stack([loss_sum.detach(), correct])
+        if bucket_cb is not None:
+            for i, _ in enumerate(self.L.buckets(1e9)):
+                bucket_cb(i)
+        return stats
+
+    @torch.no_grad()
+    def evaluate(self, images, labels):
+        x = preprocess(images.to(self.device), self.crop, False)
+        self.model.stats = self.params
+        logits = self.model.logits(self.params, x, training=False)
+        lab = labels.to(self.device)
+        loss_sum = F.cross_entropy(logits, lab, reduction="sum")
+        return torch.stack([loss_sum, (logits.argmax(1) == lab).sum().float()])

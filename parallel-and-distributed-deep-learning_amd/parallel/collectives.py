@@ -1,0 +1,67 @@
+"""Bucketed gradient all-reduce over the flat gradient buffer (RCCL over xGMI on GPU,
+gloo on CPU).
+
+The reference gets its gradient all-reduce from TF's NcclAllReduce (MirroredStrategy,
+imagenet-resnet50-mirror.py:21), MWMS CollectiveReduce with NCCL (multiworkers.py:20-25)
+or Horovod's fused all-reduce (imagenet-resnet50-hvd.py:101).  Here every bucket is a
+contiguous slice of ONE flat fp32 buffer laid out in backward-completion order, so there is
+nothing to pack: `on_bucket_ready(i)` is called by the engine right after the kernels that
+produce bucket i have been enqueued, and issues `all_reduce(grads[s:e], async_op=True)`.
+ProcessGroupNCCL orders the collective after those kernels (stream event) and runs it on
+its own stream, overlapping the rest of backward; `finish()` makes the compute stream wait.
+Buckets default to 32 MiB: large enough that each of the ring channels RCCL spreads over
+the 7 xGMI links of an MI355X carries multi-MiB chunks, small enough (4 kernel buckets + a
+per-channel tail) to overlap with the backward of the earlier layers.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+class BucketAllReducer:
+    def __init__(self, grads: torch.Tensor, buckets: List[Tuple[int, int]], average: bool = False,
+                 group: Optional[dist.ProcessGroup] = None, comm_dtype: str = "fp32", timeline=None):
+        self.grads = grads
+        self.buckets = list(buckets)
+        self.average = average
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.comm_dtype = comm_dtype
+        self.timeline = timeline
+        self.works = []
+        self._lowp = None
+        if comm_dtype == "bf16":
+            self._lowp = torch.empty(grads.numel(), dtype=torch.bfloat16, device=grads.device)
+
+    def begin(self):
+        self.works = []
+
+    def on_bucket_ready(self, i: int):
+        s, e = self.buckets[i]
+        if self.timeline is not None:
+            self.timeline.instant(f"bucket{i}_ready", args={"bytes": (e - s) * 4})
+        if self._lowp is not None:
+            buf = self._lowp[s:e]
+            buf.copy_(self.grads[s:e])
+            w = dist.all_reduce(buf, group=self.group, async_op=True)
+            self.works.append((w, i, buf))
+        else:
+            w = dist.all_reduce(self.grads[s:e], group=self.group, async_op=True)
+            self.works.append((w, i, None))
+
+    def finish(self):
+        for w, i, buf in self.works:
+            w.wait()
+            if buf is not None:
+                s, e = self.buckets[i]
+                self.grads[s:e].copy_(buf)
+        self.works = []
+        if self.average and self.world > 1:
+            self.grads.div_(self.world)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        if self.world > 1:
+            dist.broadcast(t, src, group=self.group)

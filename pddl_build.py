@@ -1,0 +1,33 @@
+"""Build the native HIP extension in-tree for gfx950 and place it next to the package.
+
+    python pddl_build.py            # hipcc cross-compiles; no GPU needed
+"""
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "parallel-and-distributed-deep-learning_amd")
+
+
+def build(verbose: bool = False) -> str:
+    env = dict(os.environ)
+    env.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
+    env.setdefault("MAX_JOBS", "8")
+    cmd = [sys.executable, "setup.py", "build_ext", "--inplace"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        sys.stderr.write((r.stdout or "")[-4000:] + (r.stderr or "")[-4000:])
+        raise RuntimeError("native build failed")
+    built = sorted(glob.glob(os.path.join(ROOT, "_pddl_native*.so")))
+    if not built:
+        raise RuntimeError("native build produced no shared object")
+    dst = os.path.join(PKG, os.path.basename(built[-1]))
+    shutil.move(built[-1], dst)
+    return dst
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

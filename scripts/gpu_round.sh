@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU session: kernel tests -> engine tests -> smoke -> bench.  Stops at the first
+# GPU fault / abort / timeout (exit codes other than 0 = pass and 1 = test failure).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    kernels) step kernels 600 python -m pytest tests/test_gpu_kernels.py -x -q ;;
+    engine)  step engine 600 python -m pytest tests/test_gpu_engine.py -x -q ;;
+    gputests) step gputests 900 python -m pytest tests -m gpu -x -q ;;
+    smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench64) step bench64 600 python bench.py --steps 20 --warmup 5 --batch 64 ;;
+    prof)    step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 ;;
+  esac
+done

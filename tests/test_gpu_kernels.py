@@ -1,0 +1,290 @@
+"""Numerics of every native HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+All tests run on the MI355X through the in-tree `_pddl_native` extension (no fallback).
+bf16 inputs are generated once and the fp32 reference consumes the SAME rounded values,
+so tolerances only cover fp32-accumulation order and the final bf16 rounding.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def N():
+    from pddl.ops.native import require_native
+    return require_native()
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def conv_ref(x, w, stride, pad):
+    # x NHWC, w OHWI -> NHWC fp32
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=stride, padding=pad)
+    return y.permute(0, 2, 3, 1)
+
+
+CONV_CASES = [
+    # N, H, C, Cout, R, stride, pad
+    (2, 14, 64, 64, 1, 1, 0),
+    (3, 9, 64, 128, 3, 1, 1),
+    (2, 14, 256, 512, 1, 2, 0),
+    (2, 7, 128, 136, 3, 1, 1),
+    (1, 15, 64, 256, 1, 2, 0),
+    (2, 10, 192, 64, 1, 1, 0),
+    (4, 8, 512, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("with_res", [False, True])
+def test_igemm_forward(case, with_res):
+    torch.manual_seed(0)
+    n, h, c, co, r, st, pad = case
+    x = rnd(n, h, h, c)
+    w = rnd(co, r, r, c, scale=0.05)
+    ho = (h + 2 * pad - r) // st + 1
+    scale = torch.rand(co, device=dev) + 0.5
+    shift = torch.randn(co, device=dev)
+    res = rnd(n, ho, ho, co) if with_res else None
+    out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
+    N().igemm(x, None, h, h, r, r, st, pad, ho, ho, w.view(co, -1), 0, scale, shift, res, None, None, out, 1,
+              None, 0, 0, 0, 0, 0)
+    ref = conv_ref(x, w, st, pad) * scale + shift
+    if with_res:
+        ref = ref + res.float()
+    ref = ref.relu()
+    assert rel(out, ref) < 1e-2
+
+
+def test_igemm_split_outputs_and_f32():
+    torch.manual_seed(1)
+    n, h, c, f = 2, 8, 64, 64
+    x = rnd(n, h, h, c)
+    w = rnd(5 * f, 1, 1, c, scale=0.1)
+    scale = torch.rand(5 * f, device=dev) + 0.5
+    shift = torch.randn(5 * f, device=dev)
+    y1 = torch.empty(n, 4, 4, f, dtype=torch.bfloat16, device=dev)
+    sc = torch.empty(n, 4, 4, 4 * f, dtype=torch.bfloat16, device=dev)
+    N().igemm(x, None, h, h, 1, 1, 2, 0, 4, 4, w.view(5 * f, c), 0, scale, shift, None, None, None, y1, 1,
+              sc, 0, f, 0, 0, 0)
+    ref = conv_ref(x, w, 2, 0) * scale + shift
+    assert rel(y1, ref[..., :f].relu()) < 1e-2
+    assert rel(sc, ref[..., f:]) < 1e-2
+    # fp32 dense epilogue
+    a = rnd(6, 2048)
+    wd = rnd(1000, 2048, scale=0.02)
+    bias = torch.randn(1000, device=dev)
+    ones = torch.ones(1000, device=dev)
+    out = torch.empty(6, 1000, device=dev)
+    N().igemm(a.view(6, 1, 1, 2048), None, 1, 1, 1, 1, 1, 0, 1, 1, wd, 2, ones, bias, None, None, None, out, 0,
+              None, 0, 0, 0, 0, 0)
+    ref = a.float() @ wd.float().t() + bias
+    assert rel(out, ref) < 1e-3
+
+
+def dgrad_weights(w, a):
+    # W'[c][r'][s'][co] = a[co] * W[co][R-1-r'][S-1-s'][c]
+    wt = (w.float() * a.view(-1, 1, 1, 1)).flip(1).flip(2).permute(3, 1, 2, 0).contiguous()
+    return wt.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("case", [(2, 9, 64, 128, 3, 1, 1), (2, 14, 64, 256, 1, 1, 0), (2, 14, 256, 128, 1, 2, 0),
+                                  (1, 15, 128, 64, 1, 2, 0)])
+def test_igemm_dgrad(case):
+    torch.manual_seed(2)
+    n, h, cin, co, r, st, pad = case
+    ho = (h + 2 * pad - r) // st + 1
+    g = rnd(n, ho, ho, co)
+    w = rnd(co, r, r, cin, scale=0.05)
+    a = torch.rand(co, device=dev) + 0.5
+    add = rnd(n, h, h, cin)
+    mask = rnd(n, h, h, cin)
+    out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
+    wt = dgrad_weights(w, a)
+    pd = r - 1 - pad
+    N().igemm(g, None, ho, ho, r, r, 1, pd, ho, ho, wt.view(cin, -1), 1, None, None, None, mask, add, out, 0,
+              None, 0, 0, 1 if st == 2 else 0, h, h)
+    gs = (g.float() * a).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_input((n, cin, h, h), w.float().permute(0, 3, 1, 2), gs, stride=st, padding=pad)
+    ref = (ref.permute(0, 2, 3, 1) + add.float()) * (mask.float() > 0)
+    assert rel(out, ref) < 1e-2
+
+
+def test_igemm_dgrad_dual_source():
+    torch.manual_seed(3)
+    n, h, cin, f = 2, 14, 256, 128
+    ho = 7
+    g1 = rnd(n, ho, ho, f)
+    g0 = rnd(n, ho, ho, 4 * f)
+    w1 = rnd(f, 1, 1, cin, scale=0.05)
+    w0 = rnd(4 * f, 1, 1, cin, scale=0.05)
+    a1 = torch.rand(f, device=dev) + 0.5
+    a0 = torch.rand(4 * f, device=dev) + 0.5
+    wt = torch.cat([dgrad_weights(w1, a1).view(cin, f), dgrad_weights(w0, a0).view(cin, 4 * f)], 1).contiguous()
+    mask = rnd(n, h, h, cin)
+    out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
+    N().igemm(g1, g0, ho, ho, 1, 1, 1, 0, ho, ho, wt, 1, None, None, None, mask, None, out, 0, None, 0, 0, 1, h, h)
+    r1 = torch.nn.grad.conv2d_input((n, cin, h, h), w1.float().permute(0, 3, 1, 2),
+                                    (g1.float() * a1).permute(0, 3, 1, 2), stride=2)
+    r0 = torch.nn.grad.conv2d_input((n, cin, h, h), w0.float().permute(0, 3, 1, 2),
+                                    (g0.float() * a0).permute(0, 3, 1, 2), stride=2)
+    ref = (r1 + r0).permute(0, 2, 3, 1) * (mask.float() > 0)
+    assert rel(out, ref) < 1e-2
+
+
+WG_CASES = [
+    (2, 14, 64, 256, 1, 1, 0),
+    (3, 9, 64, 64, 3, 1, 1),
+    (2, 14, 256, 512, 1, 2, 0),
+    (2, 7, 128, 128, 3, 1, 1),
+    (4, 28, 64, 64, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", WG_CASES)
+def test_wgrad(case):
+    torch.manual_seed(4)
+    n, h, cin, co, r, st, pad = case
+    ho = (h + 2 * pad - r) // st + 1
+    x = rnd(n, h, h, cin)
+    g = rnd(n, ho, ho, co)
+    dw = torch.zeros(co, r * r * cin, device=dev)
+    N().wgrad(x, h, h, r, r, st, pad, ho, ho, g, None, 0, dw, r * r * cin, 0)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (co, cin, r, r),
+                                      g.float().permute(0, 3, 1, 2), stride=st, padding=pad)
+    ref = ref.permute(0, 2, 3, 1).reshape(co, -1)
+    assert rel(dw, ref) < 5e-3
+
+
+def test_wgrad_dual_and_padded_k():
+    torch.manual_seed(5)
+    # dual gradient source (conv1 + conv0 of a projection block)
+    n, h, cin, f = 2, 8, 128, 64
+    x = rnd(n, h, h, cin)
+    g1 = rnd(n, h, h, f)
+    g0 = rnd(n, h, h, 4 * f)
+    dw = torch.zeros(5 * f, cin, device=dev)
+    N().wgrad(x, h, h, 1, 1, 1, 0, h, h, g1, g0, f, dw, cin, 0)
+    ref = torch.cat([g1, g0], -1).float().reshape(-1, 5 * f).t() @ x.float().reshape(-1, cin)
+    assert rel(dw, ref) < 5e-3
+    # stem-style: rows of 192, only the first 147 columns, Cout 64; dense-style Cout 1000
+    a = rnd(3, 5, 5, 192)
+    g = rnd(3, 5, 5, 64)
+    dw = torch.zeros(64, 147, device=dev)
+    N().wgrad(a, 5, 5, 1, 1, 1, 0, 5, 5, g, None, 0, dw, 147, 0)
+    ref = g.float().reshape(-1, 64).t() @ a.float().reshape(-1, 192)[:, :147]
+    assert rel(dw, ref) < 5e-3
+    p = rnd(16, 2048)
+    dl = torch.zeros(16, 1024, dtype=torch.bfloat16, device=dev)
+    dl[:, :1000] = rnd(16, 1000)
+    dw = torch.zeros(1000, 2048, device=dev)
+    N().wgrad(p.view(16, 1, 1, 2048), 1, 1, 1, 1, 1, 0, 1, 1, dl, None, 0, dw, 2048, 0)
+    ref = dl[:, :1000].float().t() @ p.float()
+    assert rel(dw, ref) < 5e-3
+
+
+def test_maxpool_and_gap():
+    torch.manual_seed(6)
+    n, h, c = 2, 12, 64
+    x = torch.relu(torch.randn(n, h, h, c, device=dev)).to(torch.bfloat16)
+    ho = (h + 2 - 3) // 2 + 1
+    y = torch.empty(n, ho, ho, c, dtype=torch.bfloat16, device=dev)
+    idx = torch.empty(n, ho, ho, c, dtype=torch.uint8, device=dev)
+    N().maxpool_fwd(x, y, idx)
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    yr = F.max_pool2d(F.pad(xr, (1, 1, 1, 1)), 3, 2)
+    assert torch.equal(y.float(), yr.permute(0, 2, 3, 1).detach())
+    gy = rnd(n, ho, ho, c)
+    yr.backward(gy.float().permute(0, 3, 1, 2))
+    gx = torch.empty_like(x)
+    N().maxpool_bwd(gy, idx, x, gx)
+    ref = xr.grad.permute(0, 2, 3, 1) * (x.float() > 0)
+    assert rel(gx, ref) < 1e-2
+    # GAP
+    z = torch.relu(torch.randn(n, 7, 7, 256, device=dev)).to(torch.bfloat16)
+    p = torch.empty(n, 256, dtype=torch.bfloat16, device=dev)
+    N().gap_fwd(z, p)
+    assert rel(p, z.float().mean((1, 2))) < 1e-2
+    gp = rnd(n, 256)
+    gz = torch.empty_like(z)
+    N().gap_bwd(gp, z, gz)
+    ref = (gp.float() / 49).view(n, 1, 1, 256) * (z.float() > 0)
+    assert rel(gz, ref) < 1e-2
+
+
+def test_colsum_softmax_xent():
+    torch.manual_seed(7)
+    g = rnd(1000, 64)
+    out = torch.zeros(64, device=dev)
+    N().colsum(g, 64, out)
+    assert rel(out, g.float().sum(0)) < 1e-4
+    g = rnd(3000, 2048)
+    out = torch.zeros(2048, device=dev)
+    N().colsum(g, 2048, out)
+    assert rel(out, g.float().sum(0)) < 1e-4
+    B = 37
+    logits = torch.randn(B, 1000, device=dev) * 3
+    lab = torch.randint(0, 1000, (B,), device=dev)
+    dl = torch.empty(B, 1024, dtype=torch.bfloat16, device=dev)
+    ls = torch.zeros(1, device=dev)
+    cr = torch.zeros(1, device=dev)
+    N().softmax_xent(logits, lab, 1000, 1.0 / B, dl, ls, cr)
+    lr = logits.clone().requires_grad_(True)
+    loss = F.cross_entropy(lr, lab, reduction="sum")
+    (loss / B).backward()
+    assert abs(ls.item() - loss.item()) / loss.item() < 1e-5
+    assert cr.item() == (logits.argmax(1) == lab).sum().item()
+    assert rel(dl[:, :1000], lr.grad) < 1e-2
+    assert dl[:, 1000:].float().abs().max().item() == 0
+
+
+def test_optimizers():
+    torch.manual_seed(8)
+    n = 4096
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    m = torch.randn(n, device=dev).abs() * 0.1
+    v = torch.rand(n, device=dev) * 0.1
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    lr, b1, b2, eps, t = 1e-3, 0.9, 0.999, 1e-7, 3
+    lr_t = lr * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
+    N().adam(p, g, m, v, lr_t, b1, b2, eps, 1.0)
+    mr = b1 * mr + (1 - b1) * g
+    vr = b2 * vr + (1 - b2) * g * g
+    pr = pr - lr_t * mr / (vr.sqrt() + eps)
+    assert torch.allclose(p, pr, atol=1e-6) and torch.allclose(m, mr) and torch.allclose(v, vr)
+    mom = torch.randn(n, device=dev)
+    p2, mo2 = p.clone(), mom.clone()
+    N().sgd(p, g, mom, 0.1, 0.9, 0.0, False, 1.0)
+    mo2 = 0.9 * mo2 - 0.1 * g
+    assert torch.allclose(mom, mo2, atol=1e-6) and torch.allclose(p, p2 + mo2, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["identity", "resize", "crop"])
+def test_stem_im2col(mode):
+    from pddl.models.reference import preprocess
+    torch.manual_seed(9)
+    B, S = 2, 32
+    img = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev)
+    flip = torch.tensor([0, 1], dtype=torch.uint8, device=dev)
+    crop = {"identity": 32, "resize": 40, "crop": 24}[mode]
+    m = {"identity": 0, "resize": 1, "crop": 2}[mode]
+    oy, ox = (3, 5) if mode == "crop" else (0, 0)
+    ho = (crop + 6 - 7) // 2 + 1
+    out = torch.empty(B, ho, ho, 192, dtype=torch.bfloat16, device=dev)
+    N().stem_im2col(img, flip, m, crop, crop, oy, ox, out)
+    x = preprocess(img, crop, True, flip, (oy, ox))
+    cols = F.unfold(F.pad(x, (3, 3, 3, 3)), 7, stride=2)            # [B, 3*49, L]  (c, r, s) order
+    cols = cols.view(B, 3, 7, 7, -1).permute(0, 4, 2, 3, 1).reshape(B, ho, ho, 147)
+    assert rel(out[..., :147], cols) < 5e-3
+    assert out[..., 147:].float().abs().max().item() == 0
