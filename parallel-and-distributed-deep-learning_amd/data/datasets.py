@@ -1,0 +1,179 @@
+"""Input pipeline with the reference's tf.data semantics.
+
+Reference pipeline (imagenet-resnet50.py:28-49): tfds ImageNet2012 -> map(resize_with_crop
+to 224) -> batch(B, drop_remainder=True) -> prefetch; Horovod shards AFTER batching
+(hvd.py:77-78, each rank takes every size-th batch); MWMS uses AutoShardPolicy.DATA
+(multiworkers.py:66-69: element-wise sharding); PS repeats forever (ps.py:118-119).
+
+Sources (no network on the target machines, so no tfds download):
+  * SyntheticImageNet — deterministic uint8 [224,224,3] images + labels generated on the
+    device (the benchmark data, BASELINE.json "synthetic 3x224x224").
+  * RecordsImageNet — a directory of raw uint8 records (`<split>.u8` = N x 224 x 224 x 3,
+    `<split>_labels.i64`), memory-mapped and gathered by the native loader thread pool
+    (csrc/runtime/loader.cpp) into pinned buffers, then copied asynchronously to the GPU.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Iterator, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+
+class ImageSource:
+    num_examples: int
+    image_size: int
+    num_classes: int
+
+    def fetch(self, idx: np.ndarray, device) -> Tuple[torch.Tensor, torch.Tensor]:
+        raise NotImplementedError
+
+
+class SyntheticImageNet(ImageSource):
+    """Deterministic synthetic ImageNet: image i depends only on (seed, i)."""
+
+    def __init__(self, num_examples: int, image_size: int = 224, num_classes: int = 1000, seed: int = 0,
+                 fixed: bool = False):
+        self.num_examples = num_examples
+        self.image_size = image_size
+        self.num_classes = num_classes
+        self.seed = seed
+        self.fixed = fixed          # benchmark mode: one device-resident batch reused
+        self._cache = {}
+
+    def fetch(self, idx: np.ndarray, device):
+        n = len(idx)
+        S = self.image_size
+        if self.fixed:
+            key = (n, str(device))
+            if key not in self._cache:
+                g = torch.Generator(device=device).manual_seed(self.seed)
+                self._cache[key] = (
+                    torch.randint(0, 256, (n, S, S, 3), dtype=torch.uint8, device=device, generator=g),
+                    torch.randint(0, self.num_classes, (n,), dtype=torch.int64, device=device, generator=g))
+            return self._cache[key]
+        # per-example deterministic content: hash of the index seeds a counter-based fill
+        lab = torch.from_numpy((np.asarray(idx, dtype=np.int64) * 2654435761 + self.seed) % self.num_classes)
+        g = torch.Generator(device=device).manual_seed(int(self.seed * 1000003 + int(idx[0]) * 7919 + n))
+        img = torch.randint(0, 256, (n, S, S, 3), dtype=torch.uint8, device=device, generator=g)
+        return img, lab.to(device)
+
+
+class RecordsImageNet(ImageSource):
+    """Raw uint8 records, memory-mapped; batches gathered by the native loader."""
+
+    def __init__(self, root: str, split: str = "train", image_size: int = 224, num_classes: int = 1000,
+                 threads: int = 8):
+        self.path = os.path.join(root, f"{split}.u8")
+        lab = os.path.join(root, f"{split}_labels.i64")
+        self.labels = np.fromfile(lab, dtype=np.int64)
+        self.num_examples = len(self.labels)
+        self.image_size = image_size
+        self.num_classes = num_classes
+        self.row = image_size * image_size * 3
+        sz = os.path.getsize(self.path)
+        if sz != self.row * self.num_examples:
+            raise ValueError(f"{self.path}: size {sz} != {self.num_examples} x {self.row}")
+        self._loader = None
+        self.threads = threads
+
+    def _native(self):
+        if self._loader is None:
+            from ..ops.native import native_available, require_native
+            if native_available() and hasattr(require_native(), "Loader"):
+                self._loader = require_native().Loader(self.path, self.row, self.threads)
+            else:
+                self._loader = np.memmap(self.path, dtype=np.uint8, mode="r").reshape(self.num_examples, -1)
+        return self._loader
+
+    def fetch(self, idx: np.ndarray, device):
+        ld = self._native()
+        S = self.image_size
+        if isinstance(ld, np.memmap):
+            host = torch.from_numpy(np.ascontiguousarray(ld[idx]))
+        else:
+            host = torch.empty((len(idx), self.row), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+            ld.gather(torch.from_numpy(np.asarray(idx, dtype=np.int64)), host)
+        img = host.view(len(idx), S, S, 3).to(device, non_blocking=True)
+        lab = torch.from_numpy(self.labels[idx]).to(device, non_blocking=True)
+        return img, lab
+
+
+def write_records(root: str, split: str, images: np.ndarray, labels: np.ndarray) -> None:
+    """Write a RecordsImageNet split (images uint8 [N,S,S,3], labels int)."""
+    os.makedirs(root, exist_ok=True)
+    np.ascontiguousarray(images, dtype=np.uint8).tofile(os.path.join(root, f"{split}.u8"))
+    np.asarray(labels, dtype=np.int64).tofile(os.path.join(root, f"{split}_labels.i64"))
+
+
+@dataclass
+class Pipeline:
+    """batch -> shard -> (repeat) iterator over an ImageSource, tf.data style.
+
+    shard_by="batch"  : Horovod semantics, batch(B) then shard(num_shards, index)
+    shard_by="element": MWMS AutoShardPolicy.DATA, shard elements then batch(B)
+    """
+    source: ImageSource
+    batch_size: int
+    num_shards: int = 1
+    shard_index: int = 0
+    shard_by: str = "batch"
+    drop_remainder: bool = True
+    repeat: bool = False
+    shuffle: bool = False
+    seed: int = 0
+
+    def num_batches(self) -> int:
+        n = self.source.num_examples
+        if self.shard_by == "element":
+            n_local = len(range(self.shard_index, n, self.num_shards))
+            return n_local // self.batch_size if self.drop_remainder else math.ceil(n_local / self.batch_size)
+        nb = n // self.batch_size if self.drop_remainder else math.ceil(n / self.batch_size)
+        return len(range(self.shard_index, nb, self.num_shards))
+
+    def _order(self, epoch: int) -> np.ndarray:
+        n = self.source.num_examples
+        if self.shuffle:
+            return np.random.default_rng(self.seed + epoch).permutation(n)
+        return np.arange(n)
+
+    def batches(self, epoch: int = 0) -> Iterator[np.ndarray]:
+        while True:
+            order = self._order(epoch)
+            B = self.batch_size
+            if self.shard_by == "element":
+                local = order[self.shard_index::self.num_shards]
+                nb = len(local) // B if self.drop_remainder else math.ceil(len(local) / B)
+                for i in range(nb):
+                    yield local[i * B:(i + 1) * B]
+            else:
+                nb = len(order) // B if self.drop_remainder else math.ceil(len(order) / B)
+                for i in range(self.shard_index, nb, self.num_shards):
+                    yield order[i * B:(i + 1) * B]
+            if not self.repeat:
+                return
+            epoch += 1
+
+    def iterate(self, device, epoch: int = 0, prefetch: int = 2):
+        """Yields (images, labels) on `device`; fetches run one batch ahead."""
+        it = self.batches(epoch)
+        pending = []
+        for idx in it:
+            pending.append(self.source.fetch(idx, device))
+            if len(pending) > prefetch:
+                yield pending.pop(0)
+        while pending:
+            yield pending.pop(0)
+
+
+def make_source(spec: str, split: str, cfg) -> ImageSource:
+    if spec == "synthetic" or spec == "synthetic_fixed":
+        n = cfg.train_images if split == "train" else cfg.val_images
+        return SyntheticImageNet(n, cfg.image_size, cfg.num_classes, seed=cfg.seed + (0 if split == "train" else 1),
+                                 fixed=spec == "synthetic_fixed")
+    if spec.startswith("records:"):
+        return RecordsImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+    raise ValueError(f"unknown data spec {spec!r}")

@@ -262,7 +262,7 @@ def test_optimizers():
     mr = b1 * mr + (1 - b1) * g
     vr = b2 * vr + (1 - b2) * g * g
     pr = pr - lr_t * mr / (vr.sqrt() + eps)
-    assert torch.allclose(p, pr, atol=1e-6) and torch.allclose(m, mr) and torch.allclose(v, vr)
+    assert torch.allclose(p, pr, atol=1e-6) and torch.allclose(m, mr, atol=1e-6) and torch.allclose(v, vr, atol=1e-6)
     mom = torch.randn(n, device=dev)
     p2, mo2 = p.clone(), mom.clone()
     N().sgd(p, g, mom, 0.1, 0.9, 0.0, False, 1.0)
