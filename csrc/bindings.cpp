@@ -42,7 +42,7 @@ int old(const OptT& t) { return t.has_value() ? ld(*t) : 0; }
 void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
            int64_t Ho, int64_t Wo, Tensor b, int64_t mode, OptT scale, OptT shift, OptT res, OptT mask, OptT add,
            Tensor out, int64_t relu, OptT out2, int64_t relu2, int64_t n_split, int64_t up2, int64_t Hf,
-           int64_t Wf) {
+           int64_t Wf, OptT colsum) {
   pddl::IgemmParams p{};
   PCHECK(a1.is_contiguous(), "A source must be contiguous NHWC");
   p.a1 = bfp(a1);
@@ -78,6 +78,8 @@ void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64
   if (out2.has_value()) { p.out2 = bfpm(*out2); p.ldo2 = ld(*out2); }
   p.relu2 = (int)relu2; p.n_split = (int)n_split;
   p.up2 = (int)up2; p.Hf = (int)Hf; p.Wf = (int)Wf;
+  p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;
+  if (p.colsum) PCHECK(colsum->numel() >= p.Nn, "colsum too short");
   const int64_t rows_out = up2 ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
   PCHECK(out.numel() / std::max<int64_t>(1, out.size(-1)) >= (out2.has_value() ? p.M : rows_out) ||
              out.dim() >= 2,
@@ -103,24 +105,28 @@ void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
   ok(pddl::wgrad_launch(p, cur_stream()), "wgrad");
 }
 
-void stem_im2col(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_t oy, int64_t ox, Tensor out) {
+void stem_s2d(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_t oy, int64_t ox, Tensor out) {
   pddl::StemParams p{};
   PCHECK(in.is_cuda() && in.is_contiguous() && in.dim() == 4 && in.size(3) == 3, "stem input must be [B,H,W,3]");
   PCHECK(in.scalar_type() == torch::kUInt8 || in.scalar_type() == torch::kFloat32, "stem input uint8 or fp32");
   p.in = in.data_ptr(); p.in_u8 = in.scalar_type() == torch::kUInt8;
   p.B = (int)in.size(0); p.Hin = (int)in.size(1); p.Win = (int)in.size(2);
   p.Hc = (int)Hc; p.Wc = (int)Wc; p.mode = (int)mode; p.oy = (int)oy; p.ox = (int)ox;
+  if (mode == 2) PCHECK(oy >= 0 && ox >= 0 && oy + Hc <= p.Hin && ox + Wc <= p.Win, "crop window out of range");
   if (flip.has_value()) {
-    PCHECK(flip->scalar_type() == torch::kUInt8 && flip->numel() == p.B, "flip flags [B] uint8");
+    PCHECK(flip->scalar_type() == torch::kUInt8 && flip->numel() == p.B && flip->is_cuda(), "flip flags [B] uint8");
     p.flip = flip->data_ptr<uint8_t>();
   }
   p.scale = 1.f / 255.f;
-  p.Ho = (int)((Hc + 6 - 7) / 2 + 1); p.Wo = (int)((Wc + 6 - 7) / 2 + 1);
-  p.out = bfpm(out); p.ldo = ld(out);
-  PCHECK(out.numel() >= (int64_t)p.B * p.Ho * p.Wo * p.ldo, "stem output too small");
-  ok(pddl::stem_im2col_launch(p, cur_stream()), "stem_im2col");
+  p.Hs = (int)((Hc + 6) / 2); p.Ws = (int)((Wc + 6) / 2);
+  PCHECK(out.is_contiguous() && out.numel() >= (int64_t)p.B * p.Hs * p.Ws * 16, "stem s2d output too small");
+  p.out = bfpm(out);
+  ok(pddl::stem_s2d_launch(p, cur_stream()), "stem_s2d");
 }
-
+void stem_wgrad_fold(Tensor g2, Tensor dw, int64_t cout) {
+  PCHECK(g2.numel() >= cout * 256 && dw.numel() >= cout * 147, "stem fold sizes");
+  ok(pddl::stem_wgrad_fold_launch(f32p(g2), f32p(dw), (int)cout, cur_stream()), "stem_wgrad_fold");
+}
 void maxpool_fwd(Tensor x, Tensor y, Tensor idx) {
   PCHECK(x.is_contiguous() && y.is_contiguous() && idx.is_contiguous() && idx.scalar_type() == torch::kUInt8,
          "maxpool layouts");
@@ -128,10 +134,10 @@ void maxpool_fwd(Tensor x, Tensor y, Tensor idx) {
                               (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), cur_stream()),
      "maxpool_fwd");
 }
-void maxpool_bwd(Tensor gy, Tensor idx, OptT xmask, Tensor gx) {
+void maxpool_bwd(Tensor gy, Tensor idx, OptT xmask, Tensor gx, OptT colsum) {
   ok(pddl::maxpool_bwd_launch(bfp(gy), idx.data_ptr<uint8_t>(), obfp(xmask), bfpm(gx), (int)gx.size(0),
                               (int)gx.size(1), (int)gx.size(2), (int)gx.size(3), (int)gy.size(1), (int)gy.size(2),
-                              cur_stream()),
+                              colsum.has_value() ? f32p(*colsum) : nullptr, cur_stream()),
      "maxpool_bwd");
 }
 void gap_fwd(Tensor x, Tensor y) {
@@ -139,9 +145,9 @@ void gap_fwd(Tensor x, Tensor y) {
                           cur_stream()),
      "gap_fwd");
 }
-void gap_bwd(Tensor gp, Tensor ymask, Tensor g) {
+void gap_bwd(Tensor gp, Tensor ymask, Tensor g, OptT colsum) {
   ok(pddl::gap_bwd_launch(bfp(gp), ld(gp), bfp(ymask), bfpm(g), (int)g.size(0), (int)(g.size(1) * g.size(2)),
-                          (int)g.size(3), cur_stream()),
+                          (int)g.size(3), colsum.has_value() ? f32p(*colsum) : nullptr, cur_stream()),
      "gap_bwd");
 }
 void colsum(Tensor g, int64_t C, Tensor out) {
@@ -198,7 +204,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "pddl MI355X (gfx950) HIP kernels";
   m.def("igemm", &igemm);
   m.def("wgrad", &wgrad);
-  m.def("stem_im2col", &stem_im2col);
+  m.def("stem_s2d", &stem_s2d);
+  m.def("stem_wgrad_fold", &stem_wgrad_fold);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("gap_fwd", &gap_fwd);

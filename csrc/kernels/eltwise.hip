@@ -1,6 +1,6 @@
 // Memory-bound kernels around the implicit-GEMM convs (gfx950):
-//   * stem_im2col  : Rescaling(1/255) -> RandomCrop/resize -> RandomFlip -> ZeroPadding2D(3)
-//                    -> 7x7/s2 im2col rows, in one pass (reference imagenet-resnet50.py:53-55
+//   * stem_s2d     : Rescaling(1/255) -> RandomCrop/resize -> RandomFlip -> ZeroPadding2D(3)
+//                    -> 2x2 space-to-depth (16 ch), in one pass (reference imagenet-resnet50.py:53-55
 //                    and the Keras ResNet50 stem)
 //   * maxpool      : ZeroPadding2D(1) + MaxPooling2D(3, 2) forward (argmax byte) and backward
 //                    (gather form, fused with the ReLU mask of conv1's output)  (N6)
@@ -41,35 +41,50 @@ __device__ __forceinline__ float stem_pix(const StemParams& p, int b, int y, int
   return v * p.scale;
 }
 
-__global__ void stem_im2col_kernel(StemParams p, long nchunks) {
-  const int cpr = p.ldo / 8;  // 16-byte chunks per row
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nchunks; q += (long)gridDim.x * blockDim.x) {
-    const long row = q / cpr;
-    const int ck = (int)(q - row * cpr);
-    const int b = (int)(row / (p.Ho * p.Wo));
-    const int rem = (int)(row - (long)b * p.Ho * p.Wo);
-    const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
-    float v[8];
+// Space-to-depth stem input: one thread per s2d pixel, two 16-byte stores.
+__global__ void stem_s2d_kernel(StemParams p, long npix) {
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < npix; q += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(q % p.Ws);
+    const long t = q / p.Ws;
+    const int i = (int)(t % p.Hs), b = (int)(t / p.Hs);
+    float v[16];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = ck * 8 + e;
-      float val = 0.f;
-      if (k < 147) {
-        const int r = k / 21, rm = k - r * 21, s = rm / 3, c = rm - s * 3;
-        const int y = 2 * ho - 3 + r, x = 2 * wo - 3 + s;
-        if (y >= 0 && y < p.Hc && x >= 0 && x < p.Wc) val = stem_pix(p, b, y, x, c);
-      }
-      v[e] = val;
+    for (int d = 0; d < 4; ++d) {
+      const int y = 2 * i + (d >> 1) - 3, x = 2 * j + (d & 1) - 3;
+      const bool in = y >= 0 && y < p.Hc && x >= 0 && x < p.Wc;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[d * 4 + c] = in ? stem_pix(p, b, y, x, c) : 0.f;
+      v[d * 4 + 3] = 0.f;
     }
-    *reinterpret_cast<uint4*>(p.out + row * p.ldo + ck * 8) = pack8(v);
+    uint4* o = reinterpret_cast<uint4*>(p.out + q * 16);
+    o[0] = pack8(v);
+    o[1] = pack8(v + 8);
   }
 }
 
-const char* stem_im2col_launch(const StemParams& p, hipStream_t s) {
-  if (p.ldo % 8 || p.ldo < 152) return "stem: ldo must be >= 152 and a multiple of 8";
-  const long nchunks = (long)p.B * p.Ho * p.Wo * (p.ldo / 8);
-  const int grid = (int)lmin((nchunks + 255) / 256, 65536);
-  hipLaunchKernelGGL(stem_im2col_kernel, dim3(grid), dim3(256), 0, s, p, nchunks);
+const char* stem_s2d_launch(const StemParams& p, hipStream_t s) {
+  if ((p.Hc + 6) != 2 * p.Hs || (p.Wc + 6) != 2 * p.Ws) return "stem_s2d: Hs must be (Hc + 6) / 2 (even crop)";
+  const long npix = (long)p.B * p.Hs * p.Ws;
+  const int grid = (int)lmin((npix + 255) / 256, 16384);
+  hipLaunchKernelGGL(stem_s2d_kernel, dim3(grid), dim3(256), 0, s, p, npix);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+__device__ __forceinline__ int s2d_col(int r, int s, int c) {
+  return ((r >> 1) * 4 + (s >> 1)) * 16 + ((r & 1) * 2 + (s & 1)) * 4 + c;
+}
+
+__global__ void stem_wgrad_fold_kernel(const float* __restrict__ g2, float* __restrict__ dw, int cout) {
+  const int n = cout * 147;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int co = e / 147, k = e - co * 147;
+    const int r = k / 21, rm = k - r * 21, s = rm / 3, c = rm - s * 3;
+    dw[e] += g2[co * 256 + s2d_col(r, s, c)];
+  }
+}
+const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStream_t s) {
+  hipLaunchKernelGGL(stem_wgrad_fold_kernel, dim3((cout * 147 + 255) / 256), dim3(256), 0, s, g2, dw, cout);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
@@ -115,11 +130,14 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
   }
 }
 
+// Column sums of the output are accumulated per thread: with a grid stride that is a
+// multiple of C/8 every thread keeps one channel group, folded across the wave at the end.
 __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
                                    const bf16_t* __restrict__ xmask, bf16_t* __restrict__ gx,
-                                   int B, int H, int W, int C, int Ho, int Wo) {
+                                   int B, int H, int W, int C, int Ho, int Wo, float* __restrict__ colsum) {
   const int cg = C / 8;
   const long total = (long)B * H * W * cg;
+  float cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     const int g = (int)(t % cg);
     const long pix = t / cg;
@@ -156,7 +174,21 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t*
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] = mv[e] > 0.f ? acc[e] : 0.f;
     }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] += acc[e];
     *reinterpret_cast<uint4*>(gx + o) = pack8(acc);
+  }
+  if (colsum) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = cg; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], o, 64);
+    if (lane < cg) {
+      const int g = (int)((blockIdx.x * (long)blockDim.x + threadIdx.x) % cg);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) unsafeAtomicAdd(colsum + g * 8 + e, cs[e]);
+    }
   }
 }
 
@@ -171,10 +203,11 @@ const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, int
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uint16_t* xmask, uint16_t* gx, int B,
-                               int H, int W, int C, int Ho, int Wo, hipStream_t s) {
+                               int H, int W, int C, int Ho, int Wo, float* colsum, hipStream_t s) {
   if (C % 8) return "maxpool: C % 8";
+  if (colsum && (64 % (C / 8))) return "maxpool: fused colsum needs C/8 to divide 64";
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long)B * H * W * C / 8)), dim3(256), 0, s, gy, idx, xmask,
-                     gx, B, H, W, C, Ho, Wo);
+                     gx, B, H, W, C, Ho, Wo, colsum);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
@@ -199,20 +232,26 @@ __global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
   }
 }
 __global__ void gap_bwd_kernel(const bf16_t* __restrict__ gp, int ldgp, const bf16_t* __restrict__ ymask,
-                               bf16_t* __restrict__ g, int B, int HW, int C) {
+                               bf16_t* __restrict__ g, int B, int HW, int C, float* __restrict__ colsum) {
   const int cg = C / 8;
-  const long total = (long)B * HW * cg;
+  const long total = (long)B * cg;
   const float inv = 1.f / HW;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int gg = (int)(t % cg);
-    const long row = t / cg;
-    const int b = (int)(row / HW);
-    float v[8], mv[8];
+    const int gg = (int)(t % cg), b = (int)(t / cg);
+    float v[8], cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unpack8(*reinterpret_cast<const uint4*>(gp + (long)b * ldgp + gg * 8), v);
-    unpack8(*reinterpret_cast<const uint4*>(ymask + row * C + gg * 8), mv);
+    for (int i = 0; i < HW; ++i) {
+      const long row = (long)b * HW + i;
+      float mv[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(ymask + row * C + gg * 8), mv);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = mv[e] > 0.f ? v[e] * inv : 0.f;
-    *reinterpret_cast<uint4*>(g + row * C + gg * 8) = pack8(v);
+      for (int e = 0; e < 8; ++e) { o[e] = mv[e] > 0.f ? v[e] * inv : 0.f; cs[e] += o[e]; }
+      *reinterpret_cast<uint4*>(g + row * C + gg * 8) = pack8(o);
+    }
+    if (colsum) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) unsafeAtomicAdd(colsum + gg * 8 + e, cs[e]);
+    }
   }
 }
 const char* gap_fwd_launch(const uint16_t* x, uint16_t* y, int B, int HW, int C, hipStream_t s) {
@@ -222,10 +261,10 @@ const char* gap_fwd_launch(const uint16_t* x, uint16_t* y, int B, int HW, int C,
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 const char* gap_bwd_launch(const uint16_t* gp, int ldgp, const uint16_t* ymask, uint16_t* g, int B, int HW, int C,
-                           hipStream_t s) {
+                           float* colsum, hipStream_t s) {
   if (C % 8 || ldgp % 8) return "gap: C % 8";
-  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)B * HW * C / 8)), dim3(256), 0, s, gp, ldgp, ymask, g, B,
-                     HW, C);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)B * C / 8)), dim3(256), 0, s, gp, ldgp, ymask, g, B,
+                     HW, C, colsum);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
@@ -342,6 +381,21 @@ __global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __re
     *a_out = a;
     *b_out = (bi - mu) * a + be;
   };
+  if (l.mode == 1) {  // stem: scatter into the 4x4x16 space-to-depth layout (zeros stay zero)
+    const int nf = l.cout * RSC;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nf; e += gridDim.x * blockDim.x) {
+      const int co = e / RSC, k = e - co * RSC;
+      const int r = k / (l.S * l.cin), rm = k - r * l.S * l.cin, s = rm / l.cin, c = rm - s * l.cin;
+      wbf[l.wf_off + (long)co * l.kpad + s2d_col(r, s, c)] = f2bf(prm[l.w_off + e]);
+      if (k == 0) {
+        float a, b;
+        fold(co, &a, &b);
+        scale[l.ch_off + co] = a;
+        shift[l.ch_off + co] = b;
+      }
+    }
+    return;
+  }
   const long nf = (long)l.cout * l.kpad;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nf; e += (long)gridDim.x * blockDim.x) {
     const int co = (int)(e / l.kpad), k = (int)(e - (long)co * l.kpad);

@@ -29,7 +29,7 @@
 
 namespace pddl {
 
-template <int BM, int BN, int WTM, int WTN>
+template <int BM, int BN, int WTM, int WTN, int NSTAGE>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int WAVES_N = BN / WTN;
@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   constexpr int AI = BM / 32, BI = BN / 32;  // 1 KiB LDS-DMA pieces per wave per tile
   constexpr int EPI_LD = WTN + 4;
   constexpr int EPI_BYTES = 4 * 32 * EPI_LD * 4;
-  constexpr int SMEM = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
+  constexpr int SMEM = (NSTAGE * STAGE > EPI_BYTES) ? NSTAGE * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -112,8 +112,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   const int a_off = (wm * WTM + (lane & 15)) * 128;
   const int b_off = (wn * WTN + (lane & 15)) * 128;
   for (int t = 0; t < KT; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < KT) load_tile(t + 1, cur ^ 1);
+    const int cur = NSTAGE == 2 ? (t & 1) : 0;
+    if (NSTAGE == 2 && t + 1 < KT) load_tile(t + 1, cur ^ 1);
     const char* As = smem + cur * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -130,6 +130,10 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+    if (NSTAGE == 1 && t + 1 < KT) {
+      __syncthreads();            // every wave is done reading the single buffer
+      load_tile(t + 1, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -145,6 +149,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   bool relu = p.relu != 0;
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
   int ldo = p.ldo, col = gn;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (p.mode != EPI_DGRAD && col_ok) {
     const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
     const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
@@ -224,6 +229,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
             }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) csum[e] += w[e];
             *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pack8(w);
           }
         }
@@ -231,11 +238,26 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
     }
     __syncthreads();
   }
+  // Fused per-channel column sums of the written gradient (BN beta / conv bias grads):
+  // fold the lanes that share columns, then one atomic per column per wave.
+  if (p.colsum) {
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
+    if (rr == 0 && col_ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) unsafeAtomicAdd(p.colsum + gn + e, csum[e]);
+    }
+  }
 }
 
 static bool igemm_check(const IgemmParams& p, const char** why) {
   if (p.K % 64 || p.K1 % 64) { *why = "K must be a multiple of 64"; return false; }
-  if (p.C1 % 64 || (p.a2 && p.C2 % 64)) { *why = "channels must be multiples of 64"; return false; }
+  // A k-tile (64 elements) must be contiguous in memory: C % 64 == 0, or the "window" form
+  // S * C == 64 with stride 1 / pad 0 (space-to-depth stem: 4 taps x 16 channels).
+  const bool window = (p.C1 * p.S == 64) && p.stride == 1 && p.pad == 0 && !p.a2;
+  if ((p.C1 % 64 && !window) || (p.a2 && p.C2 % 64)) { *why = "channels must be multiples of 64"; return false; }
   if (p.a2 && (p.K - p.K1) % 64) { *why = "second source K must be a multiple of 64"; return false; }
   if (p.Nn % 8 || p.ldb % 8 || p.ldo % 8) { *why = "N / ldb / ldo must be multiples of 8"; return false; }
   if (p.M <= 0 || p.Nn <= 0 || p.K <= 0) { *why = "empty problem"; return false; }
@@ -246,12 +268,15 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream) {
   const char* why = nullptr;
   if (!igemm_check(p, &why)) return why;
+  const bool one = p.K <= 64;   // single k-tile: no double buffer, twice the blocks per CU
   if (p.Nn <= 64) {
     const int nwg = ((p.M + 255) / 256) * ((p.Nn + 63) / 64);
-    hipLaunchKernelGGL((igemm_kernel<256, 64, 64, 64>), dim3(nwg), dim3(256), 0, stream, p);
+    if (one) hipLaunchKernelGGL((igemm_kernel<256, 64, 64, 64, 1>), dim3(nwg), dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((igemm_kernel<256, 64, 64, 64, 2>), dim3(nwg), dim3(256), 0, stream, p);
   } else {
     const int nwg = ((p.M + 127) / 128) * ((p.Nn + 127) / 128);
-    hipLaunchKernelGGL((igemm_kernel<128, 128, 64, 64>), dim3(nwg), dim3(256), 0, stream, p);
+    if (one) hipLaunchKernelGGL((igemm_kernel<128, 128, 64, 64, 1>), dim3(nwg), dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((igemm_kernel<128, 128, 64, 64, 2>), dim3(nwg), dim3(256), 0, stream, p);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);

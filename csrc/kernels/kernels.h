@@ -28,6 +28,7 @@ struct IgemmParams {
   void* out; int ldo; int relu;
   void* out2; int ldo2; int relu2; int n_split;     // FWD: columns >= n_split -> out2
   int up2; int Hf, Wf;                              // DGRAD: scatter to a 2x finer grid
+  float* colsum;                                    // DGRAD: += per-column sums of the output
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
 
@@ -52,17 +53,22 @@ struct StemParams {
   int oy, ox;
   const uint8_t* flip;                // per-image horizontal flip flags (nullable)
   float scale;                        // Rescaling(1/255)
-  uint16_t* out; int Ho, Wo, ldo;     // im2col rows [B*Ho*Wo][ldo], k = (r*7+s)*3+c, zero padded
+  uint16_t* out; int Hs, Ws;          // space-to-depth image [B][Hs][Ws][16], Hs = (Hc + 6) / 2
 };
-const char* stem_im2col_launch(const StemParams& p, hipStream_t s);
+// Preprocess + ZeroPadding2D(3) + 2x2 space-to-depth: channel (dy*2+dx)*4 + c of pixel (i, j)
+// is the padded preprocessed pixel (2i+dy-3, 2j+dx-3, c) (c = 3 is zero).  The 7x7/s2 stem
+// conv then becomes a 4x4/s1 "window" implicit GEMM with K = 4*4*16 = 256.
+const char* stem_s2d_launch(const StemParams& p, hipStream_t s);
+// Fold the s2d-domain stem weight gradient [64][256] back to [64][7][7][3] (added into dw).
+const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStream_t s);
 
 const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, int B, int H, int W, int C,
                                int Ho, int Wo, hipStream_t s);
 const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uint16_t* xmask, uint16_t* gx,
-                               int B, int H, int W, int C, int Ho, int Wo, hipStream_t s);
+                               int B, int H, int W, int C, int Ho, int Wo, float* colsum, hipStream_t s);
 const char* gap_fwd_launch(const uint16_t* x, uint16_t* y, int B, int HW, int C, hipStream_t s);
 const char* gap_bwd_launch(const uint16_t* gp, int ldgp, const uint16_t* ymask, uint16_t* g, int B, int HW, int C,
-                           hipStream_t s);
+                           float* colsum, hipStream_t s);
 const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, hipStream_t s);
 const char* softmax_xent_launch(const float* logits, int ldl, const int64_t* labels, int B, int ncls,
                                 float gscale, uint16_t* dlogits, int ldd, float* loss_sum, float* correct,
@@ -78,6 +84,7 @@ struct PrepLayer {
   int cout_pad;
   int bias_off, gamma_off, beta_off, mean_off, var_off;   // -1 when absent
   int ch_off;         // offset of this layer's folded scale/shift (per output channel)
+  int mode;           // 0: dense [cout][kpad] rows; 1: stem in the 4x4x16 space-to-depth layout
 };
 const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems,
                         uint16_t* wbf, float* scale, float* shift, float eps, hipStream_t s);

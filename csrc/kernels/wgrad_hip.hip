@@ -181,16 +181,25 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   WgradParams p = pin;
   const bool fast = (p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0);
-  if (!fast && p.C % 64) return "wgrad: C must be a multiple of 64 for the gather path";
+  // window form (space-to-depth stem): S taps x C channels = 64 contiguous elements
+  const bool window = (p.C * p.S == 64) && p.stride == 1 && p.pad == 0;
+  if (!fast && p.C % 64 && !window) return "wgrad: C must be a multiple of 64 for the gather path";
   if (p.Cout % 8 || p.ldg % 8 || (fast && p.ldx % 8)) return "wgrad: Cout / ldg / ldx must be multiples of 8";
   if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "wgrad: empty problem";
   if (!fast && (long)p.N * p.H * p.W * p.C >= (1L << 31)) return "wgrad: input too large";
   const int ntiles = ((p.Cout + 127) / 128) * ((p.K + 127) / 128);
   int splits = p.splits;
   if (splits <= 0) {
-    splits = (2048 + ntiles - 1) / ntiles;
-    const int maxs = (p.M + 255) / 256;  // at least 4 iterations per workgroup
-    if (splits > maxs) splits = maxs;
+    // Every split adds one 64 KiB fp32 atomic tile (~1.3 TB/s chip-wide), so a workgroup
+    // should own >= ~48 m-iterations (3072 rows); but keep >= 256 workgroups when the
+    // tile count alone cannot fill the 256 CUs.
+    const int fill = (1536 + ntiles - 1) / ntiles;
+    const int work = (p.M + 3071) / 3072;
+    splits = fill < work ? fill : work;
+    if ((long)ntiles * splits < 256) {
+      const int f2 = (256 + ntiles - 1) / ntiles, w2 = (p.M + 511) / 512;
+      splits = f2 < w2 ? f2 : w2;
+    }
     if (splits < 1) splits = 1;
   }
   int mps = (p.M + splits - 1) / splits;

@@ -29,7 +29,8 @@ import torch
 from ..ops.native import require_native
 from .resnet50 import BN_EPS, ParamLayout
 
-_PREP_FMT = "<6i2q7i4x"
+_PREP_FMT = "<6i2q8i"
+STEM_K = 256   # 4x4 taps x 16 channels of the space-to-depth stem
 _FIN_FMT = "<5i"
 _BNG_FMT = "<9i"
 
@@ -68,11 +69,14 @@ class HipEngine:
         self.nch = _ceil(off, 64)
         # ---- one zeroed-per-step workspace: grads | colsum | dgamma_raw | stats
         n_tr = L.n_trainable
-        self.ws = torch.zeros(n_tr + 2 * self.nch + 64, dtype=torch.float32, device=dev)
+        nst = 64 * STEM_K
+        self.ws = torch.zeros(n_tr + 2 * self.nch + 64 + nst, dtype=torch.float32, device=dev)
         self.grads = self.ws[:n_tr]
         self.colsum = self.ws[n_tr:n_tr + self.nch]
         self.dgr = self.ws[n_tr + self.nch:n_tr + 2 * self.nch]
         self.stats = self.ws[n_tr + 2 * self.nch:n_tr + 2 * self.nch + 2]
+        o = n_tr + 2 * self.nch + 64
+        self.stem_dw2 = self.ws[o:o + nst].view(64, STEM_K)   # s2d-domain stem weight grad
         self.scale = torch.ones(self.nch, dtype=torch.float32, device=dev)
         self.shift = torch.zeros(self.nch, dtype=torch.float32, device=dev)
         self._build_weight_tables()
@@ -84,7 +88,7 @@ class HipEngine:
         wf: Dict[str, int] = {}
         off = 0
         for c in L.convs:
-            kpad = _ceil(c.k * c.k * c.cin, 64)
+            kpad = STEM_K if c is L.stem else _ceil(c.k * c.k * c.cin, 64)
             wf[c.name] = off
             off += c.cout * kpad
         wf["dense"] = off
@@ -122,13 +126,14 @@ class HipEngine:
                 wd_off, ld = wd["dense"], wd_ld["dense"]
             else:
                 name, cout, R, cin = c.name, c.cout, c.k, c.cin
-                kpad = _ceil(R * R * cin, 64)
+                kpad = STEM_K if c is L.stem else _ceil(R * R * cin, 64)
                 bias = L.off(c.name, "bias")
                 gam, bet = L.off(c.bn, "gamma"), L.off(c.bn, "beta")
                 mu, var = L.off(c.bn, "moving_mean"), L.off(c.bn, "moving_variance")
                 wd_off, ld = wd.get(c.name, -1), wd_ld.get(c.name, 0)
+            mode = 1 if c is L.stem else 0
             rows.append(struct.pack(_PREP_FMT, L.off(name, "kernel"), cout, R, R, cin, kpad, wf[name], wd_off, ld,
-                                    bias, gam, bet, mu, var, self.ch[name]))
+                                    bias, gam, bet, mu, var, self.ch[name], mode))
             max_el = max(max_el, cout * kpad)
         self._prep_tab = self._dev_table(rows)
         self._prep_n = len(rows)
@@ -169,7 +174,9 @@ class HipEngine:
         H1 = (crop + 6 - 7) // 2 + 1
         H2 = (H1 + 2 - 3) // 2 + 1
         self.H1, self.H2 = H1, H2
-        self.stem_col = torch.empty(B, H1, H1, 192, **bf)
+        self.Hs = (crop + 6) // 2
+        assert crop % 2 == 0, "crop must be even (space-to-depth stem)"
+        self.stem_x2 = torch.empty(B, self.Hs, self.Hs, 16, **bf)
         self.c1 = torch.empty(B, H1, H1, 64, **bf)
         self.pool = torch.empty(B, H2, H2, 64, **bf)
         self.pidx = torch.empty(B, H2, H2, 64, dtype=torch.uint8, device=dev)
@@ -234,14 +241,14 @@ class HipEngine:
     def _forward(self, images, B, training, flip, crop_offset):
         N, L = self.N, self.L
         mode, oy, ox = self._stem_mode(training, crop_offset)
-        col = self.stem_col[:B]
-        N.stem_im2col(images, flip if training else None, mode, self.crop, self.crop, oy, ox, col)
-        H1, H2 = self.H1, self.H2
+        x2 = self.stem_x2[:B]
+        N.stem_s2d(images, flip if training else None, mode, self.crop, self.crop, oy, ox, x2)
+        H1, H2, Hs = self.H1, self.H2, self.Hs
         s = L.stem
         c1 = self.c1[:B]
-        N.igemm(col, None, H1, H1, 1, 1, 1, 0, H1, H1, self._wf(s.name, 64, 192), 0,
+        N.igemm(x2, None, Hs, Hs, 4, 4, 1, 0, H1, H1, self._wf(s.name, 64, STEM_K), 0,
                 self.scale[self.ch[s.name]:], self.shift[self.ch[s.name]:], None, None, None, c1, 1,
-                None, 0, 0, 0, 0, 0)
+                None, 0, 0, 0, 0, 0, None)
         pool = self.pool[:B]
         N.maxpool_fwd(c1, pool, self.pidx[:B])
         x = pool
@@ -254,26 +261,28 @@ class HipEngine:
             ch1 = self.ch[c1n]
             if b.proj:
                 N.igemm(x, None, H, H, 1, 1, b.stride, 0, Ho, Ho, self._wf(c1n, 5 * f, cin), 0,
-                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, a["sc"][:B], 0, f, 0, 0, 0)
+                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, a["sc"][:B], 0, f, 0, 0, 0,
+                        None)
                 res = a["sc"][:B]
             else:
                 N.igemm(x, None, H, H, 1, 1, 1, 0, Ho, Ho, self._wf(c1n, f, cin), 0,
-                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, None, 0, 0, 0, 0, 0)
+                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, None, 0, 0, 0, 0, 0, None)
                 res = x
             c2 = b.convs["2"].name
             N.igemm(y1, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wf(c2, f, 9 * f), 0,
-                    self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0, 0, 0)
+                    self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0, 0, 0,
+                    None)
             c3 = b.convs["3"].name
             N.igemm(y2, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(c3, 4 * f, f), 0,
-                    self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 0, 0, 0)
+                    self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 0, 0, 0,
+                    None)
             x = out
         pooled = self.pooled[:B]
-        H5 = self.H5
         N.gap_fwd(x, pooled)
         logits = self.logits[:B]
         chd = self.ch["dense"]
         N.igemm(pooled.view(B, 1, 1, 2048), None, 1, 1, 1, 1, 1, 0, 1, 1, self._wf("dense", self.num_classes, 2048), 2,
-                self.scale[chd:], self.shift[chd:], None, None, None, logits, 0, None, 0, 0, 0, 0, 0)
+                self.scale[chd:], self.shift[chd:], None, None, None, logits, 0, None, 0, 0, 0, 0, 0, None)
         return x
 
     def _labels(self, labels, B):
@@ -312,15 +321,15 @@ class HipEngine:
         dpooled = self.dpooled[:B]
         N.igemm(dl.view(B, 1, 1, self.ncls_pad), None, 1, 1, 1, 1, 1, 0, 1, 1,
                 self._wdv("dense", 2048, self.ncls_pad), 1, None, None, None, None, None, dpooled, 0,
-                None, 0, 0, 0, 0, 0)
+                None, 0, 0, 0, 0, 0, None)
         e = L.entry("dense", "kernel")
         done_upto(e.offset + e.size)
         cur = 0
         H5 = self.H5
-        gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
-        N.gap_bwd(dpooled, x5, gout)
-        # ---- blocks
         blocks = L.blocks
+        gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
+        N.gap_bwd(dpooled, x5, gout, self.colsum[self.ch[blocks[-1].convs["3"].name]:])
+        # ---- blocks (column sums of every produced gradient are fused into its producer)
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
             a = self.acts[b.name]
@@ -328,47 +337,45 @@ class HipEngine:
             f, cin = b.filters, b.cin
             x_in = self.acts[blocks[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
             mask_in = x_in if bi > 0 else None
+            cs_in = self.colsum[self.ch[blocks[bi - 1].convs["3"].name]:] if bi > 0 else None
             y1, y2 = a["y1"][:B], a["y2"][:B]
             gout = self.gbuf[cur][: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
             c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
             # conv3
-            N.colsum(gout, 4 * f, self.colsum[self.ch[c3n]:])
             N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)
             g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
             N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2, None,
-                    g2, 0, None, 0, 0, 0, 0, 0)
+                    g2, 0, None, 0, 0, 0, 0, 0, self.colsum[self.ch[c2n]:])
             # conv2 (3x3)
-            N.colsum(g2, f, self.colsum[self.ch[c2n]:])
             N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
             g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
             N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1, None,
-                    g1, 0, None, 0, 0, 0, 0, 0)
+                    g1, 0, None, 0, 0, 0, 0, 0, self.colsum[self.ch[c1n]:])
             # conv1 (+ conv0)
-            N.colsum(g1, f, self.colsum[self.ch[c1n]:])
             nxt = 1 - cur
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
             if b.proj:
                 N.wgrad(x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0)
                 N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
                 N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, 5 * f), 1, None, None, None,
-                        mask_in, None, gx, 0, None, 0, 0, 1 if b.stride == 2 else 0, H, H)
+                        mask_in, None, gx, 0, None, 0, 0, 1 if b.stride == 2 else 0, H, H, cs_in)
                 last = L.entry(b.convs["0"].name, "kernel")
             else:
                 N.wgrad(x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0)
                 N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
                 N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, f), 1, None, None, None,
-                        mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0)
+                        mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0, cs_in)
                 last = L.entry(c1n, "kernel")
             done_upto(last.offset + last.size)
             cur = nxt
-        # ---- stem
-        H1, H2 = self.H1, self.H2
+        # ---- stem (space-to-depth wgrad, folded back to 7x7x3)
+        H1, H2, Hs = self.H1, self.H2, self.Hs
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
         gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
-        N.maxpool_bwd(gpool, self.pidx[:B], self.c1[:B], gc1)
         s = L.stem
-        N.colsum(gc1, 64, self.colsum[self.ch[s.name]:])
-        N.wgrad(self.stem_col[:B], H1, H1, 1, 1, 1, 0, H1, H1, gc1, None, 0, self._gview(s.name, 64, 147), 147, 0)
+        N.maxpool_bwd(gpool, self.pidx[:B], self.c1[:B], gc1, self.colsum[self.ch[s.name]:])
+        N.wgrad(self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
+        N.stem_wgrad_fold(self.stem_dw2, self._gview(s.name, 64, 147), 64)
         N.wgrad_finalize(self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)
         done_upto(L.kernels_end)
         N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)

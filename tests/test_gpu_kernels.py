@@ -58,7 +58,7 @@ def test_igemm_forward(case, with_res):
     res = rnd(n, ho, ho, co) if with_res else None
     out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
     N().igemm(x, None, h, h, r, r, st, pad, ho, ho, w.view(co, -1), 0, scale, shift, res, None, None, out, 1,
-              None, 0, 0, 0, 0, 0)
+              None, 0, 0, 0, 0, 0, None)
     ref = conv_ref(x, w, st, pad) * scale + shift
     if with_res:
         ref = ref + res.float()
@@ -76,7 +76,7 @@ def test_igemm_split_outputs_and_f32():
     y1 = torch.empty(n, 4, 4, f, dtype=torch.bfloat16, device=dev)
     sc = torch.empty(n, 4, 4, 4 * f, dtype=torch.bfloat16, device=dev)
     N().igemm(x, None, h, h, 1, 1, 2, 0, 4, 4, w.view(5 * f, c), 0, scale, shift, None, None, None, y1, 1,
-              sc, 0, f, 0, 0, 0)
+              sc, 0, f, 0, 0, 0, None)
     ref = conv_ref(x, w, 2, 0) * scale + shift
     assert rel(y1, ref[..., :f].relu()) < 1e-2
     assert rel(sc, ref[..., f:]) < 1e-2
@@ -87,7 +87,7 @@ def test_igemm_split_outputs_and_f32():
     ones = torch.ones(1000, device=dev)
     out = torch.empty(6, 1000, device=dev)
     N().igemm(a.view(6, 1, 1, 2048), None, 1, 1, 1, 1, 1, 0, 1, 1, wd, 2, ones, bias, None, None, None, out, 0,
-              None, 0, 0, 0, 0, 0)
+              None, 0, 0, 0, 0, 0, None)
     ref = a.float() @ wd.float().t() + bias
     assert rel(out, ref) < 1e-3
 
@@ -112,12 +112,14 @@ def test_igemm_dgrad(case):
     out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
     wt = dgrad_weights(w, a)
     pd = r - 1 - pad
+    cs = torch.zeros(cin, device=dev)
     N().igemm(g, None, ho, ho, r, r, 1, pd, ho, ho, wt.view(cin, -1), 1, None, None, None, mask, add, out, 0,
-              None, 0, 0, 1 if st == 2 else 0, h, h)
+              None, 0, 0, 1 if st == 2 else 0, h, h, cs)
     gs = (g.float() * a).permute(0, 3, 1, 2)
     ref = torch.nn.grad.conv2d_input((n, cin, h, h), w.float().permute(0, 3, 1, 2), gs, stride=st, padding=pad)
     ref = (ref.permute(0, 2, 3, 1) + add.float()) * (mask.float() > 0)
     assert rel(out, ref) < 1e-2
+    assert rel(cs, out.float().sum((0, 1, 2))) < 1e-3
 
 
 def test_igemm_dgrad_dual_source():
@@ -133,7 +135,7 @@ def test_igemm_dgrad_dual_source():
     wt = torch.cat([dgrad_weights(w1, a1).view(cin, f), dgrad_weights(w0, a0).view(cin, 4 * f)], 1).contiguous()
     mask = rnd(n, h, h, cin)
     out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
-    N().igemm(g1, g0, ho, ho, 1, 1, 1, 0, ho, ho, wt, 1, None, None, None, mask, None, out, 0, None, 0, 0, 1, h, h)
+    N().igemm(g1, g0, ho, ho, 1, 1, 1, 0, ho, ho, wt, 1, None, None, None, mask, None, out, 0, None, 0, 0, 1, h, h, None)
     r1 = torch.nn.grad.conv2d_input((n, cin, h, h), w1.float().permute(0, 3, 1, 2),
                                     (g1.float() * a1).permute(0, 3, 1, 2), stride=2)
     r0 = torch.nn.grad.conv2d_input((n, cin, h, h), w0.float().permute(0, 3, 1, 2),
@@ -207,9 +209,11 @@ def test_maxpool_and_gap():
     gy = rnd(n, ho, ho, c)
     yr.backward(gy.float().permute(0, 3, 1, 2))
     gx = torch.empty_like(x)
-    N().maxpool_bwd(gy, idx, x, gx)
+    cs = torch.zeros(c, device=dev)
+    N().maxpool_bwd(gy, idx, x, gx, cs)
     ref = xr.grad.permute(0, 2, 3, 1) * (x.float() > 0)
     assert rel(gx, ref) < 1e-2
+    assert rel(cs, gx.float().sum((0, 1, 2))) < 1e-3
     # GAP
     z = torch.relu(torch.randn(n, 7, 7, 256, device=dev)).to(torch.bfloat16)
     p = torch.empty(n, 256, dtype=torch.bfloat16, device=dev)
@@ -217,9 +221,11 @@ def test_maxpool_and_gap():
     assert rel(p, z.float().mean((1, 2))) < 1e-2
     gp = rnd(n, 256)
     gz = torch.empty_like(z)
-    N().gap_bwd(gp, z, gz)
+    cs = torch.zeros(256, device=dev)
+    N().gap_bwd(gp, z, gz, cs)
     ref = (gp.float() / 49).view(n, 1, 1, 256) * (z.float() > 0)
     assert rel(gz, ref) < 1e-2
+    assert rel(cs, gz.float().sum((0, 1, 2))) < 1e-3
 
 
 def test_colsum_softmax_xent():
@@ -271,7 +277,9 @@ def test_optimizers():
 
 
 @pytest.mark.parametrize("mode", ["identity", "resize", "crop"])
-def test_stem_im2col(mode):
+def test_stem_s2d_conv_and_wgrad(mode):
+    """Preprocess + space-to-depth + 4x4 window igemm == Keras stem conv (7x7/s2 after
+    ZeroPadding2D(3)); s2d wgrad folded back == conv2d_weight."""
     from pddl.models.reference import preprocess
     torch.manual_seed(9)
     B, S = 2, 32
@@ -280,11 +288,34 @@ def test_stem_im2col(mode):
     crop = {"identity": 32, "resize": 40, "crop": 24}[mode]
     m = {"identity": 0, "resize": 1, "crop": 2}[mode]
     oy, ox = (3, 5) if mode == "crop" else (0, 0)
-    ho = (crop + 6 - 7) // 2 + 1
-    out = torch.empty(B, ho, ho, 192, dtype=torch.bfloat16, device=dev)
-    N().stem_im2col(img, flip, m, crop, crop, oy, ox, out)
-    x = preprocess(img, crop, True, flip, (oy, ox))
-    cols = F.unfold(F.pad(x, (3, 3, 3, 3)), 7, stride=2)            # [B, 3*49, L]  (c, r, s) order
-    cols = cols.view(B, 3, 7, 7, -1).permute(0, 4, 2, 3, 1).reshape(B, ho, ho, 147)
-    assert rel(out[..., :147], cols) < 5e-3
-    assert out[..., 147:].float().abs().max().item() == 0
+    hs = (crop + 6) // 2
+    ho = crop // 2
+    x2 = torch.empty(B, hs, hs, 16, dtype=torch.bfloat16, device=dev)
+    N().stem_s2d(img, flip, m, crop, crop, oy, ox, x2)
+    x = preprocess(img, crop, True, flip, (oy, ox))                 # NCHW fp32
+    ref_x2 = F.pixel_unshuffle(F.pad(x, (3, 3, 3, 3)), 2)           # [B, 3*4, hs, hs]  (c, dy, dx)
+    got = x2.float().view(B, hs, hs, 2, 2, 4)[..., :3].permute(0, 5, 3, 4, 1, 2).reshape(B, 12, hs, hs)
+    assert rel(got, ref_x2) < 5e-3
+    # conv through the window GEMM with weights in the s2d layout
+    w = torch.randn(64, 7, 7, 3, device=dev) * 0.05
+    w2 = torch.zeros(64, 4, 4, 2, 2, 4, device=dev)
+    for r in range(7):
+        for s_ in range(7):
+            w2[:, r // 2, s_ // 2, r % 2, s_ % 2, :3] = w[:, r, s_, :]
+    w2 = w2.view(64, 256).to(torch.bfloat16)
+    ones, zeros = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+    y = torch.empty(B, ho, ho, 64, dtype=torch.bfloat16, device=dev)
+    N().igemm(x2, None, hs, hs, 4, 4, 1, 0, ho, ho, w2, 0, ones, zeros, None, None, None, y, 0, None, 0, 0, 0, 0, 0,
+              None)
+    xb = x2.float().view(B, hs, hs, 2, 2, 4)[..., :3].permute(0, 5, 1, 3, 2, 4).reshape(B, 3, 2 * hs, 2 * hs)
+    wq = w2.float().view(64, 4, 4, 2, 2, 4)[..., :3]
+    wq = wq.permute(0, 5, 1, 3, 2, 4).reshape(64, 3, 8, 8)[:, :, :7, :7]
+    ref = F.conv2d(xb, wq, stride=2).permute(0, 2, 3, 1)
+    assert rel(y, ref) < 1e-2
+    g = rnd(B, ho, ho, 64)
+    dw2 = torch.zeros(64, 256, device=dev)
+    N().wgrad(x2, hs, hs, 4, 4, 1, 0, ho, ho, g, None, 0, dw2, 256, 0)
+    dw = torch.zeros(64, 147, device=dev)
+    N().stem_wgrad_fold(dw2, dw, 64)
+    refw = torch.nn.grad.conv2d_weight(xb, (64, 3, 7, 7), g.float().permute(0, 3, 1, 2), stride=2)
+    assert rel(dw.view(64, 7, 7, 3), refw.permute(0, 2, 3, 1)) < 5e-3
