@@ -79,7 +79,8 @@ void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64
   p.relu2 = (int)relu2; p.n_split = (int)n_split;
   p.up2 = (int)up2; p.Hf = (int)Hf; p.Wf = (int)Wf;
   p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;
-  if (p.colsum) PCHECK(colsum->numel() >= p.Nn, "colsum too short");
+  if (p.colsum)
+    PCHECK(colsum->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn) * p.Nn, "colsum partial buffer too short");
   const int64_t rows_out = up2 ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
   PCHECK(out.numel() / std::max<int64_t>(1, out.size(-1)) >= (out2.has_value() ? p.M : rows_out) ||
              out.dim() >= 2,
@@ -155,6 +156,12 @@ void colsum(Tensor g, int64_t C, Tensor out) {
   const int64_t M = g.numel() / g.size(-1);
   ok(pddl::colsum_launch(bfp(g), (int)M, (int)C, ldg, f32p(out), cur_stream()), "colsum");
 }
+void colsum_reduce(Tensor part, Tensor table, int64_t nlayers, Tensor colsum) {
+  PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::ColRedLayer), "colsum_reduce table size");
+  ok(pddl::colsum_reduce_launch(f32p(part), reinterpret_cast<const pddl::ColRedLayer*>(table.data_ptr()),
+                                (int)nlayers, f32p(colsum), cur_stream()),
+     "colsum_reduce");
+}
 void softmax_xent(Tensor logits, Tensor labels, int64_t ncls, double gscale, Tensor dlogits, Tensor loss_sum,
                   Tensor correct) {
   PCHECK(labels.scalar_type() == torch::kInt64 && labels.is_cuda(), "labels int64 GPU");
@@ -212,6 +219,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gap_bwd", &gap_bwd);
   m.def("colsum", &colsum);
   m.def("softmax_xent", &softmax_xent);
+  m.def("colsum_reduce", &colsum_reduce);
+  m.def("igemm_partial_rows", &pddl::igemm_partial_rows);
+  m.def("maxpool_bwd_partial_rows", &pddl::maxpool_bwd_partial_rows);
+  m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);
   m.def("prep", &prep);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("bn_grad", &bn_grad);

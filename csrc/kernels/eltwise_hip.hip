@@ -90,6 +90,8 @@ const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStre
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
+static int grid_for(long n) { return (int)lmin((n + 255) / 256, 8192); }
+
 // --------------------------------------------------------------------------- maxpool
 // Window of output (ho, wo) covers input rows 2ho-1 .. 2ho+1 (ZeroPadding2D(1) then 3x3/s2
 // valid).  Padded taps are real zeros (as in Keras); the first maximum in scan order wins.
@@ -179,21 +181,21 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t*
     for (int e = 0; e < 8; ++e) cs[e] += acc[e];
     *reinterpret_cast<uint4*>(gx + o) = pack8(acc);
   }
-  if (colsum) {
+  if (colsum) {  // one partial row of C sums per wave (plain stores)
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int o = cg; o < 64; o <<= 1)
 #pragma unroll
       for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], o, 64);
     if (lane < cg) {
-      const int g = (int)((blockIdx.x * (long)blockDim.x + threadIdx.x) % cg);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) unsafeAtomicAdd(colsum + g * 8 + e, cs[e]);
+      const long wave = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+      float4* dst = reinterpret_cast<float4*>(colsum + wave * C + lane * 8);
+      dst[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      dst[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
     }
   }
 }
-
-static int grid_for(long n) { return (int)lmin((n + 255) / 256, 8192); }
+int maxpool_bwd_partial_rows(int B, int H, int W, int C) { return grid_for((long)B * H * W * C / 8) * 4; }
 
 const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, int B, int H, int W, int C, int Ho,
                                int Wo, hipStream_t s) {
@@ -249,9 +251,10 @@ __global__ void gap_bwd_kernel(const bf16_t* __restrict__ gp, int ldgp, const bf
       for (int e = 0; e < 8; ++e) { o[e] = mv[e] > 0.f ? v[e] * inv : 0.f; cs[e] += o[e]; }
       *reinterpret_cast<uint4*>(g + row * C + gg * 8) = pack8(o);
     }
-    if (colsum) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) unsafeAtomicAdd(colsum + gg * 8 + e, cs[e]);
+    if (colsum) {  // partial row b (plain stores)
+      float4* dst = reinterpret_cast<float4*>(colsum + (long)b * C + gg * 8);
+      dst[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      dst[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
     }
   }
 }
@@ -312,6 +315,27 @@ const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, 
   int gy = (M + rpb - 1) / rpb;
   if ((long)gx * gy > 4096) { gy = (4096 + gx - 1) / gx; rpb = (M + gy - 1) / gy; gy = (M + rpb - 1) / rpb; }
   hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, s, g, M, C, ldg, rpb, out);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// Fold partial column-sum rows: grid (row chunks, layers); one atomic per column per block.
+__global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRedLayer* __restrict__ L,
+                                     float* __restrict__ colsum) {
+  const ColRedLayer l = L[blockIdx.y];
+  const int chunks = gridDim.x;
+  const int r0 = (int)((long)l.rows * blockIdx.x / chunks), r1 = (int)((long)l.rows * (blockIdx.x + 1) / chunks);
+  if (r0 >= r1) return;
+  for (int c = threadIdx.x; c < l.C; c += blockDim.x) {
+    float s = 0.f;
+    const float* p = part + l.part + c;
+    for (int r = r0; r < r1; ++r) s += p[(long)r * l.C];
+    unsafeAtomicAdd(colsum + l.out + c, s);
+  }
+}
+const char* colsum_reduce_launch(const float* part, const ColRedLayer* layers_dev, int nlayers, float* colsum,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(32, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

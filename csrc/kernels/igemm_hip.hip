@@ -240,17 +240,25 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
     __syncthreads();
   }
   // Fused per-channel column sums of the written gradient (BN beta / conv bias grads):
-  // fold the lanes that share columns, then one atomic per column per wave.
+  // fold the lanes that share columns, then each wave stores ONE partial row (plain
+  // stores; atomics from every workgroup onto the same 64-2048 addresses serialize).
+  // Rows are indexed (m-tile, wave-row); colsum_reduce folds them.
   if (p.colsum) {
 #pragma unroll
     for (int o = LPR; o < 64; o <<= 1)
 #pragma unroll
       for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
     if (rr == 0 && col_ok) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) unsafeAtomicAdd(p.colsum + gn + e, csum[e]);
+      float4* dst = reinterpret_cast<float4*>(p.colsum + (long)(tm * (BM / WTM) + wm) * p.Nn + gn);
+      dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
     }
   }
+}
+
+int igemm_partial_rows(int M, int Nn) {
+  const int BM = Nn <= 64 ? 256 : 128;
+  return ((M + BM - 1) / BM) * (BM / 64);
 }
 
 static bool igemm_check(const IgemmParams& p, const char** why) {

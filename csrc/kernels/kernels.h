@@ -28,9 +28,10 @@ struct IgemmParams {
   void* out; int ldo; int relu;
   void* out2; int ldo2; int relu2; int n_split;     // FWD: columns >= n_split -> out2
   int up2; int Hf, Wf;                              // DGRAD: scatter to a 2x finer grid
-  float* colsum;                                    // DGRAD: += per-column sums of the output
+  float* colsum;                                    // DGRAD: per-wave partial column sums [rows][Nn]
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
+int igemm_partial_rows(int M, int Nn);               // rows of the partial column-sum buffer
 
 struct WgradParams {
   const uint16_t* x; int N, H, W, C;   // conv input, NHWC (or [M][ldx] rows for 1x1/s1)
@@ -70,6 +71,12 @@ const char* gap_fwd_launch(const uint16_t* x, uint16_t* y, int B, int HW, int C,
 const char* gap_bwd_launch(const uint16_t* gp, int ldgp, const uint16_t* ymask, uint16_t* g, int B, int HW, int C,
                            float* colsum, hipStream_t s);
 const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, hipStream_t s);
+// Partial column sums written by the fused producers (igemm dgrad, maxpool_bwd, gap_bwd):
+// colsum[l.out + c] += sum_t part[l.part + t * C + c] for every layer of the table.
+struct ColRedLayer { long part; int rows, C, out; int pad; };
+const char* colsum_reduce_launch(const float* part, const ColRedLayer* layers_dev, int nlayers, float* colsum,
+                                 hipStream_t s);
+int maxpool_bwd_partial_rows(int B, int H, int W, int C);
 const char* softmax_xent_launch(const float* logits, int ldl, const int64_t* labels, int B, int ncls,
                                 float gscale, uint16_t* dlogits, int ldd, float* loss_sum, float* correct,
                                 hipStream_t s);

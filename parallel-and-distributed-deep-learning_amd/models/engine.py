@@ -32,6 +32,7 @@ from .resnet50 import BN_EPS, ParamLayout
 _PREP_FMT = "<6i2q8i"
 STEM_K = 256   # 4x4 taps x 16 channels of the space-to-depth stem
 _FIN_FMT = "<5i"
+_CRED_FMT = "<q4i"
 _BNG_FMT = "<9i"
 
 
@@ -55,6 +56,7 @@ class HipEngine:
         assert struct.calcsize(_PREP_FMT) == self.N.PREP_LAYER_BYTES
         assert struct.calcsize(_FIN_FMT) == self.N.FIN_LAYER_BYTES
         assert struct.calcsize(_BNG_FMT) == self.N.BNGRAD_LAYER_BYTES
+        assert struct.calcsize(_CRED_FMT) == self.N.COLRED_LAYER_BYTES
         dev = self.device
         L = layout
         self.params = torch.zeros(L.total, dtype=torch.float32, device=dev)
@@ -207,6 +209,36 @@ class HipEngine:
         self.dpooled = torch.empty(B, 2048, **bf)
         self.labels_dev = torch.zeros(B, dtype=torch.int64, device=dev)
         self.cap = B
+        self._cred = {}
+        self.colpart = torch.empty(self._colred(B)[2], dtype=torch.float32, device=dev)
+
+    def _colred(self, B):
+        """Partial column-sum regions of every fused producer for batch B:
+        (offsets by consumer layer, device reduce table, total floats)."""
+        if B in self._cred:
+            return self._cred[B]
+        N, L = self.N, self.L
+        offs, rows, off = {}, [], 0
+
+        def add(layer, nrows, C):
+            nonlocal off
+            offs[layer] = off
+            rows.append(struct.pack(_CRED_FMT, off, nrows, C, self.ch[layer], 0))
+            off += nrows * C
+        blocks = L.blocks
+        add(blocks[-1].convs["3"].name, B, 2048)                              # gap_bwd
+        for bi in range(len(blocks) - 1, -1, -1):
+            b = blocks[bi]
+            H, Ho = self.geo[b.name]
+            M = B * Ho * Ho
+            add(b.convs["2"].name, N.igemm_partial_rows(M, b.filters), b.filters)   # c3 dgrad -> g2
+            add(b.convs["1"].name, N.igemm_partial_rows(M, b.filters), b.filters)   # c2 dgrad -> g1
+            if bi > 0:                                                               # c1 dgrad -> g_out(prev)
+                add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin), b.cin)
+        add(L.stem.name, N.maxpool_bwd_partial_rows(B, self.H1, self.H1, 64), 64)
+        res = (offs, self._dev_table(rows), off, len(rows))
+        self._cred[B] = res
+        return res
 
     # ------------------------------------------------------------------ params
     def init(self, seed=0):
@@ -328,7 +360,12 @@ class HipEngine:
         H5 = self.H5
         blocks = L.blocks
         gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
-        N.gap_bwd(dpooled, x5, gout, self.colsum[self.ch[blocks[-1].convs["3"].name]:])
+        coffs, ctab, _, cn = self._colred(B)
+        cp = self.colpart
+
+        def part(layer):
+            return cp[coffs[layer]:]
+        N.gap_bwd(dpooled, x5, gout, part(blocks[-1].convs["3"].name))
         # ---- blocks (column sums of every produced gradient are fused into its producer)
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
@@ -337,7 +374,7 @@ class HipEngine:
             f, cin = b.filters, b.cin
             x_in = self.acts[blocks[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
             mask_in = x_in if bi > 0 else None
-            cs_in = self.colsum[self.ch[blocks[bi - 1].convs["3"].name]:] if bi > 0 else None
+            cs_in = part(blocks[bi - 1].convs["3"].name) if bi > 0 else None
             y1, y2 = a["y1"][:B], a["y2"][:B]
             gout = self.gbuf[cur][: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
             c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
@@ -345,12 +382,12 @@ class HipEngine:
             N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)
             g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
             N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2, None,
-                    g2, 0, None, 0, 0, 0, 0, 0, self.colsum[self.ch[c2n]:])
+                    g2, 0, None, 0, 0, 0, 0, 0, part(c2n))
             # conv2 (3x3)
             N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
             g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
             N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1, None,
-                    g1, 0, None, 0, 0, 0, 0, 0, self.colsum[self.ch[c1n]:])
+                    g1, 0, None, 0, 0, 0, 0, 0, part(c1n))
             # conv1 (+ conv0)
             nxt = 1 - cur
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
@@ -373,11 +410,12 @@ class HipEngine:
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
         gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
         s = L.stem
-        N.maxpool_bwd(gpool, self.pidx[:B], self.c1[:B], gc1, self.colsum[self.ch[s.name]:])
+        N.maxpool_bwd(gpool, self.pidx[:B], self.c1[:B], gc1, part(s.name))
         N.wgrad(self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
         N.stem_wgrad_fold(self.stem_dw2, self._gview(s.name, 64, 147), 64)
         N.wgrad_finalize(self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)
         done_upto(L.kernels_end)
+        N.colsum_reduce(cp, ctab, cn, self.colsum)
         N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
         if bucket_cb is not None:
             while nb[0] < len(bks):

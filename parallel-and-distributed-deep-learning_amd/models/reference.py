@@ -123,7 +123,8 @@ class TorchEngine:
     def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0), bucket_cb=None):
         # leaf over the trainable prefix; BN statistics are read (and, in train mode,
         # updated in place) straight from the flat buffer
-        p = self.params[: self.L.n_trainable].detach().requires_grad_(True)
+        # (a copy: BN statistics share the flat buffer and train-mode BN updates them in place)
+        p = self.params[: self.L.n_trainable].clone().requires_grad_(True)
         self.model.stats = self.params
         x = preprocess(images.to(self.device), self.crop, True, flip, crop_offset)
         logits = self.model.logits(p, x, training=True)

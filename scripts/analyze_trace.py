@@ -18,8 +18,8 @@ def schedule(B, crop):
     H1 = (crop + 6 - 7) // 2 + 1
     H2 = (H1 + 2 - 3) // 2 + 1
     ev = []
-    ev.append(("stem_im2col", "stem", 0, B * H1 * H1 * 192 * 2))
-    ev.append(("igemm", "conv1 fwd", 2 * B * H1 * H1 * 147 * 64, B * H1 * H1 * (192 + 64) * 2))
+    ev.append(("stem_s2d", "stem", 0, B * H1 * H1 * 4 * 32))
+    ev.append(("igemm", "conv1 fwd", 2 * B * H1 * H1 * 256 * 64, B * H1 * H1 * 64 * 2))
     ev.append(("maxpool_fwd", "pool", 0, B * (H1 * H1 + H2 * H2) * 64 * 2))
     H = H2
     geo = []
@@ -43,20 +43,17 @@ def schedule(B, crop):
     for b, H, Ho in reversed(geo):
         f, cin = b.filters, b.cin
         M = B * Ho * Ho
-        ev.append(("colsum", f"{b.name} g3", 0, M * 4 * f * 2))
         ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * M * f * 4 * f, (M * f + M * 4 * f) * 2))
         ev.append(("igemm", f"{b.name} c3 dgrad", 2 * M * f * 4 * f, (M * 4 * f + 2 * M * f) * 2))
-        ev.append(("colsum", f"{b.name} g2", 0, M * f * 2))
         ev.append(("wgrad", f"{b.name} c2 wgrad", 2 * M * 9 * f * f, 2 * M * f * 2))
         ev.append(("igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2))
-        ev.append(("colsum", f"{b.name} g1", 0, M * f * 2))
         n1 = 5 * f if b.proj else f
         ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * n1, (M * n1 + B * H * H * cin) * 2))
         ev.append(("wgrad_finalize", b.name, 0, 0))
         ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2))
     ev.append(("maxpool_bwd", "pool", 0, 0))
-    ev.append(("colsum", "stem", 0, 0))
-    ev.append(("wgrad", "conv1 wgrad", 2 * B * H1 * H1 * 147 * 64, 0))
+    ev.append(("wgrad", "conv1 wgrad", 2 * B * H1 * H1 * 256 * 64, 0))
+    ev.append(("stem_wgrad_fold", "fold", 0, 0))
     ev.append(("wgrad_finalize", "stem", 0, 0))
     ev.append(("bn_grad", "bn", 0, 0))
     ev.append(("adam", "adam", 0, 0))
@@ -73,7 +70,7 @@ def main():
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
     ev = schedule(B, crop)
     # find start of last complete step: last stem_im2col such that len(ev) rows follow
-    starts = [i for i, r in enumerate(rows) if "stem_im2col" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(rows) if "stem_s2d" in r["Kernel_Name"]]
     st = None
     for s in reversed(starts):
         if s + len(ev) <= len(rows):
