@@ -319,23 +319,39 @@ const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, 
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
-// Fold partial column-sum rows: grid (row chunks, layers); one atomic per column per block.
+// Fold partial column-sum rows: grid (row chunks, layers).  A block = RL row-lanes x C
+// columns (C <= 256) reduced through LDS, then one atomic per column per block.
 __global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRedLayer* __restrict__ L,
                                      float* __restrict__ colsum) {
+  __shared__ float red[256];
   const ColRedLayer l = L[blockIdx.y];
   const int chunks = gridDim.x;
   const int r0 = (int)((long)l.rows * blockIdx.x / chunks), r1 = (int)((long)l.rows * (blockIdx.x + 1) / chunks);
   if (r0 >= r1) return;
-  for (int c = threadIdx.x; c < l.C; c += blockDim.x) {
+  const int t = threadIdx.x;
+  if (l.C <= 256) {
+    const int RL = 256 / l.C;
+    const int c = t % l.C, rl = t / l.C;
     float s = 0.f;
-    const float* p = part + l.part + c;
-    for (int r = r0; r < r1; ++r) s += p[(long)r * l.C];
-    unsafeAtomicAdd(colsum + l.out + c, s);
+    if (rl < RL)
+      for (int r = r0 + rl; r < r1; r += RL) s += part[l.part + (long)r * l.C + c];
+    red[t] = s;
+    __syncthreads();
+    if (t < l.C) {
+      for (int i = 1; i < RL; ++i) s += red[t + i * l.C];
+      unsafeAtomicAdd(colsum + l.out + c, s);
+    }
+  } else {
+    for (int c = t; c < l.C; c += blockDim.x) {
+      float s = 0.f;
+      for (int r = r0; r < r1; ++r) s += part[l.part + (long)r * l.C + c];
+      unsafeAtomicAdd(colsum + l.out + c, s);
+    }
   }
 }
 const char* colsum_reduce_launch(const float* part, const ColRedLayer* layers_dev, int nlayers, float* colsum,
                                  hipStream_t s) {
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(32, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(128, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

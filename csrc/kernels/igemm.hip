@@ -276,7 +276,8 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream) {
   const char* why = nullptr;
   if (!igemm_check(p, &why)) return why;
-  const bool one = p.K <= 64;   // single k-tile: no double buffer, twice the blocks per CU
+  // short K (<= 2 k-tiles) is memory-bound: single LDS stage for twice the resident blocks
+  const bool one = p.K <= 128;
   if (p.Nn <= 64) {
     const int nwg = ((p.M + 255) / 256) * ((p.Nn + 63) / 64);
     if (one) hipLaunchKernelGGL((igemm_kernel<256, 64, 64, 64, 1>), dim3(nwg), dim3(256), 0, stream, p);

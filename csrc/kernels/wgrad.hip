@@ -25,21 +25,31 @@ namespace pddl {
 // 32-lane half of ds_read_b64_tr_b16 touches get distinct even chunk XORs, so the 16
 // 16-byte chunks they read cover all 64 banks exactly once.
 __device__ __forceinline__ int tr_swz(int row) { return ((row & 3) | ((row >> 1) & 4)) << 1; }
+// Same property for [m][64 x bf16] (128-byte row) images: two rows share a 256-byte bank
+// row, so the even/odd rows of a half take chunk XORs {0,2,4,6} within their 8 chunks.
+__device__ __forceinline__ int tr_swz128(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }
 
-template <bool FAST>
+// BM = 128: 2x2 waves, wave tile 64 (co) x 64 (k).  BM = 64 (Cout = 64 layers: the stem and
+// stage 2): 1x4 waves, wave tile 64 x 32, gradient tile with 128-byte rows.
+template <bool FAST, int BM>
 __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split) {
-  constexpr int TILE_BYTES = 64 * 256;        // 64 m-rows x 128 bf16
-  constexpr int STAGE = 2 * TILE_BYTES;       // G tile + X tile
-  constexpr int EPI_LD = 68;
+  constexpr int G_BYTES = 64 * BM * 2;        // 64 m-rows x BM bf16
+  constexpr int X_BYTES = 64 * 256;           // 64 m-rows x 128 bf16
+  constexpr int STAGE = G_BYTES + X_BYTES;
+  constexpr int WAVES_N = BM == 128 ? 2 : 4;
+  constexpr int WTN = 128 / WAVES_N;          // k columns per wave
+  constexpr int TN = WTN / 16;
+  constexpr int EPI_LD = WTN + 4;
+  constexpr int GI = G_BYTES / 4096;          // 1 KiB G pieces per wave
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tco = (p.Cout + 127) / 128, tk = (p.K + 127) / 128, ntiles = tco * tk;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int tco = (p.Cout + BM - 1) / BM, tk = (p.K + 127) / 128, ntiles = tco * tk;
   const int splits = (p.M + m_per_split - 1) / m_per_split;
   const int wg = xcd_remap(blockIdx.x, ntiles * splits);
   const int tile = wg % ntiles, split = wg / ntiles;
-  const int co0 = (tile % tco) * 128, k0 = (tile / tco) * 128;
+  const int co0 = (tile % tco) * BM, k0 = (tile / tco) * 128;
   const int mbeg = split * m_per_split;
   const int mend = min(p.M, mbeg + m_per_split);
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
@@ -59,21 +69,27 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 
   auto load_tile = [&](int mb, int buf) {
     char* gb = smem + buf * STAGE;
-    char* xb = gb + TILE_BYTES;
+    char* xb = gb + G_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < GI; ++i) {  // gradient operand
+      int row, chunk;
+      if (BM == 128) { row = (wave * GI + i) * 4 + lrow; chunk = lpos ^ tr_swz(row); }
+      else { row = (wave * GI + i) * 8 + (lane >> 3); chunk = (lane & 7) ^ tr_swz128(row); }
+      const int m = mb + row;
+      const int co = co0 + chunk * 8;
+      const bf16_t* gs = zero;
+      if (m < mend && co < p.Cout) {
+        if (p.g2 && co >= p.co_split) gs = p.g2 + (long)m * p.ldg2 + (co - p.co_split);
+        else gs = p.g + (long)m * p.ldg + co;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)gs, LDS_PTR(gb + (wave * GI + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // input operand
       const int row = (wave * 4 + i) * 4 + lrow;
       const int chunk = lpos ^ tr_swz(row);
       const int m = mb + row;
       const bool mok = m < mend;
-      // gradient operand
-      const int co = co0 + chunk * 8;
-      const bf16_t* gs = zero;
-      if (mok && co < p.Cout) {
-        if (p.g2 && co >= p.co_split) gs = p.g2 + (long)m * p.ldg2 + (co - p.co_split);
-        else gs = p.g + (long)m * p.ldg + co;
-      }
-      __builtin_amdgcn_global_load_lds((const void*)gs, LDS_PTR(gb + (wave * 4 + i) * 1024), 16, 0, 0);
       // input operand
       const bf16_t* xs = zero;
       if (FAST) {
@@ -95,11 +111,11 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
     }
   };
 
-  v4f acc[4][4];
+  v4f acc[4][TN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   // Fragment-read lane geometry (T10): group G = lane>>4 reads rows 8G + 4h + q, q = (lane&15)>>2,
   // columns 4p..4p+3, p = lane&3.
@@ -114,29 +130,31 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
     const int cur = it & 1;
     if (it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
     const char* gb = smem + cur * STAGE;
-    const char* xb = gb + TILE_BYTES;
+    const char* xb = gb + G_BYTES;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
-      int roff[2], rsw[2];
+      int roff[2], rsw[2], goff[2], gsw[2];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int row = kh * 32 + 8 * G + 4 * h2 + q;
         roff[h2] = row * 256 + (pp & 1) * 8;
         rsw[h2] = tr_swz(row);
+        goff[h2] = row * (BM * 2) + (pp & 1) * 8;
+        gsw[h2] = BM == 128 ? rsw[h2] : tr_swz128(row);
       }
-      v8bf af[4], bfr[4];
+      v8bf af[4], bfr[TN];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ch = wm * 8 + i * 2 + (pp >> 1);
         v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) v4bf*)(gb + roff[0] + ((ch ^ rsw[0]) << 4)));
+            (__attribute__((address_space(3))) v4bf*)(gb + goff[0] + ((ch ^ gsw[0]) << 4)));
         v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) v4bf*)(gb + roff[1] + ((ch ^ rsw[1]) << 4)));
+            (__attribute__((address_space(3))) v4bf*)(gb + goff[1] + ((ch ^ gsw[1]) << 4)));
         af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ch = wn * 8 + j * 2 + (pp >> 1);
+      for (int j = 0; j < TN; ++j) {
+        const int ch = wn * (WTN / 8) + j * 2 + (pp >> 1);
         v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
             (__attribute__((address_space(3))) v4bf*)(xb + roff[0] + ((ch ^ rsw[0]) << 4)));
         v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
@@ -146,7 +164,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -154,23 +172,27 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   }
   if (nit == 0) return;
 
-  // Epilogue: per-wave 32x64 fp32 staging, then one 256-byte atomic row per instruction.
+  // Epilogue: per-wave 32 x WTN fp32 staging, then row-contiguous atomics (256 B per wave
+  // instruction: one 64-float row, or two 32-float rows for WTN = 32).
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
-  const int kcol = k0 + wn * 64 + lane;
+  constexpr int RPA = 64 / WTN;  // rows per atomic instruction
+  const int kcol = k0 + wn * WTN + (lane % WTN);
+  const int rsub = lane / WTN;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
           stage[(i2 * 16 + (lane >> 4) * 4 + jj) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 2 + i2][j][jj];
     __syncthreads();
     if (kcol < p.K) {
-      for (int r = 0; r < 32; ++r) {
-        const int co = co0 + wm * 64 + pass * 32 + r;
-        if (co < p.Cout) unsafeAtomicAdd(p.dw + (long)co * p.ld_dw + kcol, stage[r * EPI_LD + lane]);
+      for (int r = 0; r < 32; r += RPA) {
+        const int co = co0 + wm * 64 + pass * 32 + r + rsub;
+        if (co < p.Cout)
+          unsafeAtomicAdd(p.dw + (long)co * p.ld_dw + kcol, stage[(r + rsub) * EPI_LD + (lane % WTN)]);
       }
     }
     __syncthreads();
@@ -186,7 +208,8 @@ const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   if (p.Cout % 8 || p.ldg % 8 || (fast && p.ldx % 8)) return "wgrad: Cout / ldg / ldx must be multiples of 8";
   if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "wgrad: empty problem";
   if (!fast && (long)p.N * p.H * p.W * p.C >= (1L << 31)) return "wgrad: input too large";
-  const int ntiles = ((p.Cout + 127) / 128) * ((p.K + 127) / 128);
+  const int BM = p.Cout <= 64 ? 64 : 128;
+  const int ntiles = ((p.Cout + BM - 1) / BM) * ((p.K + 127) / 128);
   int splits = p.splits;
   if (splits <= 0) {
     // Every split adds one 64 KiB fp32 atomic tile (~1.3 TB/s chip-wide), so a workgroup
@@ -205,10 +228,13 @@ const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   mps = (mps + 63) / 64 * 64;
   splits = (p.M + mps - 1) / mps;
   const int nwg = ntiles * splits;
-  if (fast)
-    hipLaunchKernelGGL(wgrad_kernel<true>, dim3(nwg), dim3(256), 0, stream, p, mps);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<false>, dim3(nwg), dim3(256), 0, stream, p, mps);
+  if (BM == 64) {
+    if (fast) hipLaunchKernelGGL((wgrad_kernel<true, 64>), dim3(nwg), dim3(256), 0, stream, p, mps);
+    else hipLaunchKernelGGL((wgrad_kernel<false, 64>), dim3(nwg), dim3(256), 0, stream, p, mps);
+  } else {
+    if (fast) hipLaunchKernelGGL((wgrad_kernel<true, 128>), dim3(nwg), dim3(256), 0, stream, p, mps);
+    else hipLaunchKernelGGL((wgrad_kernel<false, 128>), dim3(nwg), dim3(256), 0, stream, p, mps);
+  }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

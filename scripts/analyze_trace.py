@@ -55,6 +55,7 @@ def schedule(B, crop):
     ev.append(("wgrad", "conv1 wgrad", 2 * B * H1 * H1 * 256 * 64, 0))
     ev.append(("stem_wgrad_fold", "fold", 0, 0))
     ev.append(("wgrad_finalize", "stem", 0, 0))
+    ev.append(("colsum_reduce", "cred", 0, 0))
     ev.append(("bn_grad", "bn", 0, 0))
     ev.append(("adam", "adam", 0, 0))
     ev.append(("prep", "prep", 0, 0))
