@@ -207,8 +207,15 @@ void cast_f32(Tensor x, Tensor y) { ok(pddl::cast_f32_launch(bfp(x), f32p(y), x.
 
 }  // namespace
 
+void register_rccl(pybind11::module& m);
+void register_fusion(pybind11::module& m);
+void register_loader(pybind11::module& m);
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.doc() = "pddl MI355X (gfx950) HIP kernels";
+  m.doc() = "pddl MI355X (gfx950) HIP kernels + native runtime (RCCL comm, fusion engine, loader)";
+  register_rccl(m);
+  register_fusion(m);
+  register_loader(m);
   m.def("igemm", &igemm);
   m.def("wgrad", &wgrad);
   m.def("stem_s2d", &stem_s2d);

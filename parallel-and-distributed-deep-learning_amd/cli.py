@@ -1,0 +1,68 @@
+"""Shared `main` of the drop-in entry scripts.
+
+Each reference script (8 files under /root/reference) has a same-named script at the
+repository root that calls `run(<preset>)`: identical defaults (batch, crop, optimizer,
+epochs, callbacks, checkpoint file name), CLI overrides on top.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+from typing import List, Optional
+
+from .config import config_from_args
+
+
+def _banner(cfg, strategy):
+    import torch
+    print(f"Using pddl {__import__('pddl').__version__} (torch {torch.__version__}, HIP {torch.version.hip}), "
+          f"strategy={cfg.strategy}, replicas={strategy.num_replicas_in_sync}, "
+          f"per-replica batch={strategy.per_replica_batch}, global batch={strategy.global_batch}, "
+          f"crop={cfg.crop}, bn={cfg.bn_mode}, optimizer={cfg.optimizer}", flush=True)
+
+
+def model_summary(cfg) -> str:
+    from .models.resnet50 import ParamLayout
+    L = ParamLayout(cfg.num_classes)
+    return (f'Model: "{cfg.model_name}"\n'
+            f"  input_1 (InputLayer) [(None, {cfg.image_size}, {cfg.image_size}, 3)]\n"
+            f"  rescaling (Rescaling)  random_crop (RandomCrop {cfg.crop}x{cfg.crop})  random_flip (RandomFlip)\n"
+            f"  resnet50 (Functional) (None, 2048)   {L.count() - 2048 * cfg.num_classes - cfg.num_classes:,}\n"
+            f"  dense (Dense) (None, {cfg.num_classes})  {2048 * cfg.num_classes + cfg.num_classes:,}\n"
+            f"Total params: {L.count():,}\nTrainable params: {L.count(True):,}\n"
+            f"Non-trainable params: {L.count(False):,}")
+
+
+def run(preset: str, argv: Optional[List[str]] = None, extra=None) -> int:
+    from .parallel.strategies import make_strategy
+    from .train.trainer import Trainer, default_callbacks
+    cfg = config_from_args(preset, argv, extra)
+    if cfg.strategy == "ps":
+        from .parallel.parameter_server import run_ps_job
+        return run_ps_job(cfg)
+    strategy = make_strategy(cfg)
+    trainer = Trainer(cfg, strategy)
+    if strategy.is_chief:
+        _banner(cfg, strategy)
+        if cfg.verbose:
+            print(model_summary(cfg), flush=True)
+    cbs = default_callbacks(cfg, strategy)
+    trainer.fit(cfg.epochs, cbs)
+    if cfg.timeline and hasattr(strategy, "write_timeline"):
+        strategy.write_timeline(cfg.timeline)
+    if cfg.save:
+        fname = os.path.join(cfg.save_dir, cfg.checkpoint_name(n_gpus=strategy.num_replicas_in_sync))
+        if strategy.is_chief:
+            print("Saving model to ", fname, flush=True)
+        trainer.save(fname)
+    if cfg.strategy in ("horovod", "multiworker"):
+        print("All done for rank", strategy.rank, flush=True)
+    try:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+    except Exception:
+        pass
+    return 0

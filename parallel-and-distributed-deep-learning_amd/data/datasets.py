@@ -55,11 +55,19 @@ class SyntheticImageNet(ImageSource):
                     torch.randint(0, 256, (n, S, S, 3), dtype=torch.uint8, device=device, generator=g),
                     torch.randint(0, self.num_classes, (n,), dtype=torch.int64, device=device, generator=g))
             return self._cache[key]
-        # per-example deterministic content: hash of the index seeds a counter-based fill
-        lab = torch.from_numpy((np.asarray(idx, dtype=np.int64) * 2654435761 + self.seed) % self.num_classes)
-        g = torch.Generator(device=device).manual_seed(int(self.seed * 1000003 + int(idx[0]) * 7919 + n))
-        img = torch.randint(0, 256, (n, S, S, 3), dtype=torch.uint8, device=device, generator=g)
-        return img, lab.to(device)
+        # per-example deterministic content (counter-based hash of (seed, example, pixel)):
+        # the same example has the same pixels whatever batch / shard it is fetched in
+        ii = torch.as_tensor(np.asarray(idx, dtype=np.int64), device=device).view(-1, 1)
+        p = torch.arange(S * S * 3, dtype=torch.int64, device=device).view(1, -1)
+        x = ii * 0x9E3779B1 + p * 0x85EBCA77 + (self.seed + 1) * 0xC2B2AE3D
+        x = x ^ (x >> 15)
+        x = x * 0x2C1B3C6D
+        x = x ^ (x >> 12)
+        x = x * 0x297A2D39
+        x = x ^ (x >> 15)
+        img = (x & 255).to(torch.uint8).view(n, S, S, 3)
+        lab = (ii.view(-1) * 2654435761 + self.seed) % self.num_classes
+        return img, lab
 
 
 class RecordsImageNet(ImageSource):

@@ -120,7 +120,7 @@ class TorchEngine:
     def after_update(self):
         pass
 
-    def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0), bucket_cb=None):
+    def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0), bucket_cb=None, buckets=None):
         # leaf over the trainable prefix; BN statistics are read (and, in train mode,
         # updated in place) straight from the flat buffer
         # (a copy: BN statistics share the flat buffer and train-mode BN updates them in place)
@@ -135,8 +135,8 @@ class TorchEngine:
             self.grads.copy_(p.grad)
             correct = (logits.argmax(1) == lab).sum().float()
             stats = torch.stack([loss_sum.detach(), correct])
-        if bucket_cb is not None:
-            for i, _ in enumerate(self.L.buckets(1e9)):
+        if bucket_cb is not None:   # autograd produces every gradient at once: all buckets ready
+            for i in range(len(buckets) if buckets is not None else 1):
                 bucket_cb(i)
         return stats
 

@@ -1,0 +1,475 @@
+"""Asynchronous parameter-server training (SURVEY.md C21-C25, §2.2 "Async parameter server").
+
+Reference (imagenet-resnet50-ps.py): create_in_process_cluster(W, P) (:31-65) starts W worker
+and P PS gRPC servers; MinSizePartitioner(min_shard_bytes=256 KiB, max_shards=P) (:75-78)
+shards the variables; ParameterServerStrategy + ClusterCoordinator (:80-84) schedule train
+steps onto workers asynchronously; every step pulls the variables from the PS, computes
+gradients on the worker and applies Adam on the PS-resident variables, with no cross-worker
+synchronisation; GRPC_FAIL_FAST=use_caller (:69) surfaces failures to the coordinator;
+fit(steps_per_epoch=312500) (:142-143) over repeat()-ed datasets.
+
+MI355X-native design:
+  * roles are PROCESSES, one GPU each (e.g. 2 PS + 6 workers on an 8-GPU node); a single
+    launch spawns the whole "in-process cluster" (or torchrun provides WORLD_SIZE = P + W);
+  * the PS holds only its shards of the flat fp32 parameter buffer plus their Adam slots and
+    applies the fused HIP Adam kernel to each arriving gradient (async, staleness unbounded,
+    as in the reference);
+  * data plane: one 2-rank process group per (worker, PS) pair — RCCL send/recv over xGMI on
+    GPU, gloo on CPU — so every PS serves its workers from independent threads;
+  * control plane (closure scheduling, heartbeats, LR broadcast, stop) is the c10d TCPStore:
+    a worker claims step tickets; the coordinator re-queues the ticket of a worker that misses
+    its heartbeats (ClusterCoordinator's closure re-queue); PDDL_FAULT=kill_worker:<i>@<step>
+    injects a worker failure for tests.  A PS failure aborts the job (reference parity).
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import math
+import os
+import sys
+import threading
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..models.resnet50 import ParamLayout
+
+
+def add_ps_args(ap: argparse.ArgumentParser):
+    """Q6: accept --ps N --worker M (the evident intent) and the positional form `N M`."""
+    ap.add_argument("--ps", type=int, dest="num_ps")
+    ap.add_argument("--worker", "--workers", type=int, dest="num_workers")
+    ap.add_argument("positional", nargs="*", type=int)
+
+
+def parse_ps_counts(ns) -> Tuple[int, int]:
+    num_ps = getattr(ns, "num_ps", None)
+    num_w = getattr(ns, "num_workers", None)
+    pos = list(getattr(ns, "positional", []) or [])
+    if num_ps is None and pos:
+        num_ps = pos.pop(0)
+    if num_w is None and pos:
+        num_w = pos.pop(0)
+    return (num_ps or 1), (num_w or 1)
+
+
+# ----------------------------------------------------------------------- partitioning
+def min_size_partitions(keras_shape, dtype_bytes: int, min_shard_bytes: int, max_shards: int) -> int:
+    """tf.distribute.experimental.partitioners.MinSizePartitioner: number of axis-0 shards."""
+    nbytes = int(np.prod(keras_shape)) * dtype_bytes
+    n = max(1, min(max_shards, nbytes // max(1, min_shard_bytes)))
+    return int(min(n, keras_shape[0]))
+
+
+@dataclass
+class Shard:
+    name: str
+    offset: int
+    size: int
+    ps: int
+
+
+def partition_variables(L: ParamLayout, num_ps: int, min_shard_bytes: int = 256 << 10) -> List[Shard]:
+    """Shard every trainable variable (MinSizePartitioner, split along the first axis of the
+    internal layout) and place shards on PS tasks round-robin in creation order."""
+    shards: List[Shard] = []
+    rr = 0
+    for e in sorted((e for e in L.entries.values() if e.trainable), key=lambda e: e.offset):
+        n = min_size_partitions(e.keras_shape, 4, min_shard_bytes, num_ps)
+        rows = e.shape[0]
+        n = max(1, min(n, rows))
+        per_row = e.size // rows
+        bounds = [round(i * rows / n) for i in range(n + 1)]
+        for i in range(n):
+            r0, r1 = bounds[i], bounds[i + 1]
+            shards.append(Shard(f"{e.name}/part_{i}", e.offset + r0 * per_row, (r1 - r0) * per_row, rr % num_ps))
+            rr += 1
+    return shards
+
+
+def ps_ranges(shards: List[Shard], num_ps: int) -> List[List[Tuple[int, int]]]:
+    out = [[] for _ in range(num_ps)]
+    for s in shards:
+        out[s.ps].append((s.offset, s.size))
+    return out
+
+
+def _gather(flat: torch.Tensor, ranges) -> torch.Tensor:
+    return torch.cat([flat[o:o + n] for o, n in ranges])
+
+
+def _scatter(flat: torch.Tensor, ranges, packed: torch.Tensor) -> None:
+    p = 0
+    for o, n in ranges:
+        flat[o:o + n].copy_(packed[p:p + n])
+        p += n
+
+
+# ----------------------------------------------------------------------- roles
+OP_PUSH, OP_PULL, OP_STOP = 0.0, 1.0, 2.0
+
+
+class _Cluster:
+    def __init__(self, cfg, rank: int, world: int, num_ps: int, device):
+        self.cfg = cfg
+        self.rank, self.world, self.num_ps = rank, world, num_ps
+        self.num_workers = world - num_ps
+        self.device = device
+        self.is_ps = rank < num_ps
+        self.store = dist.distributed_c10d._get_default_store()
+        # one 2-rank group per (worker, ps) pair; every rank must create every group in order
+        self.pair: Dict[Tuple[int, int], dist.ProcessGroup] = {}
+        for w in range(num_ps, world):
+            for p in range(num_ps):
+                self.pair[(w, p)] = dist.new_group([p, w])
+        L = ParamLayout(cfg.num_classes)
+        self.L = L
+        self.shards = partition_variables(L, num_ps, cfg.min_shard_bytes)
+        self.ranges = ps_ranges(self.shards, num_ps)
+        self.sizes = [sum(n for _, n in r) for r in self.ranges]
+
+
+def _hb_key(w):
+    return f"hb/{w}"
+
+
+class PSServer:
+    """Holds shard p of the parameters + Adam slots; one service thread per worker."""
+
+    def __init__(self, cl: _Cluster, init_params: torch.Tensor):
+        self.cl = cl
+        p = cl.rank
+        self.n = cl.sizes[p]
+        dev = cl.device
+        self.params = _gather(init_params, cl.ranges[p]).to(dev).contiguous()
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.t = 0
+        self.lock = threading.Lock()
+        self.dead = set()
+        self.updates = 0
+
+    def _adam(self, g: torch.Tensor, lr: float):
+        cfg = self.cl.cfg
+        self.t += 1
+        b1, b2, eps = cfg.beta1, cfg.beta2, cfg.adam_eps
+        lr_t = lr * math.sqrt(1 - b2 ** self.t) / (1 - b1 ** self.t)
+        if self.params.is_cuda:
+            from ..ops.native import native
+            native.adam(self.params, g, self.m, self.v, lr_t, b1, b2, eps, 1.0)
+        else:
+            self.m.mul_(b1).add_(g, alpha=1 - b1)
+            self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
+            self.params.sub_(lr_t * self.m / (self.v.sqrt() + eps))
+
+    def serve(self, w: int):
+        cl = self.cl
+        grp = cl.pair[(w, cl.rank)]
+        ctrl = torch.zeros(2, dtype=torch.float64, device=cl.device)
+        grad = torch.empty(self.n, dtype=torch.float32, device=cl.device)
+        try:
+            while True:
+                dist.recv(ctrl, src=w, group=grp)
+                op, lr = float(ctrl[0]), float(ctrl[1])
+                if op == OP_STOP:
+                    return
+                if op == OP_PUSH:
+                    dist.recv(grad, src=w, group=grp)
+                    with self.lock:
+                        self._adam(grad, lr)
+                        self.updates += 1
+                with self.lock:
+                    snap = self.params.clone()
+                dist.send(snap, dst=w, group=grp)
+        except Exception as e:  # worker died: its closure is re-queued by the coordinator
+            self.dead.add(w)
+            print(f"[ps {cl.rank}] lost worker {w}: {type(e).__name__}", flush=True)
+
+    def run(self):
+        cl = self.cl
+        threads = [threading.Thread(target=self.serve, args=(w,), daemon=True) for w in range(cl.num_ps, cl.world)]
+        for t in threads:
+            t.start()
+        if cl.rank == 0:
+            self.monitor(threads)
+        for t in threads:
+            t.join()
+
+    def monitor(self, threads):
+        """Coordinator duty on PS 0: heartbeat watch + closure re-queue of dead workers."""
+        cl = self.cl
+        timeout = float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30"))
+        requeued = set()
+        while any(t.is_alive() for t in threads):
+            time.sleep(0.2)
+            now = time.time()
+            for w in range(cl.num_ps, cl.world):
+                if w in requeued:
+                    continue
+                try:
+                    last = float(cl.store.get(_hb_key(w)).decode())
+                except Exception:
+                    continue
+                finished = cl.store.check([f"fin/{w}"])
+                if not finished and now - last > timeout:
+                    cur = int(cl.store.get(f"cur/{w}").decode()) if cl.store.check([f"cur/{w}"]) else -1
+                    if cur >= 0:
+                        cl.store.add("requeue", 1)
+                    requeued.add(w)
+                    cl.store.add("dead_workers", 1)
+                    print(f"[coordinator] worker {w} missed heartbeats for {now - last:.1f}s: re-queued its "
+                          f"step {cur}", flush=True)
+
+
+class PSWorker:
+    def __init__(self, cl: _Cluster, engine, pipeline_factory):
+        self.cl = cl
+        self.engine = engine
+        self.pipeline_factory = pipeline_factory
+        self.packed = [torch.empty(n, dtype=torch.float32, device=cl.device) for n in cl.sizes]
+        self.widx = cl.rank - cl.num_ps
+
+    def _exchange(self, op: float, lr: float):
+        cl = self.cl
+        ctrl = torch.tensor([op, lr], dtype=torch.float64, device=cl.device)
+        reqs = []
+        for p in range(cl.num_ps):
+            grp = cl.pair[(cl.rank, p)]
+            dist.send(ctrl, dst=p, group=grp)
+            if op == OP_PUSH:
+                dist.send(_gather(self.engine.grads, cl.ranges[p]).contiguous(), dst=p, group=grp)
+        for p in range(cl.num_ps):
+            dist.recv(self.packed[p], src=p, group=cl.pair[(cl.rank, p)])
+            _scatter(self.engine.params, cl.ranges[p], self.packed[p])
+        self.engine.after_update()
+
+    def stop(self):
+        cl = self.cl
+        ctrl = torch.tensor([OP_STOP, 0.0], dtype=torch.float64, device=cl.device)
+        for p in range(cl.num_ps):
+            dist.send(ctrl, dst=p, group=cl.pair[(cl.rank, p)])
+        cl.store.set(f"fin/{cl.rank}", "1")
+
+
+def _claim(store, spe: int, epoch: int) -> int:
+    """Claim the next step ticket of `epoch`; -1 when the epoch's steps are exhausted
+    (re-queued tickets of dead workers extend the budget)."""
+    t = store.add(f"claim/{epoch}", 1) - 1
+    budget = spe + store.add("requeue", 0)
+    return t if t < budget else -1
+
+
+def _fault_step(rank_in_workers: int) -> Optional[int]:
+    spec = os.environ.get("PDDL_FAULT", "")
+    if spec.startswith("kill_worker:"):
+        who, at = spec.split(":", 1)[1].split("@")
+        if int(who) == rank_in_workers:
+            return int(at)
+    return None
+
+
+def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    use_gpu = cfg.device != "cpu" and torch.cuda.is_available()
+    if use_gpu:
+        n = torch.cuda.device_count()
+        torch.cuda.set_device(rank % n)
+        device = torch.device("cuda", rank % n)
+    else:
+        device = torch.device("cpu")
+    backend = "nccl" if use_gpu else "gloo"
+    dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=int(os.environ.get("PDDL_PS_TIMEOUT", "120"))),
+                            **({"device_id": device} if use_gpu else {}))
+    cl = _Cluster(cfg, rank, world, num_ps, device)
+    from ..parallel.strategies import build_engine
+    torch.manual_seed(cfg.seed)
+    if cl.is_ps:
+        L = cl.L
+        init = torch.zeros(L.total)
+        L.init_params(init, cfg.seed)
+        if cfg.weights and cfg.weights != "none":
+            from .strategies import build_engine as _be
+            tmp = _be(cfg.replace(device="cpu"), torch.device("cpu"), 1)
+            tmp.params.copy_(init)
+            from ..utils.checkpoint import load_pretrained
+            load_pretrained(cfg.weights, tmp)
+            init = tmp.params
+        srv = PSServer(cl, init)
+        dist.barrier()
+        srv.run()
+        if result_q is not None:
+            result_q.put(("ps", rank, srv.updates, sorted(srv.dead)))
+        dist.destroy_process_group()
+        return
+    # ---------------------------------------------------------------- worker
+    eng = build_engine(cfg, device, max(cfg.batch_size, cfg.val_batch_size or 0))
+    eng.init(seed=cfg.seed)
+    if cfg.weights and cfg.weights != "none":
+        from ..utils.checkpoint import load_pretrained
+        load_pretrained(cfg.weights, eng)
+        eng.after_update()
+    from ..data.datasets import Pipeline, make_source
+    widx = rank - num_ps
+    src = make_source(cfg.data, "train", cfg)
+    pipe = Pipeline(src, cfg.batch_size, repeat=True, shuffle=cfg.data != "synthetic", seed=cfg.seed + 17 * widx)
+    worker = PSWorker(cl, eng, None)
+    dist.barrier()
+    lr = cfg.lr
+    worker._exchange(OP_PULL, lr)                     # initial pull (variables live on the PS)
+    store = cl.store
+    spe = cfg.steps_per_epoch or pipe.num_batches()
+    if cfg.max_steps:
+        spe = min(spe, cfg.max_steps)
+    fault_at = _fault_step(widx)
+    it = pipe.iterate(device)
+    from .strategies import Augment
+    aug = Augment(cfg, device, cfg.seed + 7919 * widx)
+    history = []
+    stats_acc = torch.zeros(3, dtype=torch.float64)
+    steps_done = 0
+    for epoch in range(cfg.epochs):
+        if store.check(["stop"]):
+            break
+        if store.check(["lr"]):
+            lr = float(store.get("lr").decode())
+        acc = torch.zeros(3, dtype=torch.float64)
+        while True:
+            t = _claim(store, spe, epoch)
+            if t < 0:
+                break
+            store.set(f"cur/{rank}", str(t))
+            store.set(_hb_key(rank), str(time.time()))
+            if fault_at is not None and steps_done == fault_at:
+                print(f"[worker {widx}] injected failure at step {steps_done}", flush=True)
+                os._exit(17)
+            images, labels = next(it)
+            B = images.shape[0]
+            flip, off = aug(B)
+            s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off)
+            acc[:2] += s.detach().double().cpu()
+            acc[2] += B
+            worker._exchange(OP_PUSH, lr)
+            store.set(f"cur/{rank}", "-1")
+            store.add(f"done/{epoch}", 1)
+            steps_done += 1
+        store.set(_hb_key(rank), str(time.time()))
+        # epoch end: worker 0 (coordinator-side logic) validates and runs the callbacks
+        store.add(f"acc/{epoch}/loss", int(acc[0].item() * 1e6))
+        store.add(f"acc/{epoch}/correct", int(acc[1].item()))
+        store.add(f"acc/{epoch}/n", int(acc[2].item()))
+        store.add(f"epoch_end/{epoch}", 1)
+        if widx == 0:
+            alive = cl.num_workers - store.add("dead_workers", 0)
+            _wait_count(store, f"epoch_end/{epoch}", alive)
+            n = max(1, store.add(f"acc/{epoch}/n", 0))
+            logs = {"loss": store.add(f"acc/{epoch}/loss", 0) / 1e6 / n,
+                    "accuracy": store.add(f"acc/{epoch}/correct", 0) / n, "steps": store.add(f"done/{epoch}", 0)}
+            if cfg.validation_steps:
+                logs.update(_validate(cfg, eng, device))
+            history.append(logs)
+            print(f"Epoch {epoch + 1}/{cfg.epochs} - {logs['steps']}/{spe} steps - loss: {logs['loss']:.4f} - "
+                  f"accuracy: {logs['accuracy']:.4f}" + (f" - val_loss: {logs['val_loss']:.4f}"
+                                                          if 'val_loss' in logs else ""), flush=True)
+            store.set(f"epoch_go/{epoch}", "1")
+        else:
+            _wait_key(store, f"epoch_go/{epoch}")
+    worker.stop()
+    if widx == 0 and cfg.save:
+        from ..utils.checkpoint import save_keras_h5
+        path = os.path.join(cfg.save_dir, cfg.checkpoint_name())
+        save_keras_h5(path, eng, None, cfg)
+        print("Saving model to ", path, flush=True)
+    if result_q is not None:
+        result_q.put(("worker", rank, steps_done, history))
+    dist.destroy_process_group()
+
+
+def _wait_count(store, key, n, timeout=600):
+    t0 = time.time()
+    while store.add(key, 0) < n:
+        if time.time() - t0 > timeout:
+            raise TimeoutError(key)
+        time.sleep(0.05)
+
+
+def _wait_key(store, key, timeout=600):
+    t0 = time.time()
+    while not store.check([key]):
+        if time.time() - t0 > timeout:
+            raise TimeoutError(key)
+        time.sleep(0.05)
+
+
+def _validate(cfg, eng, device):
+    from ..data.datasets import Pipeline, make_source
+    src = make_source(cfg.data, "val", cfg)
+    pipe = Pipeline(src, cfg.val_batch_size or cfg.batch_size, repeat=True)
+    tot = torch.zeros(3, dtype=torch.float64)
+    it = pipe.iterate(device)
+    for _ in range(cfg.validation_steps):
+        im, lb = next(it)
+        s = eng.evaluate(im, lb)
+        tot[:2] += s.double().cpu()
+        tot[2] += im.shape[0]
+    return {"val_loss": float(tot[0] / tot[2]), "val_accuracy": float(tot[1] / tot[2])}
+
+
+def run_ps_job(cfg, num_ps: Optional[int] = None, num_workers: Optional[int] = None, return_results=False):
+    """Entry of imagenet-resnet50-ps.py.  Under torchrun (WORLD_SIZE = P + W) every process
+    takes its role from RANK; otherwise spawn the whole cluster locally (the reference's
+    create_in_process_cluster, imagenet-resnet50-ps.py:31-65)."""
+    ns = getattr(cfg, "_ns", None)
+    if ns is not None and (num_ps is None or num_workers is None):
+        num_ps, num_workers = parse_ps_counts(ns)
+    num_ps = num_ps or cfg.num_ps
+    num_workers = num_workers or cfg.num_workers
+    os.environ["GRPC_FAIL_FAST"] = "use_caller"   # reference parity flag (ps.py:69); failures surface via c10d
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        assert world == num_ps + num_workers, "WORLD_SIZE must equal --ps + --worker"
+        _ps_main(int(os.environ["RANK"]), world, num_ps, cfg, int(os.environ.get("MASTER_PORT", "29500")))
+        return 0
+    import torch.multiprocessing as mp
+    from .launch import pick_unused_port
+    world = num_ps + num_workers
+    port = pick_unused_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ps_main, args=(r, world, num_ps, cfg, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    deadline = time.time() + float(os.environ.get("PDDL_PS_JOB_TIMEOUT", "3600"))
+    alive = set(range(world))
+    while alive and time.time() < deadline:
+        for i, p in enumerate(procs):
+            if i in alive and not p.is_alive():
+                alive.discard(i)
+        while not q.empty():
+            results.append(q.get())
+        time.sleep(0.1)
+    for p in procs:
+        p.join(timeout=5)
+        if p.is_alive():
+            p.kill()
+    while not q.empty():
+        results.append(q.get())
+    ps_fail = [i for i in range(num_ps) if procs[i].exitcode not in (0, None)]
+    if ps_fail:
+        raise RuntimeError(f"parameter server(s) {ps_fail} failed")
+    return results if return_results else 0
+
+
+class ParameterServerStrategy:
+    """Marker so `make_strategy(cfg)` can name the PS strategy; training runs through
+    `run_ps_job` (roles are processes, not a single fit loop)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg

@@ -1,0 +1,468 @@
+"""Distribution strategies, one interface for the strategy-agnostic fit loop.
+
+| reference                                     | here                      | transport                       |
+|-----------------------------------------------|---------------------------|---------------------------------|
+| no strategy (imagenet-resnet50.py)            | SingleStrategy            | —                               |
+| MirroredStrategy (imagenet-resnet50-mirror.py:21)     | MirroredStrategy  | native RcclComm (ncclCommInitAll), one replica thread per GPU |
+| MultiWorkerMirroredStrategy (multiworkers.py:20-26)   | MultiWorkerStrategy | 1 GPU/process: c10d "nccl" (RCCL); R GPUs/process: native RcclComm over all P*R ranks |
+| Horovod (imagenet-resnet50-hvd.py:15-115)     | HorovodStrategy           | native FusionEngine over c10d (RCCL), buckets overlapped with backward |
+| ParameterServerStrategy (imagenet-resnet50-ps.py:75-84) | parallel/parameter_server.py | p2p push/pull |
+
+Interface: setup(trainer), train_pipeline()/val_pipeline() (= distribute
+dataset), train_step(images, labels), eval_step, reduce_metrics(t), set_lr, broadcast_state,
+is_chief, num_replicas_in_sync, save.  Gradient math: every replica scales its loss by
+1 / global_batch, so a SUM all-reduce yields the global-batch mean gradient (= Horovod's
+Average of per-rank means; = Mirrored's sum of per-replica grads of loss/global_batch).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..data.datasets import Pipeline, make_source
+from ..models.resnet50 import ParamLayout
+from ..train.optim import make_optimizer
+from .collectives import BucketAllReducer
+from .launch import ClusterInfo, export_torch_env, resolve_cluster
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available() and torch.cuda.device_count() > 0
+
+
+def build_engine(cfg, device: torch.device, cap: int):
+    """HIP engine (bf16 MFMA kernels) on a GPU; the fp32 PyTorch reference engine on CPU
+    (config 1 of BASELINE.json: CPU plumbing) or for the non-default fp32 / train-BN modes."""
+    L = ParamLayout(cfg.num_classes)
+    if device.type == "cuda" and cfg.precision == "bf16" and cfg.bn_mode == "frozen":
+        from ..models.engine import HipEngine
+        return HipEngine(L, cap, crop=cfg.crop, image_size=cfg.image_size, device=device,
+                         num_classes=cfg.num_classes)
+    from ..models.reference import TorchEngine
+    return TorchEngine(L, cap, crop=cfg.crop, device=device, bn_mode=cfg.bn_mode, num_classes=cfg.num_classes)
+
+
+class Augment:
+    """RandomFlip (per image) and RandomCrop offset (per batch, crop < input) draws."""
+
+    def __init__(self, cfg, device, seed):
+        self.cfg = cfg
+        self.device = device
+        self.gen = torch.Generator(device=device).manual_seed(seed)
+        self.rng = np.random.default_rng(seed)
+
+    def __call__(self, B):
+        flip = None
+        if self.cfg.flip:
+            flip = torch.randint(0, 2, (B,), dtype=torch.uint8, device=self.device, generator=self.gen)
+        off = (0, 0)
+        if self.cfg.crop < self.cfg.image_size:
+            m = self.cfg.image_size - self.cfg.crop
+            off = (int(self.rng.integers(0, m + 1)), int(self.rng.integers(0, m + 1)))
+        return flip, off
+
+
+class Strategy:
+    name = "base"
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.rank = 0
+        self.world = 1
+        self.local_replicas = 1
+        self.device = torch.device("cpu")
+        self.engine = None
+        self.opt = None
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def num_replicas_in_sync(self) -> int:
+        return self.world * self.local_replicas
+
+    @property
+    def is_chief(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def per_replica_batch(self) -> int:
+        return self.cfg.batch_size
+
+    @property
+    def global_batch(self) -> int:
+        return self.per_replica_batch * self.num_replicas_in_sync
+
+    @property
+    def metrics_device(self):
+        return self.device
+
+    def _pick_device(self, local_index: int = 0) -> torch.device:
+        want = self.cfg.device
+        if want == "cpu" or (want == "auto" and not gpu_available()):
+            return torch.device("cpu")
+        torch.cuda.set_device(local_index)
+        return torch.device("cuda", local_index)
+
+    # ------------------------------------------------------------------ setup
+    def setup(self, trainer):
+        self._build(trainer)
+        self._load_initial_weights()
+
+    def _make_engine_and_opt(self, device, cap):
+        eng = build_engine(self.cfg, device, cap)
+        eng.init(seed=self.cfg.seed)
+        opt = make_optimizer(self.cfg.optimizer, eng, lr=self.cfg.lr, momentum=self.cfg.momentum,
+                             nesterov=self.cfg.nesterov, weight_decay=self.cfg.weight_decay, beta1=self.cfg.beta1,
+                             beta2=self.cfg.beta2, eps=self.cfg.adam_eps)
+        return eng, opt
+
+    def _build(self, trainer):
+        raise NotImplementedError
+
+    def _load_initial_weights(self):
+        w = self.cfg.weights
+        if self.cfg.resume:
+            from ..utils.checkpoint import load_checkpoint
+            for eng, opt in self._replicas():
+                load_checkpoint(self.cfg.resume, eng, opt)
+                eng.after_update()
+        elif w and w != "none":
+            from ..utils.checkpoint import load_pretrained
+            for eng, _ in self._replicas():
+                load_pretrained(w, eng)
+                eng.after_update()
+
+    def _replicas(self):
+        return [(self.engine, self.opt)]
+
+    # ------------------------------------------------------------------ data
+    def _pipe(self, split: str, batch: int, shards: int, index: int) -> Pipeline:
+        cfg = self.cfg
+        src = make_source(cfg.data, split, cfg)
+        return Pipeline(src, batch, num_shards=shards, shard_index=index, shard_by=cfg.shard_by,
+                        repeat=cfg.strategy == "ps", seed=cfg.seed)
+
+    def train_pipeline(self) -> Pipeline:
+        return self._pipe("train", self.per_replica_batch * self.local_replicas, self.world, self.rank)
+
+    def val_pipeline(self) -> Pipeline:
+        vb = (self.cfg.val_batch_size or self.cfg.batch_size) * self.local_replicas
+        return self._pipe("val", vb, self.world, self.rank)
+
+    # ------------------------------------------------------------------ steps
+    def set_lr(self, lr: float):
+        for _, opt in self._replicas():
+            opt.lr = lr
+
+    def eval_step(self, images, labels):
+        return self.engine.evaluate(images, labels).clone()
+
+    def reduce_metrics(self, t: torch.Tensor) -> torch.Tensor:
+        return t.cpu()
+
+    def broadcast_state(self, trainer, root: int = 0):
+        pass
+
+    def sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def save(self, trainer, path: str, include_optimizer: bool = True):
+        if not self.is_chief:
+            return
+        from ..utils.checkpoint import save_keras_h5
+        save_keras_h5(path, self.engine, self.opt if include_optimizer else None, self.cfg)
+
+
+class SingleStrategy(Strategy):
+    """One process, one device (imagenet-resnet50.py)."""
+    name = "single"
+
+    def _build(self, trainer):
+        self.device = self._pick_device(0)
+        cap = max(self.cfg.batch_size, self.cfg.val_batch_size or 0)
+        self.engine, self.opt = self._make_engine_and_opt(self.device, cap)
+        self.aug = Augment(self.cfg, self.device, self.cfg.seed)
+
+    def train_step(self, images, labels):
+        B = images.shape[0]
+        flip, off = self.aug(B)
+        s = self.engine.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off).clone()
+        self.opt.step()
+        self.engine.after_update()
+        return s
+
+
+class _ProcessGroupMixin:
+    def _init_process_group(self, info: ClusterInfo):
+        export_torch_env(info)
+        self.rank, self.world = info.rank, info.world_size
+        self.info = info
+        if not dist.is_initialized():
+            backend = "nccl" if self.device.type == "cuda" else "gloo"
+            kw = {}
+            if self.device.type == "cuda":
+                kw["device_id"] = self.device
+            dist.init_process_group(backend, init_method="env://", rank=info.rank, world_size=info.world_size, **kw)
+
+    def reduce_metrics(self, t):
+        if self.world > 1:
+            x = t.to(self.device if self.device.type == "cuda" else "cpu", torch.float64)
+            dist.all_reduce(x)
+            return x.cpu()
+        return t.cpu()
+
+    def broadcast_state(self, trainer, root=0):
+        if self.world <= 1:
+            return
+        dist.broadcast(self.engine.params, root)
+        for t in self.opt.state_tensors().values():
+            dist.broadcast(t, root)
+        self.engine.after_update()
+
+
+class HorovodStrategy(_ProcessGroupMixin, Strategy):
+    """One process per GPU (horovodrun / mpirun / torchrun / srun), Horovod semantics:
+    shard-after-batch data (hvd.py:77-78), rank-0 broadcast, metric averaging, LR scaled by
+    size + warmup (callbacks), and gradient buckets all-reduced by the native fusion engine
+    while backward runs (DistributedOptimizer, hvd.py:101)."""
+    name = "horovod"
+
+    def __init__(self, cfg, comm: str = "fusion"):
+        super().__init__(cfg)
+        self.comm = os.environ.get("PDDL_COMM", comm)
+
+    def _build(self, trainer):
+        info = resolve_cluster(port_base=self.cfg.port_base)
+        self.device = self._pick_device(info.local_rank if gpu_available() else 0)
+        self._init_process_group(info)
+        cap = max(self.cfg.batch_size, self.cfg.val_batch_size or 0)
+        self.engine, self.opt = self._make_engine_and_opt(self.device, cap)
+        self.aug = Augment(self.cfg, self.device, self.cfg.seed + 1000 * self.rank)
+        self.buckets = self.engine.L.buckets(self.cfg.bucket_mb)
+        self.fusion = None
+        self.reducer = None
+        if self.world > 1:
+            if self.comm == "fusion":
+                from ..ops.native import native_available, require_native
+                if native_available():
+                    self.fusion = require_native().FusionEngine(
+                        dist.group.WORLD, self.engine.grads, [(s, e - s) for s, e in self.buckets],
+                        float(os.environ.get("PDDL_STALL_TIMEOUT", "60")), False, self.rank)
+                    if self.cfg.timeline:
+                        self.fusion.set_timeline(True)
+            if self.fusion is None:
+                self.reducer = BucketAllReducer(self.engine.grads, self.buckets, comm_dtype=self.cfg.grad_dtype)
+
+    def train_step(self, images, labels):
+        B = images.shape[0]
+        flip, off = self.aug(B)
+        gscale = 1.0 / (B * self.world)
+        cb = None
+        if self.fusion is not None:
+            self.fusion.begin_step()
+            cb = self.fusion.bucket_ready
+        elif self.reducer is not None:
+            self.reducer.begin()
+            cb = self.reducer.on_bucket_ready
+        s = self.engine.forward_backward(images, labels, gscale, flip=flip, crop_offset=off, bucket_cb=cb,
+                                         buckets=self.buckets).clone()
+        if self.fusion is not None:
+            self.fusion.finish()
+        elif self.reducer is not None:
+            self.reducer.finish()
+        self.opt.step()
+        self.engine.after_update()
+        return s
+
+    def write_timeline(self, path: str):
+        if self.fusion is not None:
+            with open(f"{path}.rank{self.rank}.json", "w") as f:
+                f.write(self.fusion.timeline_json())
+
+
+class MultiWorkerStrategy(HorovodStrategy):
+    """MultiWorkerMirroredStrategy (imagenet-resnet50-multiworkers.py): SLURM-resolved worker
+    processes (SlurmClusterResolver(port_base=12345)), element-wise DATA sharding, synchronous
+    all-reduce.  With several GPUs per worker process (PDDL_LOCAL_GPUS=R, e.g. 2 procs x 4
+    GPUs), each process runs R replica threads and ONE native RCCL communicator spans all
+    P*R replicas (unique id exchanged through the c10d store)."""
+    name = "multiworker"
+
+    def __init__(self, cfg, local_gpus: Optional[int] = None):
+        super().__init__(cfg, comm="bucket")
+        self.req_local = int(os.environ.get("PDDL_LOCAL_GPUS", local_gpus or 1))
+
+    def _build(self, trainer):
+        if self.req_local <= 1 or not gpu_available():
+            return super()._build(trainer)
+        info = resolve_cluster(port_base=self.cfg.port_base)
+        R = self.req_local
+        self.local_replicas = R
+        devs = [info.local_rank * R + i for i in range(R)]
+        self.device = self._pick_device(devs[0])
+        # control plane: gloo process group over the same rendezvous
+        export_torch_env(info)
+        self.rank, self.world = info.rank, info.world_size
+        if not dist.is_initialized():
+            dist.init_process_group("gloo", init_method="env://", rank=info.rank, world_size=info.world_size)
+        self.mirror = _LocalReplicas(self.cfg, devs, global_rank_base=self.rank * R, world_ranks=self.world * R)
+        self.engine, self.opt = self.mirror.replicas[0]
+
+    def _replicas(self):
+        return self.mirror.replicas if hasattr(self, "mirror") else super()._replicas()
+
+    def train_step(self, images, labels):
+        if not hasattr(self, "mirror"):
+            return super().train_step(images, labels)
+        return self.mirror.step(images, labels, self.global_batch)
+
+    def broadcast_state(self, trainer, root=0):
+        if hasattr(self, "mirror"):
+            self.mirror.broadcast()
+        else:
+            super().broadcast_state(trainer, root)
+
+
+class _LocalReplicas:
+    """R model replicas in this process, one per GPU, driven by replica threads; gradients are
+    summed with ONE grouped RCCL all-reduce across every replica of the job (in-process
+    ncclCommInitAll for Mirrored, ncclCommInitRank over P processes for multi-worker).  On CPU
+    the replicas run sequentially and the reduction is an in-process sum (test double)."""
+
+    def __init__(self, cfg, devices: List, global_rank_base: int = 0, world_ranks: Optional[int] = None):
+        self.cfg = cfg
+        self.devices = [torch.device(d) if not isinstance(d, int) else torch.device("cuda", d) for d in devices]
+        self.R = len(self.devices)
+        cap = max(cfg.batch_size, cfg.val_batch_size or 0)
+        self.replicas = []
+        self.augs = []
+        for i, d in enumerate(self.devices):
+            if d.type == "cuda":
+                torch.cuda.set_device(d)
+            eng = build_engine(cfg, d, cap)
+            eng.init(seed=cfg.seed)
+            opt = make_optimizer(cfg.optimizer, eng, lr=cfg.lr, momentum=cfg.momentum, nesterov=cfg.nesterov,
+                                 weight_decay=cfg.weight_decay, beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.adam_eps)
+            self.replicas.append((eng, opt))
+            self.augs.append(Augment(cfg, d, cfg.seed + 7919 * (global_rank_base + i)))
+        self.comm = None
+        self.gpu = self.devices[0].type == "cuda"
+        if self.gpu:
+            from ..ops.native import require_native
+            N = require_native()
+            world_ranks = world_ranks or self.R
+            if world_ranks == self.R:
+                self.comm = N.RcclComm.init_all([d.index for d in self.devices])
+            else:
+                uid = N.RcclComm.unique_id() if global_rank_base == 0 else b""
+                obj = [uid]
+                dist.broadcast_object_list(obj, src=0)
+                self.comm = N.RcclComm(world_ranks, obj[0], [global_rank_base + i for i in range(self.R)],
+                                       [d.index for d in self.devices])
+
+    def broadcast(self):
+        if self.comm is not None:
+            self.comm.broadcast([e.params for e, _ in self.replicas], 0)
+            for k in self.replicas[0][1].state_tensors():
+                self.comm.broadcast([o.state_tensors()[k] for _, o in self.replicas], 0)
+        else:
+            p0 = self.replicas[0][0].params
+            for e, o in self.replicas[1:]:
+                e.params.copy_(p0)
+                for k, t in o.state_tensors().items():
+                    t.copy_(self.replicas[0][1].state_tensors()[k])
+        for e, _ in self.replicas:
+            e.after_update()
+
+    def step(self, images, labels, global_batch: int):
+        R = self.R
+        B = images.shape[0] // R
+        stats = [None] * R
+
+        def run(i):
+            eng, _ = self.replicas[i]
+            d = self.devices[i]
+            if d.type == "cuda":
+                torch.cuda.set_device(d)
+            im = images[i * B:(i + 1) * B].to(d, non_blocking=True)
+            lb = labels[i * B:(i + 1) * B].to(d, non_blocking=True)
+            flip, off = self.augs[i](B)
+            stats[i] = eng.forward_backward(im, lb, 1.0 / global_batch, flip=flip, crop_offset=off).clone()
+
+        if self.gpu and R > 1:
+            th = [threading.Thread(target=run, args=(i,)) for i in range(R)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        else:
+            for i in range(R):
+                run(i)
+        grads = [e.grads for e, _ in self.replicas]
+        if self.comm is not None:
+            self.comm.all_reduce(grads, "sum")
+        elif R > 1:
+            tot = grads[0].clone()
+            for g in grads[1:]:
+                tot += g
+            for g in grads:
+                g.copy_(tot)
+        for e, o in self.replicas:
+            o.step()
+            e.after_update()
+        out = stats[0].to(self.devices[0])
+        for s in stats[1:]:
+            out = out + s.to(self.devices[0])
+        return out
+
+
+class MirroredStrategy(Strategy):
+    """tf.distribute.MirroredStrategy (imagenet-resnet50-mirror.py:21): one process drives
+    every local GPU; the global batch 32*R (mirror.py:54) is split into R replica batches."""
+    name = "mirrored"
+
+    def __init__(self, cfg, devices: Optional[List] = None):
+        super().__init__(cfg)
+        self._devices = devices
+
+    def _build(self, trainer):
+        if self._devices is not None:
+            devs = self._devices
+        elif self.cfg.device != "cpu" and gpu_available():
+            devs = list(range(torch.cuda.device_count()))
+        else:
+            devs = ["cpu"] * int(os.environ.get("PDDL_CPU_REPLICAS", "1"))
+        self.mirror = _LocalReplicas(self.cfg, devs)
+        self.local_replicas = self.mirror.R
+        self.engine, self.opt = self.mirror.replicas[0]
+        self.device = self.mirror.devices[0]
+
+    def _replicas(self):
+        return self.mirror.replicas
+
+    def train_step(self, images, labels):
+        return self.mirror.step(images, labels, self.global_batch)
+
+    def broadcast_state(self, trainer, root=0):
+        self.mirror.broadcast()
+
+
+def make_strategy(cfg) -> Strategy:
+    s = cfg.strategy
+    if s == "single":
+        return SingleStrategy(cfg)
+    if s == "horovod":
+        return HorovodStrategy(cfg)
+    if s == "multiworker":
+        return MultiWorkerStrategy(cfg)
+    if s == "mirrored":
+        return MirroredStrategy(cfg)
+    if s == "ps":
+        from .parameter_server import ParameterServerStrategy
+        return ParameterServerStrategy(cfg)
+    raise ValueError(f"unknown strategy {s!r}")

@@ -21,12 +21,15 @@ def build(verbose: bool = False) -> str:
     if r.returncode != 0:
         sys.stderr.write((r.stdout or "")[-4000:] + (r.stderr or "")[-4000:])
         raise RuntimeError("native build failed")
-    built = sorted(glob.glob(os.path.join(ROOT, "_pddl_native*.so")))
-    if not built:
-        raise RuntimeError("native build produced no shared object")
-    dst = os.path.join(PKG, os.path.basename(built[-1]))
-    shutil.move(built[-1], dst)
-    return dst
+    out = []
+    for name in ("_pddl_native", "_pddl_h5"):
+        built = sorted(glob.glob(os.path.join(ROOT, f"{name}*.so")))
+        if not built:
+            raise RuntimeError(f"native build produced no {name} shared object")
+        dst = os.path.join(PKG, os.path.basename(built[-1]))
+        shutil.move(built[-1], dst)
+        out.append(dst)
+    return out[0]
 
 
 if __name__ == "__main__":

@@ -1,0 +1,140 @@
+"""Parameter-server job (async, sharded, fault-injected), Keras-layout .h5 checkpoints and the
+drop-in entry scripts — all on CPU."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _cfg(preset, **kw):
+    from pddl.config import make_config
+    base = dict(device="cpu", data="synthetic", image_size=32, crop=32, flip=False, epochs=1, verbose=0, save=False,
+                train_images=64, val_images=8, seed=1)
+    base.update(kw)
+    return make_config(preset, **base)
+
+
+# ------------------------------------------------------------------ parameter server
+def test_ps_async_job_runs_and_applies_every_step():
+    from pddl.parallel.parameter_server import run_ps_job
+    cfg = _cfg("ps", steps_per_epoch=6, validation_steps=1, batch_size=2, epochs=2)
+    res = run_ps_job(cfg, num_ps=2, num_workers=2, return_results=True)
+    ps = [r for r in res if r[0] == "ps"]
+    wk = [r for r in res if r[0] == "worker"]
+    assert len(ps) == 2 and len(wk) == 2
+    assert sum(r[2] for r in wk) == 12                       # 2 epochs x 6 steps, split asynchronously
+    assert all(r[2] == 12 for r in ps)                       # every PS applied every push
+    hist = [r for r in wk if r[3]][0][3]
+    assert len(hist) == 2 and "val_loss" in hist[0]
+
+
+def test_ps_worker_failure_requeues_closure(monkeypatch):
+    from pddl.parallel.parameter_server import run_ps_job
+    monkeypatch.setenv("PDDL_FAULT", "kill_worker:1@1")
+    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
+    cfg = _cfg("ps", steps_per_epoch=6, batch_size=2, epochs=1)
+    res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
+    wk = [r for r in res if r[0] == "worker"]
+    ps = [r for r in res if r[0] == "ps"]
+    assert len(wk) == 1                                      # the killed worker reported nothing
+    assert ps[0][3] == [2]                                   # PS saw worker rank 2 die
+    assert ps[0][2] >= 6                                     # all 6 closures done despite the failure
+
+
+# ------------------------------------------------------------------ checkpoint
+def _engine():
+    from pddl.models.reference import TorchEngine
+    from pddl.models.resnet50 import ParamLayout
+    e = TorchEngine(ParamLayout(), 1, crop=32)
+    e.init(seed=3)
+    return e
+
+
+def test_keras_h5_roundtrip_and_layout(tmp_path):
+    from pddl.train.optim import Adam
+    from pddl.utils.checkpoint import h5, load_checkpoint, save_keras_h5
+    e = _engine()
+    opt = Adam(e, lr=1e-3)
+    e.grads.normal_()
+    opt.step()
+    path = str(tmp_path / "ImageNet-ResNet50_ImageNet-reuse.h5")
+    save_keras_h5(path, e, opt, _cfg("single"))
+    m = h5()
+    assert m.read_attr(path, "", "backend") == "tensorflow"
+    mc = json.loads(m.read_attr(path, "", "model_config"))
+    assert mc["config"]["layers"][4]["name"] == "resnet50"
+    assert len([l for l in mc["config"]["layers"][4]["config"]["layers"] if l["class_name"] == "Conv2D"]) == 53
+    assert m.read_attr(path, "model_weights", "layer_names") == ["input_1", "rescaling", "random_crop",
+                                                                  "random_flip", "resnet50", "dense"]
+    wn = m.read_attr(path, "model_weights/resnet50", "weight_names")
+    assert len(wn) == 53 * 2 + 53 * 4 and wn[0] == "conv1_conv/kernel:0"
+    k = m.read_dataset(path, "model_weights/resnet50/conv1_conv/kernel:0")
+    assert k.shape == (7, 7, 3, 64)                                       # Keras HWIO
+    assert m.read_dataset(path, "model_weights/dense/dense/kernel:0").shape == (2048, 1000)
+    on = m.read_attr(path, "optimizer_weights", "weight_names")
+    assert on[0] == "Adam/iter:0" and "Adam/conv1_conv/kernel/m:0" in on and len(on) == 1 + 2 * 214
+    # round trip
+    e2 = _engine()
+    e2.params.zero_()
+    opt2 = Adam(e2, lr=1e-3)
+    load_checkpoint(path, e2, opt2)
+    for ent in e.L.entries.values():      # (alignment padding between tensors is not saved)
+        sl = slice(ent.offset, ent.offset + ent.size)
+        assert torch.equal(e2.params[sl], e.params[sl]), ent.name
+        if ent.trainable:
+            assert torch.equal(opt2.m[sl], opt.m[sl]) and torch.equal(opt2.v[sl], opt.v[sl]), ent.name
+    assert opt2.iterations == 1
+    # h5dump sees the Keras group layout
+    r = subprocess.run(["/opt/conda/bin/h5dump", "-n", path], capture_output=True, text=True)
+    if r.returncode == 0:
+        assert "/model_weights/resnet50/conv5_block3_3_bn/moving_variance:0" in r.stdout
+
+
+def test_pretrained_weights_only_file(tmp_path):
+    """The Keras applications `_notop.h5` layout (root layer_names, <layer>/<layer>/kernel:0)."""
+    from pddl.utils.checkpoint import h5, load_pretrained
+    e = _engine()
+    L = e.L
+    rng = np.random.default_rng(0)
+    k = rng.standard_normal((7, 7, 3, 64)).astype(np.float32)
+    g = rng.standard_normal(64).astype(np.float32)
+    path = str(tmp_path / "notop.h5")
+    h5().write(path, [("conv1_conv/conv1_conv/kernel:0", k), ("conv1_bn/conv1_bn/gamma:0", g)],
+               [("", "layer_names", ["conv1_conv", "conv1_bn"]), ("conv1_conv", "weight_names",
+                                                                  ["conv1_conv/kernel:0"]),
+                ("conv1_bn", "weight_names", ["conv1_bn/gamma:0"])])
+    n = load_pretrained(path, e)
+    assert n == 2
+    w = L.view(e.params, "conv1_conv", "kernel")        # OHWI
+    assert np.allclose(w.permute(1, 2, 3, 0).numpy(), k)
+    assert np.allclose(L.view(e.params, "conv1_bn", "gamma").numpy(), g)
+
+
+# ------------------------------------------------------------------ entry scripts
+@pytest.mark.parametrize("script,extra", [
+    ("imagenet-resnet50.py", []),
+    ("imagenet-resnet50-mirror.py", []),
+])
+def test_entry_script_trains_and_saves(tmp_path, script, extra):
+    args = [sys.executable, os.path.join(ROOT, script), "--device", "cpu", "--epochs", "1", "--max-steps", "2",
+            "--batch-size", "2", "--crop", "32", "--image-size", "32", "--save-dir", str(tmp_path),
+            "--validation-steps", "1", "--verbose", "2"] + extra
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Epoch 1/1" in r.stdout and "val_loss" in r.stdout
+    assert any(f.endswith("-reuse.h5") for f in os.listdir(tmp_path)), os.listdir(tmp_path)
+
+
+def test_ps_script_cli(tmp_path):
+    args = [sys.executable, os.path.join(ROOT, "imagenet-resnet50-ps.py"), "--ps", "1", "--worker", "1",
+            "--device", "cpu", "--epochs", "1", "--steps-per-epoch", "2", "--validation-steps", "1",
+            "--batch-size", "2", "--crop", "32", "--image-size", "32", "--save-dir", str(tmp_path)]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "ImageNet-ResNet50_ImageNet_PS-reuse.h5" in os.listdir(tmp_path)

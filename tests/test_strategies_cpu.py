@@ -1,0 +1,96 @@
+"""Strategy equivalence on CPU (gloo, spawned processes; SURVEY.md §4 "strategy equivalence"):
+N-rank synchronous data parallelism with global batch B must produce the same weights after
+k steps as one process with batch B.  Exercises the native FusionEngine (C++ background
+thread over the c10d gloo group), bucketed all-reduce, sharding policies and Mirrored
+in-process replicas."""
+import os
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+STEPS = 2
+
+
+def _cfg(preset, **kw):
+    from pddl.config import make_config
+    base = dict(device="cpu", data="synthetic", image_size=32, crop=32, flip=False, epochs=1, max_steps=STEPS,
+                verbose=0, save=False, train_images=64, val_images=8, seed=5, lr=1e-2)
+    base.update(kw)
+    return make_config(preset, **base)
+
+
+def _train(preset, **kw):
+    from pddl.parallel.strategies import make_strategy
+    from pddl.train.trainer import Trainer
+    cfg = _cfg(preset, **kw)
+    st = make_strategy(cfg)
+    tr = Trainer(cfg, st)
+    hist = tr.fit(1, [], validation=False)
+    return st, hist
+
+
+def _rank_main(rank, world, port, preset, kw, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import pddl  # noqa
+    st, hist = _train(preset, **kw)
+    n = st.engine.L.n_trainable
+    q.put((rank, st.engine.params[:n].numpy().copy(), hist.history["loss"][0],
+           type(getattr(st, "fusion", None)).__name__))
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(world, preset, kw):
+    from pddl.parallel.launch import pick_unused_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = pick_unused_port()
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, preset, kw, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=600) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return [(r, torch.from_numpy(p), l, f) for r, p, l, f in sorted(out, key=lambda t: t[0])]
+
+
+@pytest.fixture(scope="module")
+def single_b4():
+    st, hist = _train("single", batch_size=4)
+    return st.engine.params[:st.engine.L.n_trainable].clone(), hist.history["loss"][0]
+
+
+def _close(a, b):
+    return ((a - b).norm() / b.norm()).item() < 1e-5
+
+
+def test_horovod_2_ranks_equals_single_global_batch(single_b4):
+    ref, ref_loss = single_b4
+    out = _spawn(2, "horovod", dict(batch_size=2, lr=1e-2, lr_scale_by_size=False, warmup_epochs=0,
+                                    shard_by="batch"))
+    assert out[0][3] == "FusionEngine"          # the native C++ fusion engine was used
+    for _, p, loss, _ in out:
+        assert _close(p, ref)
+    assert abs(out[0][2] - ref_loss) <= 1e-5 * abs(ref_loss)
+
+
+def test_multiworker_element_sharding_equals_single(single_b4):
+    ref, _ = single_b4
+    out = _spawn(2, "multiworker", dict(batch_size=2, val_batch_size=2))
+    for _, p, _, _ in out:
+        assert _close(p, ref)
+
+
+def test_mirrored_two_cpu_replicas_equals_single(single_b4, monkeypatch):
+    ref, _ = single_b4
+    monkeypatch.setenv("PDDL_CPU_REPLICAS", "2")
+    st, _ = _train("mirrored", batch_size=2)
+    assert st.num_replicas_in_sync == 2 and st.global_batch == 4
+    for eng, _ in st.mirror.replicas:
+        assert _close(eng.params[:eng.L.n_trainable], ref)
