@@ -20,6 +20,7 @@ for s in "$@"; do
     kernels) step kernels 600 python -m pytest tests/test_gpu_kernels.py -x -q ;;
     engine)  step engine 600 python -m pytest tests/test_gpu_engine.py -x -q ;;
     gputests) step gputests 900 python -m pytest tests -m gpu -x -q ;;
+    runtime) step runtime 600 python -m pytest tests/test_gpu_runtime.py -x -q ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench64) step bench64 600 python bench.py --steps 20 --warmup 5 --batch 64 ;;
