@@ -227,6 +227,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum);
   m.def("softmax_xent", &softmax_xent);
   m.def("colsum_reduce", &colsum_reduce);
+  m.def("set_variant", [](const std::string& which, int v) {
+    if (which == "igemm") pddl::g_igemm_variant = v;
+    else if (which == "igemm_deep") pddl::g_igemm_deep = v;
+    else if (which == "wgrad") pddl::g_wgrad_variant = v;
+    else TORCH_CHECK(false, "unknown kernel knob ", which);
+  });
   m.def("igemm_partial_rows", &pddl::igemm_partial_rows);
   m.def("maxpool_bwd_partial_rows", &pddl::maxpool_bwd_partial_rows);
   m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);

@@ -437,32 +437,72 @@ __global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __re
     }
     return;
   }
-  const long nf = (long)l.cout * l.kpad;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nf; e += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(e / l.kpad), k = (int)(e - (long)co * l.kpad);
-    const float w = k < RSC ? prm[l.w_off + (long)co * RSC + k] : 0.f;
-    wbf[l.wf_off + e] = f2bf(w);
-    if (l.wd_off >= 0 && k < RSC) {
-      float a, b;
-      fold(co, &a, &b);
-      const int rs = k / l.cin, c = k - rs * l.cin;
-      const int r = rs / l.S, s = rs - r * l.S;
-      const long d = (((long)c * l.R + (l.R - 1 - r)) * l.S + (l.S - 1 - s)) * l.cout_pad + co;
-      wbf[l.wd_off + d] = f2bf(a * w);
-    }
-    if (k == 0) {
-      float a, b;
-      fold(co, &a, &b);
-      scale[l.ch_off + co] = a;
-      shift[l.ch_off + co] = b;
-    }
+  // every non-stem layer has kpad == R*S*cin: the forward copy is a flat fp32 -> bf16 cast
+  const long nf = (long)l.cout * RSC;
+  const long n4 = nf / 4;
+  const float4* src = reinterpret_cast<const float4*>(prm + l.w_off);
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
+    const float4 w = src[e];
+    uint2 o;
+    o.x = pack2(w.x, w.y);
+    o.y = pack2(w.z, w.w);
+    *reinterpret_cast<uint2*>(wbf + l.wf_off + e * 4) = o;
+  }
+  for (int co = blockIdx.x * blockDim.x + threadIdx.x; co < l.cout; co += gridDim.x * blockDim.x) {
+    float a, b;
+    fold(co, &a, &b);
+    scale[l.ch_off + co] = a;
+    shift[l.ch_off + co] = b;
   }
 }
+
+// dgrad weights W'[c][R-1-r][S-1-s][co] = a[co] * W[co][r][s][c]: per (layer, tap) a batch of
+// [cout][cin] -> [cin][cout] transposes through a 64x64 LDS tile (coalesced both ways).
+__global__ void prep_dgrad_kernel(const float* __restrict__ prm, const PrepLayer* __restrict__ L,
+                                  uint16_t* __restrict__ wbf, float eps) {
+  __shared__ float tile[64][65];
+  const PrepLayer l = L[blockIdx.y];
+  if (l.wd_off < 0 || l.mode != 0) return;
+  const int taps = l.R * l.S;
+  const int tco = (l.cout + 63) / 64, tci = (l.cin + 63) / 64;
+  const int ntiles = taps * tco * tci;
+  const int RSC = taps * l.cin;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tap = t / (tco * tci), rem = t - tap * tco * tci;
+    const int co0 = (rem / tci) * 64, c0 = (rem % tci) * 64;
+    const int r = tap / l.S, s = tap - r * l.S;
+    // load: thread -> (row co = co0 + i, col c = c0 + j), 16 rows per pass
+    const int j = threadIdx.x & 63, i0 = threadIdx.x >> 6;
+    for (int i = i0; i < 64; i += 4) {
+      const int co = co0 + i, c = c0 + j;
+      tile[i][j] = (co < l.cout && c < l.cin) ? prm[l.w_off + (long)co * RSC + tap * l.cin + c] : 0.f;
+    }
+    __syncthreads();
+    // store: thread -> (row c = c0 + i, col co = co0 + j), scaled by the folded BN a[co]
+    const int co = co0 + j;
+    float a = 1.f;
+    if (co < l.cout && (l.gamma_off >= 0 || l.var_off >= 0)) {
+      const float g = l.gamma_off >= 0 ? prm[l.gamma_off + co] : 1.f;
+      const float var = l.var_off >= 0 ? prm[l.var_off + co] : 1.f - eps;
+      a = g * rsqrtf(var + eps);
+    }
+    for (int i = i0; i < 64; i += 4) {
+      const int c = c0 + i;
+      if (c < l.cin && co < l.cout) {
+        const long d = (((long)c * l.R + (l.R - 1 - r)) * l.S + (l.S - 1 - s)) * l.cout_pad + co;
+        wbf[l.wd_off + d] = f2bf(a * tile[j][i]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems, uint16_t* wbf,
                         float* scale, float* shift, float eps, hipStream_t s) {
-  int gx = (max_elems + 255) / 256;
-  if (gx > 256) gx = 256;
+  int gx = (max_elems / 4 + 255) / 256;
+  if (gx > 512) gx = 512;
   hipLaunchKernelGGL(prep_kernel, dim3(gx, nlayers), dim3(256), 0, s, params, layers_dev, wbf, scale, shift, eps);
+  hipLaunchKernelGGL(prep_dgrad_kernel, dim3(576, nlayers), dim3(256), 0, s, params, layers_dev, wbf, eps);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -106,14 +106,28 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   const int KT = p.K / 64;
-  load_tile(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   const int a_off = (wm * WTM + (lane & 15)) * 128;
   const int b_off = (wn * WTN + (lane & 15)) * 128;
+  load_tile(0, 0);
+  if (NSTAGE == 3 && KT > 1) load_tile(1, 1);
+  if (NSTAGE != 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   for (int t = 0; t < KT; ++t) {
-    const int cur = NSTAGE == 2 ? (t & 1) : 0;
-    if (NSTAGE == 2 && t + 1 < KT) load_tile(t + 1, cur ^ 1);
+    int cur;
+    if (NSTAGE == 3) {
+      // 3-deep ring: tile t landed (tile t+1 may stay in flight across the barrier), every
+      // wave finished reading tile t-1, so its buffer can take tile t+2.  Raw s_barrier: a
+      // __syncthreads() here would drain the LDS-DMA queue (vmcnt(0)).
+      if (t + 1 < KT) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(AI + BI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      cur = t % 3;
+      if (t + 2 < KT) load_tile(t + 2, (t + 2) % 3);
+    } else {
+      cur = NSTAGE == 2 ? (t & 1) : 0;
+      if (NSTAGE == 2 && t + 1 < KT) load_tile(t + 1, cur ^ 1);
+    }
     const char* As = smem + cur * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -134,9 +148,12 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
       __syncthreads();            // every wave is done reading the single buffer
       load_tile(t + 1, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (NSTAGE != 3) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
+  if (NSTAGE == 3) __syncthreads();   // all LDS reads done before the epilogue reuses LDS
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
@@ -260,6 +277,9 @@ int igemm_partial_rows(int M, int Nn) {
   return ((M + BM - 1) / BM) * (BM / 64);
 }
 
+int g_igemm_variant = 0;   // 0 = heuristic; 1, 2, 3 = forced pipeline depth
+int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256
+
 static bool igemm_check(const IgemmParams& p, const char** why) {
   if (p.K % 64 || p.K1 % 64) { *why = "K must be a multiple of 64"; return false; }
   // A k-tile (64 elements) must be contiguous in memory: C % 64 == 0, or the "window" form
@@ -277,16 +297,20 @@ const char* igemm_launch(const IgemmParams& p, hipStream_t stream) {
   const char* why = nullptr;
   if (!igemm_check(p, &why)) return why;
   // short K (<= 2 k-tiles) is memory-bound: single LDS stage for twice the resident blocks
-  const bool one = p.K <= 128;
-  if (p.Nn <= 64) {
-    const int nwg = ((p.M + 255) / 256) * ((p.Nn + 63) / 64);
-    if (one) hipLaunchKernelGGL((igemm_kernel<256, 64, 64, 64, 1>), dim3(nwg), dim3(256), 0, stream, p);
-    else hipLaunchKernelGGL((igemm_kernel<256, 64, 64, 64, 2>), dim3(nwg), dim3(256), 0, stream, p);
-  } else {
-    const int nwg = ((p.M + 127) / 128) * ((p.Nn + 127) / 128);
-    if (one) hipLaunchKernelGGL((igemm_kernel<128, 128, 64, 64, 1>), dim3(nwg), dim3(256), 0, stream, p);
-    else hipLaunchKernelGGL((igemm_kernel<128, 128, 64, 64, 2>), dim3(nwg), dim3(256), 0, stream, p);
+  // Pipeline depth by K (variant knob for A/B timing: 0 = heuristic, 1/2/3 = forced stages)
+  const int KT = p.K / 64;
+  int ns = g_igemm_variant;
+  if (ns == 0) ns = KT <= 2 ? 1 : (KT >= 4 ? g_igemm_deep : 2);
+  if (ns == 3 && KT < 3) ns = 2;
+#define IG_LAUNCH(BM_, BN_)                                                                                 \
+  {                                                                                                        \
+    const int nwg = ((p.M + BM_ - 1) / BM_) * ((p.Nn + BN_ - 1) / BN_);                                     \
+    if (ns == 1) hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, 1>), dim3(nwg), dim3(256), 0, stream, p); \
+    else if (ns == 2) hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, 2>), dim3(nwg), dim3(256), 0, stream, p); \
+    else hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, 3>), dim3(nwg), dim3(256), 0, stream, p);      \
   }
+  if (p.Nn <= 64) IG_LAUNCH(256, 64) else IG_LAUNCH(128, 128)
+#undef IG_LAUNCH
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -31,7 +31,7 @@ __device__ __forceinline__ int tr_swz128(int row) { return (((row >> 1) & 1) | (
 
 // BM = 128: 2x2 waves, wave tile 64 (co) x 64 (k).  BM = 64 (Cout = 64 layers: the stem and
 // stage 2): 1x4 waves, wave tile 64 x 32, gradient tile with 128-byte rows.
-template <bool FAST, int BM>
+template <bool FAST, int BM, int NSTAGE>
 __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split) {
   constexpr int G_BYTES = 64 * BM * 2;        // 64 m-rows x BM bf16
   constexpr int X_BYTES = 64 * 256;           // 64 m-rows x 128 bf16
@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   constexpr int TN = WTN / 16;
   constexpr int EPI_LD = WTN + 4;
   constexpr int GI = G_BYTES / 4096;          // 1 KiB G pieces per wave
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -123,12 +123,25 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   const int nit = (mend - mbeg + 63) / 64;
   if (nit > 0) {
     load_tile(mbeg, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (NSTAGE == 3 && nit > 1) load_tile(mbeg + 64, 1);
+    if (NSTAGE == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
   for (int it = 0; it < nit; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
+    int cur;
+    if (NSTAGE == 3) {
+      // 3-deep LDS ring, counted vmcnt keeps the next tile's LDS-DMA in flight across the
+      // raw barrier (cdna_hip_programming.md §5 "Pipelining across barriers")
+      if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(GI + 4) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      cur = it % 3;
+      if (it + 2 < nit) load_tile(mbeg + (it + 2) * 64, (it + 2) % 3);
+    } else {
+      cur = it & 1;
+      if (it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
+    }
     const char* gb = smem + cur * STAGE;
     const char* xb = gb + G_BYTES;
 #pragma unroll
@@ -167,10 +180,13 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (NSTAGE == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
   if (nit == 0) return;
+  if (NSTAGE == 3) __syncthreads();
 
   // Epilogue: per-wave 32 x WTN fp32 staging, then row-contiguous atomics (256 B per wave
   // instruction: one 64-float row, or two 32-float rows for WTN = 32).
@@ -198,6 +214,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
     __syncthreads();
   }
 }
+
+int g_wgrad_variant = 0;   // 0 = default (3-stage), 2 / 3 = forced pipeline depth
 
 const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   WgradParams p = pin;
@@ -228,13 +246,18 @@ const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   mps = (mps + 63) / 64 * 64;
   splits = (p.M + mps - 1) / mps;
   const int nwg = ntiles * splits;
-  if (BM == 64) {
-    if (fast) hipLaunchKernelGGL((wgrad_kernel<true, 64>), dim3(nwg), dim3(256), 0, stream, p, mps);
-    else hipLaunchKernelGGL((wgrad_kernel<false, 64>), dim3(nwg), dim3(256), 0, stream, p, mps);
-  } else {
-    if (fast) hipLaunchKernelGGL((wgrad_kernel<true, 128>), dim3(nwg), dim3(256), 0, stream, p, mps);
-    else hipLaunchKernelGGL((wgrad_kernel<false, 128>), dim3(nwg), dim3(256), 0, stream, p, mps);
+  const int ns = g_wgrad_variant == 0 ? 3 : g_wgrad_variant;
+#define WG_LAUNCH(F_, BM_)                                                                                   \
+  {                                                                                                         \
+    if (ns == 3) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 3>), dim3(nwg), dim3(256), 0, stream, p, mps);     \
+    else hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 2>), dim3(nwg), dim3(256), 0, stream, p, mps);            \
   }
+  if (BM == 64) {
+    if (fast) WG_LAUNCH(true, 64) else WG_LAUNCH(false, 64)
+  } else {
+    if (fast) WG_LAUNCH(true, 128) else WG_LAUNCH(false, 128)
+  }
+#undef WG_LAUNCH
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -373,7 +373,9 @@ class HipEngine:
             H, Ho = self.geo[b.name]
             f, cin = b.filters, b.cin
             x_in = self.acts[blocks[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
-            mask_in = x_in if bi > 0 else None
+            # conv2_block1's input is the max-pool output y: the stem's ReLU mask at every argmax
+            # position equals (y > 0), so it is applied here instead of re-reading conv1's output
+            mask_in = x_in
             cs_in = part(blocks[bi - 1].convs["3"].name) if bi > 0 else None
             y1, y2 = a["y1"][:B], a["y2"][:B]
             gout = self.gbuf[cur][: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
@@ -410,7 +412,7 @@ class HipEngine:
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
         gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
         s = L.stem
-        N.maxpool_bwd(gpool, self.pidx[:B], self.c1[:B], gc1, part(s.name))
+        N.maxpool_bwd(gpool, self.pidx[:B], None, gc1, part(s.name))
         N.wgrad(self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
         N.stem_wgrad_fold(self.stem_dw2, self._gview(s.name, 64, 147), 64)
         N.wgrad_finalize(self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)

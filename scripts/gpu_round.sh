@@ -24,6 +24,7 @@ for s in "$@"; do
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench64) step bench64 600 python bench.py --steps 20 --warmup 5 --batch 64 ;;
+    kbench)  step kbench 600 python bench/kernels.py --json gpurun_out/kbench.json ;;
     prof)    step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 ;;
   esac
 done
