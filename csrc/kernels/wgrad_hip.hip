@@ -247,7 +247,7 @@ const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   mps = (mps + 63) / 64 * 64;
   splits = (p.M + mps - 1) / mps;
   const int nwg = ntiles * splits;
-  const int ns = g_wgrad_variant == 0 ? 3 : g_wgrad_variant;
+  const int ns = g_wgrad_variant == 0 ? 2 : g_wgrad_variant;   // 2 stages + 2 blocks/CU beat 3 stages + 1 block (measured)
 #define WG_LAUNCH(F_, BM_)                                                                                   \
   {                                                                                                         \
     if (ns == 3) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 3>), dim3(nwg), dim3(256), 0, stream, p, mps);     \
