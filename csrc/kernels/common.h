@@ -46,6 +46,11 @@ static __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
 __host__ __device__ __forceinline__ long lmin(long a, long b) { return a < b ? a : b; }
 
+// Division by a runtime divisor d as one 64-bit multiply + shift: exact for
+// 0 <= x < 2^40 / d (every row index of the ResNet-50 GEMMs: x < 2^26, d < 2^14).
+__host__ __device__ __forceinline__ uint64_t fdiv_magic(int d) { return ((1ull << 40) + d - 1) / (uint64_t)d; }
+__device__ __forceinline__ int fdiv(int x, uint64_t magic) { return (int)(((uint64_t)(uint32_t)x * magic) >> 40); }
+
 // Bijective XCD-aware remap of the linear workgroup id (cdna_hip_programming
 // §5 "XCD swizzle must be bijective"): consecutive logical tiles land on the
 // same XCD so blocks sharing an operand panel share that XCD's L2.

@@ -55,19 +55,23 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   // logical 16-byte chunk (lane & 7) ^ (row & 7).
   const int chunk_sw = (lane & 7) ^ ((lane >> 3) & 7);
 
-  // A-row bookkeeping (fixed over the k loop).
-  int a_pix[AI], a_hi[AI], a_wi[AI];
+  // A-row bookkeeping (fixed over the k loop): the element offset of the row's tap (0, 0)
+  // in each source; a k-tile then only adds a wave-uniform (r*W + s)*C + c0.
+  int a_hi[AI], a_wi[AI], a_o1[AI], a_o2[AI];
+  const bool no_halo = p.R == 1 && p.S == 1 && p.pad == 0;   // 1x1: only the row itself can be invalid
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int m = m0 + (wave * AI + i) * 8 + (lane >> 3);
     if (m < p.M) {
       const int n = m / HoWo, rem = m - n * HoWo;
       const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
-      a_pix[i] = n * p.H * p.W;
       a_hi[i] = ho * p.stride - p.pad;
       a_wi[i] = wo * p.stride - p.pad;
+      const int pix = (n * p.H + a_hi[i]) * p.W + a_wi[i];
+      a_o1[i] = pix * p.C1 + chunk_sw * 8;
+      a_o2[i] = pix * p.C2 + chunk_sw * 8;
     } else {
-      a_pix[i] = 0; a_hi[i] = -(1 << 28); a_wi[i] = 0;
+      a_hi[i] = -(1 << 28); a_wi[i] = 0; a_o1[i] = 0; a_o2[i] = 0;
     }
   }
   const bf16_t* b_row[BI];
@@ -80,16 +84,18 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   auto load_tile = [&](int t, int buf) {
     const int kk0 = t * 64;
     const bf16_t* src; int C, kr;
-    if (kk0 < p.K1) { src = p.a1; C = p.C1; kr = kk0; }
+    const bool first = kk0 < p.K1;
+    if (first) { src = p.a1; C = p.C1; kr = kk0; }
     else { src = p.a2; C = p.C2; kr = kk0 - p.K1; }
     const int rs = kr / C, c0 = kr - rs * C;
     const int r = rs / p.S, s = rs - r * p.S;
+    const int delta = (r * p.W + s) * C + c0;
     char* abase = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const int hi = a_hi[i] + r, wi = a_wi[i] + s;
-      const bool ok = ((unsigned)hi < (unsigned)p.H) && ((unsigned)wi < (unsigned)p.W);
-      const bf16_t* g = ok ? src + ((a_pix[i] + hi * p.W + wi) * C + c0 + chunk_sw * 8) : zero;
+      const bool ok = no_halo ? a_hi[i] >= 0
+                              : ((unsigned)(a_hi[i] + r) < (unsigned)p.H) && ((unsigned)(a_wi[i] + s) < (unsigned)p.W);
+      const bf16_t* g = ok ? src + ((first ? a_o1[i] : a_o2[i]) + delta) : zero;
       __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(abase + (wave * AI + i) * 1024), 16, 0, 0);
     }
     char* bbase = abase + A_BYTES;

@@ -55,6 +55,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   const int mend = min(p.M, mbeg + m_per_split);
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
   const int HoWo = p.Ho * p.Wo;
+  // multiply-shift division constants (the row decode runs for every row of every tile)
+  const uint64_t mg_hw = fdiv_magic(HoWo), mg_w = fdiv_magic(p.Wo);
 
   // (r, s, c0) of the two 64-column halves of this k tile (generic path only).
   int hr[2], hs[2], hc[2]; bool hv[2];
@@ -101,8 +103,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
         const int r = h ? hr[1] : hr[0], s = h ? hs[1] : hs[0], c = h ? hc[1] : hc[0];
         const bool v = h ? hv[1] : hv[0];
         if (mok && v) {
-          const int n = m / HoWo, rem = m - n * HoWo;
-          const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+          const int n = fdiv(m, mg_hw), rem = m - n * HoWo;
+          const int ho = fdiv(rem, mg_w), wo = rem - ho * p.Wo;
           const int hi = ho * p.stride - p.pad + r, wi = wo * p.stride - p.pad + s;
           if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
             xs = p.x + ((long)((n * p.H + hi) * p.W + wi) * p.C + c + (chunk & 7) * 8);
