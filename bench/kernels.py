@@ -60,7 +60,21 @@ def main():
 
         def wg():
             N.wgrad(x, H, H, R, R, st, pad, Ho, Ho, g, None, 0, dw, R * R * C, 0)
-        for kind, fn, knob, variants in (("igemm", fwd, "igemm", [2, 3]), ("wgrad", wg, "wgrad", [2, 3])):
+        # MIOpen (PyTorch conv, bf16 channels_last) on the same shapes: a same-device yardstick
+        xt = x.permute(0, 3, 1, 2)
+        wt = w.view(Co, R, R, C).permute(0, 3, 1, 2)
+        gt = g.permute(0, 3, 1, 2)
+
+        def mi_fwd():
+            torch.nn.functional.conv2d(xt, wt, stride=st, padding=pad)
+
+        def mi_wg():
+            torch.ops.aten.convolution_backward(gt, xt, wt, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                [False, True, False])
+        mrow = {"layer": name, "kernel": "miopen", "fwd_us": round(timeit(mi_fwd), 1), "wgrad_us": round(timeit(mi_wg), 1)}
+        print(json.dumps(mrow), flush=True)
+        res.append(mrow)
+        for kind, fn, knob, variants in (("igemm", fwd, "igemm", [2]), ("wgrad", wg, "wgrad", [2])):
             t = {v: [] for v in variants}
             for _ in range(a.rounds):
                 for v in variants:

@@ -16,8 +16,11 @@ def build(verbose: bool = False) -> str:
     env = dict(os.environ)
     env.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
     env.setdefault("MAX_JOBS", "8")
-    cmd = [sys.executable, "setup.py", "build_ext", "--inplace"]
+    # object files stay outside the tree so GPU-box snapshots only carry the .so files
+    cmd = [sys.executable, "setup.py", "build_ext", "--inplace", "--build-temp",
+           os.path.join(os.environ.get("TMPDIR", "/tmp"), "pddl_build_temp")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=not verbose, text=True)
+    shutil.rmtree(os.path.join(ROOT, "build"), ignore_errors=True)
     if r.returncode != 0:
         sys.stderr.write((r.stdout or "")[-4000:] + (r.stderr or "")[-4000:])
         raise RuntimeError("native build failed")
