@@ -56,7 +56,7 @@ def main():
 
         def fwd():
             N.igemm(x, None, H, H, R, R, st, pad, Ho, Ho, w, 0, sc, sh, None, None, None, y, 1, None, 0, 0, 0, 0, 0,
-                    None)
+                    None, None)
 
         def wg():
             N.wgrad(x, H, H, R, R, st, pad, Ho, Ho, g, None, 0, dw, R * R * C, 0)
@@ -74,6 +74,18 @@ def main():
         mrow = {"layer": name, "kernel": "miopen", "fwd_us": round(timeit(mi_fwd), 1), "wgrad_us": round(timeit(mi_wg), 1)}
         print(json.dumps(mrow), flush=True)
         res.append(mrow)
+        # hipBLASLt on the same-FLOP plain GEMMs (im2col'd A already in memory, no epilogue):
+        # the library ceiling for these M / N / K
+        M, K = B * Ho * Ho, R * R * C
+        am = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        bm = (torch.randn(K, Co, device=dev) * 0.05).to(torch.bfloat16)
+        gm = torch.randn(M, Co, device=dev).to(torch.bfloat16)
+        f_us, w_us = timeit(lambda: torch.mm(am, bm)), timeit(lambda: torch.mm(gm.t(), am))
+        brow = {"layer": name, "kernel": "hipblaslt", "fwd_us": round(f_us, 1), "fwd_tflops": round(flops / f_us / 1e6, 1),
+                "wgrad_us": round(w_us, 1), "wgrad_tflops": round(flops / w_us / 1e6, 1)}
+        print(json.dumps(brow), flush=True)
+        res.append(brow)
+        del am, bm, gm
         for kind, fn, knob, variants in (("igemm", fwd, "igemm", [2]), ("wgrad", wg, "wgrad", [2])):
             t = {v: [] for v in variants}
             for _ in range(a.rounds):

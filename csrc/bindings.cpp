@@ -42,7 +42,7 @@ int old(const OptT& t) { return t.has_value() ? ld(*t) : 0; }
 void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
            int64_t Ho, int64_t Wo, Tensor b, int64_t mode, OptT scale, OptT shift, OptT res, OptT mask, OptT add,
            Tensor out, int64_t relu, OptT out2, int64_t relu2, int64_t n_split, int64_t up2, int64_t Hf,
-           int64_t Wf, OptT colsum) {
+           int64_t Wf, OptT colsum, OptT bits_out) {
   pddl::IgemmParams p{};
   PCHECK(a1.is_contiguous(), "A source must be contiguous NHWC");
   p.a1 = bfp(a1);
@@ -70,7 +70,20 @@ void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64
   }
   p.scale = of32p(scale); p.shift = of32p(shift);
   p.res = obfp(res); p.ld_res = old(res);
-  p.mask = obfp(mask); p.ld_mask = old(mask);
+  if (mask.has_value() && mask->scalar_type() == torch::kUInt8) {
+    // bitmask [rows][Nn/8]: bit e of byte c/8 is (x[row][c] > 0)
+    PCHECK(mode == pddl::EPI_DGRAD && mask->is_cuda() && mask->size(-1) * 8 >= p.Nn, "bitmask mask shape");
+    p.bits_mask = mask->data_ptr<uint8_t>(); p.ld_bits_mask = ld(*mask);
+  } else {
+    p.mask = obfp(mask); p.ld_mask = old(mask);
+  }
+  if (bits_out.has_value()) {
+    PCHECK(mode == pddl::EPI_FWD && bits_out->scalar_type() == torch::kUInt8 && bits_out->is_cuda(),
+           "bits_out must be a uint8 tensor of a forward epilogue");
+    const int64_t seg0 = out2.has_value() ? n_split : p.Nn;
+    PCHECK(bits_out->size(-1) * 8 >= seg0 && bits_out->numel() / bits_out->size(-1) >= p.M, "bits_out too small");
+    p.bits_out = bits_out->data_ptr<uint8_t>(); p.ld_bits_out = ld(*bits_out);
+  }
   p.add = obfp(add); p.ld_add = old(add);
   if (mode == pddl::EPI_F32) p.out = f32p(out); else p.out = bfpm(out);
   p.ldo = ld(out);
@@ -128,10 +141,14 @@ void stem_wgrad_fold(Tensor g2, Tensor dw, int64_t cout) {
   PCHECK(g2.numel() >= cout * 256 && dw.numel() >= cout * 147, "stem fold sizes");
   ok(pddl::stem_wgrad_fold_launch(f32p(g2), f32p(dw), (int)cout, cur_stream()), "stem_wgrad_fold");
 }
-void maxpool_fwd(Tensor x, Tensor y, Tensor idx) {
+void maxpool_fwd(Tensor x, Tensor y, Tensor idx, OptT bits) {
   PCHECK(x.is_contiguous() && y.is_contiguous() && idx.is_contiguous() && idx.scalar_type() == torch::kUInt8,
          "maxpool layouts");
-  ok(pddl::maxpool_fwd_launch(bfp(x), bfpm(y), idx.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1),
+  if (bits.has_value())
+    PCHECK(bits->scalar_type() == torch::kUInt8 && bits->is_contiguous() && bits->numel() * 8 >= y.numel(),
+           "maxpool bits [B,Ho,Wo,C/8] uint8");
+  ok(pddl::maxpool_fwd_launch(bfp(x), bfpm(y), idx.data_ptr<uint8_t>(),
+                              bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr, (int)x.size(0), (int)x.size(1),
                               (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), cur_stream()),
      "maxpool_fwd");
 }

@@ -38,6 +38,20 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// ReLU bitmask of 8 packed bf16 values: bit e = (value e > 0), i.e. nonzero with a clear
+// sign bit.  Derived from the stored (rounded) values so it matches a bf16 mask exactly.
+__device__ __forceinline__ uint32_t pos_bits8(const uint4& u) {
+  const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+  uint32_t byte = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t lo = w4[e] & 0xffffu, hi = w4[e] >> 16;
+    byte |= (uint32_t)(lo != 0 && !(lo & 0x8000u)) << (2 * e);
+    byte |= (uint32_t)(hi != 0 && !(hi & 0x8000u)) << (2 * e + 1);
+  }
+  return byte;
+}
+
 // 64 bytes of zeros: the source of every out-of-bounds LDS-DMA lane (padding
 // rows of the implicit-GEMM gather, tile overhang).  LDS-DMA cannot write a
 // literal, so invalid lanes read from here instead.  One copy per translation

@@ -96,7 +96,7 @@ static int grid_for(long n) { return (int)lmin((n + 255) / 256, 8192); }
 // Window of output (ho, wo) covers input rows 2ho-1 .. 2ho+1 (ZeroPadding2D(1) then 3x3/s2
 // valid).  Padded taps are real zeros (as in Keras); the first maximum in scan order wins.
 __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
-                                   int B, int H, int W, int C, int Ho, int Wo) {
+                                   uint8_t* __restrict__ bits, int B, int H, int W, int C, int Ho, int Wo) {
   const int cg = C / 8;
   const long total = (long)B * Ho * Wo * cg;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
@@ -125,7 +125,9 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
           if (v[e] > best[e]) { best[e] = v[e]; bi[e] = (uint8_t)(r * 3 + s); }
       }
     const long o = pix * C + g * 8;
-    *reinterpret_cast<uint4*>(y + o) = pack8(best);
+    const uint4 yv = pack8(best);
+    *reinterpret_cast<uint4*>(y + o) = yv;
+    if (bits) bits[o >> 3] = (uint8_t)pos_bits8(yv);
     uint2 pk;
     pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
     pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
@@ -197,11 +199,11 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t*
 }
 int maxpool_bwd_partial_rows(int B, int H, int W, int C) { return grid_for((long)B * H * W * C / 8) * 4; }
 
-const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, int B, int H, int W, int C, int Ho,
+const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, uint8_t* bits, int B, int H, int W, int C, int Ho,
                                int Wo, hipStream_t s) {
   if (C % 8) return "maxpool: C % 8";
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)B * Ho * Wo * C / 8)), dim3(256), 0, s, x, y, idx, B,
-                     H, W, C, Ho, Wo);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)B * Ho * Wo * C / 8)), dim3(256), 0, s, x, y, idx, bits,
+                     B, H, W, C, Ho, Wo);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

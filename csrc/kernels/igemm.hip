@@ -172,6 +172,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   bool relu = p.relu != 0;
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
   int ldo = p.ldo, col = gn;
+  bool seg0 = true;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (p.mode != EPI_DGRAD && col_ok) {
     const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
@@ -181,6 +182,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
     sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
     if (p.out2 && gn >= p.n_split) {
       out = reinterpret_cast<bf16_t*>(p.out2); ldo = p.ldo2; relu = p.relu2 != 0; col = gn - p.n_split;
+      seg0 = false;
     }
   }
 #pragma unroll
@@ -214,7 +216,11 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
           }
-          *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pack8(v);
+          const uint4 pk = pack8(v);
+          *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pk;
+          if (p.bits_out && seg0) {
+            p.bits_out[(long)gm * p.ld_bits_out + (col >> 3)] = (uint8_t)pos_bits8(pk);
+          }
         } else if (p.mode == EPI_F32) {
           float* o = reinterpret_cast<float*>(p.out) + (long)gm * p.ldo + gn;
 #pragma unroll
@@ -251,6 +257,10 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
               unpack8(*reinterpret_cast<const uint4*>(p.mask + rq * p.ld_mask + gn), mv);
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
+            } else if (p.bits_mask) {
+              const uint32_t byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) csum[e] += w[e];

@@ -29,6 +29,9 @@ struct IgemmParams {
   void* out2; int ldo2; int relu2; int n_split;     // FWD: columns >= n_split -> out2
   int up2; int Hf, Wf;                              // DGRAD: scatter to a 2x finer grid
   float* colsum;                                    // DGRAD: per-wave partial column sums [rows][Nn]
+  // ReLU masks as bitmasks (bit e of byte [row][c/8] = value[row][8*(c/8)+e] > 0):
+  uint8_t* bits_out; int ld_bits_out;               // FWD: write the mask of the (segment-0) output
+  const uint8_t* bits_mask; int ld_bits_mask;       // DGRAD: multiply by the bit instead of (mask > 0)
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
 int igemm_partial_rows(int M, int Nn);               // rows of the partial column-sum buffer
@@ -64,7 +67,7 @@ const char* stem_s2d_launch(const StemParams& p, hipStream_t s);
 // Fold the s2d-domain stem weight gradient [64][256] back to [64][7][7][3] (added into dw).
 const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStream_t s);
 
-const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, int B, int H, int W, int C,
+const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, uint8_t* bits, int B, int H, int W, int C,
                                int Ho, int Wo, hipStream_t s);
 const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uint16_t* xmask, uint16_t* gx,
                                int B, int H, int W, int C, int Ho, int Wo, float* colsum, hipStream_t s);

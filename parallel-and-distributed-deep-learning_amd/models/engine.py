@@ -21,6 +21,7 @@ for the fp32 oracle and tests/test_gpu_engine.py for the parity checks).
 """
 from __future__ import annotations
 
+import os
 import struct
 from typing import Callable, Dict, List, Optional
 
@@ -42,7 +43,7 @@ def _ceil(a, b):
 
 class HipEngine:
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
-                 device="cuda", bn_mode: str = "frozen", num_classes: int = 1000):
+                 device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
         if bn_mode != "frozen":
             raise NotImplementedError("HipEngine: bn_mode='train' runs on the TorchEngine path for now")
         self.N = require_native()
@@ -53,6 +54,9 @@ class HipEngine:
         self.image_size = image_size
         self.num_classes = num_classes
         self.ncls_pad = _ceil(num_classes, 64)
+        if bitmask is None:
+            bitmask = os.environ.get("PDDL_BITMASK", "1") != "0"
+        self.bitmask = bool(bitmask)
         assert struct.calcsize(_PREP_FMT) == self.N.PREP_LAYER_BYTES
         assert struct.calcsize(_FIN_FMT) == self.N.FIN_LAYER_BYTES
         assert struct.calcsize(_BNG_FMT) == self.N.BNGRAD_LAYER_BYTES
@@ -182,6 +186,11 @@ class HipEngine:
         self.c1 = torch.empty(B, H1, H1, 64, **bf)
         self.pool = torch.empty(B, H2, H2, 64, **bf)
         self.pidx = torch.empty(B, H2, H2, 64, dtype=torch.uint8, device=dev)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        # ReLU masks of every masked dgrad as bitmasks (1 bit per element instead of re-reading
+        # the 16-bit activation): written by the forward epilogues, read by the dgrad epilogues
+        self.bits: Dict[str, Dict[str, torch.Tensor]] = {}
+        self.pool_bits = torch.empty(B, H2, H2, 8, **u8) if self.bitmask else None
         self.acts: Dict[str, Dict[str, torch.Tensor]] = {}
         H = H2
         inner = 0
@@ -195,6 +204,10 @@ class HipEngine:
             if b.proj:
                 a["sc"] = torch.empty(B, Ho, Ho, 4 * f, **bf)
             self.acts[b.name] = a
+            if self.bitmask:
+                self.bits[b.name] = {"y1": torch.empty(B, Ho, Ho, f // 8, **u8),
+                                     "y2": torch.empty(B, Ho, Ho, f // 8, **u8),
+                                     "out": torch.empty(B, Ho, Ho, f // 2, **u8)}
             self.geo[b.name] = (H, Ho)
             inner = max(inner, B * Ho * Ho * f)
             outer = max(outer, B * H * H * b.cin, B * Ho * Ho * 4 * f)
@@ -280,12 +293,14 @@ class HipEngine:
         c1 = self.c1[:B]
         N.igemm(x2, None, Hs, Hs, 4, 4, 1, 0, H1, H1, self._wf(s.name, 64, STEM_K), 0,
                 self.scale[self.ch[s.name]:], self.shift[self.ch[s.name]:], None, None, None, c1, 1,
-                None, 0, 0, 0, 0, 0, None)
+                None, 0, 0, 0, 0, 0, None, None)
         pool = self.pool[:B]
-        N.maxpool_fwd(c1, pool, self.pidx[:B])
+        use_bits = training and self.bitmask
+        N.maxpool_fwd(c1, pool, self.pidx[:B], self.pool_bits[:B] if use_bits else None)
         x = pool
         for b in L.blocks:
             a = self.acts[b.name]
+            bt = {k: v[:B] for k, v in self.bits[b.name].items()} if use_bits else {}
             H, Ho = self.geo[b.name]
             f, cin = b.filters, b.cin
             y1, y2, out = a["y1"][:B], a["y2"][:B], a["out"][:B]
@@ -294,27 +309,28 @@ class HipEngine:
             if b.proj:
                 N.igemm(x, None, H, H, 1, 1, b.stride, 0, Ho, Ho, self._wf(c1n, 5 * f, cin), 0,
                         self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, a["sc"][:B], 0, f, 0, 0, 0,
-                        None)
+                        None, bt.get("y1"))
                 res = a["sc"][:B]
             else:
                 N.igemm(x, None, H, H, 1, 1, 1, 0, Ho, Ho, self._wf(c1n, f, cin), 0,
-                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, None, 0, 0, 0, 0, 0, None)
+                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, None, 0, 0, 0, 0, 0, None,
+                        bt.get("y1"))
                 res = x
             c2 = b.convs["2"].name
             N.igemm(y1, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wf(c2, f, 9 * f), 0,
                     self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0, 0, 0,
-                    None)
+                    None, bt.get("y2"))
             c3 = b.convs["3"].name
             N.igemm(y2, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(c3, 4 * f, f), 0,
                     self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 0, 0, 0,
-                    None)
+                    None, bt.get("out"))
             x = out
         pooled = self.pooled[:B]
         N.gap_fwd(x, pooled)
         logits = self.logits[:B]
         chd = self.ch["dense"]
         N.igemm(pooled.view(B, 1, 1, 2048), None, 1, 1, 1, 1, 1, 0, 1, 1, self._wf("dense", self.num_classes, 2048), 2,
-                self.scale[chd:], self.shift[chd:], None, None, None, logits, 0, None, 0, 0, 0, 0, 0, None)
+                self.scale[chd:], self.shift[chd:], None, None, None, logits, 0, None, 0, 0, 0, 0, 0, None, None)
         return x
 
     def _labels(self, labels, B):
@@ -353,7 +369,7 @@ class HipEngine:
         dpooled = self.dpooled[:B]
         N.igemm(dl.view(B, 1, 1, self.ncls_pad), None, 1, 1, 1, 1, 1, 0, 1, 1,
                 self._wdv("dense", 2048, self.ncls_pad), 1, None, None, None, None, None, dpooled, 0,
-                None, 0, 0, 0, 0, 0, None)
+                None, 0, 0, 0, 0, 0, None, None)
         e = L.entry("dense", "kernel")
         done_upto(e.offset + e.size)
         cur = 0
@@ -376,6 +392,10 @@ class HipEngine:
             # conv2_block1's input is the max-pool output y: the stem's ReLU mask at every argmax
             # position equals (y > 0), so it is applied here instead of re-reading conv1's output
             mask_in = x_in
+            y1m, y2m = a["y1"][:B], a["y2"][:B]
+            if self.bitmask:
+                mask_in = self.bits[blocks[bi - 1].name]["out"][:B] if bi > 0 else self.pool_bits[:B]
+                y1m, y2m = self.bits[b.name]["y1"][:B], self.bits[b.name]["y2"][:B]
             cs_in = part(blocks[bi - 1].convs["3"].name) if bi > 0 else None
             y1, y2 = a["y1"][:B], a["y2"][:B]
             gout = self.gbuf[cur][: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
@@ -383,13 +403,13 @@ class HipEngine:
             # conv3
             N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)
             g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
-            N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2, None,
-                    g2, 0, None, 0, 0, 0, 0, 0, part(c2n))
+            N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m, None,
+                    g2, 0, None, 0, 0, 0, 0, 0, part(c2n), None)
             # conv2 (3x3)
             N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
             g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
-            N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1, None,
-                    g1, 0, None, 0, 0, 0, 0, 0, part(c1n))
+            N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1m, None,
+                    g1, 0, None, 0, 0, 0, 0, 0, part(c1n), None)
             # conv1 (+ conv0)
             nxt = 1 - cur
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
@@ -397,13 +417,13 @@ class HipEngine:
                 N.wgrad(x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0)
                 N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
                 N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, 5 * f), 1, None, None, None,
-                        mask_in, None, gx, 0, None, 0, 0, 1 if b.stride == 2 else 0, H, H, cs_in)
+                        mask_in, None, gx, 0, None, 0, 0, 1 if b.stride == 2 else 0, H, H, cs_in, None)
                 last = L.entry(b.convs["0"].name, "kernel")
             else:
                 N.wgrad(x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0)
                 N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
                 N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, f), 1, None, None, None,
-                        mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0, cs_in)
+                        mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0, cs_in, None)
                 last = L.entry(c1n, "kernel")
             done_upto(last.offset + last.size)
             cur = nxt

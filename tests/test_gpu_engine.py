@@ -77,3 +77,24 @@ def test_engine_trains():
     assert losses[-1] < losses[0] * 0.5, losses
     ev = he.evaluate(img, lab)
     assert torch.isfinite(ev).all()
+
+
+def test_engine_bitmask_equivalent():
+    """ReLU masks carried as bitmasks give the same step as masks re-read from bf16 activations."""
+    from pddl.models.engine import HipEngine
+    from pddl.models.resnet50 import ParamLayout
+    torch.manual_seed(0)
+    B = 4
+    L = ParamLayout()
+    img = torch.randint(0, 256, (B, 128, 128, 3), dtype=torch.uint8, device="cuda")
+    lab = torch.randint(0, 1000, (B,), device="cuda")
+    out = []
+    for bm in (False, True):
+        he = HipEngine(L, B, crop=128, image_size=128, bitmask=bm)
+        he.init(seed=5)
+        s = he.forward_backward(img, lab, 1.0 / B).clone()
+        out.append((s, he.grads.clone()))
+    torch.cuda.synchronize()
+    assert torch.allclose(out[0][0], out[1][0], rtol=1e-5)
+    r = ((out[0][1] - out[1][1]).norm() / out[0][1].norm()).item()
+    assert r < 1e-4, r

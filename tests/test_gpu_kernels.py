@@ -58,7 +58,7 @@ def test_igemm_forward(case, with_res):
     res = rnd(n, ho, ho, co) if with_res else None
     out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
     N().igemm(x, None, h, h, r, r, st, pad, ho, ho, w.view(co, -1), 0, scale, shift, res, None, None, out, 1,
-              None, 0, 0, 0, 0, 0, None)
+              None, 0, 0, 0, 0, 0, None, None)
     ref = conv_ref(x, w, st, pad) * scale + shift
     if with_res:
         ref = ref + res.float()
@@ -76,7 +76,7 @@ def test_igemm_split_outputs_and_f32():
     y1 = torch.empty(n, 4, 4, f, dtype=torch.bfloat16, device=dev)
     sc = torch.empty(n, 4, 4, 4 * f, dtype=torch.bfloat16, device=dev)
     N().igemm(x, None, h, h, 1, 1, 2, 0, 4, 4, w.view(5 * f, c), 0, scale, shift, None, None, None, y1, 1,
-              sc, 0, f, 0, 0, 0, None)
+              sc, 0, f, 0, 0, 0, None, None)
     ref = conv_ref(x, w, 2, 0) * scale + shift
     assert rel(y1, ref[..., :f].relu()) < 1e-2
     assert rel(sc, ref[..., f:]) < 1e-2
@@ -87,7 +87,7 @@ def test_igemm_split_outputs_and_f32():
     ones = torch.ones(1000, device=dev)
     out = torch.empty(6, 1000, device=dev)
     N().igemm(a.view(6, 1, 1, 2048), None, 1, 1, 1, 1, 1, 0, 1, 1, wd, 2, ones, bias, None, None, None, out, 0,
-              None, 0, 0, 0, 0, 0, None)
+              None, 0, 0, 0, 0, 0, None, None)
     ref = a.float() @ wd.float().t() + bias
     assert rel(out, ref) < 1e-3
 
@@ -123,7 +123,7 @@ def test_igemm_dgrad(case):
     rows = N().igemm_partial_rows(n * ho * ho, cin)
     part = torch.full((rows * cin,), float("nan"), device=dev)
     N().igemm(g, None, ho, ho, r, r, 1, pd, ho, ho, wt.view(cin, -1), 1, None, None, None, mask, add, out, 0,
-              None, 0, 0, 1 if st == 2 else 0, h, h, part)
+              None, 0, 0, 1 if st == 2 else 0, h, h, part, None)
     gs = (g.float() * a).permute(0, 3, 1, 2)
     ref = torch.nn.grad.conv2d_input((n, cin, h, h), w.float().permute(0, 3, 1, 2), gs, stride=st, padding=pad)
     ref = (ref.permute(0, 2, 3, 1) + add.float()) * (mask.float() > 0)
@@ -145,13 +145,51 @@ def test_igemm_dgrad_dual_source():
     wt = torch.cat([dgrad_weights(w1, a1).view(cin, f), dgrad_weights(w0, a0).view(cin, 4 * f)], 1).contiguous()
     mask = rnd(n, h, h, cin)
     out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
-    N().igemm(g1, g0, ho, ho, 1, 1, 1, 0, ho, ho, wt, 1, None, None, None, mask, None, out, 0, None, 0, 0, 1, h, h, None)
+    N().igemm(g1, g0, ho, ho, 1, 1, 1, 0, ho, ho, wt, 1, None, None, None, mask, None, out, 0, None, 0, 0, 1, h, h,
+              None, None)
     r1 = torch.nn.grad.conv2d_input((n, cin, h, h), w1.float().permute(0, 3, 1, 2),
                                     (g1.float() * a1).permute(0, 3, 1, 2), stride=2)
     r0 = torch.nn.grad.conv2d_input((n, cin, h, h), w0.float().permute(0, 3, 1, 2),
                                     (g0.float() * a0).permute(0, 3, 1, 2), stride=2)
     ref = (r1 + r0).permute(0, 2, 3, 1) * (mask.float() > 0)
     assert rel(out, ref) < 1e-2
+
+
+def pack_bits(x):
+    """Reference ReLU bitmask: bit e of byte [..., c // 8] is (x[..., 8 * (c // 8) + e] > 0)."""
+    b = (x.float() > 0).to(torch.int32).view(*x.shape[:-1], x.shape[-1] // 8, 8)
+    return (b << torch.arange(8, device=x.device, dtype=torch.int32)).sum(-1).to(torch.uint8)
+
+
+def test_bitmask_forward_and_dgrad():
+    torch.manual_seed(9)
+    n, h, c, f = 2, 8, 64, 64
+    x = rnd(n, h, h, c)
+    w = rnd(5 * f, 1, 1, c, scale=0.1)
+    scale = torch.rand(5 * f, device=dev) + 0.5
+    shift = torch.randn(5 * f, device=dev)
+    y1 = torch.empty(n, h, h, f, dtype=torch.bfloat16, device=dev)
+    sc = torch.empty(n, h, h, 4 * f, dtype=torch.bfloat16, device=dev)
+    bits = torch.full((n, h, h, f // 8), 0xAA, dtype=torch.uint8, device=dev)
+    N().igemm(x, None, h, h, 1, 1, 1, 0, h, h, w.view(5 * f, c), 0, scale, shift, None, None, None, y1, 1,
+              sc, 0, f, 0, 0, 0, None, bits)
+    assert torch.equal(bits, pack_bits(y1))
+    # a dgrad masked by the bits equals the same dgrad masked by the bf16 tensor
+    g = rnd(n, h, h, 4 * f)
+    wt = rnd(f, 4 * f, scale=0.05)
+    o1 = torch.empty(n, h, h, f, dtype=torch.bfloat16, device=dev)
+    o2 = torch.empty_like(o1)
+    for m, o in ((y1, o1), (bits, o2)):
+        N().igemm(g, None, h, h, 1, 1, 1, 0, h, h, wt, 1, None, None, None, m, None, o, 0, None, 0, 0, 0, 0, 0,
+                  None, None)
+    assert torch.equal(o1, o2)
+    # maxpool forward bits
+    xp = torch.relu(torch.randn(n, 12, 12, c, device=dev)).to(torch.bfloat16)
+    yp = torch.empty(n, 6, 6, c, dtype=torch.bfloat16, device=dev)
+    idx = torch.empty(n, 6, 6, c, dtype=torch.uint8, device=dev)
+    pb = torch.empty(n, 6, 6, c // 8, dtype=torch.uint8, device=dev)
+    N().maxpool_fwd(xp, yp, idx, pb)
+    assert torch.equal(pb, pack_bits(yp))
 
 
 WG_CASES = [
@@ -212,7 +250,7 @@ def test_maxpool_and_gap():
     ho = (h + 2 - 3) // 2 + 1
     y = torch.empty(n, ho, ho, c, dtype=torch.bfloat16, device=dev)
     idx = torch.empty(n, ho, ho, c, dtype=torch.uint8, device=dev)
-    N().maxpool_fwd(x, y, idx)
+    N().maxpool_fwd(x, y, idx, None)
     xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
     yr = F.max_pool2d(F.pad(xr, (1, 1, 1, 1)), 3, 2)
     assert torch.equal(y.float(), yr.permute(0, 2, 3, 1).detach())
@@ -317,7 +355,7 @@ def test_stem_s2d_conv_and_wgrad(mode):
     ones, zeros = torch.ones(64, device=dev), torch.zeros(64, device=dev)
     y = torch.empty(B, ho, ho, 64, dtype=torch.bfloat16, device=dev)
     N().igemm(x2, None, hs, hs, 4, 4, 1, 0, ho, ho, w2, 0, ones, zeros, None, None, None, y, 0, None, 0, 0, 0, 0, 0,
-              None)
+              None, None)
     xb = x2.float().view(B, hs, hs, 2, 2, 4)[..., :3].permute(0, 5, 1, 3, 2, 4).reshape(B, 3, 2 * hs, 2 * hs)
     wq = w2.float().view(64, 4, 4, 2, 2, 4)[..., :3]
     wq = wq.permute(0, 5, 1, 3, 2, 4).reshape(64, 3, 8, 8)[:, :, :7, :7]
