@@ -1,4 +1,4 @@
-"""Build the native HIP extension in-tree for gfx950 and place it next to the package.
+"""Build the native extensions in-tree for gfx950 (hipcc for the kernels) and place them next to the package.
 
     python pddl_build.py            # hipcc cross-compiles; no GPU needed
 """
@@ -14,7 +14,7 @@ PKG = os.path.join(ROOT, "parallel-and-distributed-deep-learning_amd")
 
 def build(verbose: bool = False) -> str:
     env = dict(os.environ)
-    env.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
+    env.setdefault("PDDL_OFFLOAD_ARCH", "gfx950")
     env.setdefault("MAX_JOBS", "8")
     # object files stay outside the tree so GPU-box snapshots only carry the .so files
     cmd = [sys.executable, "setup.py", "build_ext", "--inplace", "--build-temp",

@@ -1,48 +1,77 @@
-"""Build the in-tree native extension `_pddl_native` (HIP kernels for gfx950 + torch bindings).
+"""Build the in-tree native extensions.
 
-    PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace
+    python pddl_build.py                      (what __graft_entry__.build() runs)
 
-The built shared object is moved next to the Python package
-(`parallel-and-distributed-deep-learning_amd/_pddl_native*.so`) by `pddl_build.py`;
-`__graft_entry__.build()` drives both steps.
+`_pddl_native`: the gfx950 HIP kernels (csrc/kernels/*.hip) are compiled by hipcc directly
+into position-independent objects -- no source translation step touches them -- and linked
+with the host-side torch bindings and runtime (csrc/bindings.cpp, csrc/runtime/*.cpp), which
+are plain C++ against the HIP runtime and PyTorch-ROCm headers.
+
+`_pddl_h5`: Keras-layout .h5 checkpoints through the system HDF5 1.10 (separate module so the
+kernels never depend on libhdf5 being loadable).
+
+The built shared objects are moved next to the Python package by `pddl_build.py`.
 """
 import glob
 import os
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 from setuptools import setup
-from torch.utils.cpp_extension import BuildExtension, CppExtension, CUDAExtension
+from torch.utils.cpp_extension import BuildExtension, CppExtension, include_paths, library_paths
 
-os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
 ROOT = os.path.dirname(os.path.abspath(__file__))
-kern = sorted(glob.glob(os.path.join("csrc", "kernels", "*.hip")))
-rt = sorted(glob.glob(os.path.join("csrc", "runtime", "*.cpp")))
-srcs = [os.path.join("csrc", "bindings.cpp")] + rt + kern
+ARCH = os.environ.get("PDDL_OFFLOAD_ARCH", "gfx950")
+TEMP = os.environ.get("PDDL_BUILD_TEMP", os.path.join(os.environ.get("TMPDIR", "/tmp"), "pddl_build_temp"))
+HIPCC = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+HIP_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=fast", "-fPIC", "-I" + os.path.join(ROOT, "csrc")]
+
+
+def compile_kernels():
+    """hipcc -c every kernel translation unit (rebuilt when it or a kernel header changed)."""
+    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
+    hdrs = glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.h"))
+    hdr_mtime = max(os.path.getmtime(h) for h in hdrs)
+    odir = os.path.join(TEMP, "kernels", ARCH)
+    os.makedirs(odir, exist_ok=True)
+
+    def one(src):
+        obj = os.path.join(odir, os.path.basename(src)[:-4] + ".o")
+        if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
+            return obj
+        r = subprocess.run([HIPCC, *HIP_FLAGS, "-c", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")
+        return obj
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        return list(ex.map(one, srcs))
+
+
+kernel_objs = compile_kernels()
+host_srcs = [os.path.join("csrc", "bindings.cpp")] + sorted(glob.glob(os.path.join("csrc", "runtime", "*.cpp")))
 
 setup(
     name="pddl_native",
     ext_modules=[
-        CUDAExtension(
+        CppExtension(
             "_pddl_native",
-            srcs,
-            include_dirs=[os.path.join(ROOT, "csrc"), "/opt/rocm/include"],
-            library_dirs=["/opt/rocm/lib"],
-            libraries=["rccl"],
-            extra_link_args=["-Wl,-rpath,/opt/rocm/lib"],
-            extra_compile_args={
-                "cxx": ["-O2", "-std=c++17"],
-                "nvcc": ["-O3", "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=fast"],
-            },
+            host_srcs,
+            include_dirs=[os.path.join(ROOT, "csrc")] + include_paths(device_type="cuda"),
+            library_dirs=library_paths(device_type="cuda"),
+            libraries=["amdhip64", "c10_hip", "torch_hip", "rccl"],
+            define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
+            extra_objects=kernel_objs,
+            extra_link_args=["-Wl,-rpath,/opt/rocm/lib", "-Wl,--strip-debug"],
+            extra_compile_args=["-O2", "-g0", "-std=c++17"],
         ),
-        # Keras-layout .h5 checkpoints through the system HDF5 1.10 (separate module so the
-        # kernels never depend on libhdf5 being loadable)
         CppExtension(
             "_pddl_h5",
             [os.path.join("csrc", "h5", "h5io.cpp")],
             include_dirs=["/opt/conda/include"],
             library_dirs=["/opt/conda/lib"],
             libraries=["hdf5"],
-            extra_link_args=["-Wl,-rpath,/opt/conda/lib"],
-            extra_compile_args=["-O2", "-std=c++17"],
+            extra_link_args=["-Wl,-rpath,/opt/conda/lib", "-Wl,--strip-debug"],
+            extra_compile_args=["-O2", "-g0", "-std=c++17"],
         ),
     ],
     cmdclass={"build_ext": BuildExtension.with_options(use_ninja=True)},
