@@ -52,6 +52,20 @@ __device__ __forceinline__ uint32_t pos_bits8(const uint4& u) {
   return byte;
 }
 
+// Buffer offset past every descriptor's range (operands are checked to stay below 2 GiB):
+// the buffer unit returns zeros for it.
+constexpr uint32_t OOB_OFF = 0x80000000u;
+
+// 16-byte-per-lane buffer LDS-DMA (buffer_load_dwordx4 ... lds): LDS destination = M0 base
+// (wave-uniform dst) + lane * 16; out-of-range offsets load zeros.
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, __attribute__((address_space(3))) void* dst,
+                                          uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+
 // 64 bytes of zeros: the source of every out-of-bounds LDS-DMA lane (padding
 // rows of the implicit-GEMM gather, tile overhang).  LDS-DMA cannot write a
 // literal, so invalid lanes read from here instead.  One copy per translation

@@ -18,10 +18,11 @@
 //   * 256 threads = 4 waves, wave tile 64x64 (or 64x32) of 16x16x32 bf16 MFMAs.
 //   * BK = 64: one k-tile never crosses an (r, s) tap because C % 64 == 0, so the im2col
 //     gather needs only per-row (n, ho, wo) bookkeeping plus uniform (r, s, c0) scalars.
-//   * Tiles are staged global->LDS with 16-byte LDS-DMA (global_load_lds_dwordx4); the LDS
-//     image is lane-linear, so the bank-conflict XOR swizzle is applied to the SOURCE
+//   * Tiles are staged global->LDS with 16-byte buffer LDS-DMA (buffer_load_dwordx4 ... lds);
+//     the LDS image is lane-linear, so the bank-conflict XOR swizzle is applied to the SOURCE
 //     address and the same involution on the ds_read_b128 address (rule 21).
-//   * Out-of-bounds lanes (padding taps, tile overhang) read a 64-byte zero page.
+//   * Out-of-bounds lanes (padding taps, tile overhang) use an out-of-range buffer offset,
+//     which the buffer unit turns into zeros; the k-tile shift is a scalar soffset.
 //   * Double-buffered LDS, XCD-aware bijective tile remap, LDS-staged epilogue that turns
 //     the MFMA fragment layout into 16-byte row-contiguous stores.
 #include "common.h"
@@ -29,11 +30,21 @@
 
 namespace pddl {
 
-template <int BM, int BN, int WTM, int WTN, int NSTAGE>
+// A-operand gather modes (compile-time, so the k loop carries no mode branches):
+//   AM_DIRECT: every tap of every valid row is in bounds (1x1 / pad 0, the s2d stem window):
+//              the per-lane buffer offset is loop-invariant and the k-tile's (r, s, c0) shift
+//              rides in the scalar soffset -> no vector work per load.
+//   AM_HALO:   padded convs (3x3 / pad 1): a per-row bitmask of the valid taps selects between
+//              the row's offset and an out-of-range offset (buffer loads return zeros there).
+//   AM_DUAL:   two AM_DIRECT sources concatenated along K (projection-block dgrad).
+enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
+
+template <int BM, int BN, int WTM, int WTN, int NSTAGE, int AM>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int WAVES_N = BN / WTN;
   static_assert((BM / WTM) * (BN / WTN) == 4, "4 waves per block");
+  static_assert(NSTAGE == 1 || NSTAGE == 2, "1- or 2-stage LDS pipeline");
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int AI = BM / 32, BI = BN / 32;  // 1 KiB LDS-DMA pieces per wave per tile
   constexpr int EPI_LD = WTN + 4;
@@ -41,68 +52,93 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   constexpr int SMEM = (NSTAGE * STAGE > EPI_BYTES) ? NSTAGE * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: M0 from SGPRs
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int mt = (p.M + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, mt * nt);
   const int tn = wg % nt, tm = wg / nt;
   const int m0 = tm * BM, n0 = tn * BN;
   const int HoWo = p.Ho * p.Wo;
-  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
+
+  // Buffer descriptors (wave-uniform kernel arguments only, so no waterfall loops).
+  const int pix_total = p.N * p.H * p.W;
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(p.a1, pix_total * p.C1 * 2);
+  const __amdgpu_buffer_rsrc_t ra2 =
+      make_rsrc(AM == AM_DUAL ? p.a2 : p.a1, pix_total * (AM == AM_DUAL ? p.C2 : p.C1) * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
 
   // Per-lane constant source chunk: LDS position (lane & 7) of row (lane >> 3) holds the
   // logical 16-byte chunk (lane & 7) ^ (row & 7).
   const int chunk_sw = (lane & 7) ^ ((lane >> 3) & 7);
 
-  // A-row bookkeeping (fixed over the k loop): the element offset of the row's tap (0, 0)
-  // in each source; a k-tile then only adds a wave-uniform (r*W + s)*C + c0.
-  int a_hi[AI], a_wi[AI], a_o1[AI], a_o2[AI];
-  const bool no_halo = p.R == 1 && p.S == 1 && p.pad == 0;   // 1x1: only the row itself can be invalid
+  // A-row bookkeeping (fixed over the k loop): byte offset of the row's tap (0, 0) in each
+  // source (OOB_OFF for rows past M) and, for AM_HALO, the bitmask of its in-bounds taps.
+  uint32_t a_o1[AI], a_o2[AI], a_taps[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int m = m0 + (wave * AI + i) * 8 + (lane >> 3);
+    a_o1[i] = OOB_OFF; a_o2[i] = OOB_OFF; a_taps[i] = 0;
     if (m < p.M) {
-      const int n = m / HoWo, rem = m - n * HoWo;
-      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
-      a_hi[i] = ho * p.stride - p.pad;
-      a_wi[i] = wo * p.stride - p.pad;
-      const int pix = (n * p.H + a_hi[i]) * p.W + a_wi[i];
-      a_o1[i] = pix * p.C1 + chunk_sw * 8;
-      a_o2[i] = pix * p.C2 + chunk_sw * 8;
-    } else {
-      a_hi[i] = -(1 << 28); a_wi[i] = 0; a_o1[i] = 0; a_o2[i] = 0;
+      const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
+      const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
+      const int hi = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
+      const int pix = (n * p.H + hi) * p.W + wi;
+      a_o1[i] = (uint32_t)((pix * p.C1 + chunk_sw * 8) * 2);
+      if (AM == AM_DUAL) a_o2[i] = (uint32_t)((pix * p.C2 + chunk_sw * 8) * 2);
+      if (AM == AM_HALO) {
+        uint32_t rows = 0, cols = 0, mk = 0;
+        for (int r = 0; r < p.R; ++r) rows |= (uint32_t)((unsigned)(hi + r) < (unsigned)p.H) << r;
+        for (int s = 0; s < p.S; ++s) cols |= (uint32_t)((unsigned)(wi + s) < (unsigned)p.W) << s;
+        for (int r = 0; r < p.R; ++r) mk |= ((rows >> r) & 1u) ? cols << (r * p.S) : 0u;
+        a_taps[i] = mk;
+      }
     }
   }
-  const bf16_t* b_row[BI];
+  uint32_t b_o[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     const int n = n0 + (wave * BI + i) * 8 + (lane >> 3);
-    b_row[i] = (n < p.Nn) ? p.b + (long)n * p.ldb + chunk_sw * 8 : nullptr;
+    b_o[i] = (n < p.Nn) ? (uint32_t)((n * p.ldb + chunk_sw * 8) * 2) : OOB_OFF;
   }
 
-  auto load_tile = [&](int t, int buf) {
-    const int kk0 = t * 64;
-    const bf16_t* src; int C, kr;
-    const bool first = kk0 < p.K1;
-    if (first) { src = p.a1; C = p.C1; kr = kk0; }
-    else { src = p.a2; C = p.C2; kr = kk0 - p.K1; }
-    const int rs = kr / C, c0 = kr - rs * C;
-    const int r = rs / p.S, s = rs - r * p.S;
-    const int delta = (r * p.W + s) * C + c0;
+  // k-tile walk state (scalar): the next tile to load is tap (r, s), channels [c0, c0 + 64)
+  // of source `src2`; a "window" tile (C * S == 64) spans all S taps of one r.
+  int ld_r = 0, ld_s = 0, ld_c0 = 0, ld_src2 = 0, ld_k = 0;
+  const bool window = p.C1 * p.S == 64 && p.C1 < 64;
+  auto load_tile = [&](int buf) {
+    const int C = ld_src2 ? p.C2 : p.C1;
+    const int delta = ((ld_r * p.W + ld_s) * C + ld_c0) * 2;   // bytes
     char* abase = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const bool ok = no_halo ? a_hi[i] >= 0
-                              : ((unsigned)(a_hi[i] + r) < (unsigned)p.H) && ((unsigned)(a_wi[i] + s) < (unsigned)p.W);
-      const bf16_t* g = ok ? src + ((first ? a_o1[i] : a_o2[i]) + delta) : zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(abase + (wave * AI + i) * 1024), 16, 0, 0);
+      void __attribute__((address_space(3)))* dst = LDS_PTR(abase + (wave * AI + i) * 1024);
+      if (AM == AM_HALO) {
+        const int tap = ld_r * p.S + ld_s;
+        const uint32_t off = ((a_taps[i] >> tap) & 1u) ? a_o1[i] + (uint32_t)delta : OOB_OFF;
+        buf_lds16(ra1, dst, off, 0);
+      } else if (AM == AM_DUAL && ld_src2) {
+        buf_lds16(ra2, dst, a_o2[i], delta);
+      } else {
+        buf_lds16(ra1, dst, a_o1[i], delta);
+      }
     }
     char* bbase = abase + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const bf16_t* g = b_row[i] ? b_row[i] + kk0 : zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(bbase + (wave * BI + i) * 1024), 16, 0, 0);
+    for (int i = 0; i < BI; ++i)
+      buf_lds16(rb, LDS_PTR(bbase + (wave * BI + i) * 1024), b_o[i], ld_k * 2);
+    // advance to the next k-tile
+    ld_k += 64;
+    if (window && !ld_src2) {
+      ++ld_r;
+    } else {
+      ld_c0 += 64;
+      if (ld_c0 == C) {
+        ld_c0 = 0;
+        if (++ld_s == p.S) { ld_s = 0; ++ld_r; }
+      }
     }
+    if (AM == AM_DUAL && !ld_src2 && ld_k == p.K1) { ld_src2 = 1; ld_r = ld_s = ld_c0 = 0; }
   };
 
   v4f acc[TM][TN];
@@ -114,26 +150,12 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   const int KT = p.K / 64;
   const int a_off = (wm * WTM + (lane & 15)) * 128;
   const int b_off = (wn * WTN + (lane & 15)) * 128;
-  load_tile(0, 0);
-  if (NSTAGE == 3 && KT > 1) load_tile(1, 1);
-  if (NSTAGE != 3) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  load_tile(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int t = 0; t < KT; ++t) {
-    int cur;
-    if (NSTAGE == 3) {
-      // 3-deep ring: tile t landed (tile t+1 may stay in flight across the barrier), every
-      // wave finished reading tile t-1, so its buffer can take tile t+2.  Raw s_barrier: a
-      // __syncthreads() here would drain the LDS-DMA queue (vmcnt(0)).
-      if (t + 1 < KT) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(AI + BI) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      cur = t % 3;
-      if (t + 2 < KT) load_tile(t + 2, (t + 2) % 3);
-    } else {
-      cur = NSTAGE == 2 ? (t & 1) : 0;
-      if (NSTAGE == 2 && t + 1 < KT) load_tile(t + 1, cur ^ 1);
-    }
+    const int cur = NSTAGE == 2 ? (t & 1) : 0;
+    if (NSTAGE == 2 && t + 1 < KT) load_tile(cur ^ 1);
     const char* As = smem + cur * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -152,14 +174,11 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
     }
     if (NSTAGE == 1 && t + 1 < KT) {
       __syncthreads();            // every wave is done reading the single buffer
-      load_tile(t + 1, 0);
+      load_tile(0);
     }
-    if (NSTAGE != 3) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  if (NSTAGE == 3) __syncthreads();   // all LDS reads done before the epilogue reuses LDS
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
@@ -231,7 +250,7 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
           long row = gm;
           int n = 0, i = 0, j = 0;
           if (p.up2) {
-            n = gm / HoWo; const int rem = gm - n * HoWo; i = rem / p.Wo; j = rem - i * p.Wo;
+            n = fdiv(gm, p.mg_howo); const int rem = gm - n * HoWo; i = fdiv(rem, p.mg_wo); j = rem - i * p.Wo;
             row = ((long)n * p.Hf + 2 * i) * p.Wf + 2 * j;
           }
 #pragma unroll
@@ -293,8 +312,12 @@ int igemm_partial_rows(int M, int Nn) {
   return ((M + BM - 1) / BM) * (BM / 64);
 }
 
-int g_igemm_variant = 0;   // 0 = heuristic; 1, 2, 3 = forced pipeline depth
-int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256
+int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth
+int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
+
+static bool igemm_no_halo(const IgemmParams& p) {
+  return p.pad == 0 && (p.Ho - 1) * p.stride + p.R <= p.H && (p.Wo - 1) * p.stride + p.S <= p.W;
+}
 
 static bool igemm_check(const IgemmParams& p, const char** why) {
   if (p.K % 64 || p.K1 % 64) { *why = "K must be a multiple of 64"; return false; }
@@ -303,30 +326,50 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
   const bool window = (p.C1 * p.S == 64) && p.stride == 1 && p.pad == 0 && !p.a2;
   if ((p.C1 % 64 && !window) || (p.a2 && p.C2 % 64)) { *why = "channels must be multiples of 64"; return false; }
   if (p.a2 && (p.K - p.K1) % 64) { *why = "second source K must be a multiple of 64"; return false; }
+  if (p.a2 && !igemm_no_halo(p)) { *why = "two A sources need an unpadded (1x1) gather"; return false; }
+  if (!igemm_no_halo(p) && p.R * p.S > 32) { *why = "padded convs support at most 32 taps"; return false; }
   if (p.Nn % 8 || p.ldb % 8 || p.ldo % 8) { *why = "N / ldb / ldo must be multiples of 8"; return false; }
   if (p.M <= 0 || p.Nn <= 0 || p.K <= 0) { *why = "empty problem"; return false; }
-  if ((long)p.N * p.H * p.W * (p.C1 > p.C2 ? p.C1 : p.C2) >= (1L << 31)) { *why = "input too large for 32-bit offsets"; return false; }
+  if ((long)p.M * p.Ho * p.Wo >= (1L << 40)) { *why = "too many output rows for the magic-number row decode"; return false; }
+  // buffer offsets are 32-bit byte offsets with 0x80000000 reserved as "out of range"
+  if ((long)p.N * p.H * p.W * (p.C1 > p.C2 ? p.C1 : p.C2) * 2 >= (1L << 31) || (long)p.Nn * p.ldb * 2 >= (1L << 31)) {
+    *why = "operand too large for 31-bit buffer offsets"; return false;
+  }
   return true;
 }
 
-const char* igemm_launch(const IgemmParams& p, hipStream_t stream) {
+const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   const char* why = nullptr;
-  if (!igemm_check(p, &why)) return why;
-  // short K (<= 2 k-tiles) is memory-bound: single LDS stage for twice the resident blocks
-  // Pipeline depth by K (variant knob for A/B timing: 0 = heuristic, 1/2/3 = forced stages)
+  if (!igemm_check(p_in, &why)) return why;
+  IgemmParams p = p_in;
+  p.mg_howo = fdiv_magic(p.Ho * p.Wo);
+  p.mg_wo = fdiv_magic(p.Wo);
+  // Pipeline depth by K: short K (<= 2 k-tiles) is memory-bound -> single LDS stage for
+  // twice the resident blocks (variant knob for A/B timing: 0 = heuristic, 1/2 = forced).
   const int KT = p.K / 64;
   int ns = g_igemm_variant;
-  if (ns == 0) ns = KT <= 2 ? 1 : (KT >= 4 ? g_igemm_deep : 2);
-  if (ns == 3 && KT < 3) ns = 2;
-#define IG_LAUNCH(BM_, BN_)                                                                                 \
-  {                                                                                                        \
-    const int nwg = ((p.M + BM_ - 1) / BM_) * ((p.Nn + BN_ - 1) / BN_);                                     \
-    if (ns == 1) hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, 1>), dim3(nwg), dim3(256), 0, stream, p); \
-    else if (ns == 2) hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, 2>), dim3(nwg), dim3(256), 0, stream, p); \
-    else hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, 3>), dim3(nwg), dim3(256), 0, stream, p);      \
+  if (ns == 0) ns = KT <= 2 ? 1 : 2;
+  const int am = p.a2 ? AM_DUAL : (igemm_no_halo(p) ? AM_DIRECT : AM_HALO);
+  // (explicit launches per instantiation: taking kernel addresses through a conditional
+  // expression leaves the host stubs uninstantiated with this compiler)
+#define IG_GO(BM_, BN_, NS_, AM_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, NS_, AM_>), dim3(nwg), dim3(256), 0, stream, p)
+#define IG_LAUNCH(BM_, BN_)                                             \
+  {                                                                    \
+    const int nwg = ((p.M + BM_ - 1) / BM_) * ((p.Nn + BN_ - 1) / BN_); \
+    if (ns == 1) {                                                     \
+      if (am == AM_DIRECT) IG_GO(BM_, BN_, 1, AM_DIRECT);              \
+      else if (am == AM_HALO) IG_GO(BM_, BN_, 1, AM_HALO);             \
+      else IG_GO(BM_, BN_, 1, AM_DUAL);                                \
+    } else {                                                           \
+      if (am == AM_DIRECT) IG_GO(BM_, BN_, 2, AM_DIRECT);              \
+      else if (am == AM_HALO) IG_GO(BM_, BN_, 2, AM_HALO);             \
+      else IG_GO(BM_, BN_, 2, AM_DUAL);                                \
+    }                                                                  \
   }
   if (p.Nn <= 64) IG_LAUNCH(256, 64) else IG_LAUNCH(128, 128)
 #undef IG_LAUNCH
+#undef IG_GO
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

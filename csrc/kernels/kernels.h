@@ -32,6 +32,7 @@ struct IgemmParams {
   // ReLU masks as bitmasks (bit e of byte [row][c/8] = value[row][8*(c/8)+e] > 0):
   uint8_t* bits_out; int ld_bits_out;               // FWD: write the mask of the (segment-0) output
   const uint8_t* bits_mask; int ld_bits_mask;       // DGRAD: multiply by the bit instead of (mask > 0)
+  uint64_t mg_howo, mg_wo;                          // set by igemm_launch: magic divisors (fdiv)
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
 int igemm_partial_rows(int M, int Nn);               // rows of the partial column-sum buffer

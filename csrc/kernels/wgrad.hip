@@ -31,7 +31,7 @@ __device__ __forceinline__ int tr_swz128(int row) { return (((row >> 1) & 1) | (
 
 // BM = 128: 2x2 waves, wave tile 64 (co) x 64 (k).  BM = 64 (Cout = 64 layers: the stem and
 // stage 2): 1x4 waves, wave tile 64 x 32, gradient tile with 128-byte rows.
-template <bool FAST, int BM, int NSTAGE>
+template <bool FAST, int BM, int NSTAGE>  // NSTAGE: LDS buffers (the loop is written for 2)
 __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split) {
   constexpr int G_BYTES = 64 * BM * 2;        // 64 m-rows x BM bf16
   constexpr int X_BYTES = 64 * 256;           // 64 m-rows x 128 bf16
@@ -43,7 +43,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   constexpr int GI = G_BYTES / 4096;          // 1 KiB G pieces per wave
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int tco = (p.Cout + BM - 1) / BM, tk = (p.K + 127) / 128, ntiles = tco * tk;
   const int splits = (p.M + m_per_split - 1) / m_per_split;
@@ -52,10 +53,14 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   const int co0 = (tile % tco) * BM, k0 = (tile / tco) * 128;
   const int mbeg = split * m_per_split;
   const int mend = min(p.M, mbeg + m_per_split);
-  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_zero_page);
   const int HoWo = p.Ho * p.Wo;
   // multiply-shift division constants (the row decode runs for every row of every tile)
   const uint64_t mg_hw = fdiv_magic(HoWo), mg_w = fdiv_magic(p.Wo);
+
+  // buffer descriptors: 32-bit lane offsets, the m-step in the scalar soffset, and
+  // out-of-range offsets (padding taps, tile overhang) load zeros
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.g, p.M * p.ldg * 2);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, FAST ? p.M * p.ldx * 2 : p.N * p.H * p.W * p.C * 2);
 
   // (r, s, c0) of the two 64-column halves of this k tile (generic path only).
   int hr[2], hs[2], hc[2]; bool hv[2];
@@ -68,48 +73,56 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 
   // Loader lane geometry: piece i of wave w covers rows (w*4+i)*4 .. +3, 16 chunks per row.
   const int lrow = lane >> 4, lpos = lane & 15;
+  // loop-invariant lane offsets of the gradient pieces (relative to row mb) and their source
+  uint32_t g_off[GI]; int g_row[GI];
+#pragma unroll
+  for (int i = 0; i < GI; ++i) {
+    int row, chunk;
+    if (BM == 128) { row = (wave * GI + i) * 4 + lrow; chunk = lpos ^ tr_swz(row); }
+    else { row = (wave * GI + i) * 8 + (lane >> 3); chunk = (lane & 7) ^ tr_swz128(row); }
+    const int co = co0 + chunk * 8;
+    g_row[i] = row;
+    g_off[i] = co >= p.Cout ? OOB_OFF : (uint32_t)((row * p.ldg + co) * 2);
+  }
+  uint32_t x_off[4];   // FAST: loop-invariant input offsets
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 4 + lrow;
+    const int kc = k0 + (lpos ^ tr_swz(row)) * 8;
+    x_off[i] = (FAST && kc < p.K) ? (uint32_t)((row * p.ldx + kc) * 2) : OOB_OFF;
+  }
 
   auto load_tile = [&](int mb, int buf) {
     char* gb = smem + buf * STAGE;
     char* xb = gb + G_BYTES;
+    const bool full = mb + 64 <= mend;   // scalar: only the split's last tile has dead rows
 #pragma unroll
     for (int i = 0; i < GI; ++i) {  // gradient operand
-      int row, chunk;
-      if (BM == 128) { row = (wave * GI + i) * 4 + lrow; chunk = lpos ^ tr_swz(row); }
-      else { row = (wave * GI + i) * 8 + (lane >> 3); chunk = (lane & 7) ^ tr_swz128(row); }
-      const int m = mb + row;
-      const int co = co0 + chunk * 8;
-      const bf16_t* gs = zero;
-      if (m < mend && co < p.Cout) {
-        if (p.g2 && co >= p.co_split) gs = p.g2 + (long)m * p.ldg2 + (co - p.co_split);
-        else gs = p.g + (long)m * p.ldg + co;
-      }
-      __builtin_amdgcn_global_load_lds((const void*)gs, LDS_PTR(gb + (wave * GI + i) * 1024), 16, 0, 0);
+      const uint32_t off = (full || mb + g_row[i] < mend) ? g_off[i] : OOB_OFF;
+      buf_lds16(rg, LDS_PTR(gb + (wave * GI + i) * 1024), off, mb * p.ldg * 2);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // input operand
       const int row = (wave * 4 + i) * 4 + lrow;
-      const int chunk = lpos ^ tr_swz(row);
       const int m = mb + row;
-      const bool mok = m < mend;
-      // input operand
-      const bf16_t* xs = zero;
+      const bool mok = full || m < mend;
       if (FAST) {
-        const int kc = k0 + chunk * 8;
-        if (mok && kc < p.K) xs = p.x + (long)m * p.ldx + kc;
+        buf_lds16(rx, LDS_PTR(xb + (wave * 4 + i) * 1024), mok ? x_off[i] : OOB_OFF, mb * p.ldx * 2);
       } else {
+        const int chunk = lpos ^ tr_swz(row);
         const int h = chunk >> 3;
         const int r = h ? hr[1] : hr[0], s = h ? hs[1] : hs[0], c = h ? hc[1] : hc[0];
         const bool v = h ? hv[1] : hv[0];
+        uint32_t off = OOB_OFF;
         if (mok && v) {
           const int n = fdiv(m, mg_hw), rem = m - n * HoWo;
           const int ho = fdiv(rem, mg_w), wo = rem - ho * p.Wo;
           const int hi = ho * p.stride - p.pad + r, wi = wo * p.stride - p.pad + s;
           if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
-            xs = p.x + ((long)((n * p.H + hi) * p.W + wi) * p.C + c + (chunk & 7) * 8);
+            off = (uint32_t)((((n * p.H + hi) * p.W + wi) * p.C + c + (chunk & 7) * 8) * 2);
         }
+        buf_lds16(rx, LDS_PTR(xb + (wave * 4 + i) * 1024), off, 0);
       }
-      __builtin_amdgcn_global_load_lds((const void*)xs, LDS_PTR(xb + (wave * 4 + i) * 1024), 16, 0, 0);
     }
   };
 
@@ -125,25 +138,12 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   const int nit = (mend - mbeg + 63) / 64;
   if (nit > 0) {
     load_tile(mbeg, 0);
-    if (NSTAGE == 3 && nit > 1) load_tile(mbeg + 64, 1);
-    if (NSTAGE == 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
   for (int it = 0; it < nit; ++it) {
-    int cur;
-    if (NSTAGE == 3) {
-      // 3-deep LDS ring, counted vmcnt keeps the next tile's LDS-DMA in flight across the
-      // raw barrier (cdna_hip_programming.md §5 "Pipelining across barriers")
-      if (it + 1 < nit) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(GI + 4) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      cur = it % 3;
-      if (it + 2 < nit) load_tile(mbeg + (it + 2) * 64, (it + 2) % 3);
-    } else {
-      cur = it & 1;
-      if (it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
-    }
+    const int cur = it & 1;
+    if (it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
     const char* gb = smem + cur * STAGE;
     const char* xb = gb + G_BYTES;
 #pragma unroll
@@ -182,13 +182,10 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (NSTAGE == 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
   if (nit == 0) return;
-  if (NSTAGE == 3) __syncthreads();
 
   // Epilogue: per-wave 32 x WTN fp32 staging, then row-contiguous atomics (256 B per wave
   // instruction: one 64-float row, or two 32-float rows for WTN = 32).
@@ -217,9 +214,25 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   }
 }
 
-int g_wgrad_variant = 0;   // 0 = default (3-stage), 2 / 3 = forced pipeline depth
+int g_wgrad_variant = 0;   // A/B knob (unused: one pipeline depth remains)
 
+static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream);
+
+// A second gradient source (rows >= co_split of dW: projection blocks, where conv1 and the
+// shortcut conv share the input) runs as its own launch over the same input, so every
+// tile reads one descriptor-addressed gradient.
 const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
+  if (!pin.g2) return wgrad_launch_one(pin, stream);
+  if (pin.co_split <= 0 || pin.co_split >= pin.Cout) return "wgrad: co_split out of range";
+  WgradParams a = pin, b = pin;
+  a.g2 = nullptr; a.Cout = pin.co_split;
+  b.g2 = nullptr; b.g = pin.g2; b.ldg = pin.ldg2; b.Cout = pin.Cout - pin.co_split;
+  b.dw = pin.dw + (long)pin.co_split * pin.ld_dw;
+  const char* e = wgrad_launch_one(a, stream);
+  return e ? e : wgrad_launch_one(b, stream);
+}
+
+static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) {
   WgradParams p = pin;
   const bool fast = (p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0);
   // window form (space-to-depth stem): S taps x C channels = 64 contiguous elements
@@ -227,7 +240,10 @@ const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   if (!fast && p.C % 64 && !window) return "wgrad: C must be a multiple of 64 for the gather path";
   if (p.Cout % 8 || p.ldg % 8 || (fast && p.ldx % 8)) return "wgrad: Cout / ldg / ldx must be multiples of 8";
   if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "wgrad: empty problem";
-  if (!fast && (long)p.N * p.H * p.W * p.C >= (1L << 31)) return "wgrad: input too large";
+  // 31-bit buffer byte offsets (0x80000000 marks out-of-range lanes)
+  if ((fast ? (long)p.M * p.ldx : (long)p.N * p.H * p.W * p.C) * 2 >= (1L << 31) ||
+      (long)p.M * p.ldg * 2 >= (1L << 31))
+    return "wgrad: operand too large for 31-bit buffer offsets";
   const int BM = p.Cout <= 64 ? 64 : 128;
   const int ntiles = ((p.Cout + BM - 1) / BM) * ((p.K + 127) / 128);
   int splits = p.splits;
@@ -248,12 +264,8 @@ const char* wgrad_launch(const WgradParams& pin, hipStream_t stream) {
   mps = (mps + 63) / 64 * 64;
   splits = (p.M + mps - 1) / mps;
   const int nwg = ntiles * splits;
-  const int ns = g_wgrad_variant == 0 ? 2 : g_wgrad_variant;   // 2 stages + 2 blocks/CU beat 3 stages + 1 block (measured)
-#define WG_LAUNCH(F_, BM_)                                                                                   \
-  {                                                                                                         \
-    if (ns == 3) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 3>), dim3(nwg), dim3(256), 0, stream, p, mps);     \
-    else hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 2>), dim3(nwg), dim3(256), 0, stream, p, mps);            \
-  }
+  // 2 LDS stages + 2 blocks/CU (a 3-stage ring at 1 block/CU measured slower and was removed)
+#define WG_LAUNCH(F_, BM_) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 2>), dim3(nwg), dim3(256), 0, stream, p, mps);
   if (BM == 64) {
     if (fast) WG_LAUNCH(true, 64) else WG_LAUNCH(false, 64)
   } else {

@@ -12,6 +12,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "parallel-and-distributed-deep-learning_amd")
 
 
+def _check_undefined(so):
+    """Fail the build if any pddl symbol (e.g. a kernel's host launch stub) stayed undefined:
+    the dynamic loader would only report it at import time on the GPU box."""
+    r = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True)
+    bad = [ln.split()[-1] for ln in r.stdout.splitlines() if "4pddl" in ln]
+    if bad:
+        raise RuntimeError(f"{os.path.basename(so)} has undefined pddl symbols: {bad[:4]}")
+
+
 def build(verbose: bool = False) -> str:
     env = dict(os.environ)
     env.setdefault("PDDL_OFFLOAD_ARCH", "gfx950")
@@ -31,6 +40,7 @@ def build(verbose: bool = False) -> str:
             raise RuntimeError(f"native build produced no {name} shared object")
         dst = os.path.join(PKG, os.path.basename(built[-1]))
         shutil.move(built[-1], dst)
+        _check_undefined(dst)
         out.append(dst)
     return out[0]
 
