@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a HIP graph (1 GPU)")
     args = ap.parse_args()
 
     import torch
@@ -66,7 +67,14 @@ def main():
     flips = torch.randint(0, 2, (64, B), dtype=torch.uint8, device="cuda", generator=gen)
     gscale = 1.0 / (B * world)
 
+    graphed = None
+    if args.graph and world == 1:
+        from pddl.train.graph import GraphedTrainStep
+        graphed = GraphedTrainStep(eng, opt, B, (224, 224), gscale)
+
     def step(i):
+        if graphed is not None:
+            return graphed(images, labels, flips[i % 64])
         cb = None
         if reducer is not None:
             reducer.begin()
@@ -112,6 +120,7 @@ def main():
             "config": {"model": "ResNet-50 Keras-v1 (25,636,712 params, random init)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": args.crop,
                        "parallelism": f"dp{world}", "optimizer": args.optimizer, "bn": "frozen (training=False)",
+                       "hip_graph": bool(graphed is not None),
                        "strategy": "horovod-style 1 proc/GPU, RCCL bucketed all-reduce overlapped with backward"
                        if world > 1 else "single-process"},
             "final_loss": round(loss, 4),

@@ -119,7 +119,8 @@ void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
   ok(pddl::wgrad_launch(p, cur_stream()), "wgrad");
 }
 
-void stem_s2d(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_t oy, int64_t ox, Tensor out) {
+void stem_s2d(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_t oy, int64_t ox, Tensor out,
+              OptT crop_dev) {
   pddl::StemParams p{};
   PCHECK(in.is_cuda() && in.is_contiguous() && in.dim() == 4 && in.size(3) == 3, "stem input must be [B,H,W,3]");
   PCHECK(in.scalar_type() == torch::kUInt8 || in.scalar_type() == torch::kFloat32, "stem input uint8 or fp32");
@@ -127,6 +128,12 @@ void stem_s2d(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_
   p.B = (int)in.size(0); p.Hin = (int)in.size(1); p.Win = (int)in.size(2);
   p.Hc = (int)Hc; p.Wc = (int)Wc; p.mode = (int)mode; p.oy = (int)oy; p.ox = (int)ox;
   if (mode == 2) PCHECK(oy >= 0 && ox >= 0 && oy + Hc <= p.Hin && ox + Wc <= p.Win, "crop window out of range");
+  if (crop_dev.has_value()) {
+    // the caller keeps the device offsets within [0, Hin - Hc] x [0, Win - Wc]
+    PCHECK(crop_dev->is_cuda() && crop_dev->scalar_type() == torch::kInt32 && crop_dev->numel() >= 2,
+           "crop_dev: device int32[2]");
+    p.crop_dev = crop_dev->data_ptr<int32_t>();
+  }
   if (flip.has_value()) {
     PCHECK(flip->scalar_type() == torch::kUInt8 && flip->numel() == p.B && flip->is_cuda(), "flip flags [B] uint8");
     p.flip = flip->data_ptr<uint8_t>();
@@ -208,14 +215,20 @@ void bn_grad(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor 
                           (int)nlayers, f32p(colsum), f32p(dgamma_raw), f32p(scale), (float)eps, cur_stream()),
      "bn_grad");
 }
-void adam(Tensor p, Tensor g, Tensor m, Tensor v, double lr_t, double b1, double b2, double eps, double gscale) {
+void opt_hparams(Tensor hs, double b1, double b2, bool adam) {
+  PCHECK(hs.is_cuda() && hs.scalar_type() == torch::kFloat32 && hs.numel() >= 3, "hparams: device float[>=3]");
+  ok(pddl::opt_hparams_launch(f32p(hs), (float)b1, (float)b2, adam ? 1 : 0, cur_stream()), "opt_hparams");
+}
+void adam(Tensor p, Tensor g, Tensor m, Tensor v, double lr_t, double b1, double b2, double eps, double gscale,
+          OptT hs) {
   ok(pddl::adam_launch(f32p(p), f32p(g), f32p(m), f32p(v), p.numel(), (float)lr_t, (float)b1, (float)b2, (float)eps,
-                       (float)gscale, cur_stream()),
+                       (float)gscale, of32p(hs), cur_stream()),
      "adam");
 }
-void sgd(Tensor p, Tensor g, Tensor mom, double lr, double momentum, double wd, bool nesterov, double gscale) {
+void sgd(Tensor p, Tensor g, Tensor mom, double lr, double momentum, double wd, bool nesterov, double gscale,
+         OptT hs) {
   ok(pddl::sgd_launch(f32p(p), f32p(g), f32p(mom), p.numel(), (float)lr, (float)momentum, (float)wd,
-                      nesterov ? 1 : 0, (float)gscale, cur_stream()),
+                      nesterov ? 1 : 0, (float)gscale, of32p(hs), cur_stream()),
      "sgd");
 }
 void scale_(Tensor x, double a) { ok(pddl::scale_launch(f32p(x), x.numel(), (float)a, cur_stream()), "scale"); }
@@ -256,6 +269,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("prep", &prep);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("bn_grad", &bn_grad);
+  m.def("opt_hparams", &opt_hparams);
   m.def("adam", &adam);
   m.def("sgd", &sgd);
   m.def("scale_", &scale_);

@@ -43,6 +43,7 @@ __device__ __forceinline__ float stem_pix(const StemParams& p, int b, int y, int
 
 // Space-to-depth stem input: one thread per s2d pixel, two 16-byte stores.
 __global__ void stem_s2d_kernel(StemParams p, long npix) {
+  if (p.crop_dev) { p.oy = p.crop_dev[0]; p.ox = p.crop_dev[1]; }   // graph-replayable crop offset
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < npix; q += (long)gridDim.x * blockDim.x) {
     const int j = (int)(q % p.Ws);
     const long t = q / p.Ws;

@@ -57,6 +57,7 @@ struct StemParams {
   int Hc, Wc;                         // preprocessed (cropped / resized) size
   int mode;                           // 0 identity, 1 bilinear resize, 2 crop at (oy, ox)
   int oy, ox;
+  const int32_t* crop_dev;            // optional device {oy, ox} (overrides oy/ox; HIP-graph replays)
   const uint8_t* flip;                // per-image horizontal flip flags (nullable)
   float scale;                        // Rescaling(1/255)
   uint16_t* out; int Hs, Ws;          // space-to-depth image [B][Hs][Ws][16], Hs = (Hc + 6) / 2
@@ -121,10 +122,12 @@ const char* bn_grad_launch(const float* params, float* grads, const BnGradLayer*
                            hipStream_t s);
 
 // ---- optimizers (optim.hip) ----
+// hs (nullable): device {t, lr, lr_t}; when given, the step size is read from hs[2].
+const char* opt_hparams_launch(float* hs, float b1, float b2, int adam, hipStream_t s);
 const char* adam_launch(float* p, const float* g, float* m, float* v, long n, float lr_t, float b1, float b2,
-                        float eps, float gscale, hipStream_t s);
+                        float eps, float gscale, const float* hs, hipStream_t s);
 const char* sgd_launch(float* p, const float* g, float* mom, long n, float lr, float momentum, float wd,
-                       int nesterov, float gscale, hipStream_t s);
+                       int nesterov, float gscale, const float* hs, hipStream_t s);
 const char* scale_launch(float* x, long n, float a, hipStream_t s);
 const char* cast_bf16_launch(const float* x, uint16_t* y, long n, hipStream_t s);
 const char* cast_f32_launch(const uint16_t* x, float* y, long n, hipStream_t s);

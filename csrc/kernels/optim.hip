@@ -13,8 +13,19 @@
 
 namespace pddl {
 
+// Device-resident step hyper-parameters hs = {t, lr, lr_t}: one thread advances the step
+// counter and derives the step size, so a captured training step (HIP graph) replays with
+// the right bias correction and with learning-rate changes the host writes between replays.
+__global__ void opt_hparams_kernel(float* hs, float b1, float b2, int adam) {
+  const float t = hs[0] + 1.f;
+  hs[0] = t;
+  hs[2] = adam ? hs[1] * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t)) : hs[1];
+}
+
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, long n4, float lr_t, float b1, float b2, float eps, float gs) {
+                            float* __restrict__ v, long n4, float lr_t, float b1, float b2, float eps, float gs,
+                            const float* __restrict__ hs) {
+  if (hs) lr_t = hs[2];
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
     const float4 gg = reinterpret_cast<const float4*>(g)[i];
@@ -36,7 +47,8 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 }
 
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ mom, long n4,
-                           float lr, float mu, float wd, int nesterov, float gs) {
+                           float lr, float mu, float wd, int nesterov, float gs, const float* __restrict__ hs) {
+  if (hs) lr = hs[2];
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
     const float4 gg = reinterpret_cast<const float4*>(g)[i];
@@ -71,17 +83,22 @@ static int grid_of(long n) { return (int)lmin((n + 255) / 256, 4096); }
     return e == hipSuccess ? nullptr : hipGetErrorString(e); \
   }
 
+const char* opt_hparams_launch(float* hs, float b1, float b2, int adam, hipStream_t s) {
+  hipLaunchKernelGGL(opt_hparams_kernel, dim3(1), dim3(1), 0, s, hs, b1, b2, adam);
+  LAUNCH_RET
+}
 const char* adam_launch(float* p, const float* g, float* m, float* v, long n, float lr_t, float b1, float b2,
-                        float eps, float gscale, hipStream_t s) {
+                        float eps, float gscale, const float* hs, hipStream_t s) {
   if (n % 4) return "adam: n must be a multiple of 4";
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_of(n / 4)), dim3(256), 0, s, p, g, m, v, n / 4, lr_t, b1, b2, eps, gscale);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_of(n / 4)), dim3(256), 0, s, p, g, m, v, n / 4, lr_t, b1, b2, eps, gscale,
+                     hs);
   LAUNCH_RET
 }
 const char* sgd_launch(float* p, const float* g, float* mom, long n, float lr, float momentum, float wd, int nesterov,
-                       float gscale, hipStream_t s) {
+                       float gscale, const float* hs, hipStream_t s) {
   if (n % 4) return "sgd: n must be a multiple of 4";
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_of(n / 4)), dim3(256), 0, s, p, g, mom, n / 4, lr, momentum, wd, nesterov,
-                     gscale);
+                     gscale, hs);
   LAUNCH_RET
 }
 const char* scale_launch(float* x, long n, float a, hipStream_t s) {

@@ -287,7 +287,10 @@ class HipEngine:
         N, L = self.N, self.L
         mode, oy, ox = self._stem_mode(training, crop_offset)
         x2 = self.stem_x2[:B]
-        N.stem_s2d(images, flip if training else None, mode, self.crop, self.crop, oy, ox, x2)
+        crop_dev = None
+        if mode == 2 and isinstance(crop_offset, torch.Tensor):   # device offsets (graph capture)
+            crop_dev, oy, ox = crop_offset, 0, 0
+        N.stem_s2d(images, flip if training else None, mode, self.crop, self.crop, oy, ox, x2, crop_dev)
         H1, H2, Hs = self.H1, self.H2, self.Hs
         s = L.stem
         c1 = self.c1[:B]

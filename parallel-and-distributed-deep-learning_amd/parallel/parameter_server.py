@@ -161,7 +161,7 @@ class PSServer:
         lr_t = lr * math.sqrt(1 - b2 ** self.t) / (1 - b1 ** self.t)
         if self.params.is_cuda:
             from ..ops.native import native
-            native.adam(self.params, g, self.m, self.v, lr_t, b1, b2, eps, 1.0)
+            native.adam(self.params, g, self.m, self.v, lr_t, b1, b2, eps, 1.0, None)
         else:
             self.m.mul_(b1).add_(g, alpha=1 - b1)
             self.v.mul_(b2).addcmul_(g, g, value=1 - b2)

@@ -1,0 +1,83 @@
+"""HIP-graph capture of the whole training step (preprocess -> forward -> backward ->
+optimizer -> bf16 weight re-prep) for one GPU.
+
+The reference's per-step work is issued op by op by the TF runtime (imagenet-resnet50.py:67
+`model.fit`); here the ~180 kernel launches of a step are recorded once into a HIP graph and
+replayed with a single launch, which removes host launch cost and inter-kernel gaps (it is
+what keeps small per-GPU batches, e.g. the reference's 32, from being launch-bound).
+
+Everything that changes between steps lives in device memory the graph reads:
+  * inputs are copied into static buffers (images, labels, flip flags, crop offset),
+  * the optimizer's step counter and learning rate are the device buffer `opt.hs`
+    (train/optim.py), advanced by a kernel inside the graph; host LR changes are written to
+    it between replays.
+Multi-GPU steps keep eager launches: their collectives are issued from the bucket callbacks.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+
+class GraphedTrainStep:
+    def __init__(self, engine, optimizer, batch: int, image_hw: Tuple[int, int], gscale: float,
+                 image_dtype=torch.uint8):
+        if not engine.params.is_cuda:
+            raise RuntimeError("GraphedTrainStep needs the GPU engine")
+        self.engine, self.opt, self.B, self.gscale = engine, optimizer, batch, float(gscale)
+        dev = engine.params.device
+        H, W = image_hw
+        self.images = torch.zeros(batch, H, W, 3, dtype=image_dtype, device=dev)
+        self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
+        self.flip = torch.zeros(batch, dtype=torch.uint8, device=dev)
+        self.crop = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.stats = None
+
+    def _body(self):
+        eng = self.engine
+        stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip, crop_offset=self.crop)
+        self.opt.step()
+        eng.after_update()
+        return stats
+
+    def _load(self, images, labels, flip, crop_offset):
+        self.images.copy_(images, non_blocking=True)
+        self.labels.copy_(labels, non_blocking=True)
+        if flip is None:
+            self.flip.zero_()
+        else:
+            self.flip.copy_(flip, non_blocking=True)
+        if isinstance(crop_offset, torch.Tensor):
+            self.crop.copy_(crop_offset, non_blocking=True)
+        else:
+            oy, ox = crop_offset
+            H, W = self.images.shape[1:3]
+            c = self.engine.crop
+            if not (0 <= oy <= H - c and 0 <= ox <= W - c) and c < H:
+                raise ValueError("crop offset out of range")
+            self.crop.copy_(torch.tensor([oy, ox], dtype=torch.int32), non_blocking=True)
+
+    def capture(self):
+        """Record the step.  Call after one eager step of the engine (its lazily built tables
+        exist); capture itself runs no kernels, so it does not advance training."""
+        self.opt.sync_hparams()
+        torch.cuda.synchronize()
+        it = self.opt._iterations
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.stats = self._body()
+        self.opt._iterations = it    # the capture pass did not step (no setter: hs is current)
+        self.graph = g
+
+    def __call__(self, images, labels, flip=None, crop_offset=(0, 0)):
+        self._load(images, labels, flip, crop_offset)
+        if self.graph is None:
+            out = self._body()        # first call: eager (builds the engine's tables), then capture
+            self.capture()
+            return out
+        self.opt.sync_hparams()
+        self.graph.replay()
+        self.opt._iterations += 1
+        return self.stats

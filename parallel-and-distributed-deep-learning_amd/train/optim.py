@@ -12,18 +12,55 @@ import torch
 
 
 class FlatOptimizer:
+    """On the GPU the step counter and learning rate live in a device buffer
+    `hs = {t, lr, lr_t}` advanced by a one-thread kernel, so a captured step (HIP graph)
+    replays correctly; host-side changes (LR callbacks, checkpoint restore) are written to it
+    before the next step, outside any capture."""
+
     def __init__(self, engine, lr: float):
         self.engine = engine
         self.n = engine.L.n_trainable
-        self.lr = float(lr)
-        self.iterations = 0          # Keras `optimizer.iterations`
         self.params = engine.params[: self.n]
         self.grads = engine.grads
         self.gscale = 1.0
+        self.hs = torch.zeros(4, dtype=torch.float32, device=self.params.device) if self.params.is_cuda else None
+        self._lr = float(lr)
+        self._iterations = 0         # Keras `optimizer.iterations`
+        self._dirty = True
 
     @property
     def on_gpu(self):
         return self.params.is_cuda
+
+    @property
+    def lr(self):
+        return self._lr
+
+    @lr.setter
+    def lr(self, v):
+        self._lr = float(v)
+        self._dirty = True
+
+    @property
+    def iterations(self):
+        return self._iterations
+
+    @iterations.setter
+    def iterations(self, v):
+        self._iterations = int(v)
+        self._dirty = True
+
+    def sync_hparams(self):
+        """Write host-side lr / step count into the device buffer (never inside a capture)."""
+        if self.hs is not None and self._dirty:
+            self.hs.copy_(torch.tensor([float(self._iterations), self._lr, 0.0, 0.0]), non_blocking=False)
+            self._dirty = False
+
+    def _device_step(self, adam: bool, b1=0.0, b2=0.0):
+        from ..ops.native import native
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_hparams()
+        native.opt_hparams(self.hs, b1, b2, adam)
 
     def state_tensors(self):
         return {}
@@ -37,13 +74,15 @@ class Adam(FlatOptimizer):
         self.v = torch.zeros_like(self.params)
 
     def step(self):
-        self.iterations += 1
-        t = self.iterations
-        lr_t = self.lr * math.sqrt(1 - self.b2 ** t) / (1 - self.b1 ** t)
         if self.on_gpu:
             from ..ops.native import native
-            native.adam(self.params, self.grads, self.m, self.v, lr_t, self.b1, self.b2, self.eps, self.gscale)
+            self._device_step(True, self.b1, self.b2)
+            self._iterations += 1
+            native.adam(self.params, self.grads, self.m, self.v, 0.0, self.b1, self.b2, self.eps, self.gscale, self.hs)
         else:
+            self._iterations += 1
+            t = self._iterations
+            lr_t = self.lr * math.sqrt(1 - self.b2 ** t) / (1 - self.b1 ** t)
             g = self.grads * self.gscale
             self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
             self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
@@ -60,11 +99,13 @@ class SGD(FlatOptimizer):
         self.mom = torch.zeros_like(self.params)
 
     def step(self):
-        self.iterations += 1
         if self.on_gpu:
             from ..ops.native import native
-            native.sgd(self.params, self.grads, self.mom, self.lr, self.mu, self.wd, self.nesterov, self.gscale)
+            self._device_step(False)
+            self._iterations += 1
+            native.sgd(self.params, self.grads, self.mom, 0.0, self.mu, self.wd, self.nesterov, self.gscale, self.hs)
         else:
+            self._iterations += 1
             g = self.grads * self.gscale + self.wd * self.params
             self.mom.mul_(self.mu).sub_(self.lr * g)
             if self.nesterov:

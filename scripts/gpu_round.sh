@@ -23,6 +23,7 @@ for s in "$@"; do
     runtime) step runtime 600 python -m pytest tests/test_gpu_runtime.py -x -q ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    benchg) step benchg 600 python bench.py --steps 20 --warmup 5 --graph 1 ;;
     benchnb) step benchnb 600 env PDDL_BITMASK=0 python bench.py --steps 20 --warmup 5 ;;
     bench64) step bench64 600 python bench.py --steps 20 --warmup 5 --batch 64 ;;
     kbench)  step kbench 600 python bench/kernels.py --json gpurun_out/kbench.json ;;

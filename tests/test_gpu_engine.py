@@ -98,3 +98,40 @@ def test_engine_bitmask_equivalent():
     assert torch.allclose(out[0][0], out[1][0], rtol=1e-5)
     r = ((out[0][1] - out[1][1]).norm() / out[0][1].norm()).item()
     assert r < 1e-4, r
+
+
+def test_graphed_step_matches_eager():
+    """A HIP-graph replay of the full step (fwd, bwd, Adam with device-side step count,
+    weight re-prep) follows the same trajectory as eager steps."""
+    from pddl.models.engine import HipEngine
+    from pddl.models.resnet50 import ParamLayout
+    from pddl.train.graph import GraphedTrainStep
+    from pddl.train.optim import make_optimizer
+    torch.manual_seed(0)
+    B = 4
+    L = ParamLayout()
+    img = torch.randint(0, 256, (4, B, 96, 96, 3), dtype=torch.uint8, device="cuda")
+    lab = torch.randint(0, 1000, (4, B), device="cuda")
+    flips = torch.randint(0, 2, (4, B), dtype=torch.uint8, device="cuda")
+    res = []
+    for graphed in (False, True):
+        he = HipEngine(L, B, crop=80, image_size=96)
+        he.init(seed=7)
+        opt = make_optimizer("adam", he, lr=1e-3)
+        gs = GraphedTrainStep(he, opt, B, (96, 96), 1.0 / B) if graphed else None
+        losses = []
+        for i in range(4):
+            off = (i, 2 * i)
+            if graphed:
+                s = gs(img[i], lab[i], flips[i], off)
+            else:
+                s = he.forward_backward(img[i], lab[i], 1.0 / B, flip=flips[i], crop_offset=off)
+                opt.step()
+                he.after_update()
+            losses.append(s[0].item())
+        res.append((losses, he.params.clone(), opt.iterations))
+    torch.cuda.synchronize()
+    (l0, p0, it0), (l1, p1, it1) = res
+    assert it0 == it1 == 4
+    assert all(abs(a - b) <= 1e-3 * abs(a) for a, b in zip(l0, l1)), (l0, l1)
+    assert ((p0 - p1).norm() / p0.norm()).item() < 1e-4

@@ -313,16 +313,36 @@ def test_optimizers():
     pr, mr, vr = p.clone(), m.clone(), v.clone()
     lr, b1, b2, eps, t = 1e-3, 0.9, 0.999, 1e-7, 3
     lr_t = lr * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
-    N().adam(p, g, m, v, lr_t, b1, b2, eps, 1.0)
+    N().adam(p, g, m, v, lr_t, b1, b2, eps, 1.0, None)
     mr = b1 * mr + (1 - b1) * g
     vr = b2 * vr + (1 - b2) * g * g
     pr = pr - lr_t * mr / (vr.sqrt() + eps)
     assert torch.allclose(p, pr, atol=1e-6) and torch.allclose(m, mr, atol=1e-6) and torch.allclose(v, vr, atol=1e-6)
     mom = torch.randn(n, device=dev)
     p2, mo2 = p.clone(), mom.clone()
-    N().sgd(p, g, mom, 0.1, 0.9, 0.0, False, 1.0)
+    N().sgd(p, g, mom, 0.1, 0.9, 0.0, False, 1.0, None)
     mo2 = 0.9 * mo2 - 0.1 * g
     assert torch.allclose(mom, mo2, atol=1e-6) and torch.allclose(p, p2 + mo2, atol=1e-6)
+
+
+def test_device_hparams_adam_steps():
+    """hs = {t, lr, lr_t} advanced on the device reproduces the host bias-corrected steps."""
+    torch.manual_seed(10)
+    n = 1024
+    p, g = torch.randn(n, device=dev), torch.randn(n, device=dev)
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    lr, b1, b2, eps = 1e-3, 0.9, 0.999, 1e-7
+    hs = torch.tensor([0.0, lr, 0.0, 0.0], device=dev)
+    for t in range(1, 6):
+        N().opt_hparams(hs, b1, b2, True)
+        N().adam(p, g, m, v, 0.0, b1, b2, eps, 1.0, hs)
+        lr_t = lr * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
+        mr = b1 * mr + (1 - b1) * g
+        vr = b2 * vr + (1 - b2) * g * g
+        pr = pr - lr_t * mr / (vr.sqrt() + eps)
+    assert hs[0].item() == 5.0
+    assert torch.allclose(p, pr, atol=1e-6, rtol=1e-5)
 
 
 @pytest.mark.parametrize("mode", ["identity", "resize", "crop"])
@@ -340,7 +360,11 @@ def test_stem_s2d_conv_and_wgrad(mode):
     hs = (crop + 6) // 2
     ho = crop // 2
     x2 = torch.empty(B, hs, hs, 16, dtype=torch.bfloat16, device=dev)
-    N().stem_s2d(img, flip, m, crop, crop, oy, ox, x2)
+    N().stem_s2d(img, flip, m, crop, crop, oy, ox, x2, None)
+    if mode == "crop":   # the device-offset form (graph replays) gives the same image
+        x2d = torch.empty_like(x2)
+        N().stem_s2d(img, flip, m, crop, crop, 0, 0, x2d, torch.tensor([oy, ox], dtype=torch.int32, device=dev))
+        assert torch.equal(x2d, x2)
     x = preprocess(img, crop, True, flip, (oy, ox))                 # NCHW fp32
     ref_x2 = F.pixel_unshuffle(F.pad(x, (3, 3, 3, 3)), 2)           # [B, 3*4, hs, hs]  (c, dy, dx)
     got = x2.float().view(B, hs, hs, 2, 2, 4)[..., :3].permute(0, 5, 3, 4, 1, 2).reshape(B, 12, hs, hs)
