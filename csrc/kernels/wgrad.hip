@@ -16,6 +16,10 @@
 // tiles go through LDS and are added with row-contiguous (256 B per wave instruction)
 // no-return fp32 atomics into the flat fp32 gradient buffer (MI355X_MICROARCH.md "Global
 // float atomics": ~1.3 TB/s chip-wide, so splits are sized to keep atomic bytes small).
+#include <array>
+#include <map>
+#include <mutex>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -32,7 +36,7 @@ __device__ __forceinline__ int tr_swz128(int row) { return (((row >> 1) & 1) | (
 // BM = 128: 2x2 waves, wave tile 64 (co) x 64 (k).  BM = 64 (Cout = 64 layers: the stem and
 // stage 2): 1x4 waves, wave tile 64 x 32, gradient tile with 128-byte rows.
 template <bool FAST, int BM, int NSTAGE>  // NSTAGE: LDS buffers (the loop is written for 2)
-__global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split) {
+__global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split, const int2* __restrict__ rowinfo) {
   constexpr int G_BYTES = 64 * BM * 2;        // 64 m-rows x BM bf16
   constexpr int X_BYTES = 64 * 256;           // 64 m-rows x 128 bf16
   constexpr int STAGE = G_BYTES + X_BYTES;
@@ -53,9 +57,6 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   const int co0 = (tile % tco) * BM, k0 = (tile / tco) * 128;
   const int mbeg = split * m_per_split;
   const int mend = min(p.M, mbeg + m_per_split);
-  const int HoWo = p.Ho * p.Wo;
-  // multiply-shift division constants (the row decode runs for every row of every tile)
-  const uint64_t mg_hw = fdiv_magic(HoWo), mg_w = fdiv_magic(p.Wo);
 
   // buffer descriptors: 32-bit lane offsets, the m-step in the scalar soffset, and
   // out-of-range offsets (padding taps, tile overhang) load zeros
@@ -85,12 +86,29 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
     g_off[i] = co >= p.Cout ? OOB_OFF : (uint32_t)((row * p.ldg + co) * 2);
   }
   uint32_t x_off[4];   // FAST: loop-invariant input offsets
+  int x_delta[4], x_tap[4];   // generic: per-piece element shift of the lane's (r, s, c) and tap bit
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (wave * 4 + i) * 4 + lrow;
-    const int kc = k0 + (lpos ^ tr_swz(row)) * 8;
+    const int chunk = lpos ^ tr_swz(row);
+    const int kc = k0 + chunk * 8;
     x_off[i] = (FAST && kc < p.K) ? (uint32_t)((row * p.ldx + kc) * 2) : OOB_OFF;
+    const int h = chunk >> 3;
+    const int r = h ? hr[1] : hr[0], s = h ? hs[1] : hs[0], c = h ? hc[1] : hc[0];
+    x_delta[i] = (r * p.W + s) * p.C + c + (chunk & 7) * 8;
+    x_tap[i] = (h ? hv[1] : hv[0]) ? r * p.S + s : 31 + 1;   // bit 32: never set -> zero
   }
+  // Generic path: the im2col row geometry comes from a per-layer table rowinfo[m] =
+  // {pixel index of tap (0, 0), bitmask of in-bounds taps}, prefetched one tile ahead into
+  // registers (4 rows per lane), so the gather costs a mask test and one multiply-add.
+  int2 ri[4];
+  auto fetch_rows = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = min(mb + (wave * 4 + i) * 4 + lrow, p.M - 1);
+      ri[i] = rowinfo[m];
+    }
+  };
 
   auto load_tile = [&](int mb, int buf) {
     char* gb = smem + buf * STAGE;
@@ -104,26 +122,16 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // input operand
       const int row = (wave * 4 + i) * 4 + lrow;
-      const int m = mb + row;
-      const bool mok = full || m < mend;
+      const bool mok = full || mb + row < mend;
       if (FAST) {
         buf_lds16(rx, LDS_PTR(xb + (wave * 4 + i) * 1024), mok ? x_off[i] : OOB_OFF, mb * p.ldx * 2);
       } else {
-        const int chunk = lpos ^ tr_swz(row);
-        const int h = chunk >> 3;
-        const int r = h ? hr[1] : hr[0], s = h ? hs[1] : hs[0], c = h ? hc[1] : hc[0];
-        const bool v = h ? hv[1] : hv[0];
-        uint32_t off = OOB_OFF;
-        if (mok && v) {
-          const int n = fdiv(m, mg_hw), rem = m - n * HoWo;
-          const int ho = fdiv(rem, mg_w), wo = rem - ho * p.Wo;
-          const int hi = ho * p.stride - p.pad + r, wi = wo * p.stride - p.pad + s;
-          if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
-            off = (uint32_t)((((n * p.H + hi) * p.W + wi) * p.C + c + (chunk & 7) * 8) * 2);
-        }
+        const bool ok = mok && x_tap[i] < 32 && ((ri[i].y >> x_tap[i]) & 1);
+        const uint32_t off = ok ? (uint32_t)((ri[i].x * p.C + x_delta[i]) * 2) : OOB_OFF;
         buf_lds16(rx, LDS_PTR(xb + (wave * 4 + i) * 1024), off, 0);
       }
     }
+    if (!FAST) fetch_rows(mb + 64);   // next tile's rows (landed by the loop's vmcnt(0))
   };
 
   v4f acc[4][TN];
@@ -137,6 +145,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   const int G = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const int nit = (mend - mbeg + 63) / 64;
   if (nit > 0) {
+    if (!FAST) fetch_rows(mbeg);
     load_tile(mbeg, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -214,6 +223,41 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   }
 }
 
+// rowinfo[m] = {(n*H + ho*stride - pad)*W + wo*stride - pad, bit (r*S + s) set iff tap (r, s)
+// of output row m reads inside the image}.
+__global__ void rowinfo_kernel(int2* __restrict__ out, int M, int Ho, int Wo, int H, int W, int stride, int pad,
+                               int R, int S) {
+  for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
+    const int n = m / (Ho * Wo), rem = m - n * Ho * Wo, ho = rem / Wo, wo = rem - ho * Wo;
+    const int hi = ho * stride - pad, wi = wo * stride - pad;
+    uint32_t mk = 0;
+    for (int r = 0; r < R; ++r)
+      for (int s = 0; s < S; ++s)
+        if ((unsigned)(hi + r) < (unsigned)H && (unsigned)(wi + s) < (unsigned)W) mk |= 1u << (r * S + s);
+    out[m] = make_int2((n * H + hi) * W + wi, (int)mk);
+  }
+}
+
+// One table per (device, geometry), built on first use on the caller's stream and kept for
+// the process lifetime (a handful of geometries per network; first use must not be inside a
+// graph capture -- the engines always run one eager step first).
+static const int2* rowinfo_for(const WgradParams& p, hipStream_t stream, const char** why) {
+  static std::mutex mu;
+  static std::map<std::array<int, 10>, int2*> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  const std::array<int, 10> key{dev, p.M, p.Ho, p.Wo, p.H, p.W, p.stride, p.pad, p.R, p.S};
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int2* buf = nullptr;
+  if (hipMalloc(&buf, sizeof(int2) * (size_t)p.M) != hipSuccess) { *why = "wgrad: rowinfo allocation failed"; return nullptr; }
+  hipLaunchKernelGGL(rowinfo_kernel, dim3((p.M + 255) / 256 < 8192 ? (p.M + 255) / 256 : 8192), dim3(256), 0, stream,
+                     buf, p.M, p.Ho, p.Wo, p.H, p.W, p.stride, p.pad, p.R, p.S);
+  cache[key] = buf;
+  return buf;
+}
+
 int g_wgrad_variant = 0;   // A/B knob (unused: one pipeline depth remains)
 
 static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream);
@@ -240,6 +284,7 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
   if (!fast && p.C % 64 && !window) return "wgrad: C must be a multiple of 64 for the gather path";
   if (p.Cout % 8 || p.ldg % 8 || (fast && p.ldx % 8)) return "wgrad: Cout / ldg / ldx must be multiples of 8";
   if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "wgrad: empty problem";
+  if (!fast && p.R * p.S > 32) return "wgrad: at most 32 taps";
   // 31-bit buffer byte offsets (0x80000000 marks out-of-range lanes)
   if ((fast ? (long)p.M * p.ldx : (long)p.N * p.H * p.W * p.C) * 2 >= (1L << 31) ||
       (long)p.M * p.ldg * 2 >= (1L << 31))
@@ -265,7 +310,13 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
   splits = (p.M + mps - 1) / mps;
   const int nwg = ntiles * splits;
   // 2 LDS stages + 2 blocks/CU (a 3-stage ring at 1 block/CU measured slower and was removed)
-#define WG_LAUNCH(F_, BM_) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 2>), dim3(nwg), dim3(256), 0, stream, p, mps);
+  const int2* ri = nullptr;
+  if (!fast) {
+    const char* why = nullptr;
+    ri = rowinfo_for(p, stream, &why);
+    if (!ri) return why;
+  }
+#define WG_LAUNCH(F_, BM_) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 2>), dim3(nwg), dim3(256), 0, stream, p, mps, ri);
   if (BM == 64) {
     if (fast) WG_LAUNCH(true, 64) else WG_LAUNCH(false, 64)
   } else {

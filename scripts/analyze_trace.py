@@ -48,7 +48,11 @@ def schedule(B, crop):
         ev.append(("wgrad", f"{b.name} c2 wgrad", 2 * M * 9 * f * f, 2 * M * f * 2))
         ev.append(("igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2))
         n1 = 5 * f if b.proj else f
-        ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * n1, (M * n1 + B * H * H * cin) * 2))
+        if b.proj:   # conv1 and the shortcut conv: one wgrad launch per gradient source
+            ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * f, (M * f + B * H * H * cin) * 2))
+            ev.append(("wgrad", f"{b.name} c0 wgrad", 2 * M * cin * 4 * f, (M * 4 * f + B * H * H * cin) * 2))
+        else:
+            ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * n1, (M * n1 + B * H * H * cin) * 2))
         ev.append(("wgrad_finalize", b.name, 0, 0))
         ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2))
     ev.append(("maxpool_bwd", "pool", 0, 0))
@@ -57,6 +61,7 @@ def schedule(B, crop):
     ev.append(("wgrad_finalize", "stem", 0, 0))
     ev.append(("colsum_reduce", "cred", 0, 0))
     ev.append(("bn_grad", "bn", 0, 0))
+    ev.append(("opt_hparams", "hparams", 0, 0))
     ev.append(("adam", "adam", 0, 0))
     ev.append(("prep", "prep", 0, 0))
     return ev
