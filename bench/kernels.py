@@ -86,13 +86,13 @@ def main():
         print(json.dumps(brow), flush=True)
         res.append(brow)
         del am, bm, gm
-        for kind, fn, knob, variants in (("igemm", fwd, "igemm", [2]), ("wgrad", wg, "wgrad", [2])):
+        for kind, fn, knob, variants in (("igemm", fwd, "igemm_big", [0, 2]), ("wgrad", wg, "wgrad", [0])):
             t = {v: [] for v in variants}
             for _ in range(a.rounds):
                 for v in variants:
                     N.set_variant(knob, v)
                     t[v].append(timeit(fn))
-            N.set_variant(knob, 0)
+            N.set_variant(knob, 1 if knob == "igemm_big" else 0)
             row = {"layer": name, "kernel": kind}
             for v in variants:
                 us = statistics.median(t[v])

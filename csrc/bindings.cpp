@@ -93,7 +93,7 @@ void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64
   p.up2 = (int)up2; p.Hf = (int)Hf; p.Wf = (int)Wf;
   p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;
   if (p.colsum)
-    PCHECK(colsum->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn) * p.Nn, "colsum partial buffer too short");
+    PCHECK(colsum->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn, p.K) * p.Nn, "colsum partial buffer too short");
   const int64_t rows_out = up2 ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
   PCHECK(out.numel() / std::max<int64_t>(1, out.size(-1)) >= (out2.has_value() ? p.M : rows_out) ||
              out.dim() >= 2,
@@ -260,6 +260,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_variant", [](const std::string& which, int v) {
     if (which == "igemm") pddl::g_igemm_variant = v;
     else if (which == "igemm_deep") pddl::g_igemm_deep = v;
+    else if (which == "igemm_big") pddl::g_igemm_big = v;
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });

@@ -39,16 +39,22 @@ namespace pddl {
 //   AM_DUAL:   two AM_DIRECT sources concatenated along K (projection-block dgrad).
 enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 
-template <int BM, int BN, int WTM, int WTN, int NSTAGE, int AM>
-__global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
+// Block tile BM x BN of NW waves, each wave a 64x64 tile of 16x16x32 MFMAs.
+//   NW = 4, NSTAGE 1/2: 2 blocks per CU, the next k-tile's LDS-DMA overlaps this tile's MFMAs.
+//   NW = 8 (256x128), NSTAGE 3: one 144 KiB block per CU, 2 waves per SIMD; a 3-deep LDS ring
+//   keeps two k-tiles in flight (counted vmcnt across a raw barrier) for compute-bound layers.
+template <int BM, int BN, int NW, int NSTAGE, int AM>
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmParams p) {
+  constexpr int WTM = 64, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int WAVES_N = BN / WTN;
-  static_assert((BM / WTM) * (BN / WTN) == 4, "4 waves per block");
-  static_assert(NSTAGE == 1 || NSTAGE == 2, "1- or 2-stage LDS pipeline");
+  static_assert((BM / WTM) * (BN / WTN) == NW, "wave grid must cover the block tile");
+  static_assert(NSTAGE >= 1 && NSTAGE <= 3, "1- to 3-stage LDS pipeline");
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  constexpr int AI = BM / 32, BI = BN / 32;  // 1 KiB LDS-DMA pieces per wave per tile
+  constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // 1 KiB LDS-DMA pieces per wave per tile
+  static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows must split evenly over the waves");
   constexpr int EPI_LD = WTN + 4;
-  constexpr int EPI_BYTES = 4 * 32 * EPI_LD * 4;
+  constexpr int EPI_BYTES = NW * 32 * EPI_LD * 4;
   constexpr int SMEM = (NSTAGE * STAGE > EPI_BYTES) ? NSTAGE * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -151,11 +157,25 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   const int a_off = (wm * WTM + (lane & 15)) * 128;
   const int b_off = (wn * WTN + (lane & 15)) * 128;
   load_tile(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (NSTAGE == 3) {
+    if (KT > 1) load_tile(1);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   for (int t = 0; t < KT; ++t) {
-    const int cur = NSTAGE == 2 ? (t & 1) : 0;
-    if (NSTAGE == 2 && t + 1 < KT) load_tile(cur ^ 1);
+    int cur;
+    if (NSTAGE == 3) {
+      // tile t landed (tile t+1 stays in flight across the raw barrier: a __syncthreads()
+      // would drain vmcnt), and every wave finished tile t-1, whose buffer takes tile t+2
+      if (t + 1 < KT) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(AI + BI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      cur = t % 3;
+      if (t + 2 < KT) load_tile((t + 2) % 3);
+    } else {
+      cur = NSTAGE == 2 ? (t & 1) : 0;
+      if (NSTAGE == 2 && t + 1 < KT) load_tile(cur ^ 1);
+    }
     const char* As = smem + cur * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -176,9 +196,12 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
       __syncthreads();            // every wave is done reading the single buffer
       load_tile(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (NSTAGE != 3) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
+  if (NSTAGE == 3) __syncthreads();   // all fragment reads done before the epilogue reuses LDS
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
@@ -307,12 +330,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(IgemmParams p) {
   }
 }
 
-int igemm_partial_rows(int M, int Nn) {
-  const int BM = Nn <= 64 ? 256 : 128;
-  return ((M + BM - 1) / BM) * (BM / 64);
-}
-
-int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth
+int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wave tiles)
+int g_igemm_big = 1;       // 8-wave 256x128 3-stage tile: 0 never, 1 heuristic, 2 always (Nn > 64)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
 
 static bool igemm_no_halo(const IgemmParams& p) {
@@ -338,6 +357,21 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
   return true;
 }
 
+// Tile configuration of a problem: 0 = 256x64 / 4 waves (Nn <= 64), 1 = 128x128 / 4 waves,
+// 2 = 256x128 / 8 waves / 3-stage ring (compute-bound: K >= 256 and >= 2 tiles per CU).
+static int igemm_config(int M, int Nn, int K) {
+  if (Nn <= 64) return 0;
+  const long big_tiles = (long)((M + 255) / 256) * ((Nn + 127) / 128);
+  if (g_igemm_big == 2 || (g_igemm_big == 1 && K >= 256 && big_tiles >= 512)) return 2;
+  return 1;
+}
+static int igemm_bm(int cfg) { return cfg == 1 ? 128 : 256; }
+
+int igemm_partial_rows(int M, int Nn, int K) {
+  const int BM = igemm_bm(igemm_config(M, Nn, K));
+  return ((M + BM - 1) / BM) * (BM / 64);
+}
+
 const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   const char* why = nullptr;
   if (!igemm_check(p_in, &why)) return why;
@@ -352,23 +386,25 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   const int am = p.a2 ? AM_DUAL : (igemm_no_halo(p) ? AM_DIRECT : AM_HALO);
   // (explicit launches per instantiation: taking kernel addresses through a conditional
   // expression leaves the host stubs uninstantiated with this compiler)
-#define IG_GO(BM_, BN_, NS_, AM_) \
-  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 64, 64, NS_, AM_>), dim3(nwg), dim3(256), 0, stream, p)
-#define IG_LAUNCH(BM_, BN_)                                             \
-  {                                                                    \
-    const int nwg = ((p.M + BM_ - 1) / BM_) * ((p.Nn + BN_ - 1) / BN_); \
-    if (ns == 1) {                                                     \
-      if (am == AM_DIRECT) IG_GO(BM_, BN_, 1, AM_DIRECT);              \
-      else if (am == AM_HALO) IG_GO(BM_, BN_, 1, AM_HALO);             \
-      else IG_GO(BM_, BN_, 1, AM_DUAL);                                \
-    } else {                                                           \
-      if (am == AM_DIRECT) IG_GO(BM_, BN_, 2, AM_DIRECT);              \
-      else if (am == AM_HALO) IG_GO(BM_, BN_, 2, AM_HALO);             \
-      else IG_GO(BM_, BN_, 2, AM_DUAL);                                \
-    }                                                                  \
+#define IG_GO(BM_, BN_, NW_, NS_, AM_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, NW_, NS_, AM_>), dim3(nwg), dim3(NW_ * 64), 0, stream, p)
+#define IG_MODES(BM_, BN_, NW_, NS_)                                 \
+  {                                                                  \
+    if (am == AM_DIRECT) IG_GO(BM_, BN_, NW_, NS_, AM_DIRECT);       \
+    else if (am == AM_HALO) IG_GO(BM_, BN_, NW_, NS_, AM_HALO);      \
+    else IG_GO(BM_, BN_, NW_, NS_, AM_DUAL);                         \
   }
-  if (p.Nn <= 64) IG_LAUNCH(256, 64) else IG_LAUNCH(128, 128)
-#undef IG_LAUNCH
+  const int cfg = igemm_config(p.M, p.Nn, p.K);
+  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : 128;
+  const int nwg = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
+  if (cfg == 2) {
+    IG_MODES(256, 128, 8, 3)
+  } else if (cfg == 1) {
+    if (ns == 1) IG_MODES(128, 128, 4, 1) else IG_MODES(128, 128, 4, 2)
+  } else {
+    if (ns == 1) IG_MODES(256, 64, 4, 1) else IG_MODES(256, 64, 4, 2)
+  }
+#undef IG_MODES
 #undef IG_GO
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);

@@ -244,10 +244,11 @@ class HipEngine:
             b = blocks[bi]
             H, Ho = self.geo[b.name]
             M = B * Ho * Ho
-            add(b.convs["2"].name, N.igemm_partial_rows(M, b.filters), b.filters)   # c3 dgrad -> g2
-            add(b.convs["1"].name, N.igemm_partial_rows(M, b.filters), b.filters)   # c2 dgrad -> g1
-            if bi > 0:                                                               # c1 dgrad -> g_out(prev)
-                add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin), b.cin)
+            f = b.filters
+            add(b.convs["2"].name, N.igemm_partial_rows(M, f, 4 * f), f)          # c3 dgrad -> g2
+            add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)          # c2 dgrad -> g1
+            if bi > 0:                                                           # c1 dgrad -> g_out(prev)
+                add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin, 5 * f if b.proj else f), b.cin)
         add(L.stem.name, N.maxpool_bwd_partial_rows(B, self.H1, self.H1, 64), 64)
         res = (offs, self._dev_table(rows), off, len(rows))
         self._cred[B] = res

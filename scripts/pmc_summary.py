@@ -19,19 +19,25 @@ def main(root):
             agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k in sorted(agg):
         c = {n: sum(v) / len(v) for n, v in agg[k].items()}
-        wc = c.get("SQ_WAVE_CYCLES", 0) or 1
-        busy = c.get("SQ_BUSY_CYCLES", 0) or 1
-        line = [k[:70]]
-        if "SQ_WAIT_ANY" in c:
-            line.append(f"wait_any {c['SQ_WAIT_ANY'] / wc:5.2f} wait_inst {c['SQ_WAIT_INST_ANY'] / wc:5.2f} "
-                        f"active {c['SQ_ACTIVE_INST_ANY'] / wc:5.2f} mfma_busy/busy {c['SQ_VALU_MFMA_BUSY_CYCLES'] / busy:6.2f}")
-        if "SQ_LDS_BANK_CONFLICT" in c:
-            line.append(f"lds_conf/active {c['SQ_LDS_BANK_CONFLICT'] / max(1, c['SQ_LDS_IDX_ACTIVE']):5.3f} "
-                        f"valu/mfma {c['SQ_INSTS_VALU'] / max(1, c['SQ_INSTS_MFMA']):5.1f}")
-        if "TCC_HIT_sum" in c:
-            line.append(f"L2 hit {c['TCC_HIT_sum'] / max(1, c['TCC_HIT_sum'] + c['TCC_MISS_sum']):5.2f} "
-                        f"unaligned {c.get('SQ_LDS_UNALIGNED_STALL', 0):.0f}")
-        print(" | ".join(line))
+
+        def ratio(a, b):
+            return c[a] / c[b] if a in c and b in c and c[b] else None
+        derived = {
+            "lds_active/cu_busy": ratio("SQ_LDS_IDX_ACTIVE", "SQ_BUSY_CU_CYCLES"),
+            "mfma_busy/cu_busy": ratio("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES"),
+            "lds_data_fifo_full/cu_busy": ratio("SQ_LDS_DATA_FIFO_FULL", "SQ_BUSY_CU_CYCLES"),
+            "wait_any/wave": ratio("SQ_WAIT_ANY", "SQ_WAVE_CYCLES"),
+            "wait_inst/wave": ratio("SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"),
+            "wait_inst_lds/wave": ratio("SQ_WAIT_INST_LDS", "SQ_WAVE_CYCLES"),
+            "active/wave": ratio("SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES"),
+            "valu/mfma": ratio("SQ_INSTS_VALU", "SQ_INSTS_MFMA"),
+            "salu/mfma": ratio("SQ_INSTS_SALU", "SQ_INSTS_MFMA"),
+            "lds_insts/mfma": ratio("SQ_INSTS_LDS", "SQ_INSTS_MFMA"),
+            "lds_bank_conf/lds_active": ratio("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"),
+            "L2_hit": (c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+                       if "TCC_HIT_sum" in c and (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]) else None),
+        }
+        print(k[:80] + " | " + " ".join(f"{n} {v:.3f}" for n, v in derived.items() if v is not None))
 
 
 if __name__ == "__main__":

@@ -120,7 +120,7 @@ def test_igemm_dgrad(case):
     out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
     wt = dgrad_weights(w, a)
     pd = r - 1 - pad
-    rows = N().igemm_partial_rows(n * ho * ho, cin)
+    rows = N().igemm_partial_rows(n * ho * ho, cin, r * r * co)
     part = torch.full((rows * cin,), float("nan"), device=dev)
     N().igemm(g, None, ho, ho, r, r, 1, pd, ho, ho, wt.view(cin, -1), 1, None, None, None, mask, add, out, 0,
               None, 0, 0, 1 if st == 2 else 0, h, h, part, None)
@@ -130,6 +130,52 @@ def test_igemm_dgrad(case):
     assert rel(out, ref) < 1e-2
     cs = _fold(part, rows, cin)
     assert rel(cs, ref.sum((0, 1, 2))) < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual"])
+def test_igemm_big_tile_matches(kind):
+    """The 8-wave 256x128 3-stage configuration computes the same result (same k order)
+    as the 4-wave 128x128 one, including the fused epilogues."""
+    torch.manual_seed(12)
+    n, h, ho = 3, 14, 7
+    if kind == "fwd3x3":
+        x = rnd(n, h, h, 128)
+        w = rnd(256, 9 * 128, scale=0.05)
+        sc, sh = torch.rand(256, device=dev) + 0.5, torch.randn(256, device=dev)
+    elif kind == "fwd1x1res":
+        x = rnd(n, h, h, 256)
+        w = rnd(320, 256, scale=0.05)
+        sc, sh = torch.rand(320, device=dev) + 0.5, torch.randn(320, device=dev)
+    else:
+        g1, g0 = rnd(n, ho, ho, 128), rnd(n, ho, ho, 512)
+        wt = rnd(256, 640, scale=0.05)
+        mask = rnd(n, h, h, 256)
+    outs = []
+    for big in (0, 2):
+        N().set_variant("igemm_big", big)
+        try:
+            if kind == "fwd3x3":
+                y = torch.empty(n, h, h, 256, dtype=torch.bfloat16, device=dev)
+                N().igemm(x, None, h, h, 3, 3, 1, 1, h, h, w, 0, sc, sh, None, None, None, y, 1, None, 0, 0, 0, 0, 0,
+                          None, None)
+                outs.append(y.float())
+            elif kind == "fwd1x1res":
+                y1 = torch.empty(n, h, h, 64, dtype=torch.bfloat16, device=dev)
+                y2 = torch.empty(n, h, h, 256, dtype=torch.bfloat16, device=dev)
+                bits = torch.zeros(n, h, h, 8, dtype=torch.uint8, device=dev)
+                N().igemm(x, None, h, h, 1, 1, 1, 0, h, h, w, 0, sc, sh, None, None, None, y1, 1, y2, 0, 64, 0, 0, 0,
+                          None, bits)
+                outs.append(torch.cat([y1.float().flatten(), y2.float().flatten(), bits.float().flatten()]))
+            else:
+                out = torch.empty(n, h, h, 256, dtype=torch.bfloat16, device=dev)
+                rows = N().igemm_partial_rows(n * ho * ho, 256, 640)
+                part = torch.full((rows * 256,), float("nan"), device=dev)
+                N().igemm(g1, g0, ho, ho, 1, 1, 1, 0, ho, ho, wt, 1, None, None, None, mask, None, out, 0, None, 0, 0,
+                          1, h, h, part, None)
+                outs.append(torch.cat([out.float().flatten(), _fold(part, rows, 256)]))
+        finally:
+            N().set_variant("igemm_big", 1)
+    assert rel(outs[1], outs[0]) < 1e-5
 
 
 def test_igemm_dgrad_dual_source():
