@@ -92,7 +92,7 @@ def main():
                 for v in variants:
                     N.set_variant(knob, v)
                     t[v].append(timeit(fn))
-            N.set_variant(knob, 1 if knob == "igemm_big" else 0)
+            N.set_variant(knob, 0)
             row = {"layer": name, "kernel": kind}
             for v in variants:
                 us = statistics.median(t[v])

@@ -331,7 +331,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
 }
 
 int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wave tiles)
-int g_igemm_big = 1;       // 8-wave 256x128 3-stage tile: 0 never, 1 heuristic, 2 always (Nn > 64)
+int g_igemm_big = 0;       // 8-wave 256x128 3-stage tile: 0 never (default: measured slower on every
+                           // ResNet-50 layer, kbench A/B), 1 heuristic, 2 always (Nn > 64)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
 
 static bool igemm_no_halo(const IgemmParams& p) {
