@@ -215,6 +215,15 @@ void bn_grad(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor 
                           (int)nlayers, f32p(colsum), f32p(dgamma_raw), f32p(scale), (float)eps, cur_stream()),
      "bn_grad");
 }
+void synth(Tensor idx, int64_t seed, int64_t ncls, Tensor img, Tensor lab) {
+  PCHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt64 && img.scalar_type() == torch::kUInt8 &&
+             lab.scalar_type() == torch::kInt64 && img.is_contiguous() && img.size(0) == idx.numel() &&
+             lab.numel() == idx.numel(),
+         "synth: idx int64 [n], img uint8 [n,...], lab int64 [n]");
+  ok(pddl::synth_launch(idx.data_ptr<int64_t>(), (int)idx.numel(), (long)(img.numel() / std::max<int64_t>(1, idx.numel())),
+                        seed, (int)ncls, img.data_ptr<uint8_t>(), lab.data_ptr<int64_t>(), cur_stream()),
+     "synth");
+}
 void opt_hparams(Tensor hs, double b1, double b2, bool adam) {
   PCHECK(hs.is_cuda() && hs.scalar_type() == torch::kFloat32 && hs.numel() >= 3, "hparams: device float[>=3]");
   ok(pddl::opt_hparams_launch(f32p(hs), (float)b1, (float)b2, adam ? 1 : 0, cur_stream()), "opt_hparams");
@@ -270,6 +279,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("prep", &prep);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("bn_grad", &bn_grad);
+  m.def("synth", &synth);
   m.def("opt_hparams", &opt_hparams);
   m.def("adam", &adam);
   m.def("sgd", &sgd);

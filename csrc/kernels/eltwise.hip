@@ -565,4 +565,48 @@ const char* bn_grad_launch(const float* params, float* grads, const BnGradLayer*
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
+// ---------------------------------------------------------------------- synthetic data
+// Deterministic synthetic ImageNet (data/datasets.py SyntheticImageNet): byte p of example i
+// is a counter-based hash of (seed, i, p) -- the same example has the same pixels in every
+// batch, shard and process.  Integer semantics follow the torch int64 reference exactly
+// (wrapping multiplies, arithmetic right shifts).
+__device__ __forceinline__ int64_t synth_mix(int64_t i, int64_t p, int64_t seed) {
+  uint64_t u = (uint64_t)i * 0x9E3779B1ull + (uint64_t)p * 0x85EBCA77ull + (uint64_t)(seed + 1) * 0xC2B2AE3Dull;
+  int64_t x = (int64_t)u;
+  x ^= x >> 15;
+  x = (int64_t)((uint64_t)x * 0x2C1B3C6Dull);
+  x ^= x >> 12;
+  x = (int64_t)((uint64_t)x * 0x297A2D39ull);
+  x ^= x >> 15;
+  return x;
+}
+__global__ void synth_kernel(const int64_t* __restrict__ idx, int n, long per, int64_t seed, int ncls,
+                             uint8_t* __restrict__ img, int64_t* __restrict__ lab) {
+  const long total4 = (long)n * per / 4;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total4; t += (long)gridDim.x * blockDim.x) {
+    const long e0 = t * 4;
+    const int b = (int)(e0 / per);
+    const long p0 = e0 - (long)b * per;
+    const int64_t i = idx[b];
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w |= (uint32_t)(synth_mix(i, p0 + k, seed) & 255) << (8 * k);
+    reinterpret_cast<uint32_t*>(img)[t] = w;
+  }
+  if (blockIdx.x == 0)
+    for (int b = threadIdx.x; b < n; b += blockDim.x) {
+      const uint64_t v = (uint64_t)idx[b] * 2654435761ull + (uint64_t)seed;
+      lab[b] = (int64_t)(v % (uint64_t)ncls);
+    }
+}
+const char* synth_launch(const int64_t* idx, int n, long per, int64_t seed, int ncls, uint8_t* img, int64_t* lab,
+                         hipStream_t s) {
+  if (per % 4) return "synth: bytes per example must be a multiple of 4";
+  const long total4 = (long)n * per / 4;
+  const int grid = (int)lmin((total4 + 255) / 256, 16384);
+  hipLaunchKernelGGL(synth_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, idx, n, per, seed, ncls, img, lab);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
 }  // namespace pddl

@@ -121,6 +121,10 @@ const char* bn_grad_launch(const float* params, float* grads, const BnGradLayer*
                            const float* colsum, const float* dgamma_raw, const float* scale, float eps,
                            hipStream_t s);
 
+// Deterministic synthetic images / labels for example ids idx[0..n) (uint8 [n][per], int64 [n]).
+const char* synth_launch(const int64_t* idx, int n, long per, int64_t seed, int ncls, uint8_t* img, int64_t* lab,
+                         hipStream_t s);
+
 // ---- optimizers (optim.hip) ----
 // hs (nullable): device {t, lr, lr_t}; when given, the step size is read from hs[2].
 const char* opt_hparams_launch(float* hs, float b1, float b2, int adam, hipStream_t s);

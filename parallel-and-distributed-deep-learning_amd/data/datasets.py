@@ -56,7 +56,15 @@ class SyntheticImageNet(ImageSource):
                     torch.randint(0, self.num_classes, (n,), dtype=torch.int64, device=device, generator=g))
             return self._cache[key]
         # per-example deterministic content (counter-based hash of (seed, example, pixel)):
-        # the same example has the same pixels whatever batch / shard it is fetched in
+        # the same example has the same pixels whatever batch / shard it is fetched in.
+        # On the GPU one native kernel generates the batch (csrc/kernels/eltwise.hip synth).
+        if torch.device(device).type == "cuda":
+            from ..ops.native import require_native
+            ii = torch.as_tensor(np.asarray(idx, dtype=np.int64)).to(device, non_blocking=True)
+            img = torch.empty(n, S, S, 3, dtype=torch.uint8, device=device)
+            lab = torch.empty(n, dtype=torch.int64, device=device)
+            require_native().synth(ii, self.seed, self.num_classes, img, lab)
+            return img, lab
         ii = torch.as_tensor(np.asarray(idx, dtype=np.int64), device=device).view(-1, 1)
         p = torch.arange(S * S * 3, dtype=torch.int64, device=device).view(1, -1)
         x = ii * 0x9E3779B1 + p * 0x85EBCA77 + (self.seed + 1) * 0xC2B2AE3D

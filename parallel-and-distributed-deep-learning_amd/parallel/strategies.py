@@ -187,10 +187,19 @@ class SingleStrategy(Strategy):
         cap = max(self.cfg.batch_size, self.cfg.val_batch_size or 0)
         self.engine, self.opt = self._make_engine_and_opt(self.device, cap)
         self.aug = Augment(self.cfg, self.device, self.cfg.seed)
+        self.graphed = None
+        if self.cfg.graphs and self.device.type == "cuda" and hasattr(self.engine, "wbf"):
+            from ..train.graph import GraphedTrainStep   # HIP-graph replay of the whole step
+            B = self.cfg.batch_size
+            self.graphed = GraphedTrainStep(self.engine, self.opt, B, (self.cfg.image_size, self.cfg.image_size),
+                                            1.0 / B)
 
     def train_step(self, images, labels):
         B = images.shape[0]
         flip, off = self.aug(B)
+        if self.graphed is not None and B == self.graphed.B and tuple(images.shape[1:3]) == self.graphed.images.shape[1:3]:
+            return self.graphed(images.to(self.device, non_blocking=True), labels.to(self.device, non_blocking=True),
+                                flip, off).clone()
         s = self.engine.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off).clone()
         self.opt.step()
         self.engine.after_update()

@@ -438,3 +438,14 @@ def test_stem_s2d_conv_and_wgrad(mode):
     N().stem_wgrad_fold(dw2, dw, 64)
     refw = torch.nn.grad.conv2d_weight(xb, (64, 3, 7, 7), g.float().permute(0, 3, 1, 2), stride=2)
     assert rel(dw.view(64, 7, 7, 3), refw.permute(0, 2, 3, 1)) < 5e-3
+
+
+def test_synth_kernel_matches_cpu_reference():
+    """Device synthetic ImageNet == the torch int64 reference (same pixels for the same ids)."""
+    import numpy as np
+    from pddl.data.datasets import SyntheticImageNet
+    ds = SyntheticImageNet(1000, image_size=16, seed=3)
+    idx = np.array([0, 5, 999, 123, 77], dtype=np.int64)
+    ic, lc = ds.fetch(idx, "cpu")
+    ig, lg = ds.fetch(idx, "cuda")
+    assert torch.equal(ic, ig.cpu()) and torch.equal(lc, lg.cpu())

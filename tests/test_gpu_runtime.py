@@ -75,6 +75,20 @@ def test_single_strategy_fit_and_checkpoint_on_gpu(tmp_path):
         assert torch.equal(st.engine.params[sl].cpu(), st2.engine.params[sl].cpu()), e.name
 
 
+def test_single_strategy_fit_with_hip_graph():
+    """--graphs: the Keras fit loop replays the captured step (random crop offsets and flips
+    flow through device buffers); the run trains and the step count stays Keras-exact."""
+    from pddl.parallel.strategies import make_strategy
+    from pddl.train.trainer import Trainer
+    cfg = _cfg("single", graphs=True, crop=192, max_steps=5)
+    st = make_strategy(cfg)
+    tr = Trainer(cfg, st)
+    h = tr.fit(1, [])
+    assert st.graphed is not None and st.graphed.graph is not None
+    assert st.opt.iterations == 5
+    assert all(map(lambda v: v == v, h.history["loss"]))
+
+
 def test_mirrored_strategy_one_gpu_uses_rccl():
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
