@@ -23,12 +23,13 @@ for s in "$@"; do
     runtime) step runtime 600 python -m pytest tests/test_gpu_runtime.py -x -q ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench256) step bench256 600 python bench.py --steps 20 --warmup 5 --batch 256 ;;
     benchg) step benchg 600 python bench.py --steps 20 --warmup 5 --graph 1 ;;
     benchnb) step benchnb 600 env PDDL_BITMASK=0 python bench.py --steps 20 --warmup 5 ;;
     bench64) step bench64 600 python bench.py --steps 20 --warmup 5 --batch 64 ;;
     kbench)  step kbench 600 python bench/kernels.py --json gpurun_out/kbench.json ;;
     pmc)     step pmc 600 rocprofv3 -i bench/pmc.txt --kernel-trace -d gpurun_out/pmc -o run --output-format csv -- python bench/kernels.py --rounds 1 ;;
     counters) step counters 120 rocprofv3 -L ;;
-    prof)    step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 ;;
+    prof)    step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 6 --warmup 3 ;;
   esac
 done
