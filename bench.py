@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
     ap.add_argument("--crop", type=int, default=224)
     ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
+    ap.add_argument("--bn-mode", default="frozen", choices=["frozen", "train"],
+                    help="frozen = the reference's training=False BN (folded); train = batch statistics")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a HIP graph (1 GPU)")
@@ -43,7 +45,7 @@ def main():
     import torch
     import torch.distributed as dist
     import pddl  # noqa: F401
-    from pddl.models.engine import HipEngine
+    from pddl.models.engine import make_hip_engine
     from pddl.models.resnet50 import ParamLayout
     from pddl.train.optim import make_optimizer
     from pddl.parallel.collectives import BucketAllReducer
@@ -56,7 +58,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     B = args.batch
     L = ParamLayout()
-    eng = HipEngine(L, B, crop=args.crop, image_size=224)
+    eng = make_hip_engine(L, B, bn_mode=args.bn_mode, crop=args.crop, image_size=224)
     eng.init(seed=0)
     reducer = None
     if world > 1:
@@ -122,7 +124,7 @@ def main():
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (uint8 3x224x224, random labels)",
             "config": {"model": "ResNet-50 Keras-v1 (25,636,712 params, random init)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image_size": args.crop,
-                       "parallelism": f"dp{world}", "optimizer": args.optimizer, "bn": "frozen (training=False)",
+                       "parallelism": f"dp{world}", "optimizer": args.optimizer, "bn": "frozen (training=False)" if args.bn_mode == "frozen" else "train (batch statistics)",
                        "hip_graph": bool(graphed is not None),
                        "strategy": "horovod-style 1 proc/GPU, RCCL bucketed all-reduce overlapped with backward"
                        if world > 1 else "single-process"},

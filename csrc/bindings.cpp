@@ -39,10 +39,10 @@ int ld(const Tensor& t) {
 int old(const OptT& t) { return t.has_value() ? ld(*t) : 0; }
 
 // Generic implicit-GEMM (conv forward / dgrad / fp32 dense).
-void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
-           int64_t Ho, int64_t Wo, Tensor b, int64_t mode, OptT scale, OptT shift, OptT res, OptT mask, OptT add,
-           Tensor out, int64_t relu, OptT out2, int64_t relu2, int64_t n_split, int64_t up2, int64_t Hf,
-           int64_t Wf, OptT colsum, OptT bits_out) {
+void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                int64_t Ho, int64_t Wo, Tensor b, int64_t mode, OptT scale, OptT shift, OptT res, OptT mask,
+                OptT add, Tensor out, int64_t relu, OptT out2, int64_t relu2, int64_t n_split, int64_t up2,
+                int64_t Hf, int64_t Wf, OptT colsum, OptT bits_out, OptT stats) {
   pddl::IgemmParams p{};
   PCHECK(a1.is_contiguous(), "A source must be contiguous NHWC");
   p.a1 = bfp(a1);
@@ -94,11 +94,88 @@ void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64
   p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;
   if (p.colsum)
     PCHECK(colsum->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn, p.K) * p.Nn, "colsum partial buffer too short");
+  if (stats.has_value()) {
+    PCHECK(mode == pddl::EPI_FWD, "BN statistics are a forward-epilogue output");
+    p.stats = f32p(*stats);
+    PCHECK(stats->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn, p.K) * 2 * p.Nn,
+           "stats partial buffer too short");
+  }
   const int64_t rows_out = up2 ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
   PCHECK(out.numel() / std::max<int64_t>(1, out.size(-1)) >= (out2.has_value() ? p.M : rows_out) ||
              out.dim() >= 2,
          "output too small");
   ok(pddl::igemm_launch(p, cur_stream()), "igemm");
+}
+
+void igemm(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
+           int64_t Ho, int64_t Wo, Tensor b, int64_t mode, OptT scale, OptT shift, OptT res, OptT mask, OptT add,
+           Tensor out, int64_t relu, OptT out2, int64_t relu2, int64_t n_split, int64_t up2, int64_t Hf,
+           int64_t Wf, OptT colsum, OptT bits_out) {
+  igemm_impl(a1, a2, H, W, R, S, stride, pad, Ho, Wo, b, mode, scale, shift, res, mask, add, out, relu, out2, relu2,
+             n_split, up2, Hf, Wf, colsum, bits_out, c10::nullopt);
+}
+
+// ---- train-mode BatchNormalization (bn.hip)
+int64_t rows_of(const Tensor& t) { return t.numel() / std::max<int64_t>(1, t.size(-1)); }
+void bn_stats(Tensor acc, Tensor table, int64_t nlayers, int64_t max_c, bool training, Tensor params, Tensor mean,
+              Tensor inv, Tensor scale, Tensor shift, double eps, double momentum) {
+  PCHECK(table.is_cuda() && table.numel() == nlayers * (int64_t)sizeof(pddl::BnStatLayer), "bn_stats table size");
+  ok(pddl::bn_stats_launch(f32p(acc), reinterpret_cast<const pddl::BnStatLayer*>(table.data_ptr()), (int)nlayers,
+                           (int)max_c, training ? 1 : 0, f32p(params), f32p(mean), f32p(inv), f32p(scale),
+                           f32p(shift), (float)eps, (float)momentum, cur_stream()),
+     "bn_stats");
+}
+void bn_apply(Tensor z, Tensor a, Tensor b, OptT r, OptT a2, OptT b2, bool relu, Tensor y, OptT bits) {
+  PCHECK(z.is_contiguous() && y.is_contiguous(), "bn_apply: contiguous [.., C] tensors");
+  const int C = (int)z.size(-1);
+  const int64_t M = rows_of(z);
+  PCHECK(y.numel() == z.numel() && a.numel() >= C && b.numel() >= C, "bn_apply shapes");
+  if (r.has_value()) PCHECK(r->is_contiguous() && r->numel() == z.numel(), "bn_apply residual shape");
+  PCHECK(a2.has_value() == b2.has_value(), "bn_apply: a2 and b2 go together");
+  if (bits.has_value())
+    PCHECK(bits->scalar_type() == torch::kUInt8 && bits->is_contiguous() && bits->numel() * 8 >= z.numel(),
+           "bn_apply bits");
+  ok(pddl::bn_apply_launch(bfp(z), f32p(a), f32p(b), obfp(r), of32p(a2), of32p(b2), relu ? 1 : 0, bfpm(y),
+                           bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr, M, C, cur_stream()),
+     "bn_apply");
+}
+void bn_bwd_reduce(Tensor g, Tensor z, OptT z2, Tensor mean, OptT mean2, Tensor sg, Tensor sgx, OptT sg2,
+                   OptT sgx2) {
+  PCHECK(g.is_contiguous() && z.is_contiguous() && g.numel() == z.numel(), "bn_bwd_reduce shapes");
+  const int64_t C = z.size(-1);
+  PCHECK(mean.numel() >= C && sg.numel() >= C && sgx.numel() >= C, "bn_bwd_reduce per-channel arrays");
+  if (z2.has_value())
+    PCHECK(z2->is_contiguous() && z2->numel() == z.numel() && mean2.has_value() && sg2.has_value() &&
+               sgx2.has_value() && mean2->numel() >= C && sg2->numel() >= C && sgx2->numel() >= C,
+           "bn_bwd_reduce z2");
+  ok(pddl::bn_bwd_reduce_launch(bfp(g), bfp(z), obfp(z2), f32p(mean), of32p(mean2), rows_of(z), (int)C, f32p(sg),
+                                f32p(sgx), sg2.has_value() ? f32p(*sg2) : nullptr,
+                                sgx2.has_value() ? f32p(*sgx2) : nullptr, cur_stream()),
+     "bn_bwd_reduce");
+}
+pddl::BnBwdLayer bn_layer(const std::vector<double>& v) {
+  PCHECK(v.size() == 6, "BN layer: (C, ch, gamma_off, beta_off, bias_off, count)");
+  pddl::BnBwdLayer l{};
+  l.C = (int)v[0]; l.ch = (int)v[1]; l.gamma_off = (int)v[2]; l.beta_off = (int)v[3]; l.bias_off = (int)v[4];
+  l.count = (float)v[5];
+  return l;
+}
+void bn_bwd_apply(Tensor g, Tensor z, OptT z2, std::vector<double> l, std::vector<double> l2, Tensor params,
+                  Tensor mean, Tensor inv, Tensor sg, Tensor sgx, Tensor dz, OptT dz2, Tensor grads) {
+  PCHECK(g.is_contiguous() && z.is_contiguous() && dz.is_contiguous() && g.numel() == z.numel() &&
+             dz.numel() == z.numel(),
+         "bn_bwd_apply shapes");
+  const pddl::BnBwdLayer L1 = bn_layer(l);
+  PCHECK(L1.C == z.size(-1), "bn_bwd_apply: layer channels");
+  pddl::BnBwdLayer L2 = L1;
+  if (z2.has_value()) {
+    PCHECK(z2->is_contiguous() && z2->numel() == z.numel() && dz2 && dz2->numel() == z.numel(), "bn_bwd_apply z2");
+    L2 = bn_layer(l2);
+  }
+  ok(pddl::bn_bwd_apply_launch(bfp(g), bfp(z), obfp(z2), L1, L2, f32p(params), f32p(mean), f32p(inv), f32p(sg),
+                               f32p(sgx), bfpm(dz), dz2.has_value() ? bfpm(*dz2) : nullptr, f32p(grads), rows_of(z),
+                               cur_stream()),
+     "bn_bwd_apply");
 }
 
 void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Ho,
@@ -256,6 +333,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_fusion(m);
   register_loader(m);
   m.def("igemm", &igemm);
+  m.def("igemm_bn", &igemm_impl);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.attr("BNSTAT_LAYER_BYTES") = (int)sizeof(pddl::BnStatLayer);
   m.def("wgrad", &wgrad);
   m.def("stem_s2d", &stem_s2d);
   m.def("stem_wgrad_fold", &stem_wgrad_fold);

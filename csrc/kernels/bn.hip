@@ -1,0 +1,260 @@
+// Train-mode BatchNormalization (batch statistics) for CDNA4 (gfx950).
+//
+// The reference calls the backbone with training=False (imagenet-resnet50.py:57),
+// so its 53 BatchNormalization layers are per-channel affines that the frozen path folds into
+// the conv epilogues.  `bn_mode=train` (Keras BN with training=True: FusedBatchNormV3 with
+// batch statistics, momentum 0.99, epsilon 1.001e-5) runs here instead:
+//
+//   forward   conv igemm epilogue  -> z (bf16) + per-wave partial (sum z, sum z^2)   [igemm.hip]
+//             colsum_reduce        -> per-channel (S, Q)                              [eltwise.hip]
+//             bn_stats             -> mean, 1/sigma, scale = gamma/sigma, shift = beta - mean*scale,
+//                                     moving statistics update (unbiased variance)
+//             bn_apply             -> y = relu(z*scale + shift (+ residual | + bn(z0))) + ReLU bitmask
+//   backward  bn_bwd_reduce        -> Sg = sum g, Sgx = sum g*(z - mean) (mean-centred: no cancellation)
+//             bn_bwd_apply         -> dz = gamma/sigma * (g - Sg/M - (z-mean)/sigma^2 * Sgx/M),
+//                                     dgamma = Sgx/sigma, dbeta = Sg, dbias = 0
+//
+// Every elementwise pass moves 16 bytes (8 channels) per lane; per-channel coefficients are
+// recomputed from a handful of cached floats instead of a separate coefficient kernel.
+#include "common.h"
+#include "kernels.h"
+
+namespace pddl {
+
+static int bn_grid(long n) { return (int)lmin((n + 255) / 256, 16384); }
+
+// ------------------------------------------------------------------------------ stats
+__global__ void bn_stats_kernel(const float* __restrict__ acc, const BnStatLayer* __restrict__ L, int training,
+                                float* __restrict__ prm, float* __restrict__ mean, float* __restrict__ inv,
+                                float* __restrict__ scale, float* __restrict__ shift, float eps, float momentum) {
+  const BnStatLayer l = L[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= l.C) return;
+  float mu, var;
+  if (training) {
+    const double S = acc[l.sum_off + c], Q = acc[l.sq_off + c], n = l.count;
+    const double m = S / n;
+    double v = Q / n - m * m;
+    v = v > 0.0 ? v : 0.0;
+    mu = (float)m; var = (float)v;
+    // Keras moving statistics: mean and Bessel-corrected variance, momentum 0.99
+    float& mm = prm[l.mm_off + c];
+    float& mv = prm[l.mv_off + c];
+    mm = mm * momentum + (1.f - momentum) * mu;
+    mv = mv * momentum + (1.f - momentum) * (float)(v * n / (n > 1.0 ? n - 1.0 : 1.0));
+  } else {
+    mu = prm[l.mm_off + c]; var = prm[l.mv_off + c];
+  }
+  const float is = rsqrtf(var + eps);
+  const float a = prm[l.gamma_off + c] * is;
+  mean[l.ch + c] = mu;
+  inv[l.ch + c] = is;
+  scale[l.ch + c] = a;
+  shift[l.ch + c] = prm[l.beta_off + c] - mu * a;
+}
+
+const char* bn_stats_launch(const float* acc, const BnStatLayer* layers_dev, int nlayers, int max_c, int training,
+                            float* params, float* mean, float* inv, float* scale, float* shift, float eps,
+                            float momentum, hipStream_t s) {
+  hipLaunchKernelGGL(bn_stats_kernel, dim3((max_c + 255) / 256, nlayers), dim3(256), 0, s, acc, layers_dev, training,
+                     params, mean, inv, scale, shift, eps, momentum);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ------------------------------------------------------------------------------ apply
+// y = act(z*a + b (+ r | + r*a2 + b2)); bits (nullable) = ReLU bitmask of the stored y.
+__global__ void bn_apply_kernel(const bf16_t* __restrict__ z, const float* __restrict__ a, const float* __restrict__ b,
+                                const bf16_t* __restrict__ r, const float* __restrict__ a2,
+                                const float* __restrict__ b2, int relu, bf16_t* __restrict__ y,
+                                uint8_t* __restrict__ bits, long M, int C) {
+  // the grid stride is a multiple of C/8 (a power of two <= 256): every lane keeps one
+  // channel group, so its per-channel coefficients are loaded once
+  const int cg = C >> 3;
+  const long total = M * cg;
+  const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int c0 = (int)(t0 % cg) * 8;
+  float sa[8], sb[8], ra[8], rb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sa[e] = a[c0 + e]; sb[e] = b[c0 + e];
+    ra[e] = a2 ? a2[c0 + e] : 1.f; rb[e] = a2 ? b2[c0 + e] : 0.f;
+  }
+  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(z)[t], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] * sa[e] + sb[e];
+    if (r) {
+      float rv[8];
+      unpack8(reinterpret_cast<const uint4*>(r)[t], rv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rv[e] * ra[e] + rb[e];
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    const uint4 pk = pack8(v);
+    reinterpret_cast<uint4*>(y)[t] = pk;
+    if (bits) bits[t] = (uint8_t)pos_bits8(pk);
+  }
+}
+
+const char* bn_apply_launch(const uint16_t* z, const float* a, const float* b, const uint16_t* r, const float* a2,
+                            const float* b2, int relu, uint16_t* y, uint8_t* bits, long M, int C, hipStream_t s) {
+  if (C % 8 || 256 % (C / 8)) return "bn_apply: C/8 must divide 256";
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_grid(M * (C / 8))), dim3(256), 0, s, z, a, b, r, a2, b2, relu, y, bits,
+                     M, C);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ----------------------------------------------------------------------- bwd reduce
+// Per channel: Sg += sum_m g, Sgx += sum_m g*(z - mean), Sgx2 += sum_m g*(z2 - mean2).
+// A block takes a contiguous row range; lane (row-slot, column-group) keeps 8 channels in
+// registers, the row slots are folded through LDS and one fp32 atomic per channel and block
+// lands in the per-step workspace.
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ z,
+                                                            const bf16_t* __restrict__ z2,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ mean2, long M, int C,
+                                                            float* __restrict__ sg, float* __restrict__ sgx,
+                                                            float* __restrict__ sg2, float* __restrict__ sgx2) {
+  __shared__ float red[3][256 * 8 / 1];   // [sum][slot * G + col-group][e] folded below
+  const int G = C >> 3;                 // column groups (<= 256)
+  const int RPI = 256 / G;              // row slots per iteration
+  const int tid = threadIdx.x;
+  const int cgi = tid % G, slot = tid / G;
+  const long rows_per = (M + gridDim.x - 1) / gridDim.x;
+  const long r0 = blockIdx.x * rows_per, r1 = lmin(M, r0 + rows_per);
+  float s0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], mu2[8];
+  const int c0 = cgi * 8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mu[e] = mean[c0 + e]; mu2[e] = z2 ? mean2[c0 + e] : 0.f; }
+  if (slot < RPI) {
+    for (long row = r0 + slot; row < r1; row += RPI) {
+      const long o = row * G + cgi;
+      float gv[8], zv[8];
+      unpack8(reinterpret_cast<const uint4*>(g)[o], gv);
+      unpack8(reinterpret_cast<const uint4*>(z)[o], zv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s0[e] += gv[e]; s1[e] += gv[e] * (zv[e] - mu[e]); }
+      if (z2) {
+        unpack8(reinterpret_cast<const uint4*>(z2)[o], zv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s2[e] += gv[e] * (zv[e] - mu2[e]);
+      }
+    }
+  }
+  // fold the row slots: red[k][slot*G*8 + cgi*8 + e] (RPI * G <= 256 lanes -> <= 2048 floats)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][tid * 8 + e] = s0[e];
+    red[1][tid * 8 + e] = s1[e];
+    red[2][tid * 8 + e] = s2[e];
+  }
+  __syncthreads();
+  // thread t < C finalizes channel t: sum over slots of red[k][(slot*G + t/8)*8 + t%8]
+  for (int c = tid; c < C; c += 256) {
+    const int cg2 = c >> 3, e = c & 7;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int sl = 0; sl < RPI; ++sl) {
+      const int idx = (sl * G + cg2) * 8 + e;
+      a0 += red[0][idx]; a1 += red[1][idx]; a2 += red[2][idx];
+    }
+    unsafeAtomicAdd(sg + c, a0);
+    unsafeAtomicAdd(sgx + c, a1);
+    if (z2) {   // the projection shortcut's BN sees the same gradient
+      unsafeAtomicAdd(sg2 + c, a0);
+      unsafeAtomicAdd(sgx2 + c, a2);
+    }
+  }
+}
+
+const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const float* mean,
+                                 const float* mean2, long M, int C, float* sg, float* sgx, float* sg2,
+                                 float* sgx2, hipStream_t s) {
+  if (C % 8 || C > 2048) return "bn_bwd_reduce: C must be a multiple of 8 and <= 2048";
+  const int G = C / 8, rpi = 256 / G;
+  long nb = (M + (long)rpi * 64 - 1) / ((long)rpi * 64);   // >= 64 row iterations per lane
+  nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((int)nb), dim3(256), 0, s, g, z, z2, mean, mean2, M, C, sg, sgx,
+                     sg2, sgx2);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ------------------------------------------------------------------------ bwd apply
+__device__ __forceinline__ void bn_bwd_coef(const BnBwdLayer& l, const float* prm, const float* mean,
+                                            const float* inv, const float* sg, const float* sgx, int c, float* A,
+                                            float* B, float* Cc, float* mu) {
+  const float is = inv[l.ch + c];
+  const float ga = prm[l.gamma_off + c] * is;
+  const float rn = 1.f / l.count;
+  *A = ga;
+  *B = -ga * is * is * sgx[l.ch + c] * rn;
+  *Cc = -ga * sg[l.ch + c] * rn;
+  *mu = mean[l.ch + c];
+}
+
+// dz = A*g + B*(z - mean) + C (and dz2 from z2 with layer l2's coefficients; same g).
+// dz may alias g (each lane reads its g before writing).
+__global__ void bn_bwd_apply_kernel(const bf16_t* g, const bf16_t* __restrict__ z, const bf16_t* __restrict__ z2,
+                                    BnBwdLayer l, BnBwdLayer l2, const float* __restrict__ prm,
+                                    const float* __restrict__ mean, const float* __restrict__ inv,
+                                    const float* __restrict__ sg, const float* __restrict__ sgx, bf16_t* dz,
+                                    bf16_t* dz2, float* __restrict__ grads, long M) {
+  const int C = l.C, cg = C >> 3;
+  const long total = M * cg;
+  if (blockIdx.x == 0) {   // parameter gradients of the BN layer(s) and the conv bias
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      grads[l.gamma_off + c] = sgx[l.ch + c] * inv[l.ch + c];
+      grads[l.beta_off + c] = sg[l.ch + c];
+      if (l.bias_off >= 0) grads[l.bias_off + c] = 0.f;   // BN removes any per-channel shift
+      if (z2) {
+        grads[l2.gamma_off + c] = sgx[l2.ch + c] * inv[l2.ch + c];
+        grads[l2.beta_off + c] = sg[l2.ch + c];
+        if (l2.bias_off >= 0) grads[l2.bias_off + c] = 0.f;
+      }
+    }
+  }
+  const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int c0 = (int)(t0 % cg) * 8;   // fixed per lane: the grid stride is a multiple of C/8
+  float A[8], B[8], Cc[8], mu[8], A2[8], B2[8], C2[8], mu2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bn_bwd_coef(l, prm, mean, inv, sg, sgx, c0 + e, &A[e], &B[e], &Cc[e], &mu[e]);
+    if (z2) bn_bwd_coef(l2, prm, mean, inv, sg, sgx, c0 + e, &A2[e], &B2[e], &C2[e], &mu2[e]);
+  }
+  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
+    float gv[8], zv[8], o[8];
+    unpack8(reinterpret_cast<const uint4*>(g)[t], gv);
+    unpack8(reinterpret_cast<const uint4*>(z)[t], zv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = A[e] * gv[e] + B[e] * (zv[e] - mu[e]) + Cc[e];
+    if (z2) {
+      float o2[8];
+      unpack8(reinterpret_cast<const uint4*>(z2)[t], zv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o2[e] = A2[e] * gv[e] + B2[e] * (zv[e] - mu2[e]) + C2[e];
+      reinterpret_cast<uint4*>(dz2)[t] = pack8(o2);
+    }
+    reinterpret_cast<uint4*>(dz)[t] = pack8(o);
+  }
+}
+
+const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const BnBwdLayer& l,
+                                const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
+                                const float* sg, const float* sgx, uint16_t* dz, uint16_t* dz2, float* grads, long M,
+                                hipStream_t s) {
+  if (l.C % 8 || 256 % (l.C / 8)) return "bn_bwd_apply: C/8 must divide 256";
+  if (z2 && (l2.C != l.C || !dz2)) return "bn_bwd_apply: second source must match";
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(M * (l.C / 8))), dim3(256), 0, s, g, z, z2, l, l2, params,
+                     mean, inv, sg, sgx, dz, dz2, grads, M);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+}  // namespace pddl

@@ -216,6 +216,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
   int ldo = p.ldo, col = gn;
   bool seg0 = true;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // FWD stats: sum of squares
   if (p.mode != EPI_DGRAD && col_ok) {
     const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
     const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
@@ -262,6 +263,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
           *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pk;
           if (p.bits_out && seg0) {
             p.bits_out[(long)gm * p.ld_bits_out + (col >> 3)] = (uint8_t)pos_bits8(pk);
+          }
+          if (p.stats) {   // batch statistics of exactly the values the BN-apply pass will read
+            float rv[8];
+            unpack8(pk, rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { csum[e] += rv[e]; csq[e] += rv[e] * rv[e]; }
           }
         } else if (p.mode == EPI_F32) {
           float* o = reinterpret_cast<float*>(p.out) + (long)gm * p.ldo + gn;
@@ -326,6 +333,26 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
       float4* dst = reinterpret_cast<float4*>(p.colsum + (long)(tm * (BM / WTM) + wm) * p.Nn + gn);
       dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
       dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
+    }
+  }
+  // Train-mode BN: per-wave partial (sum, sum of squares) rows of the forward output, same
+  // row indexing as the column sums; colsum_reduce folds them and bn_stats finalizes.
+  if (p.stats) {
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        csum[e] += __shfl_xor(csum[e], o, 64);
+        csq[e] += __shfl_xor(csq[e], o, 64);
+      }
+    if (rr == 0 && col_ok) {
+      float* row = p.stats + (long)(tm * (BM / WTM) + wm) * 2 * p.Nn;
+      float4* d1 = reinterpret_cast<float4*>(row + gn);
+      float4* d2 = reinterpret_cast<float4*>(row + p.Nn + gn);
+      d1[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      d1[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
+      d2[0] = make_float4(csq[0], csq[1], csq[2], csq[3]);
+      d2[1] = make_float4(csq[4], csq[5], csq[6], csq[7]);
     }
   }
 }

@@ -32,6 +32,8 @@ struct IgemmParams {
   // ReLU masks as bitmasks (bit e of byte [row][c/8] = value[row][8*(c/8)+e] > 0):
   uint8_t* bits_out; int ld_bits_out;               // FWD: write the mask of the (segment-0) output
   const uint8_t* bits_mask; int ld_bits_mask;       // DGRAD: multiply by the bit instead of (mask > 0)
+  float* stats;                                     // FWD: per-wave partial [rows][2*Nn]: sum | sum of squares
+                                                    //      of the stored outputs (train-mode BN batch statistics)
   uint64_t mg_howo, mg_wo;                          // set by igemm_launch: magic divisors (fdiv)
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
@@ -120,6 +122,38 @@ struct BnGradLayer {
 const char* bn_grad_launch(const float* params, float* grads, const BnGradLayer* layers_dev, int nlayers,
                            const float* colsum, const float* dgamma_raw, const float* scale, float eps,
                            hipStream_t s);
+
+// ---- train-mode BatchNormalization (bn.hip) ----
+// Batch statistics of one BN layer from the reduced (sum, sum of squares) of its conv output.
+struct BnStatLayer {
+  int C;
+  int sum_off, sq_off;     // offsets of the reduced sums in `acc`
+  int ch;                  // offset in the per-channel mean / inv / scale / shift arrays
+  int gamma_off, beta_off, mm_off, mv_off;   // flat parameter offsets
+  float count;             // N * H * W
+  int pad;
+};
+// training: batch statistics + moving-statistics update; else the moving statistics.
+const char* bn_stats_launch(const float* acc, const BnStatLayer* layers_dev, int nlayers, int max_c, int training,
+                            float* params, float* mean, float* inv, float* scale, float* shift, float eps,
+                            float momentum, hipStream_t s);
+// y = act(z*a + b (+ r*a2 + b2 | + r)) over [M][C] bf16; bits (nullable) = ReLU bitmask of y.
+const char* bn_apply_launch(const uint16_t* z, const float* a, const float* b, const uint16_t* r, const float* a2,
+                            const float* b2, int relu, uint16_t* y, uint8_t* bits, long M, int C, hipStream_t s);
+// sg[c] += sum g, sgx[c] += sum g*(z-mean[c]) (sg2/sgx2 for z2/mean2, nullable).
+const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const float* mean,
+                                 const float* mean2, long M, int C, float* sg, float* sgx, float* sg2, float* sgx2,
+                                 hipStream_t s);
+struct BnBwdLayer {
+  int C, ch;                             // channels, per-channel array offset
+  int gamma_off, beta_off, bias_off;     // flat offsets (params for gamma, grads for all)
+  float count;
+};
+// dz = gamma/sigma * (g - Sg/M - (z - mean)/sigma^2 * Sgx/M); BN/bias parameter grads.
+const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const BnBwdLayer& l,
+                                const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
+                                const float* sg, const float* sgx, uint16_t* dz, uint16_t* dz2, float* grads, long M,
+                                hipStream_t s);
 
 // Deterministic synthetic images / labels for example ids idx[0..n) (uint8 [n][per], int64 [n]).
 const char* synth_launch(const int64_t* idx, int n, long per, int64_t seed, int ncls, uint8_t* img, int64_t* lab,

@@ -42,10 +42,14 @@ def _ceil(a, b):
 
 
 class HipEngine:
+    BN_MODES = ("frozen",)   # HipEngineBNTrain (models/engine_bn.py) runs bn_mode="train"
+
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
-        if bn_mode != "frozen":
-            raise NotImplementedError("HipEngine: bn_mode='train' runs on the TorchEngine path for now")
+        if bn_mode not in self.BN_MODES:
+            raise ValueError(f"{type(self).__name__} runs bn_mode in {self.BN_MODES}, not {bn_mode!r} "
+                             "(use make_hip_engine)")
+        self.bn_mode = bn_mode
         self.N = require_native()
         self.L = layout
         self.device = torch.device(device)
@@ -134,8 +138,7 @@ class HipEngine:
                 name, cout, R, cin = c.name, c.cout, c.k, c.cin
                 kpad = STEM_K if c is L.stem else _ceil(R * R * cin, 64)
                 bias = L.off(c.name, "bias")
-                gam, bet = L.off(c.bn, "gamma"), L.off(c.bn, "beta")
-                mu, var = L.off(c.bn, "moving_mean"), L.off(c.bn, "moving_variance")
+                gam, bet, mu, var = self._fold_offsets(c)
                 wd_off, ld = wd.get(c.name, -1), wd_ld.get(c.name, 0)
             mode = 1 if c is L.stem else 0
             rows.append(struct.pack(_PREP_FMT, L.off(name, "kernel"), cout, R, R, cin, kpad, wf[name], wd_off, ld,
@@ -167,6 +170,12 @@ class HipEngine:
                               self.ch["dense"], -1))
         self._bng_tab = self._dev_table(bg)
         self._bng_n = len(bg)
+
+    def _fold_offsets(self, c):
+        """BN parameters folded into a conv's forward epilogue / dgrad weights (frozen BN)."""
+        L = self.L
+        return (L.off(c.bn, "gamma"), L.off(c.bn, "beta"), L.off(c.bn, "moving_mean"),
+                L.off(c.bn, "moving_variance"))
 
     def _dev_table(self, rows: List[bytes]) -> torch.Tensor:
         buf = bytearray(b"".join(rows))
@@ -460,3 +469,11 @@ class HipEngine:
         N.softmax_xent(self.logits[:B], lab, self.num_classes, 0.0, self.dlogits[:B], self.stats[0:1],
                        self.stats[1:2])
         return self.stats
+
+
+def make_hip_engine(layout: ParamLayout, batch: int, bn_mode: str = "frozen", **kw) -> HipEngine:
+    """HIP engine for the BN mode: frozen (reference `training=False`, folded) or train."""
+    if bn_mode == "train":
+        from .engine_bn import HipEngineBNTrain
+        return HipEngineBNTrain(layout, batch, bn_mode="train", **kw)
+    return HipEngine(layout, batch, bn_mode=bn_mode, **kw)

@@ -1,0 +1,287 @@
+"""Train-mode BatchNormalization on the MI355X (csrc/kernels/bn.hip + the igemm statistics
+epilogue + models/engine_bn.py) against plain PyTorch fp32 references."""
+import struct
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+EPS = 1.001e-5
+
+
+def N():
+    from pddl.ops.native import require_native
+    return require_native()
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def rnd(*shape, scale=1.0, shift=0.0):
+    return (torch.randn(*shape, device=dev) * scale + shift).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("case", [(2, 14, 64, 64, 1, 1, 0), (3, 9, 64, 128, 3, 1, 1), (2, 7, 256, 320, 1, 1, 0)])
+def test_igemm_stats_epilogue(case):
+    """Partial (sum, sum^2) rows of the forward output reduce to the column statistics."""
+    torch.manual_seed(0)
+    n, h, c, co, r, st, pad = case
+    nat = N()
+    x = rnd(n, h, h, c)
+    w = rnd(co, r, r, c, scale=0.05)
+    ho = (h + 2 * pad - r) // st + 1
+    M = n * ho * ho
+    K = r * r * c
+    ones = torch.ones(co, device=dev)
+    bias = torch.randn(co, device=dev)
+    out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
+    rows = nat.igemm_partial_rows(M, co, K)
+    part = torch.full((rows * 2 * co,), float("nan"), device=dev)
+    nat.igemm_bn(x, None, h, h, r, r, st, pad, ho, ho, w.view(co, -1), 0, ones, bias, None, None, None, out, 0, None,
+                 0, 0, 0, 0, 0, None, None, part)
+    acc = torch.zeros(2 * co, device=dev)
+    tab = torch.frombuffer(bytearray(struct.pack("<q4i", 0, rows, 2 * co, 0, 0)), dtype=torch.uint8).to(dev)
+    nat.colsum_reduce(part, tab, 1, acc)
+    y = out.float().view(M, co)
+    assert rel(acc[:co], y.sum(0)) < 1e-4
+    assert rel(acc[co:], (y * y).sum(0)) < 1e-4
+
+
+def _stat_table(C, count, ch, offs):
+    return torch.frombuffer(bytearray(struct.pack("<8ifi", C, 0, C, ch, *offs, float(count), 0)),
+                            dtype=torch.uint8).to(dev)
+
+
+def test_bn_stats_apply_and_backward():
+    """Full per-layer train-BN step vs torch autograd of batch_norm(training=True) + residual + ReLU."""
+    torch.manual_seed(1)
+    nat = N()
+    M, C = 3000, 128
+    z = rnd(M, C, scale=2.0, shift=0.7)
+    r = rnd(M, C)
+    zf = z.float()
+    # flat params: gamma | beta | moving mean | moving var
+    prm = torch.cat([torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1,
+                     torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5])
+    prm0 = prm.clone()
+    acc = torch.cat([zf.sum(0), (zf * zf).sum(0)])
+    mean, inv, sc, sh = (torch.zeros(C, device=dev) for _ in range(4))
+    nat.bn_stats(acc, _stat_table(C, M, 0, (0, C, 2 * C, 3 * C)), 1, C, True, prm, mean, inv, sc, sh, EPS, 0.99)
+    bm, bv = zf.mean(0), zf.var(0, unbiased=False)
+    assert rel(mean, bm) < 1e-5 and rel(inv, torch.rsqrt(bv + EPS)) < 1e-4
+    assert rel(prm[2 * C:3 * C], 0.99 * prm0[2 * C:3 * C] + 0.01 * bm) < 1e-5
+    assert rel(prm[3 * C:], 0.99 * prm0[3 * C:] + 0.01 * zf.var(0, unbiased=True)) < 1e-4
+    y = torch.empty_like(z)
+    bits = torch.empty(M, C // 8, dtype=torch.uint8, device=dev)
+    nat.bn_apply(z, sc, sh, r, None, None, True, y, bits)
+    g_ = prm0[:C].clone().requires_grad_(True)
+    b_ = prm0[C:2 * C].clone().requires_grad_(True)
+    zz = zf.clone().requires_grad_(True)
+    yref = torch.relu(torch.nn.functional.batch_norm(zz, None, None, g_, b_, training=True, eps=EPS) + r.float())
+    assert rel(y, yref) < 1e-2
+    want_bits = (y.float() > 0).view(M, C // 8, 8).to(torch.int32)
+    packed = (want_bits << torch.arange(8, device=dev, dtype=torch.int32)).sum(-1).to(torch.uint8)
+    assert torch.equal(bits, packed)
+    # backward: g = dL/d(BN output) given the ReLU mask (as the dgrad epilogue delivers it)
+    gy = rnd(M, C)
+    g = (gy.float() * (yref > 0).float()).to(torch.bfloat16)
+    yref.backward(gy.float())
+    sg, sgx = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    nat.bn_bwd_reduce(g, z, None, mean, None, sg, sgx, None, None)
+    grads = torch.zeros(3 * C, device=dev)
+    dz = torch.empty_like(g)
+    nat.bn_bwd_apply(g, z, None, [C, 0, 0, C, 2 * C, M], [], prm0, mean, inv, sg, sgx, dz, None, grads)
+    assert rel(dz, zz.grad) < 2e-2
+    assert rel(grads[:C], g_.grad) < 1e-2 and rel(grads[C:2 * C], b_.grad) < 1e-2
+    assert grads[2 * C:].abs().max().item() == 0.0
+
+
+def test_bn_dual_source_backward_in_place():
+    """Projection block: BN3 and BN0 see the same gradient; dz0 overwrites g in place."""
+    torch.manual_seed(2)
+    nat = N()
+    M, C = 2048, 256
+    z3, z0 = rnd(M, C, shift=0.3), rnd(M, C, scale=3.0)
+    g = rnd(M, C)
+    prm = torch.cat([torch.rand(2 * C, device=dev) + 0.5, torch.zeros(2 * C, device=dev)])  # gamma3|gamma0|beta3|beta0
+    mean = torch.cat([z3.float().mean(0), z0.float().mean(0)])
+    inv = torch.cat([torch.rsqrt(z3.float().var(0, unbiased=False) + EPS),
+                     torch.rsqrt(z0.float().var(0, unbiased=False) + EPS)])
+    sg, sgx = torch.zeros(2 * C, device=dev), torch.zeros(2 * C, device=dev)
+    nat.bn_bwd_reduce(g, z3, z0, mean[:C], mean[C:], sg[:C], sgx[:C], sg[C:], sgx[C:])
+    grads = torch.zeros(6 * C, device=dev)
+    g_ref = g.float().clone()
+    dz3 = torch.empty_like(g)
+    nat.bn_bwd_apply(g, z3, z0, [C, 0, 0, 2 * C, 4 * C, M], [C, C, C, 3 * C, 5 * C, M], prm, mean, inv, sg, sgx,
+                     dz3, g, grads)
+    for zi, gi, dzi, off in ((z3, 0, dz3, 0), (z0, 1, g, C)):
+        zz = zi.float().clone().requires_grad_(True)
+        ga = prm[off:off + C].clone().requires_grad_(True)
+        out = torch.nn.functional.batch_norm(zz, None, None, ga, None, training=True, eps=EPS)
+        out.backward(g_ref)
+        assert rel(dzi, zz.grad) < 2e-2
+        assert rel(grads[off:off + C], ga.grad) < 1e-2
+
+
+def _engines(B, crop, image_size):
+    from pddl.models.engine import make_hip_engine
+    from pddl.models.reference import TorchEngine
+    from pddl.models.resnet50 import ParamLayout
+    L = ParamLayout()
+    he = make_hip_engine(L, B, bn_mode="train", crop=crop, image_size=image_size)
+    te = TorchEngine(L, B, crop=crop, device="cuda", bn_mode="train")
+    he.init(seed=3)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    host = he.params.cpu()
+    for e in L.entries.values():
+        sl = host[e.offset:e.offset + e.size]
+        if e.kind == "gamma":
+            # Train-mode BN makes a randomly initialised ResNet-50 chaotic: the bf16 rounding of
+            # the activations (~0.4% per layer) grows ~7% per conv and reaches ~50% relative
+            # difference at conv5 (scripts/debug_bn_train.py), with every layer individually
+            # exact.  Small residual-branch gammas (as in zero-init-residual training) keep the
+            # blocks near identity so the end-to-end comparison stays meaningful.
+            lo = 0.1 if e.layer.endswith("_3_bn") else 0.5
+            sl.copy_(lo + (0.2 if lo < 0.5 else 1.0) * torch.rand(e.size, generator=g))
+        elif e.kind in ("beta", "bias"):
+            sl.copy_(0.1 * torch.randn(e.size, generator=g))
+    he.params.copy_(host.cuda())
+    he.after_update()
+    te.params.copy_(he.params)
+    return L, he, te
+
+
+def _nchw(t):
+    return t.float().permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("crop,image_size", [(128, 128), (112, 128)])
+def test_train_bn_engine_matches_reference(crop, image_size):
+    """Forward end to end against the fp32 reference; backward layer by layer.
+
+    Train-mode BN makes a randomly initialised ResNet-50 chaotic: bf16 rounding of the
+    activations (~0.4% per layer, each layer individually exact) grows ~7% per conv end to end
+    (scripts/debug_bn_train.py).  So the forward is compared end to end with small
+    residual-branch gammas, and every backward stage is checked against fp32 autograd /
+    torch conv gradients applied to the engine's OWN bf16 inputs of that stage."""
+    from torch.nn.grad import conv2d_input, conv2d_weight
+    torch.manual_seed(0)
+    B = 8
+    L, he, te = _engines(B, crop, image_size)
+    img = torch.randint(0, 256, (B, image_size, image_size, 3), dtype=torch.uint8, device="cuda")
+    lab = torch.randint(0, 1000, (B,), device="cuda")
+    flip = torch.randint(0, 2, (B,), dtype=torch.uint8, device="cuda")
+    off = (3, 7) if crop < image_size else (0, 0)
+    rec = []
+    orig = he._bn_bwd
+
+    def spy(g, z, c, M, out, z2=None, c2=None, out2=None):
+        gin = g.clone()
+        orig(g, z, c, M, out, z2, c2, out2)
+        rec.append((c.name, gin, z.clone(), out.clone(), None if z2 is None else (c2.name, z2.clone(), out2.clone())))
+    he._bn_bwd = spy
+    s_h = he.forward_backward(img, lab, 1.0 / B, flip=flip, crop_offset=off).clone()
+    s_t = te.forward_backward(img, lab, 1.0 / B, flip=flip, crop_offset=off)
+    torch.cuda.synchronize()
+    assert abs(s_h[0].item() - s_t[0].item()) / s_t[0].item() < 0.01
+    # ---- forward / moving statistics / head gradients end to end
+    for e in L.entries.values():
+        if e.kind in ("moving_mean", "moving_variance"):
+            assert rel(he.params[e.offset:e.offset + e.size], te.params[e.offset:e.offset + e.size]) < 0.05, e.name
+    for name in ("dense/kernel:0", "dense/bias:0"):
+        e = L.entries[name]
+        assert rel(he.grads[e.offset:e.offset + e.size], te.grads[e.offset:e.offset + e.size]) < 0.05, name
+    # ---- backward, stage by stage, from the engine's own inputs
+    by = {r[0]: r for r in rec}
+    for r in rec:   # BN backward: dz (and the shortcut's dz0) + gamma / beta grads
+        name, g, z, dz, extra = r
+        pairs = [(name, z, dz)] + ([extra] if extra else [])
+        for cname, zi, dzi in pairs:
+            c = next(cc for cc in L.convs if cc.name == cname)
+            zz = _nchw(zi).requires_grad_(True)
+            ga = he.params[L.off(c.bn, "gamma"):][:c.cout].clone().requires_grad_(True)
+            be = torch.zeros(c.cout, device=dev, requires_grad=True)
+            torch.nn.functional.batch_norm(zz, None, None, ga, be, training=True, eps=EPS).backward(_nchw(g))
+            assert rel(_nchw(dzi), zz.grad) < 0.03, cname
+            assert rel(he.grads[L.off(c.bn, "gamma"):][:c.cout], ga.grad) < 0.03, cname
+            assert rel(he.grads[L.off(c.bn, "beta"):][:c.cout], be.grad) < 0.03, cname
+
+    def wview(c):
+        e = L.entry(c.name, "kernel")
+        return e
+
+    def check_wgrad(c, x, dz, stride, pad):
+        e = wview(c)
+        want = conv2d_weight(_nchw(x), (c.cout, c.cin, c.k, c.k), _nchw(dz), stride=stride, padding=pad)
+        got = he.grads[e.offset:e.offset + e.size].view(c.cout, c.k, c.k, c.cin).permute(0, 3, 1, 2)
+        assert rel(got, want) < 0.03, c.name
+
+    def wt(c):
+        e = wview(c)
+        return he.params[e.offset:e.offset + e.size].view(c.cout, c.k, c.k, c.cin).permute(0, 3, 1, 2)
+
+    blocks = L.blocks
+    for bi, b in enumerate(blocks):
+        a = he.acts[b.name]
+        c1, c2, c3 = b.convs["1"], b.convs["2"], b.convs["3"]
+        x_in = he.acts[blocks[bi - 1].name]["out"][:B] if bi > 0 else he.pool[:B]
+        dz3 = by[c3.name][3]
+        dz2 = by[c2.name][3]
+        dz1 = by[c1.name][3]
+        check_wgrad(c3, a["y2"][:B], dz3, 1, 0)
+        check_wgrad(c2, a["y1"][:B], dz2, 1, 1)
+        check_wgrad(c1, x_in, dz1, b.stride, 0)
+        # dgrads (bf16 weights, as the engine multiplies them), ReLU masks of the stored activations
+        g2 = conv2d_input(_nchw(a["y2"][:B]).shape, wt(c3).bfloat16().float(), _nchw(dz3)) * (_nchw(a["y2"][:B]) > 0)
+        assert rel(_nchw(by[c2.name][1]), g2) < 0.03, b.name
+        g1 = conv2d_input(_nchw(a["y1"][:B]).shape, wt(c2).bfloat16().float(), _nchw(dz2), padding=1) \
+            * (_nchw(a["y1"][:B]) > 0)
+        assert rel(_nchw(by[c1.name][1]), g1) < 0.03, b.name
+        gx = conv2d_input(_nchw(x_in).shape, wt(c1).bfloat16().float(), _nchw(dz1), stride=b.stride)
+        if b.proj:
+            c0 = b.convs["0"]
+            dz0 = by[c3.name][4][2]
+            check_wgrad(c0, x_in, dz0, b.stride, 0)
+            gx = gx + conv2d_input(_nchw(x_in).shape, wt(c0).bfloat16().float(), _nchw(dz0), stride=b.stride)
+        else:
+            gx = gx + _nchw(by[c3.name][1])          # residual gradient
+        gx = gx * (_nchw(x_in) > 0)
+        if bi > 0:
+            assert rel(_nchw(by[blocks[bi - 1].convs["3"].name][1]), gx) < 0.03, b.name
+    # stem: max-pool routing, BN backward (checked above) and the 7x7/s2 weight gradient
+    from pddl.models.reference import preprocess
+    xs = preprocess(img, crop, True, flip, off).to(torch.bfloat16).float()
+    dzs = by[L.stem.name][3]
+    want = conv2d_weight(torch.nn.functional.pad(xs, (3, 3, 3, 3)), (64, 3, 7, 7), _nchw(dzs), stride=2)
+    e = L.entry(L.stem.name, "kernel")
+    assert rel(he.grads[e.offset:e.offset + e.size].view(64, 7, 7, 3).permute(0, 3, 1, 2), want) < 0.03
+    # the conv biases feed batch-statistics BN: their gradient is exactly zero
+    for c in L.convs:
+        e = L.entry(c.name, "bias")
+        assert he.grads[e.offset:e.offset + e.size].abs().max().item() == 0.0
+    # inference uses the (updated) moving statistics
+    ev_h = he.evaluate(img, lab).clone()
+    ev_t = te.evaluate(img, lab)
+    assert abs(ev_h[0].item() - ev_t[0].item()) / ev_t[0].item() < 0.03
+
+
+def test_train_bn_engine_trains_and_graphs():
+    from pddl.train.graph import GraphedTrainStep
+    from pddl.train.optim import make_optimizer
+    torch.manual_seed(0)
+    B = 8
+    L, he, _ = _engines(B, 96, 96)
+    opt = make_optimizer("adam", he, lr=1e-3)
+    img = torch.randint(0, 256, (B, 96, 96, 3), dtype=torch.uint8, device="cuda")
+    lab = torch.randint(0, 10, (B,), device="cuda")
+    gs = GraphedTrainStep(he, opt, B, (96, 96), 1.0 / B)
+    losses = []
+    for _ in range(12):
+        s = gs(img, lab)
+        losses.append(s[0].item() / B)
+    assert losses[-1] < losses[0] * 0.5, losses
+    assert torch.isfinite(he.evaluate(img, lab)).all()
