@@ -161,7 +161,7 @@ pddl::BnBwdLayer bn_layer(const std::vector<double>& v) {
   return l;
 }
 void bn_bwd_apply(Tensor g, Tensor z, OptT z2, std::vector<double> l, std::vector<double> l2, Tensor params,
-                  Tensor mean, Tensor inv, Tensor sg, Tensor sgx, Tensor dz, OptT dz2, Tensor grads) {
+                  Tensor mean, Tensor inv, Tensor sg, Tensor sgx, Tensor dz, OptT dz2, Tensor grads, Tensor coef) {
   PCHECK(g.is_contiguous() && z.is_contiguous() && dz.is_contiguous() && g.numel() == z.numel() &&
              dz.numel() == z.numel(),
          "bn_bwd_apply shapes");
@@ -172,9 +172,14 @@ void bn_bwd_apply(Tensor g, Tensor z, OptT z2, std::vector<double> l, std::vecto
     PCHECK(z2->is_contiguous() && z2->numel() == z.numel() && dz2 && dz2->numel() == z.numel(), "bn_bwd_apply z2");
     L2 = bn_layer(l2);
   }
+  const int64_t ldc = coef.numel() / 3;
+  PCHECK(ldc >= mean.numel() && ldc >= L1.ch + L1.C && ldc >= L2.ch + L2.C, "bn_bwd_apply: coef is [3][>= channels]");
+  PCHECK(mean.numel() >= L1.ch + L1.C && mean.numel() >= L2.ch + L2.C && inv.numel() == mean.numel() &&
+             sg.numel() >= mean.numel() && sgx.numel() >= mean.numel(),
+         "bn_bwd_apply: per-channel arrays too short for the layer offsets");
   ok(pddl::bn_bwd_apply_launch(bfp(g), bfp(z), obfp(z2), L1, L2, f32p(params), f32p(mean), f32p(inv), f32p(sg),
-                               f32p(sgx), bfpm(dz), dz2.has_value() ? bfpm(*dz2) : nullptr, f32p(grads), rows_of(z),
-                               cur_stream()),
+                               f32p(sgx), f32p(coef), (int)ldc, bfpm(dz), dz2.has_value() ? bfpm(*dz2) : nullptr,
+                               f32p(grads), rows_of(z), cur_stream()),
      "bn_bwd_apply");
 }
 

@@ -14,14 +14,15 @@
 //             bn_bwd_apply         -> dz = gamma/sigma * (g - Sg/M - (z-mean)/sigma^2 * Sgx/M),
 //                                     dgamma = Sgx/sigma, dbeta = Sg, dbias = 0
 //
-// Every elementwise pass moves 16 bytes (8 channels) per lane; per-channel coefficients are
-// recomputed from a handful of cached floats instead of a separate coefficient kernel.
+// Every elementwise pass moves 16 bytes (8 channels) per lane and keeps one channel group per
+// lane (grid stride a multiple of C/8), so its per-channel coefficients load once.
 #include "common.h"
 #include "kernels.h"
 
 namespace pddl {
 
-static int bn_grid(long n) { return (int)lmin((n + 255) / 256, 16384); }
+// ~8 blocks of 256 lanes per CU; lanes loop so their per-channel setup is amortized
+static int bn_grid(long n) { return (int)lmin((n + 255) / 256, 2048); }
 
 // ------------------------------------------------------------------------------ stats
 __global__ void bn_stats_kernel(const float* __restrict__ acc, const BnStatLayer* __restrict__ L, int training,
@@ -134,6 +135,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
 #pragma unroll
   for (int e = 0; e < 8; ++e) { mu[e] = mean[c0 + e]; mu2[e] = z2 ? mean2[c0 + e] : 0.f; }
   if (slot < RPI) {
+#pragma unroll 4
     for (long row = r0 + slot; row < r1; row += RPI) {
       const long o = row * G + cgi;
       float gv[8], zv[8];
@@ -178,8 +180,10 @@ const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uin
                                  float* sgx2, hipStream_t s) {
   if (C % 8 || C > 2048) return "bn_bwd_reduce: C must be a multiple of 8 and <= 2048";
   const int G = C / 8, rpi = 256 / G;
-  long nb = (M + (long)rpi * 64 - 1) / ((long)rpi * 64);   // >= 64 row iterations per lane
-  nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+  // >= 8 row iterations per lane, <= 1024 blocks, and <= ~256K atomics per call
+  long nb = M / ((long)rpi * 8);
+  const long cap = lmin(1024, 262144 / C);
+  nb = nb < 1 ? 1 : (nb > cap ? cap : nb);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((int)nb), dim3(256), 0, s, g, z, z2, mean, mean2, M, C, sg, sgx,
                      sg2, sgx2);
   hipError_t e = hipGetLastError();
@@ -187,72 +191,77 @@ const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uin
 }
 
 // ------------------------------------------------------------------------ bwd apply
-__device__ __forceinline__ void bn_bwd_coef(const BnBwdLayer& l, const float* prm, const float* mean,
-                                            const float* inv, const float* sg, const float* sgx, int c, float* A,
-                                            float* B, float* Cc, float* mu) {
-  const float is = inv[l.ch + c];
-  const float ga = prm[l.gamma_off + c] * is;
-  const float rn = 1.f / l.count;
-  *A = ga;
-  *B = -ga * is * is * sgx[l.ch + c] * rn;
-  *Cc = -ga * sg[l.ch + c] * rn;
-  *mu = mean[l.ch + c];
+// Per channel (one thread each): dz = A*g + B*z + C with A = gamma/sigma,
+// B = -A/sigma^2 * Sgx/M (Sgx = sum g*(z-mean)), C = -A*Sg/M - B*mean; and the parameter
+// gradients dgamma = Sgx/sigma, dbeta = Sg, dbias = 0 (BN removes any per-channel shift).
+__global__ void bn_bwd_coef_kernel(BnBwdLayer l, const float* __restrict__ prm, const float* __restrict__ mean,
+                                   const float* __restrict__ inv, const float* __restrict__ sg,
+                                   const float* __restrict__ sgx, float* __restrict__ coef, int ldc,
+                                   float* __restrict__ grads) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= l.C) return;
+  const int k = l.ch + c;
+  const float is = inv[k], s0 = sg[k], s1 = sgx[k], rn = 1.f / l.count;
+  const float A = prm[l.gamma_off + c] * is;
+  const float B = -A * is * is * s1 * rn;
+  coef[k] = A;
+  coef[ldc + k] = B;
+  coef[2 * ldc + k] = -A * s0 * rn - B * mean[k];
+  grads[l.gamma_off + c] = s1 * is;
+  grads[l.beta_off + c] = s0;
+  if (l.bias_off >= 0) grads[l.bias_off + c] = 0.f;
 }
 
-// dz = A*g + B*(z - mean) + C (and dz2 from z2 with layer l2's coefficients; same g).
-// dz may alias g (each lane reads its g before writing).
-__global__ void bn_bwd_apply_kernel(const bf16_t* g, const bf16_t* __restrict__ z, const bf16_t* __restrict__ z2,
-                                    BnBwdLayer l, BnBwdLayer l2, const float* __restrict__ prm,
-                                    const float* __restrict__ mean, const float* __restrict__ inv,
-                                    const float* __restrict__ sg, const float* __restrict__ sgx, bf16_t* dz,
-                                    bf16_t* dz2, float* __restrict__ grads, long M) {
-  const int C = l.C, cg = C >> 3;
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(p);
+  *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(p + 4);
+}
+
+// dz = A*g + B*z + C (and dz2 from z2 with the second layer's coefficients; same g).
+// dz / dz2 may alias g (each lane reads its g before writing).  The grid stride is a
+// multiple of C/8, so a lane's 24 (or 48) coefficients are loaded once.
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* g, const bf16_t* __restrict__ z,
+                                                           const bf16_t* __restrict__ z2,
+                                                           const float* __restrict__ c1, const float* __restrict__ c2,
+                                                           int ldc, bf16_t* dz, bf16_t* dz2, long M, int C) {
+  const int cg = C >> 3;
   const long total = M * cg;
-  if (blockIdx.x == 0) {   // parameter gradients of the BN layer(s) and the conv bias
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      grads[l.gamma_off + c] = sgx[l.ch + c] * inv[l.ch + c];
-      grads[l.beta_off + c] = sg[l.ch + c];
-      if (l.bias_off >= 0) grads[l.bias_off + c] = 0.f;   // BN removes any per-channel shift
-      if (z2) {
-        grads[l2.gamma_off + c] = sgx[l2.ch + c] * inv[l2.ch + c];
-        grads[l2.beta_off + c] = sg[l2.ch + c];
-        if (l2.bias_off >= 0) grads[l2.bias_off + c] = 0.f;
-      }
-    }
-  }
   const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const int c0 = (int)(t0 % cg) * 8;   // fixed per lane: the grid stride is a multiple of C/8
-  float A[8], B[8], Cc[8], mu[8], A2[8], B2[8], C2[8], mu2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    bn_bwd_coef(l, prm, mean, inv, sg, sgx, c0 + e, &A[e], &B[e], &Cc[e], &mu[e]);
-    if (z2) bn_bwd_coef(l2, prm, mean, inv, sg, sgx, c0 + e, &A2[e], &B2[e], &C2[e], &mu2[e]);
-  }
+  const int c0 = (int)(t0 % cg) * 8;
+  float A[8], B[8], Cc[8], A2[8], B2[8], C2[8];
+  load8(c1 + c0, A); load8(c1 + ldc + c0, B); load8(c1 + 2 * ldc + c0, Cc);
+  if (z2) { load8(c2 + c0, A2); load8(c2 + ldc + c0, B2); load8(c2 + 2 * ldc + c0, C2); }
   for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
     float gv[8], zv[8], o[8];
     unpack8(reinterpret_cast<const uint4*>(g)[t], gv);
     unpack8(reinterpret_cast<const uint4*>(z)[t], zv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = A[e] * gv[e] + B[e] * (zv[e] - mu[e]) + Cc[e];
+    float o2[8];
     if (z2) {
-      float o2[8];
-      unpack8(reinterpret_cast<const uint4*>(z2)[t], zv);
+      float wv[8];
+      unpack8(reinterpret_cast<const uint4*>(z2)[t], wv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o2[e] = A2[e] * gv[e] + B2[e] * (zv[e] - mu2[e]) + C2[e];
-      reinterpret_cast<uint4*>(dz2)[t] = pack8(o2);
+      for (int e = 0; e < 8; ++e) o2[e] = A2[e] * gv[e] + B2[e] * wv[e] + C2[e];
     }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = A[e] * gv[e] + B[e] * zv[e] + Cc[e];
     reinterpret_cast<uint4*>(dz)[t] = pack8(o);
+    if (z2) reinterpret_cast<uint4*>(dz2)[t] = pack8(o2);
   }
 }
 
 const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const BnBwdLayer& l,
                                 const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
-                                const float* sg, const float* sgx, uint16_t* dz, uint16_t* dz2, float* grads, long M,
-                                hipStream_t s) {
+                                const float* sg, const float* sgx, float* coef, int ldc, uint16_t* dz, uint16_t* dz2,
+                                float* grads, long M, hipStream_t s) {
   if (l.C % 8 || 256 % (l.C / 8)) return "bn_bwd_apply: C/8 must divide 256";
   if (z2 && (l2.C != l.C || !dz2)) return "bn_bwd_apply: second source must match";
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(M * (l.C / 8))), dim3(256), 0, s, g, z, z2, l, l2, params,
-                     mean, inv, sg, sgx, dz, dz2, grads, M);
+  const int cb = (l.C + 255) / 256;
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(cb), dim3(256), 0, s, l, params, mean, inv, sg, sgx, coef, ldc, grads);
+  if (z2)
+    hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(cb), dim3(256), 0, s, l2, params, mean, inv, sg, sgx, coef, ldc,
+                       grads);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(M * (l.C / 8))), dim3(256), 0, s, g, z, z2, coef + l.ch,
+                     coef + l2.ch, ldc, dz, dz2, M, l.C);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

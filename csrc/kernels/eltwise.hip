@@ -353,7 +353,9 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRe
 }
 const char* colsum_reduce_launch(const float* part, const ColRedLayer* layers_dev, int nlayers, float* colsum,
                                  hipStream_t s) {
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(128, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
+  // 512 row chunks per layer: every CU gets work even for one large layer (chunks past a
+  // small layer's rows exit at once); one atomic per column per chunk
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(512, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

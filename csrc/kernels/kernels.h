@@ -150,10 +150,11 @@ struct BnBwdLayer {
   float count;
 };
 // dz = gamma/sigma * (g - Sg/M - (z - mean)/sigma^2 * Sgx/M); BN/bias parameter grads.
+// coef: scratch [3][ldc] per-channel (A, B, C) indexed by the layers' channel offsets.
 const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const BnBwdLayer& l,
                                 const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
-                                const float* sg, const float* sgx, uint16_t* dz, uint16_t* dz2, float* grads, long M,
-                                hipStream_t s);
+                                const float* sg, const float* sgx, float* coef, int ldc, uint16_t* dz, uint16_t* dz2,
+                                float* grads, long M, hipStream_t s);
 
 // Deterministic synthetic images / labels for example ids idx[0..n) (uint8 [n][per], int64 [n]).
 const char* synth_launch(const int64_t* idx, int n, long per, int64_t seed, int ncls, uint8_t* img, int64_t* lab,

@@ -51,6 +51,7 @@ class HipEngineBNTrain(HipEngine):
         self.bn_inv = torch.ones(self.nch, **f32)
         self.bn_scale = torch.ones(self.nch, **f32)
         self.bn_shift = torch.zeros(self.nch, **f32)
+        self.bcoef = torch.zeros(3 * self.nch, **f32)   # backward (A, B, C) per channel
         # zeroed per step: forward (sum, sum^2) of every igemm launch | backward sum g | sum g*(z-mean)
         self.bws = torch.zeros(off + 2 * self.nch, **f32)
         self.acc = self.bws[:off]
@@ -232,12 +233,12 @@ class HipEngineBNTrain(HipEngine):
             N.bn_bwd_reduce(g, z, None, self._chs(self.bn_mean, c), None, self._chs(self.bsg, c),
                             self._chs(self.bsgx, c), None, None)
             N.bn_bwd_apply(g, z, None, self._bn_layer(c, M), [], self.params, self.bn_mean, self.bn_inv, self.bsg,
-                           self.bsgx, out, None, self.grads)
+                           self.bsgx, out, None, self.grads, self.bcoef)
         else:
             N.bn_bwd_reduce(g, z, z2, self._chs(self.bn_mean, c), self._chs(self.bn_mean, c2), self._chs(self.bsg, c),
                             self._chs(self.bsgx, c), self._chs(self.bsg, c2), self._chs(self.bsgx, c2))
             N.bn_bwd_apply(g, z, z2, self._bn_layer(c, M), self._bn_layer(c2, M), self.params, self.bn_mean,
-                           self.bn_inv, self.bsg, self.bsgx, out, out2, self.grads)
+                           self.bn_inv, self.bsg, self.bsgx, out, out2, self.grads, self.bcoef)
 
     def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0),
                          bucket_cb: Optional[Callable[[int], None]] = None, buckets=None):

@@ -94,7 +94,8 @@ def test_bn_stats_apply_and_backward():
     nat.bn_bwd_reduce(g, z, None, mean, None, sg, sgx, None, None)
     grads = torch.zeros(3 * C, device=dev)
     dz = torch.empty_like(g)
-    nat.bn_bwd_apply(g, z, None, [C, 0, 0, C, 2 * C, M], [], prm0, mean, inv, sg, sgx, dz, None, grads)
+    nat.bn_bwd_apply(g, z, None, [C, 0, 0, C, 2 * C, M], [], prm0, mean, inv, sg, sgx, dz, None, grads,
+                     torch.zeros(3 * C, device=dev))
     assert rel(dz, zz.grad) < 2e-2
     assert rel(grads[:C], g_.grad) < 1e-2 and rel(grads[C:2 * C], b_.grad) < 1e-2
     assert grads[2 * C:].abs().max().item() == 0.0
@@ -117,7 +118,7 @@ def test_bn_dual_source_backward_in_place():
     g_ref = g.float().clone()
     dz3 = torch.empty_like(g)
     nat.bn_bwd_apply(g, z3, z0, [C, 0, 0, 2 * C, 4 * C, M], [C, C, C, 3 * C, 5 * C, M], prm, mean, inv, sg, sgx,
-                     dz3, g, grads)
+                     dz3, g, grads, torch.zeros(6 * C, device=dev))
     for zi, gi, dzi, off in ((z3, 0, dz3, 0), (z0, 1, g, C)):
         zz = zi.float().clone().requires_grad_(True)
         ga = prm[off:off + C].clone().requires_grad_(True)
