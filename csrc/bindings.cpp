@@ -331,12 +331,31 @@ void cast_f32(Tensor x, Tensor y) { ok(pddl::cast_f32_launch(bfp(x), f32p(y), x.
 void register_rccl(pybind11::module& m);
 void register_fusion(pybind11::module& m);
 void register_loader(pybind11::module& m);
+void register_ps(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "pddl MI355X (gfx950) HIP kernels + native runtime (RCCL comm, fusion engine, loader)";
   register_rccl(m);
   register_fusion(m);
   register_loader(m);
+  register_ps(m);
+  // rows: host int64 [n, 3] of (flat offset, packed offset, length), bounds-checked here
+  m.def("range_copy", [](Tensor src, Tensor dst, Tensor rows, bool scatter) {
+    PCHECK(!rows.is_cuda() && rows.scalar_type() == torch::kInt64 && rows.dim() == 2 && rows.size(1) == 3,
+           "range rows: host int64 [n, 3]");
+    Tensor r = rows.contiguous();
+    const int64_t* q = r.data_ptr<int64_t>();
+    const int64_t flat_n = scatter ? dst.numel() : src.numel(), packed_n = scatter ? src.numel() : dst.numel();
+    for (int64_t i = 0; i < r.size(0); ++i)
+      PCHECK(q[3 * i] >= 0 && q[3 * i + 1] >= 0 && q[3 * i + 2] >= 0 && q[3 * i] + q[3 * i + 2] <= flat_n &&
+                 q[3 * i + 1] + q[3 * i + 2] <= packed_n,
+             "range out of bounds");
+    static_assert(sizeof(pddl::RangeRow) == 3 * sizeof(int64_t), "RangeRow layout");
+    Tensor dev = r.to(src.device());
+    ok(pddl::range_copy_launch(f32p(src), f32p(dst), reinterpret_cast<const pddl::RangeRow*>(dev.data_ptr()),
+                               (int)r.size(0), scatter ? 1 : 0, cur_stream()),
+       "range_copy");
+  });
   m.def("igemm", &igemm);
   m.def("igemm_bn", &igemm_impl);
   m.def("bn_stats", &bn_stats);

@@ -156,6 +156,12 @@ const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint
                                 const float* sg, const float* sgx, float* coef, int ldc, uint16_t* dz, uint16_t* dz2,
                                 float* grads, long M, hipStream_t s);
 
+// ---- range gather / scatter (pack.hip) ----
+struct RangeRow { long flat, packed, len; };
+// scatter = 0: dst[packed + i] = src[flat + i]; 1: dst[flat + i] = src[packed + i].
+const char* range_copy_launch(const float* src, float* dst, const RangeRow* rows_dev, int nrows, int scatter,
+                              hipStream_t s);
+
 // Deterministic synthetic images / labels for example ids idx[0..n) (uint8 [n][per], int64 [n]).
 const char* synth_launch(const int64_t* idx, int n, long per, int64_t seed, int ncls, uint8_t* img, int64_t* lab,
                          hipStream_t s);

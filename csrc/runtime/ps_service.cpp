@@ -1,0 +1,460 @@
+// Asynchronous parameter-server data plane (the gRPC servers + RecvTensor /
+// remote ApplyAdam of the reference's ParameterServerStrategy, imagenet-resnet50-ps.py:31-84).
+//
+// MI355X-native design (one node, one GPU per role, e.g. 2 PS + 6 workers):
+//   * PS p owns its shard of the flat fp32 parameters plus the Adam slots m, v, and a
+//     per-worker gradient MAILBOX [W][n] in its own HBM.
+//   * Control plane: one POSIX shared-memory segment per PS with a slot per worker
+//     (request / done sequence numbers, op, learning rate, pid, IPC handles).  Lock-free
+//     process-shared atomics with release / acquire ordering; no RPC layer at all.
+//   * Data plane over xGMI with HIP IPC (dmabuf): a worker's pack kernel gathers its gradient
+//     ranges and writes them STRAIGHT into its mailbox slot on the PS GPU (peer writes), then
+//     bumps its request sequence number.  The PS service thread sees the request, runs the
+//     fused Adam kernel (optim.hip, TF epsilon-hat form) on the mailbox, and copies the fresh
+//     shard into the worker's receive buffer on the worker GPU (peer copy) before publishing
+//     `done`.  Updates are applied one at a time in arrival order on the PS stream, so every
+//     pull is a consistent snapshot of the shard; workers never wait for each other
+//     (unbounded staleness, as the reference's asynchronous coordinator).
+//   * CPU roles (tests, `--device cpu`): the same protocol with the mailboxes and receive
+//     buffers in shared memory and a host Adam loop.
+//   * Failure handling: a worker that dies never bumps its sequence number again (its
+//     half-written mailbox is never applied); the service loop treats a vanished worker pid
+//     as finished, and the coordinator re-queues its closure (parameter_server.py).  A worker
+//     waiting on a dead PS times out with an error (reference: a PS failure aborts the job).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kernels/kernels.h"
+
+namespace py = pybind11;
+using torch::Tensor;
+
+namespace {
+
+constexpr uint64_t kMagic = 0x5044444c50535631ull;   // "PDDLPSV1"
+constexpr int kMaxWorkers = 64;
+enum { OP_PUSH = 0, OP_PULL = 1, OP_STOP = 2 };
+
+struct alignas(128) WorkerSlot {
+  std::atomic<uint64_t> req_seq;
+  std::atomic<uint64_t> done_seq;
+  std::atomic<int32_t> op;
+  std::atomic<int32_t> rx_ready;
+  std::atomic<int32_t> pid;
+  float lr;
+  hipIpcMemHandle_t rx_handle;   // worker receive buffer (GPU roles)
+};
+
+struct PSCtrl {
+  uint64_t magic;
+  int64_t n;            // shard elements (padded to a multiple of 4)
+  int32_t workers;
+  int32_t gpu;          // 1: data in GPU memory (IPC), 0: shared memory
+  std::atomic<int32_t> ready;
+  std::atomic<uint64_t> updates;
+  hipIpcMemHandle_t mailbox_handle;
+  WorkerSlot slot[kMaxWorkers];
+};
+
+void hck(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, "pddl ps ", what, ": ", hipGetErrorString(e)); }
+void kck(const char* err, const char* what) { TORCH_CHECK(err == nullptr, "pddl ps ", what, ": ", err ? err : ""); }
+
+std::string seg_name(const std::string& job, int p, const char* what) {
+  return "/pddl_" + job + "_ps" + std::to_string(p) + what;
+}
+
+// POSIX shared-memory mapping (created by the PS, attached by workers).
+struct Shm {
+  std::string name;
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  bool owner = false;
+  void create(const std::string& n, size_t b) {
+    name = n; bytes = b; owner = true;
+    shm_unlink(n.c_str());
+    int fd = shm_open(n.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    TORCH_CHECK(fd >= 0, "pddl ps: shm_open(create) ", n, ": ", strerror(errno));
+    TORCH_CHECK(ftruncate(fd, (off_t)b) == 0, "pddl ps: ftruncate ", n);
+    ptr = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    TORCH_CHECK(ptr != MAP_FAILED, "pddl ps: mmap ", n);
+  }
+  bool attach(const std::string& n, size_t b) {
+    int fd = shm_open(n.c_str(), O_RDWR, 0600);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || (size_t)st.st_size < b) { close(fd); return false; }
+    name = n; bytes = b;
+    ptr = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    return ptr != MAP_FAILED;
+  }
+  ~Shm() {
+    if (ptr && ptr != MAP_FAILED) munmap(ptr, bytes);
+    if (owner) shm_unlink(name.c_str());
+  }
+};
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------------------ server
+class PSServer {
+ public:
+  PSServer(const std::string& job, int p, Tensor init, int workers, int device, double b1, double b2, double eps)
+      : p_(p), W_(workers), dev_(device), b1_(b1), b2_(b2), eps_(eps) {
+    TORCH_CHECK(workers >= 1 && workers <= kMaxWorkers, "pddl ps: 1..64 workers");
+    TORCH_CHECK(init.scalar_type() == torch::kFloat32 && init.dim() == 1, "pddl ps: init must be a flat fp32 shard");
+    n_real_ = init.numel();
+    n_ = (n_real_ + 3) / 4 * 4;
+    ctrl_shm_.create(seg_name(job, p, ""), sizeof(PSCtrl));
+    ctrl_ = new (ctrl_shm_.ptr) PSCtrl();
+    ctrl_->magic = kMagic;
+    ctrl_->n = n_;
+    ctrl_->workers = W_;
+    ctrl_->gpu = dev_ >= 0;
+    Tensor host = init.to(torch::kCPU).contiguous();
+    if (dev_ >= 0) {
+      hck(hipSetDevice(dev_), "set device");
+      hck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
+      hck(hipMalloc(&params_, 3 * n_ * sizeof(float)), "malloc params");
+      m_ = params_ + n_;
+      v_ = params_ + 2 * n_;
+      hck(hipMemset(params_, 0, 3 * n_ * sizeof(float)), "memset");
+      hck(hipMemcpy(params_, host.data_ptr<float>(), n_real_ * sizeof(float), hipMemcpyHostToDevice), "init copy");
+      hck(hipMalloc(&mailbox_, (size_t)W_ * n_ * sizeof(float)), "malloc mailbox");
+      hck(hipMemset(mailbox_, 0, (size_t)W_ * n_ * sizeof(float)), "memset mailbox");
+      hck(hipIpcGetMemHandle(&ctrl_->mailbox_handle, mailbox_), "ipc handle");
+      hck(hipDeviceSynchronize(), "init sync");
+      rx_ptr_.assign(W_, nullptr);
+    } else {
+      host_.assign(3 * n_, 0.f);
+      std::memcpy(host_.data(), host.data_ptr<float>(), n_real_ * sizeof(float));
+      params_ = host_.data(); m_ = params_ + n_; v_ = params_ + 2 * n_;
+      mb_shm_.create(seg_name(job, p, "_mb"), (size_t)W_ * n_ * sizeof(float));
+      rx_shm_.create(seg_name(job, p, "_rx"), (size_t)W_ * n_ * sizeof(float));
+      mailbox_ = static_cast<float*>(mb_shm_.ptr);
+    }
+    ctrl_->ready.store(1, std::memory_order_release);
+  }
+  ~PSServer() {
+    stop_.store(true);
+    if (thr_.joinable()) thr_.join();
+    if (dev_ >= 0) {
+      hipSetDevice(dev_);
+      for (float* r : rx_ptr_) if (r) hipIpcCloseMemHandle(r);
+      if (mailbox_) hipFree(mailbox_);
+      if (params_) hipFree(params_);
+      if (stream_) hipStreamDestroy(stream_);
+    }
+  }
+
+  void start() { thr_ = std::thread([this] { serve(); }); }
+  int64_t join() {
+    if (thr_.joinable()) thr_.join();
+    TORCH_CHECK(err_.empty(), "pddl ps server: ", err_);
+    return (int64_t)ctrl_->updates.load();
+  }
+  int64_t updates() const { return (int64_t)ctrl_->updates.load(); }
+  std::vector<int> dead() const { return dead_; }
+  Tensor params() const {
+    Tensor out = torch::empty({n_real_}, torch::kFloat32);
+    if (dev_ >= 0) {
+      hipSetDevice(dev_);
+      hck(hipStreamSynchronize(stream_), "sync");
+      hck(hipMemcpy(out.data_ptr<float>(), params_, n_real_ * sizeof(float), hipMemcpyDeviceToHost), "params d2h");
+    } else {
+      std::memcpy(out.data_ptr<float>(), params_, n_real_ * sizeof(float));
+    }
+    return out;
+  }
+
+ private:
+  void apply_adam(int w, float lr) {
+    ++t_;
+    const double lr_t = lr * std::sqrt(1.0 - std::pow(b2_, t_)) / (1.0 - std::pow(b1_, t_));
+    const float* g = mailbox_ + (size_t)w * n_;
+    if (dev_ >= 0) {
+      kck(pddl::adam_launch(params_, g, m_, v_, n_, (float)lr_t, (float)b1_, (float)b2_, (float)eps_, 1.f, nullptr,
+                            stream_),
+          "adam");
+    } else {
+      const float b1 = (float)b1_, b2 = (float)b2_, eps = (float)eps_, lt = (float)lr_t;
+      for (int64_t i = 0; i < n_; ++i) {
+        m_[i] = b1 * m_[i] + (1.f - b1) * g[i];
+        v_[i] = b2 * v_[i] + (1.f - b2) * g[i] * g[i];
+        params_[i] -= lt * m_[i] / (std::sqrt(v_[i]) + eps);
+      }
+    }
+  }
+  void send_snapshot(int w) {
+    WorkerSlot& s = ctrl_->slot[w];
+    if (dev_ >= 0) {
+      if (!rx_ptr_[w]) {
+        TORCH_CHECK(s.rx_ready.load(std::memory_order_acquire) == 1, "worker ", w, " has no receive buffer");
+        void* ptr = nullptr;
+        hck(hipIpcOpenMemHandle(&ptr, s.rx_handle, hipIpcMemLazyEnablePeerAccess), "open rx handle");
+        rx_ptr_[w] = static_cast<float*>(ptr);
+      }
+      hck(hipMemcpyAsync(rx_ptr_[w], params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
+      hck(hipStreamSynchronize(stream_), "sync");
+    } else {
+      std::memcpy(static_cast<float*>(rx_shm_.ptr) + (size_t)w * n_, params_, n_ * sizeof(float));
+    }
+  }
+  void serve() {
+    try {
+      if (dev_ >= 0) hck(hipSetDevice(dev_), "set device");
+      std::vector<uint64_t> seen(W_, 0);
+      std::vector<char> finished(W_, 0);
+      int n_done = 0;
+      double last_check = now_s();
+      while (n_done < W_ && !stop_.load()) {
+        bool any = false;
+        for (int w = 0; w < W_; ++w) {
+          if (finished[w]) continue;
+          WorkerSlot& s = ctrl_->slot[w];
+          const uint64_t r = s.req_seq.load(std::memory_order_acquire);
+          if (r == seen[w]) continue;
+          any = true;
+          seen[w] = r;
+          const int op = s.op.load(std::memory_order_relaxed);
+          if (op == OP_STOP) {
+            finished[w] = 1; ++n_done;
+          } else {
+            if (op == OP_PUSH) {
+              apply_adam(w, s.lr);
+              ctrl_->updates.fetch_add(1);
+            }
+            send_snapshot(w);
+          }
+          s.done_seq.store(r, std::memory_order_release);
+        }
+        if (!any) {
+          const double t = now_s();
+          if (t - last_check > 0.5) {   // a worker process that vanished counts as finished
+            last_check = t;
+            for (int w = 0; w < W_; ++w) {
+              const int pid = ctrl_->slot[w].pid.load();
+              if (!finished[w] && pid > 0 && kill(pid, 0) != 0 && errno == ESRCH) {
+                finished[w] = 1; ++n_done; dead_.push_back(w);
+              }
+            }
+          }
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+      }
+      if (dev_ >= 0) hipStreamSynchronize(stream_);
+    } catch (const std::exception& e) {
+      err_ = e.what();
+    }
+  }
+
+  int p_, W_, dev_;
+  double b1_, b2_, eps_;
+  int64_t n_real_ = 0, n_ = 0, t_ = 0;
+  Shm ctrl_shm_, mb_shm_, rx_shm_;
+  PSCtrl* ctrl_ = nullptr;
+  float* params_ = nullptr;
+  float* m_ = nullptr;
+  float* v_ = nullptr;
+  float* mailbox_ = nullptr;
+  std::vector<float> host_;
+  std::vector<float*> rx_ptr_;
+  hipStream_t stream_ = nullptr;
+  std::thread thr_;
+  std::atomic<bool> stop_{false};
+  std::vector<int> dead_;
+  std::string err_;
+};
+
+// ------------------------------------------------------------------------------ client
+struct Remote {
+  Shm ctrl_shm, mb_shm, rx_shm;
+  PSCtrl* ctrl = nullptr;
+  int64_t n = 0;
+  float* mailbox = nullptr;   // this worker's slot (peer GPU memory or shared memory)
+  void* mb_base = nullptr;    // IPC mapping base (GPU)
+  float* rx = nullptr;        // this worker's receive buffer
+  Tensor rows;                // device RangeRow table (GPU) / host (CPU)
+  std::vector<pddl::RangeRow> host_rows;
+  uint64_t seq = 0;
+};
+
+class PSClient {
+ public:
+  PSClient(const std::string& job, std::vector<std::vector<std::pair<int64_t, int64_t>>> ranges, int worker,
+           int device, double timeout_s)
+      : w_(worker), dev_(device), timeout_(timeout_s) {
+    const int P = (int)ranges.size();
+    rem_.resize(P);
+    if (dev_ >= 0) hck(hipSetDevice(dev_), "set device");
+    for (int p = 0; p < P; ++p) {
+      Remote& r = rem_[p];
+      const double t0 = now_s();
+      while (!r.ctrl_shm.attach(seg_name(job, p, ""), sizeof(PSCtrl))) {
+        TORCH_CHECK(now_s() - t0 < timeout_, "pddl ps client: PS ", p, " never came up");
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      }
+      r.ctrl = static_cast<PSCtrl*>(r.ctrl_shm.ptr);
+      while (r.ctrl->ready.load(std::memory_order_acquire) != 1) {
+        TORCH_CHECK(now_s() - t0 < timeout_, "pddl ps client: PS ", p, " not ready");
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+      TORCH_CHECK(r.ctrl->magic == kMagic && w_ < r.ctrl->workers, "pddl ps client: bad control segment");
+      TORCH_CHECK((r.ctrl->gpu != 0) == (dev_ >= 0), "pddl ps client: PS and worker must both be GPU or both CPU");
+      r.n = r.ctrl->n;
+      int64_t packed = 0;
+      for (auto& fr : ranges[p]) {
+        TORCH_CHECK(fr.first >= 0 && fr.second >= 0, "pddl ps client: negative range");
+        r.host_rows.push_back({(long)fr.first, (long)packed, (long)fr.second});
+        packed += fr.second;
+        flat_end_ = std::max<int64_t>(flat_end_, fr.first + fr.second);
+      }
+      TORCH_CHECK(packed <= r.n && (packed + 3) / 4 * 4 == r.n, "pddl ps client: ranges do not match shard ", p);
+      WorkerSlot& s = r.ctrl->slot[w_];
+      r.seq = s.done_seq.load();
+      if (dev_ >= 0) {
+        hck(hipIpcOpenMemHandle(&r.mb_base, r.ctrl->mailbox_handle, hipIpcMemLazyEnablePeerAccess), "open mailbox");
+        r.mailbox = static_cast<float*>(r.mb_base) + (size_t)w_ * r.n;
+        void* rx = nullptr;
+        hck(hipMalloc(&rx, r.n * sizeof(float)), "malloc rx");
+        hck(hipMemset(rx, 0, r.n * sizeof(float)), "memset rx");
+        hck(hipDeviceSynchronize(), "rx sync");
+        r.rx = static_cast<float*>(rx);
+        hck(hipIpcGetMemHandle(&s.rx_handle, r.rx), "rx handle");
+        s.rx_ready.store(1, std::memory_order_release);
+        auto opts = torch::TensorOptions().dtype(torch::kUInt8);
+        Tensor hrows = torch::empty({(int64_t)(r.host_rows.size() * sizeof(pddl::RangeRow))}, opts);
+        std::memcpy(hrows.data_ptr(), r.host_rows.data(), hrows.numel());
+        r.rows = hrows.to(torch::Device(torch::kCUDA, dev_));
+      } else {
+        TORCH_CHECK(r.mb_shm.attach(seg_name(job, p, "_mb"), (size_t)r.ctrl->workers * r.n * sizeof(float)) &&
+                        r.rx_shm.attach(seg_name(job, p, "_rx"), (size_t)r.ctrl->workers * r.n * sizeof(float)),
+                    "pddl ps client: cannot attach shard buffers of PS ", p);
+        r.mailbox = static_cast<float*>(r.mb_shm.ptr) + (size_t)w_ * r.n;
+        r.rx = static_cast<float*>(r.rx_shm.ptr) + (size_t)w_ * r.n;
+      }
+      s.pid.store((int32_t)getpid());
+    }
+  }
+  ~PSClient() {
+    if (dev_ >= 0) {
+      hipSetDevice(dev_);
+      for (Remote& r : rem_) {
+        if (r.mb_base) hipIpcCloseMemHandle(r.mb_base);
+        if (r.rx) hipFree(r.rx);
+      }
+    }
+  }
+
+  // push (op 0): send this worker's gradients, receive the updated shards; pull (op 1):
+  // receive only.  Writes the received shards into `params` (flat).
+  void exchange(Tensor grads, Tensor params, double lr, bool push) {
+    TORCH_CHECK(params.is_contiguous() && params.scalar_type() == torch::kFloat32, "pddl ps: flat fp32 params");
+    TORCH_CHECK((dev_ >= 0) == params.is_cuda(), "pddl ps: params on the worker's device");
+    TORCH_CHECK(params.numel() >= flat_end_ && (!push || grads.numel() >= flat_end_),
+                "pddl ps: flat buffers shorter than the shard ranges");
+    hipStream_t st = nullptr;
+    if (dev_ >= 0) st = at::hip::getCurrentHIPStream(dev_).stream();
+    for (Remote& r : rem_) {
+      WorkerSlot& s = r.ctrl->slot[w_];
+      if (push) {
+        TORCH_CHECK(grads.is_contiguous() && grads.scalar_type() == torch::kFloat32, "pddl ps: flat fp32 grads");
+        if (dev_ >= 0) {
+          kck(pddl::range_copy_launch(grads.data_ptr<float>(), r.mailbox,
+                                      reinterpret_cast<const pddl::RangeRow*>(r.rows.data_ptr()),
+                                      (int)r.host_rows.size(), 0, st),
+              "pack");
+        } else {
+          const float* g = grads.data_ptr<float>();
+          for (auto& row : r.host_rows) std::memcpy(r.mailbox + row.packed, g + row.flat, row.len * sizeof(float));
+        }
+      }
+    }
+    if (dev_ >= 0 && push) hck(hipStreamSynchronize(st), "sync push");   // peer writes complete + visible
+    for (Remote& r : rem_) {
+      WorkerSlot& s = r.ctrl->slot[w_];
+      s.lr = (float)lr;
+      s.op.store(push ? OP_PUSH : OP_PULL, std::memory_order_relaxed);
+      s.req_seq.store(++r.seq, std::memory_order_release);
+    }
+    for (size_t p = 0; p < rem_.size(); ++p) {
+      Remote& r = rem_[p];
+      wait_done(r, (int)p);
+      if (dev_ >= 0) {
+        kck(pddl::range_copy_launch(r.rx, params.data_ptr<float>(),
+                                    reinterpret_cast<const pddl::RangeRow*>(r.rows.data_ptr()),
+                                    (int)r.host_rows.size(), 1, st),
+            "unpack");
+      } else {
+        float* pp = params.data_ptr<float>();
+        for (auto& row : r.host_rows) std::memcpy(pp + row.flat, r.rx + row.packed, row.len * sizeof(float));
+      }
+    }
+  }
+  void stop() {
+    for (Remote& r : rem_) {
+      WorkerSlot& s = r.ctrl->slot[w_];
+      s.op.store(OP_STOP, std::memory_order_relaxed);
+      s.req_seq.store(++r.seq, std::memory_order_release);
+    }
+    for (size_t p = 0; p < rem_.size(); ++p) wait_done(rem_[p], (int)p);
+  }
+
+ private:
+  void wait_done(Remote& r, int p) {
+    WorkerSlot& s = r.ctrl->slot[w_];
+    const double t0 = now_s();
+    int spins = 0;
+    while (s.done_seq.load(std::memory_order_acquire) != r.seq) {
+      if (++spins > 64) {
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        TORCH_CHECK(now_s() - t0 < timeout_, "pddl ps client: parameter server ", p, " did not answer within ",
+                    timeout_, " s (PS failure aborts the job)");
+      }
+    }
+  }
+
+  int w_, dev_;
+  double timeout_;
+  int64_t flat_end_ = 0;
+  std::vector<Remote> rem_;
+};
+
+}  // namespace
+
+void register_ps(py::module& m) {
+  py::class_<PSServer, std::shared_ptr<PSServer>>(m, "PSServer")
+      .def(py::init<const std::string&, int, Tensor, int, int, double, double, double>(), py::arg("job"),
+           py::arg("ps_index"), py::arg("init_shard"), py::arg("workers"), py::arg("device"), py::arg("beta1"),
+           py::arg("beta2"), py::arg("eps"))
+      .def("start", &PSServer::start)
+      .def("join", &PSServer::join, py::call_guard<py::gil_scoped_release>())
+      .def("params", &PSServer::params)
+      .def_property_readonly("updates", &PSServer::updates)
+      .def_property_readonly("dead", &PSServer::dead);
+  py::class_<PSClient, std::shared_ptr<PSClient>>(m, "PSClient")
+      .def(py::init<const std::string&, std::vector<std::vector<std::pair<int64_t, int64_t>>>, int, int, double>(),
+           py::arg("job"), py::arg("ranges"), py::arg("worker"), py::arg("device"), py::arg("timeout_s") = 120.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("exchange", &PSClient::exchange, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &PSClient::stop, py::call_guard<py::gil_scoped_release>());
+}

@@ -14,8 +14,12 @@ MI355X-native design:
   * the PS holds only its shards of the flat fp32 parameter buffer plus their Adam slots and
     applies the fused HIP Adam kernel to each arriving gradient (async, staleness unbounded,
     as in the reference);
-  * data plane: one 2-rank process group per (worker, PS) pair — RCCL send/recv over xGMI on
-    GPU, gloo on CPU — so every PS serves its workers from independent threads;
+  * data plane (default, native): csrc/runtime/ps_service.cpp — a per-PS shared-memory control
+    segment and HIP-IPC mailboxes: a worker's pack kernel writes its gradient ranges straight
+    into its mailbox on the PS GPU over xGMI, the PS service thread applies fused Adam and
+    peer-copies the fresh shard back (CPU roles: the same protocol in shared memory);
+    PDDL_PS_IMPL=c10d selects the portable fallback: one 2-rank process group per
+    (worker, PS) pair with RCCL / gloo send/recv served from Python threads;
   * control plane (closure scheduling, heartbeats, LR broadcast, stop) is the c10d TCPStore:
     a worker claims step tickets; the coordinator re-queues the ticket of a worker that misses
     its heartbeats (ClusterCoordinator's closure re-queue); PDDL_FAULT=kill_worker:<i>@<step>
@@ -114,19 +118,32 @@ def _scatter(flat: torch.Tensor, ranges, packed: torch.Tensor) -> None:
 OP_PUSH, OP_PULL, OP_STOP = 0.0, 1.0, 2.0
 
 
+def ps_impl() -> str:
+    """Data plane: "native" (csrc/runtime/ps_service.cpp) unless PDDL_PS_IMPL=c10d."""
+    if os.environ.get("PDDL_PS_IMPL", "native") != "native":
+        return "c10d"
+    from ..ops.native import native_available, require_native
+    return "native" if native_available() and hasattr(require_native(), "PSServer") else "c10d"
+
+
 class _Cluster:
-    def __init__(self, cfg, rank: int, world: int, num_ps: int, device):
+    def __init__(self, cfg, rank: int, world: int, num_ps: int, device, impl: str = "c10d"):
         self.cfg = cfg
         self.rank, self.world, self.num_ps = rank, world, num_ps
         self.num_workers = world - num_ps
         self.device = device
         self.is_ps = rank < num_ps
+        self.impl = impl
         self.store = dist.distributed_c10d._get_default_store()
-        # one 2-rank group per (worker, ps) pair; every rank must create every group in order
+        if rank == 0:
+            self.store.set("ps_job", f"{os.getpid():x}{int(time.time() * 1e3) & 0xffffff:06x}")
+        self.job = self.store.get("ps_job").decode()
+        # c10d data plane: one 2-rank group per (worker, ps) pair; every rank creates every group
         self.pair: Dict[Tuple[int, int], dist.ProcessGroup] = {}
-        for w in range(num_ps, world):
-            for p in range(num_ps):
-                self.pair[(w, p)] = dist.new_group([p, w])
+        if impl == "c10d":
+            for w in range(num_ps, world):
+                for p in range(num_ps):
+                    self.pair[(w, p)] = dist.new_group([p, w])
         L = ParamLayout(cfg.num_classes)
         self.L = L
         self.shards = partition_variables(L, num_ps, cfg.min_shard_bytes)
@@ -226,6 +243,44 @@ class PSServer:
                           f"step {cur}", flush=True)
 
 
+class NativePSServer(PSServer):
+    """PS role on the native data plane: the C++ service thread applies every push; this
+    process keeps the coordinator duties (heartbeat watch / closure re-queue on PS 0)."""
+
+    def __init__(self, cl: _Cluster, init_params: torch.Tensor):
+        from ..ops.native import require_native
+        self.cl = cl
+        cfg = cl.cfg
+        shard = _gather(init_params, cl.ranges[cl.rank]).contiguous()
+        dev = cl.device.index if cl.device.type == "cuda" else -1
+        self.srv = require_native().PSServer(cl.job, cl.rank, shard, cl.num_workers, dev, cfg.beta1, cfg.beta2,
+                                             cfg.adam_eps)
+        self.updates = 0
+        self.dead = set()
+
+    def run(self):
+        cl = self.cl
+        self.srv.start()
+        mon = None
+        if cl.rank == 0:
+            done = threading.Event()
+
+            class _Alive:   # monitor() polls is_alive() of the service "threads"
+                def is_alive(self_inner):
+                    return not done.is_set()
+            mon = threading.Thread(target=self.monitor, args=([_Alive()],), daemon=True)
+            mon.start()
+        try:
+            self.updates = self.srv.join()
+        finally:
+            if mon is not None:
+                done.set()
+                mon.join(timeout=5)
+        self.dead = {w + cl.num_ps for w in self.srv.dead}
+        for w in sorted(self.dead):
+            print(f"[ps {cl.rank}] lost worker {w}", flush=True)
+
+
 class PSWorker:
     def __init__(self, cl: _Cluster, engine, pipeline_factory):
         self.cl = cl
@@ -236,6 +291,15 @@ class PSWorker:
 
     def _exchange(self, op: float, lr: float):
         cl = self.cl
+        if cl.impl == "native":
+            if not hasattr(self, "cli"):
+                from ..ops.native import require_native
+                dev = cl.device.index if cl.device.type == "cuda" else -1
+                self.cli = require_native().PSClient(cl.job, cl.ranges, self.widx, dev,
+                                                     float(os.environ.get("PDDL_PS_TIMEOUT", "120")))
+            self.cli.exchange(self.engine.grads, self.engine.params, lr, op == OP_PUSH)
+            self.engine.after_update()
+            return
         ctrl = torch.tensor([op, lr], dtype=torch.float64, device=cl.device)
         reqs = []
         for p in range(cl.num_ps):
@@ -250,6 +314,11 @@ class PSWorker:
 
     def stop(self):
         cl = self.cl
+        if cl.impl == "native":
+            if hasattr(self, "cli"):
+                self.cli.stop()
+            cl.store.set(f"fin/{cl.rank}", "1")
+            return
         ctrl = torch.tensor([OP_STOP, 0.0], dtype=torch.float64, device=cl.device)
         for p in range(cl.num_ps):
             dist.send(ctrl, dst=p, group=cl.pair[(cl.rank, p)])
@@ -283,11 +352,14 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         device = torch.device("cuda", rank % n)
     else:
         device = torch.device("cpu")
-    backend = "nccl" if use_gpu else "gloo"
+    impl = ps_impl()
+    # the native data plane needs c10d only for control (barriers, the TCP store): gloo
+    gpu_pg = use_gpu and impl == "c10d"
+    backend = "nccl" if gpu_pg else "gloo"
     dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=int(os.environ.get("PDDL_PS_TIMEOUT", "120"))),
-                            **({"device_id": device} if use_gpu else {}))
-    cl = _Cluster(cfg, rank, world, num_ps, device)
+                            **({"device_id": device} if gpu_pg else {}))
+    cl = _Cluster(cfg, rank, world, num_ps, device, impl=impl)
     from ..parallel.strategies import build_engine
     torch.manual_seed(cfg.seed)
     if cl.is_ps:
@@ -301,11 +373,11 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             from ..utils.checkpoint import load_pretrained
             load_pretrained(cfg.weights, tmp)
             init = tmp.params
-        srv = PSServer(cl, init)
+        srv = NativePSServer(cl, init) if cl.impl == "native" else PSServer(cl, init)
         dist.barrier()
         srv.run()
         if result_q is not None:
-            result_q.put(("ps", rank, srv.updates, sorted(srv.dead)))
+            result_q.put(("ps", rank, srv.updates, sorted(srv.dead), impl))
         dist.destroy_process_group()
         return
     # ---------------------------------------------------------------- worker

@@ -21,8 +21,10 @@ def _cfg(preset, **kw):
 
 
 # ------------------------------------------------------------------ parameter server
-def test_ps_async_job_runs_and_applies_every_step():
+@pytest.mark.parametrize("impl", ["native", "c10d"])
+def test_ps_async_job_runs_and_applies_every_step(impl, monkeypatch):
     from pddl.parallel.parameter_server import run_ps_job
+    monkeypatch.setenv("PDDL_PS_IMPL", impl)
     cfg = _cfg("ps", steps_per_epoch=6, validation_steps=1, batch_size=2, epochs=2)
     res = run_ps_job(cfg, num_ps=2, num_workers=2, return_results=True)
     ps = [r for r in res if r[0] == "ps"]
@@ -30,12 +32,15 @@ def test_ps_async_job_runs_and_applies_every_step():
     assert len(ps) == 2 and len(wk) == 2
     assert sum(r[2] for r in wk) == 12                       # 2 epochs x 6 steps, split asynchronously
     assert all(r[2] == 12 for r in ps)                       # every PS applied every push
+    assert all(r[4] == impl for r in ps)
     hist = [r for r in wk if r[3]][0][3]
     assert len(hist) == 2 and "val_loss" in hist[0]
 
 
-def test_ps_worker_failure_requeues_closure(monkeypatch):
+@pytest.mark.parametrize("impl", ["native", "c10d"])
+def test_ps_worker_failure_requeues_closure(impl, monkeypatch):
     from pddl.parallel.parameter_server import run_ps_job
+    monkeypatch.setenv("PDDL_PS_IMPL", impl)
     monkeypatch.setenv("PDDL_FAULT", "kill_worker:1@1")
     monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
     cfg = _cfg("ps", steps_per_epoch=6, batch_size=2, epochs=1)
