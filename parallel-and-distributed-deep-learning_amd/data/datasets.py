@@ -11,6 +11,8 @@ Sources (no network on the target machines, so no tfds download):
   * RecordsImageNet — a directory of raw uint8 records (`<split>.u8` = N x 224 x 224 x 3,
     `<split>_labels.i64`), memory-mapped and gathered by the native loader thread pool
     (csrc/runtime/loader.cpp) into pinned buffers, then copied asynchronously to the GPU.
+  * TFDSImageNet / JpegFolderImageNet (data/imagenet.py) — the reference's tfds TFRecord
+    shards or the untarred ILSVRC folders, decoded by the native reader (csrc/io).
 """
 from __future__ import annotations
 
@@ -192,4 +194,10 @@ def make_source(spec: str, split: str, cfg) -> ImageSource:
                                  fixed=spec == "synthetic_fixed")
     if spec.startswith("records:"):
         return RecordsImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
-    raise ValueError(f"unknown data spec {spec!r}")
+    if spec.startswith("tfds:"):
+        from .imagenet import TFDSImageNet
+        return TFDSImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+    if spec.startswith("folder:"):
+        from .imagenet import JpegFolderImageNet
+        return JpegFolderImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+    raise ValueError(f"unknown data spec {spec!r} (synthetic | records:<dir> | tfds:<dir> | folder:<dir>)")

@@ -34,7 +34,7 @@ def build(verbose: bool = False) -> str:
         sys.stderr.write((r.stdout or "")[-4000:] + (r.stderr or "")[-4000:])
         raise RuntimeError("native build failed")
     out = []
-    for name in ("_pddl_native", "_pddl_h5"):
+    for name in ("_pddl_native", "_pddl_h5", "_pddl_io"):
         built = sorted(glob.glob(os.path.join(ROOT, f"{name}*.so")))
         if not built:
             raise RuntimeError(f"native build produced no {name} shared object")

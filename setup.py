@@ -7,6 +7,9 @@ into position-independent objects -- no source translation step touches them -- 
 with the host-side torch bindings and runtime (csrc/bindings.cpp, csrc/runtime/*.cpp), which
 are plain C++ against the HIP runtime and PyTorch-ROCm headers.
 
+`_pddl_io`: the ImageNet reader (TFRecord / JPEG decode via libjpeg, resize_with_crop_or_pad),
+a separate module for the same reason.
+
 `_pddl_h5`: Keras-layout .h5 checkpoints through the system HDF5 1.10 (separate module so the
 kernels never depend on libhdf5 being loadable).
 
@@ -62,6 +65,15 @@ setup(
             define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
             extra_objects=kernel_objs,
             extra_link_args=["-Wl,-rpath,/opt/rocm/lib", "-Wl,--strip-debug"],
+            extra_compile_args=["-O2", "-g0", "-std=c++17"],
+        ),
+        CppExtension(
+            "_pddl_io",
+            [os.path.join("csrc", "io", "imagenet_io.cpp")],
+            include_dirs=["/opt/conda/include"],
+            library_dirs=["/opt/conda/lib"],
+            libraries=["jpeg"],
+            extra_link_args=["-Wl,-rpath,/opt/conda/lib", "-Wl,--strip-debug"],
             extra_compile_args=["-O2", "-g0", "-std=c++17"],
         ),
         CppExtension(
