@@ -49,6 +49,7 @@ def main():
     from pddl.models.resnet50 import ParamLayout
     from pddl.train.optim import make_optimizer
     from pddl.parallel.collectives import BucketAllReducer
+    from pddl.utils import profiling as prof
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -87,12 +88,16 @@ def main():
         stats = eng.forward_backward(images, labels, gscale, flip=flips[i % 64], bucket_cb=cb,
                                      buckets=reducer.buckets if reducer is not None else None)
         if reducer is not None:
+            prof.push("step/allreduce")
             if args.no_overlap:
                 for j in range(len(reducer.buckets)):
                     reducer.on_bucket_ready(j)
             reducer.finish()
+            prof.pop()
+        prof.push("step/optimizer")
         opt.step()
         eng.after_update()
+        prof.pop()
         return stats
 
     for i in range(args.warmup):

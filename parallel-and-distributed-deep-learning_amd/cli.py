@@ -41,6 +41,9 @@ def run(preset: str, argv: Optional[List[str]] = None, extra=None) -> int:
     if cfg.strategy == "ps":
         from .parallel.parameter_server import run_ps_job
         return run_ps_job(cfg)
+    if cfg.roctx:
+        from .utils import profiling
+        profiling.enable(True)
     strategy = make_strategy(cfg)
     trainer = Trainer(cfg, strategy)
     if strategy.is_chief:

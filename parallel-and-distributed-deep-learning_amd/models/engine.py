@@ -28,6 +28,7 @@ from typing import Callable, Dict, List, Optional
 import torch
 
 from ..ops.native import require_native
+from ..utils import profiling as prof
 from .resnet50 import BN_EPS, ParamLayout
 
 _PREP_FMT = "<6i2q8i"
@@ -359,7 +360,10 @@ class HipEngine:
         assert B <= self.cap, "batch larger than the engine's buffers"
         self.ws.zero_()
         lab = self._labels(labels, B)
+        prof.push("step/forward")
         x5 = self._forward(images, B, True, flip, crop_offset)
+        prof.pop()
+        prof.push("step/backward")
         logits = self.logits[:B]
         dl = self.dlogits[:B]
         N.softmax_xent(logits, lab, self.num_classes, float(gscale), dl, self.stats[0:1], self.stats[1:2])
@@ -452,6 +456,7 @@ class HipEngine:
         done_upto(L.kernels_end)
         N.colsum_reduce(cp, ctab, cn, self.colsum)
         N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
+        prof.pop()
         if bucket_cb is not None:
             while nb[0] < len(bks):
                 bucket_cb(nb[0])

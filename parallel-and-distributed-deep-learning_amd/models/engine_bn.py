@@ -24,6 +24,7 @@ from typing import Callable, Dict, Optional
 import torch
 
 from .engine import STEM_K, HipEngine
+from ..utils import profiling as prof
 from .resnet50 import BN_EPS, BN_MOMENTUM, ParamLayout
 
 _STAT_FMT = "<8if i"   # BnStatLayer: C, sum_off, sq_off, ch, gamma, beta, mm, mv, count, pad
@@ -248,7 +249,10 @@ class HipEngineBNTrain(HipEngine):
         self.ws.zero_()
         self.bws.zero_()
         lab = self._labels(labels, B)
+        prof.push("step/forward")
         x5 = self._forward(images, B, True, flip, crop_offset)
+        prof.pop()
+        prof.push("step/backward")
         logits = self.logits[:B]
         dl = self.dlogits[:B]
         N.softmax_xent(logits, lab, self.num_classes, float(gscale), dl, self.stats[0:1], self.stats[1:2])
@@ -336,6 +340,7 @@ class HipEngineBNTrain(HipEngine):
         N.wgrad(self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
         N.stem_wgrad_fold(self.stem_dw2, self._gview(s.name, 64, 147), 64)
         done_upto(L.kernels_end)
+        prof.pop()
         if bucket_cb is not None:
             while nb[0] < len(bks):
                 bucket_cb(nb[0])

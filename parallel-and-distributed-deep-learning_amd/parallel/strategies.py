@@ -27,6 +27,7 @@ import torch.distributed as dist
 from ..data.datasets import Pipeline, make_source
 from ..models.resnet50 import ParamLayout
 from ..train.optim import make_optimizer
+from ..utils import profiling as prof
 from .collectives import BucketAllReducer
 from .launch import ClusterInfo, export_torch_env, resolve_cluster
 
@@ -280,12 +281,16 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
             cb = self.reducer.on_bucket_ready
         s = self.engine.forward_backward(images, labels, gscale, flip=flip, crop_offset=off, bucket_cb=cb,
                                          buckets=self.buckets).clone()
+        prof.push("step/allreduce")
         if self.fusion is not None:
             self.fusion.finish()
         elif self.reducer is not None:
             self.reducer.finish()
+        prof.pop()
+        prof.push("step/optimizer")
         self.opt.step()
         self.engine.after_update()
+        prof.pop()
         return s
 
     def write_timeline(self, path: str):
@@ -388,10 +393,60 @@ class _LocalReplicas:
         for e, _ in self.replicas:
             e.after_update()
 
+    def _overlap_setup(self):
+        """Bucketed all-reduce overlapped with backward (GPU): each replica thread records an
+        event when bucket i of its flat gradient is produced; once all R replicas have bucket
+        i, a comm thread makes per-device comm streams wait on those events and issues ONE
+        grouped RCCL all-reduce of bucket i across the devices, while the replicas keep
+        computing the earlier layers' gradients.  (TF's Mirrored all-reduces one pack after
+        the whole backward, imagenet-resnet50-mirror.py:21 [lib].)"""
+        import queue
+        eng0 = self.replicas[0][0]
+        self.buckets = eng0.L.buckets(self.cfg.bucket_mb)
+        self.comm_streams = [torch.cuda.Stream(device=d) for d in self.devices]
+        self._q = queue.Queue()
+        self._lock = threading.Lock()
+
+    def _bucket_cb(self, r):
+        def cb(i):
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.devices[r]))
+            with self._lock:
+                self._events[i][r] = ev
+                self._count[i] += 1
+                full = self._count[i] == self.R
+            if full:
+                self._q.put(i)
+        return cb
+
+    def _comm_loop(self):
+        grads = [e.grads for e, _ in self.replicas]
+        for _ in range(len(self.buckets)):
+            i = self._q.get()
+            s, e = self.buckets[i]
+            for r, d in enumerate(self.devices):
+                self.comm_streams[r].wait_event(self._events[i][r])
+                torch.cuda.set_stream(self.comm_streams[r])     # thread-local current stream per device
+            self.comm.all_reduce([g[s:e] for g in grads], "sum")
+        self._done = []
+        for r, d in enumerate(self.devices):
+            ev = torch.cuda.Event()
+            ev.record(self.comm_streams[r])
+            self._done.append(ev)
+
     def step(self, images, labels, global_batch: int):
         R = self.R
         B = images.shape[0] // R
         stats = [None] * R
+        overlap = self.comm is not None and os.environ.get("PDDL_MIRROR_OVERLAP", "1") != "0"
+        if overlap:
+            if not hasattr(self, "buckets"):
+                self._overlap_setup()
+            nb = len(self.buckets)
+            self._events = [[None] * R for _ in range(nb)]
+            self._count = [0] * nb
+            comm_th = threading.Thread(target=self._comm_loop)
+            comm_th.start()
 
         def run(i):
             eng, _ = self.replicas[i]
@@ -401,7 +456,8 @@ class _LocalReplicas:
             im = images[i * B:(i + 1) * B].to(d, non_blocking=True)
             lb = labels[i * B:(i + 1) * B].to(d, non_blocking=True)
             flip, off = self.augs[i](B)
-            stats[i] = eng.forward_backward(im, lb, 1.0 / global_batch, flip=flip, crop_offset=off).clone()
+            kw = dict(bucket_cb=self._bucket_cb(i), buckets=self.buckets) if overlap else {}
+            stats[i] = eng.forward_backward(im, lb, 1.0 / global_batch, flip=flip, crop_offset=off, **kw).clone()
 
         if self.gpu and R > 1:
             th = [threading.Thread(target=run, args=(i,)) for i in range(R)]
@@ -413,7 +469,11 @@ class _LocalReplicas:
             for i in range(R):
                 run(i)
         grads = [e.grads for e, _ in self.replicas]
-        if self.comm is not None:
+        if overlap:
+            comm_th.join()
+            for r, d in enumerate(self.devices):
+                torch.cuda.current_stream(d).wait_event(self._done[r])
+        elif self.comm is not None:
             self.comm.all_reduce(grads, "sum")
         elif R > 1:
             tot = grads[0].clone()

@@ -98,3 +98,16 @@ def test_mirrored_strategy_one_gpu_uses_rccl():
     h = tr.fit(1, [])
     assert st.mirror.comm is not None and st.num_replicas_in_sync == torch.cuda.device_count()
     assert h.history["loss"][0] == h.history["loss"][0]
+    assert len(st.mirror.buckets) >= 2          # bucketed all-reduce overlapped with backward ran
+
+
+def test_single_strategy_train_mode_bn_on_hip():
+    from pddl.models.engine_bn import HipEngineBNTrain
+    from pddl.parallel.strategies import make_strategy
+    from pddl.train.trainer import Trainer
+    cfg = _cfg("single", bn_mode="train")
+    st = make_strategy(cfg)
+    tr = Trainer(cfg, st)
+    h = tr.fit(1, [])
+    assert isinstance(st.engine, HipEngineBNTrain)
+    assert h.history["loss"][0] == h.history["loss"][0]
