@@ -40,7 +40,11 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a HIP graph (1 GPU)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: BASELINE config 1 (CPU plumbing, fp32 PyTorch reference engine, batch 32)")
     args = ap.parse_args()
+    if args.device == "cpu":
+        return cpu_bench(args)
 
     import torch
     import torch.distributed as dist
@@ -137,6 +141,40 @@ def main():
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_bench(args):
+    """BASELINE.json config 1: the imagenet-resnet50.py plumbing on CPU (no GPU), fp32."""
+    import torch
+    import pddl  # noqa: F401
+    from pddl.models.reference import TorchEngine
+    from pddl.models.resnet50 import ParamLayout
+    from pddl.train.optim import make_optimizer
+    B = args.batch if args.batch != 1024 else 32
+    eng = TorchEngine(ParamLayout(), B, crop=args.crop, device="cpu", bn_mode=args.bn_mode)
+    eng.init(seed=0)
+    opt = make_optimizer(args.optimizer, eng, lr=1e-3 if args.optimizer == "adam" else 0.1)
+    g = torch.Generator().manual_seed(1234)
+    images = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 1000, (B,), dtype=torch.int64, generator=g)
+    for _ in range(args.warmup):
+        eng.forward_backward(images, labels, 1.0 / B)
+        opt.step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        stats = eng.forward_backward(images, labels, 1.0 / B)
+        opt.step()
+    dt = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "images/sec ResNet-50/ImageNet at 1/2/4/8 MI355X + scaling efficiency",
+        "value": round(B * args.steps / dt, 3), "unit": "images/sec", "n_gpus": 0, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (uint8 3x224x224, random labels)",
+        "config": {"model": "ResNet-50 Keras-v1 (25,636,712 params, random init)", "global_batch": B,
+                   "image_size": args.crop, "parallelism": "cpu", "optimizer": args.optimizer,
+                   "bn": args.bn_mode, "threads": torch.get_num_threads(),
+                   "strategy": "single-process CPU (BASELINE config 1)"},
+        "final_loss": round(stats[0].item() / B, 4)}), flush=True)
 
 
 if __name__ == "__main__":
