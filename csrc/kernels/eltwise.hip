@@ -42,12 +42,13 @@ __device__ __forceinline__ float stem_pix(const StemParams& p, int b, int y, int
 }
 
 // Space-to-depth stem input: one thread per s2d pixel, two 16-byte stores.
-__global__ void stem_s2d_kernel(StemParams p, long npix) {
+__global__ void stem_s2d_kernel(StemParams p, int npix, uint64_t mg_ws, uint64_t mg_hs) {
   if (p.crop_dev) { p.oy = p.crop_dev[0]; p.ox = p.crop_dev[1]; }   // graph-replayable crop offset
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < npix; q += (long)gridDim.x * blockDim.x) {
-    const int j = (int)(q % p.Ws);
-    const long t = q / p.Ws;
-    const int i = (int)(t % p.Hs), b = (int)(t / p.Hs);
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < npix; q += gridDim.x * blockDim.x) {
+    const int t = fdiv(q, mg_ws);
+    const int j = q - t * p.Ws;
+    const int b = fdiv(t, mg_hs);
+    const int i = t - b * p.Hs;
     float v[16];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -57,7 +58,7 @@ __global__ void stem_s2d_kernel(StemParams p, long npix) {
       for (int c = 0; c < 3; ++c) v[d * 4 + c] = in ? stem_pix(p, b, y, x, c) : 0.f;
       v[d * 4 + 3] = 0.f;
     }
-    uint4* o = reinterpret_cast<uint4*>(p.out + q * 16);
+    uint4* o = reinterpret_cast<uint4*>(p.out + (long)q * 16);
     o[0] = pack8(v);
     o[1] = pack8(v + 8);
   }
@@ -66,8 +67,9 @@ __global__ void stem_s2d_kernel(StemParams p, long npix) {
 const char* stem_s2d_launch(const StemParams& p, hipStream_t s) {
   if ((p.Hc + 6) != 2 * p.Hs || (p.Wc + 6) != 2 * p.Ws) return "stem_s2d: Hs must be (Hc + 6) / 2 (even crop)";
   const long npix = (long)p.B * p.Hs * p.Ws;
+  if (npix >= (1L << 31) - (1L << 24)) return "stem_s2d: too many pixels for 32-bit indexing";
   const int grid = (int)lmin((npix + 255) / 256, 16384);
-  hipLaunchKernelGGL(stem_s2d_kernel, dim3(grid), dim3(256), 0, s, p, npix);
+  hipLaunchKernelGGL(stem_s2d_kernel, dim3(grid), dim3(256), 0, s, p, (int)npix, fdiv_magic(p.Ws), fdiv_magic(p.Hs));
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
@@ -95,16 +97,20 @@ static int grid_for(long n) { return (int)lmin((n + 255) / 256, 8192); }
 // --------------------------------------------------------------------------- maxpool
 // Window of output (ho, wo) covers input rows 2ho-1 .. 2ho+1 (ZeroPadding2D(1) then 3x3/s2
 // valid).  Padded taps are real zeros (as in Keras); the first maximum in scan order wins.
+// Index math is 32-bit with magic-number division (the launchers check the element counts
+// fit): 64-bit div / mod per element made these kernels ALU-bound.
+struct PoolDiv { uint64_t cg, w, h; };
 __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
-                                   uint8_t* __restrict__ bits, int B, int H, int W, int C, int Ho, int Wo) {
+                                   uint8_t* __restrict__ bits, int B, int H, int W, int C, int Ho, int Wo, PoolDiv dv) {
   const int cg = C / 8;
-  const long total = (long)B * Ho * Wo * cg;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int g = (int)(t % cg);
-    const long pix = t / cg;
-    const int wo = (int)(pix % Wo);
-    const long t2 = pix / Wo;
-    const int ho = (int)(t2 % Ho), b = (int)(t2 / Ho);
+  const int total = B * Ho * Wo * cg;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int pix = fdiv(t, dv.cg);
+    const int g = t - pix * cg;
+    const int t2 = fdiv(pix, dv.w);
+    const int wo = pix - t2 * Wo;
+    const int b = fdiv(t2, dv.h);
+    const int ho = t2 - b * Ho;
     float best[8]; uint8_t bi[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
@@ -124,7 +130,7 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
         for (int e = 0; e < 8; ++e)
           if (v[e] > best[e]) { best[e] = v[e]; bi[e] = (uint8_t)(r * 3 + s); }
       }
-    const long o = pix * C + g * 8;
+    const long o = (long)pix * C + g * 8;
     const uint4 yv = pack8(best);
     *reinterpret_cast<uint4*>(y + o) = yv;
     if (bits) bits[o >> 3] = (uint8_t)pos_bits8(yv);
@@ -139,16 +145,18 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
 // multiple of C/8 every thread keeps one channel group, folded across the wave at the end.
 __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
                                    const bf16_t* __restrict__ xmask, bf16_t* __restrict__ gx,
-                                   int B, int H, int W, int C, int Ho, int Wo, float* __restrict__ colsum) {
+                                   int B, int H, int W, int C, int Ho, int Wo, float* __restrict__ colsum,
+                                   PoolDiv dv) {
   const int cg = C / 8;
-  const long total = (long)B * H * W * cg;
+  const int total = B * H * W * cg;
   float cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int g = (int)(t % cg);
-    const long pix = t / cg;
-    const int w = (int)(pix % W);
-    const long t2 = pix / W;
-    const int h = (int)(t2 % H), b = (int)(t2 / H);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int pix = fdiv(t, dv.cg);
+    const int g = t - pix * cg;
+    const int t2 = fdiv(pix, dv.w);
+    const int w = pix - t2 * W;
+    const int b = fdiv(t2, dv.h);
+    const int h = t2 - b * H;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int hp = h + 1, wp = w + 1;  // padded coordinates
     const int ho_lo = max(0, (hp - 1) / 2), ho_hi = min(Ho - 1, hp / 2);
@@ -172,7 +180,7 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t*
         }
       }
     }
-    const long o = pix * C + g * 8;
+    const long o = (long)pix * C + g * 8;
     if (xmask) {
       float mv[8];
       unpack8(*reinterpret_cast<const uint4*>(xmask + o), mv);
@@ -202,8 +210,10 @@ int maxpool_bwd_partial_rows(int B, int H, int W, int C) { return grid_for((long
 const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, uint8_t* bits, int B, int H, int W, int C, int Ho,
                                int Wo, hipStream_t s) {
   if (C % 8) return "maxpool: C % 8";
+  if ((long)B * H * W * C / 8 >= (1L << 31) - (1L << 24)) return "maxpool: too many elements for 32-bit indexing";
+  const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic(Wo), fdiv_magic(Ho)};
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)B * Ho * Wo * C / 8)), dim3(256), 0, s, x, y, idx, bits,
-                     B, H, W, C, Ho, Wo);
+                     B, H, W, C, Ho, Wo, dv);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
@@ -211,8 +221,10 @@ const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uin
                                int H, int W, int C, int Ho, int Wo, float* colsum, hipStream_t s) {
   if (C % 8) return "maxpool: C % 8";
   if (colsum && (64 % (C / 8))) return "maxpool: fused colsum needs C/8 to divide 64";
+  if ((long)B * H * W * C / 8 >= (1L << 31) - (1L << 24)) return "maxpool: too many elements for 32-bit indexing";
+  const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic(W), fdiv_magic(H)};
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long)B * H * W * C / 8)), dim3(256), 0, s, gy, idx, xmask,
-                     gx, B, H, W, C, Ho, Wo, colsum);
+                     gx, B, H, W, C, Ho, Wo, colsum, dv);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
