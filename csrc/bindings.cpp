@@ -377,6 +377,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (which == "igemm") pddl::g_igemm_variant = v;
     else if (which == "igemm_deep") pddl::g_igemm_deep = v;
     else if (which == "igemm_big") pddl::g_igemm_big = v;
+    else if (which == "igemm_pf") pddl::g_igemm_pf = v;
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });

@@ -43,7 +43,11 @@ enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 //   NW = 4, NSTAGE 1/2: 2 blocks per CU, the next k-tile's LDS-DMA overlaps this tile's MFMAs.
 //   NW = 8 (256x128), NSTAGE 3: one 144 KiB block per CU, 2 waves per SIMD; a 3-deep LDS ring
 //   keeps two k-tiles in flight (counted vmcnt across a raw barrier) for compute-bound layers.
-template <int BM, int BN, int NW, int NSTAGE, int AM>
+// PF: the epilogue's per-element operand (forward residual / dgrad residual-gradient `add`,
+// plus the dgrad ReLU bitmask) of the whole wave tile is loaded into registers before the
+// accumulators are staged through LDS, so its HBM latency overlaps the staging instead of
+// stalling every store iteration (short-K 1x1 layers are epilogue-bound).
+template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmParams p) {
   constexpr int WTM = 64, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -228,6 +232,25 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
       seg0 = false;
     }
   }
+  constexpr int NIT = 32 / RPI;
+  uint4 pre[PF ? (TM / 2) * NIT : 1];
+  uint32_t pre_bits[PF ? TM / 2 : 1];
+  const bool pf_bits = PF && p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
+  if (PF) {
+    const bf16_t* src = p.mode == EPI_FWD ? p.res : p.add;
+    const int ldp = p.mode == EPI_FWD ? p.ld_res : p.ld_add;
+#pragma unroll
+    for (int pass = 0; pass < TM / 2; ++pass) {
+      pre_bits[pass] = 0;
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int gm = m0 + wm * WTM + pass * 32 + it * RPI + rr;
+        const bool ok = gm < p.M && col_ok;
+        pre[pass * NIT + it] = ok ? *reinterpret_cast<const uint4*>(src + (long)gm * ldp + gn) : make_uint4(0, 0, 0, 0);
+        if (pf_bits && ok) pre_bits[pass] |= (uint32_t)p.bits_mask[(long)gm * p.ld_bits_mask + (gn >> 3)] << (8 * it);
+      }
+    }
+  }
 #pragma unroll
   for (int pass = 0; pass < TM / 2; ++pass) {
 #pragma unroll
@@ -251,7 +274,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
           for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
           if (p.res) {
             float rv[8];
-            unpack8(*reinterpret_cast<const uint4*>(p.res + (long)gm * p.ld_res + gn), rv);
+            uint4 r4;   // (if/else, not ?: -- an lvalue select would force `pre` into scratch)
+            if (PF) r4 = pre[pass * NIT + it];
+            else r4 = *reinterpret_cast<const uint4*>(p.res + (long)gm * p.ld_res + gn);
+            unpack8(r4, rv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += rv[e];
           }
@@ -297,7 +323,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
             for (int e = 0; e < 8; ++e) w[e] = (q == 0) ? v[e] : 0.f;
             if (p.add) {
               float av[8];
-              unpack8(*reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn), av);
+              uint4 a4;
+              if (PF) a4 = pre[pass * NIT + it];
+              else a4 = *reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn);
+              unpack8(a4, av);
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] += av[e];
             }
@@ -307,7 +336,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
             } else if (p.bits_mask) {
-              const uint32_t byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
+              uint32_t byte;
+              if (pf_bits) byte = (pre_bits[pass] >> (8 * it)) & 0xffu;
+              else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
             }
@@ -361,6 +392,7 @@ int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wav
 int g_igemm_big = 0;       // 8-wave 256x128 3-stage tile: 0 never (default: measured slower on every
                            // ResNet-50 layer, kbench A/B), 1 heuristic, 2 always (Nn > 64)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
+int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 layers with a residual / add
 
 static bool igemm_no_halo(const IgemmParams& p) {
   return p.pad == 0 && (p.Ho - 1) * p.stride + p.R <= p.H && (p.Wo - 1) * p.stride + p.S <= p.W;
@@ -425,7 +457,23 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   const int cfg = igemm_config(p.M, p.Nn, p.K);
   const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : 128;
   const int nwg = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
-  if (cfg == 2) {
+  // PF where the prefetched operand exists for every element (forward residual; dgrad
+  // residual-gradient without the stride-2 scatter).  Measured (bench/epilogue.py, b1024,
+  // profiles/r1_epilogue_prefetch_ab.json): forward +3-20% on every stage; dgrad +10-14% for
+  // K >= 256 but -8-10% for the single-stage K <= 128 tiles, whose occupancy the 24 extra
+  // VGPRs cut from 3 to 2 waves per SIMD -- so dgrad uses it only on 2-stage tiles.
+  const bool pf = g_igemm_pf && am == AM_DIRECT && cfg != 2 &&
+                  ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && ns == 2));
+  if (pf) {
+#define IG_PF(BM_, BN_, NS_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_DIRECT, true>), dim3(nwg), dim3(256), 0, stream, p)
+    if (cfg == 1) {
+      if (ns == 1) IG_PF(128, 128, 1); else IG_PF(128, 128, 2);
+    } else {
+      if (ns == 1) IG_PF(256, 64, 1); else IG_PF(256, 64, 2);
+    }
+#undef IG_PF
+  } else if (cfg == 2) {
     IG_MODES(256, 128, 8, 3)
   } else if (cfg == 1) {
     if (ns == 1) IG_MODES(128, 128, 4, 1) else IG_MODES(128, 128, 4, 2)
