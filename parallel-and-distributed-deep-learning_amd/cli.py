@@ -50,6 +50,10 @@ def run(preset: str, argv: Optional[List[str]] = None, extra=None) -> int:
         _banner(cfg, strategy)
         if cfg.verbose:
             print(model_summary(cfg), flush=True)
+    if cfg.strategy == "multiworker":
+        # the reference's informational print (imagenet-resnet50-multiworkers.py:76; 10M-image
+        # epoch assumption, Q9) -- printed by every worker, as there
+        print("Steps per epoch: ", int((10000000 / strategy.num_replicas_in_sync) / strategy.world), flush=True)
     cbs = default_callbacks(cfg, strategy)
     trainer.fit(cfg.epochs, cbs)
     if cfg.timeline and hasattr(strategy, "write_timeline"):

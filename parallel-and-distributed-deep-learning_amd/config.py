@@ -57,7 +57,7 @@ class TrainConfig:
     warmup_epochs: int = 0                         # hvd LearningRateWarmupCallback (hvd.py:115): 3
     # distribution
     strategy: str = "single"                       # single | mirrored | multiworker | horovod | ps
-    bucket_mb: float = 32.0                        # gradient bucket size (7-link xGMI tuned)
+    bucket_mb: float = 32.0                        # gradient bucket size (7-link xGMI tuned); <= 0: autotune
     grad_dtype: str = "fp32"                       # all-reduce dtype
     num_ps: int = 1
     num_workers: int = 1

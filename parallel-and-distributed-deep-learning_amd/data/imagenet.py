@@ -39,7 +39,7 @@ def io_module():
     global _io
     if _io is None:
         import torch  # noqa: F401  (libc10 first)
-        cands = sorted(glob.glob(os.path.join(_PKG, "_pddl_io*.so")))
+        cands = sorted(glob.glob(os.path.join(os.environ.get("PDDL_NATIVE_DIR") or _PKG, "_pddl_io*.so")))
         if not cands:
             raise RuntimeError("native ImageNet reader _pddl_io not built (run `python pddl_build.py`)")
         loader = importlib.machinery.ExtensionFileLoader("_pddl_io", cands[-1])

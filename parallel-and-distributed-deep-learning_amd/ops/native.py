@@ -20,6 +20,9 @@ _err = None
 def _candidates():
     pats = ["_pddl_native*.so"]
     out = []
+    override = os.environ.get("PDDL_NATIVE_DIR")   # e.g. the sanitizer build (scripts/sanitize_host.sh)
+    if override:
+        return sorted(glob.glob(os.path.join(override, pats[0])))
     for d in (_PKG, _REPO):
         for p in pats:
             out += sorted(glob.glob(os.path.join(d, p)))

@@ -253,7 +253,19 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
         cap = max(self.cfg.batch_size, self.cfg.val_batch_size or 0)
         self.engine, self.opt = self._make_engine_and_opt(self.device, cap)
         self.aug = Augment(self.cfg, self.device, self.cfg.seed + 1000 * self.rank)
-        self.buckets = self.engine.L.buckets(self.cfg.bucket_mb)
+        # bucket_mb <= 0: autotune (Horovod's HOROVOD_AUTOTUNE analogue for the fusion threshold)
+        self._tune = None
+        mb = self.cfg.bucket_mb
+        if mb <= 0 and self.world > 1:
+            self._tune = {"cands": [8.0, 16.0, 32.0, 64.0], "i": 0, "t": [], "best": []}
+            mb = self._tune["cands"][0]
+        self._make_reducer(mb if mb > 0 else 32.0)
+
+    def _make_reducer(self, bucket_mb: float):
+        if getattr(self, "fusion", None) is not None:
+            self.fusion.shutdown()
+        self.bucket_mb = bucket_mb
+        self.buckets = self.engine.L.buckets(bucket_mb)
         self.fusion = None
         self.reducer = None
         if self.world > 1:
@@ -268,7 +280,40 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
             if self.fusion is None:
                 self.reducer = BucketAllReducer(self.engine.grads, self.buckets, comm_dtype=self.cfg.grad_dtype)
 
+    _TUNE_STEPS = int(os.environ.get("PDDL_AUTOTUNE_STEPS", "4"))   # per candidate: 1 discarded + rest timed
+
+    def _autotune_step(self, images, labels):
+        """Time a few steps per bucket size; rank 0's pick (min median) is broadcast so every
+        rank builds the same buckets (the collectives must match)."""
+        import time as _t
+        tu = self._tune
+        self.sync()
+        t0 = _t.perf_counter()
+        s = self._step(images, labels)
+        self.sync()
+        tu["t"].append(_t.perf_counter() - t0)
+        if len(tu["t"]) == self._TUNE_STEPS:
+            tu["best"].append(float(np.median(tu["t"][1:] or tu["t"])))
+            tu["t"] = []
+            tu["i"] += 1
+            if tu["i"] < len(tu["cands"]):
+                self._make_reducer(tu["cands"][tu["i"]])
+            else:
+                pick = [tu["cands"][int(np.argmin(tu["best"]))]]
+                dist.broadcast_object_list(pick, src=0)
+                if self.is_chief:
+                    ms = ", ".join(f"{c:g} MiB: {b * 1e3:.1f} ms" for c, b in zip(tu["cands"], tu["best"]))
+                    print(f"[autotune] gradient bucket size {pick[0]:g} MiB ({ms})", flush=True)
+                self._make_reducer(pick[0])
+                self._tune = None
+        return s
+
     def train_step(self, images, labels):
+        if self._tune is not None:
+            return self._autotune_step(images, labels)
+        return self._step(images, labels)
+
+    def _step(self, images, labels):
         B = images.shape[0]
         flip, off = self.aug(B)
         gscale = 1.0 / (B * self.world)
@@ -434,7 +479,40 @@ class _LocalReplicas:
             ev.record(self.comm_streams[r])
             self._done.append(ev)
 
+    def _graphed_step(self, images, labels, global_batch: int):
+        """cfg.graphs: one HIP-graph replay of forward+backward per device, issued from this
+        thread (launch cost ~1 call per GPU instead of ~180 per replica thread), then ONE
+        grouped RCCL all-reduce of the flat gradients and the eager optimizer steps."""
+        from ..train.graph import GraphedTrainStep
+        R = self.R
+        B = images.shape[0] // R
+        if not hasattr(self, "graphed") or self.graphed[0].B != B:
+            H, W = images.shape[1:3]
+            self.graphed = []
+            for i, d in enumerate(self.devices):
+                with torch.cuda.device(d):
+                    eng, opt = self.replicas[i]
+                    self.graphed.append(GraphedTrainStep(eng, opt, B, (H, W), 1.0 / global_batch,
+                                                         with_optimizer=False))
+        stats = []
+        for i, d in enumerate(self.devices):
+            with torch.cuda.device(d):
+                flip, off = self.augs[i](B)
+                stats.append(self.graphed[i](images[i * B:(i + 1) * B].to(d, non_blocking=True),
+                                             labels[i * B:(i + 1) * B].to(d, non_blocking=True), flip, off))
+        self.comm.all_reduce([e.grads for e, _ in self.replicas], "sum")
+        for (e, o), d in zip(self.replicas, self.devices):
+            with torch.cuda.device(d):
+                o.step()
+                e.after_update()
+        out = stats[0].to(self.devices[0])
+        for s in stats[1:]:
+            out = out + s.to(self.devices[0])
+        return out
+
     def step(self, images, labels, global_batch: int):
+        if self.cfg.graphs and self.comm is not None:
+            return self._graphed_step(images, labels, global_batch)
         R = self.R
         B = images.shape[0] // R
         stats = [None] * R

@@ -11,7 +11,10 @@ Everything that changes between steps lives in device memory the graph reads:
   * the optimizer's step counter and learning rate are the device buffer `opt.hs`
     (train/optim.py), advanced by a kernel inside the graph; host LR changes are written to
     it between replays.
-Multi-GPU steps keep eager launches: their collectives are issued from the bucket callbacks.
+Horovod-style multi-process steps keep eager launches: their collectives are issued from the
+bucket callbacks.  The in-process Mirrored strategy replays one forward+backward graph per
+device from a single thread (no per-replica Python launch cost, no GIL contention), then runs
+the grouped all-reduce and the optimizer (`with_optimizer=False`).
 """
 from __future__ import annotations
 
@@ -21,11 +24,15 @@ import torch
 
 
 class GraphedTrainStep:
+    """with_optimizer=False records forward + backward only (Mirrored: the cross-device
+    all-reduce runs between the replay and an eager optimizer step)."""
+
     def __init__(self, engine, optimizer, batch: int, image_hw: Tuple[int, int], gscale: float,
-                 image_dtype=torch.uint8):
+                 image_dtype=torch.uint8, with_optimizer: bool = True):
         if not engine.params.is_cuda:
             raise RuntimeError("GraphedTrainStep needs the GPU engine")
         self.engine, self.opt, self.B, self.gscale = engine, optimizer, batch, float(gscale)
+        self.with_optimizer = with_optimizer
         dev = engine.params.device
         H, W = image_hw
         self.images = torch.zeros(batch, H, W, 3, dtype=image_dtype, device=dev)
@@ -38,8 +45,9 @@ class GraphedTrainStep:
     def _body(self):
         eng = self.engine
         stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip, crop_offset=self.crop)
-        self.opt.step()
-        eng.after_update()
+        if self.with_optimizer:
+            self.opt.step()
+            eng.after_update()
         return stats
 
     def _load(self, images, labels, flip, crop_offset):
@@ -62,7 +70,8 @@ class GraphedTrainStep:
     def capture(self):
         """Record the step.  Call after one eager step of the engine (its lazily built tables
         exist); capture itself runs no kernels, so it does not advance training."""
-        self.opt.sync_hparams()
+        if self.with_optimizer:
+            self.opt.sync_hparams()
         torch.cuda.synchronize()
         it = self.opt._iterations
         g = torch.cuda.CUDAGraph()
@@ -77,7 +86,9 @@ class GraphedTrainStep:
             out = self._body()        # first call: eager (builds the engine's tables), then capture
             self.capture()
             return out
-        self.opt.sync_hparams()
+        if self.with_optimizer:
+            self.opt.sync_hparams()
         self.graph.replay()
-        self.opt._iterations += 1
+        if self.with_optimizer:
+            self.opt._iterations += 1
         return self.stats

@@ -51,6 +51,11 @@ def compile_kernels():
 
 
 kernel_objs = compile_kernels()
+# PDDL_SANITIZE=1: host code (bindings, runtime, io) with AddressSanitizer + UBSan for the CPU
+# test suite (scripts/sanitize_host.sh); device code is unaffected (it is compiled above).
+SAN = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"] if os.environ.get("PDDL_SANITIZE") else []
+HOST_CFLAGS = (["-O1"] if SAN else ["-O2", "-g0"]) + ["-std=c++17"] + SAN
+STRIP = [] if SAN else ["-Wl,--strip-debug"]
 host_srcs = [os.path.join("csrc", "bindings.cpp")] + sorted(glob.glob(os.path.join("csrc", "runtime", "*.cpp")))
 
 setup(
@@ -64,8 +69,8 @@ setup(
             libraries=["amdhip64", "c10_hip", "torch_hip", "rccl"],
             define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
             extra_objects=kernel_objs,
-            extra_link_args=["-Wl,-rpath,/opt/rocm/lib", "-Wl,--strip-debug"],
-            extra_compile_args=["-O2", "-g0", "-std=c++17"],
+            extra_link_args=["-Wl,-rpath,/opt/rocm/lib"] + STRIP + SAN,
+            extra_compile_args=HOST_CFLAGS,
         ),
         CppExtension(
             "_pddl_io",
@@ -73,8 +78,8 @@ setup(
             include_dirs=["/opt/conda/include"],
             library_dirs=["/opt/conda/lib"],
             libraries=["jpeg"],
-            extra_link_args=["-Wl,-rpath,/opt/conda/lib", "-Wl,--strip-debug"],
-            extra_compile_args=["-O2", "-g0", "-std=c++17"],
+            extra_link_args=["-Wl,-rpath,/opt/conda/lib"] + STRIP + SAN,
+            extra_compile_args=HOST_CFLAGS,
         ),
         CppExtension(
             "_pddl_h5",
@@ -82,8 +87,8 @@ setup(
             include_dirs=["/opt/conda/include"],
             library_dirs=["/opt/conda/lib"],
             libraries=["hdf5"],
-            extra_link_args=["-Wl,-rpath,/opt/conda/lib", "-Wl,--strip-debug"],
-            extra_compile_args=["-O2", "-g0", "-std=c++17"],
+            extra_link_args=["-Wl,-rpath,/opt/conda/lib"] + STRIP + SAN,
+            extra_compile_args=HOST_CFLAGS,
         ),
     ],
     cmdclass={"build_ext": BuildExtension.with_options(use_ninja=True)},

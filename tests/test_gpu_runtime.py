@@ -111,3 +111,23 @@ def test_single_strategy_train_mode_bn_on_hip():
     h = tr.fit(1, [])
     assert isinstance(st.engine, HipEngineBNTrain)
     assert h.history["loss"][0] == h.history["loss"][0]
+
+
+def test_mirrored_graphed_step_matches_eager():
+    """Mirrored with --graphs (per-device forward+backward graph replays from one thread)
+    follows the eager Mirrored trajectory."""
+    from pddl.parallel.strategies import make_strategy
+    from pddl.train.trainer import Trainer
+    res = []
+    for graphs in (False, True):
+        cfg = _cfg("mirrored", graphs=graphs, flip=False, max_steps=3, batch_size=8)
+        st = make_strategy(cfg)
+        tr = Trainer(cfg, st)
+        h = tr.fit(1, [], validation=False)
+        res.append((h.history["loss"][0], st.engine.params.clone(), st.opt.iterations))
+        if graphs:
+            assert st.mirror.graphed[0].graph is not None
+    (l0, p0, i0), (l1, p1, i1) = res
+    assert i0 == i1 == 3
+    assert abs(l0 - l1) <= 1e-3 * abs(l0)
+    assert ((p0 - p1).norm() / p0.norm()).item() < 2e-3

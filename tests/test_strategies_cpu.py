@@ -39,7 +39,7 @@ def _rank_main(rank, world, port, preset, kw, q):
     st, hist = _train(preset, **kw)
     n = st.engine.L.n_trainable
     q.put((rank, st.engine.params[:n].numpy().copy(), hist.history["loss"][0],
-           type(getattr(st, "fusion", None)).__name__))
+           type(getattr(st, "fusion", None)).__name__, getattr(st, "bucket_mb", None)))
     import torch.distributed as dist
     dist.barrier()
     dist.destroy_process_group()
@@ -57,7 +57,7 @@ def _spawn(world, preset, kw):
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    return [(r, torch.from_numpy(p), l, f) for r, p, l, f in sorted(out, key=lambda t: t[0])]
+    return [(r, torch.from_numpy(p), l, f, mb) for r, p, l, f, mb in sorted(out, key=lambda t: t[0])]
 
 
 @pytest.fixture(scope="module")
@@ -75,7 +75,7 @@ def test_horovod_2_ranks_equals_single_global_batch(single_b4):
     out = _spawn(2, "horovod", dict(batch_size=2, lr=1e-2, lr_scale_by_size=False, warmup_epochs=0,
                                     shard_by="batch"))
     assert out[0][3] == "FusionEngine"          # the native C++ fusion engine was used
-    for _, p, loss, _ in out:
+    for _, p, loss, _, _ in out:
         assert _close(p, ref)
     assert abs(out[0][2] - ref_loss) <= 1e-5 * abs(ref_loss)
 
@@ -83,7 +83,7 @@ def test_horovod_2_ranks_equals_single_global_batch(single_b4):
 def test_multiworker_element_sharding_equals_single(single_b4):
     ref, _ = single_b4
     out = _spawn(2, "multiworker", dict(batch_size=2, val_batch_size=2))
-    for _, p, _, _ in out:
+    for _, p, _, _, _ in out:
         assert _close(p, ref)
 
 
@@ -94,3 +94,16 @@ def test_mirrored_two_cpu_replicas_equals_single(single_b4, monkeypatch):
     assert st.num_replicas_in_sync == 2 and st.global_batch == 4
     for eng, _ in st.mirror.replicas:
         assert _close(eng.params[:eng.L.n_trainable], ref)
+
+
+def test_horovod_bucket_autotune_picks_one_size_and_matches_fixed(monkeypatch):
+    """--bucket-mb 0: 4 candidate bucket sizes timed in turn (fusion engine rebuilt between
+    them), rank 0's pick broadcast; the trajectory equals a fixed-bucket run."""
+    monkeypatch.setenv("PDDL_AUTOTUNE_STEPS", "2")
+    kw = dict(batch_size=2, lr=1e-2, lr_scale_by_size=False, warmup_epochs=0, shard_by="batch", max_steps=9,
+              train_images=64)
+    tuned = _spawn(2, "horovod", dict(kw, bucket_mb=0))
+    fixed = _spawn(2, "horovod", dict(kw, bucket_mb=32))
+    assert tuned[0][4] in (8.0, 16.0, 32.0, 64.0) and tuned[0][4] == tuned[1][4]
+    for (_, p, _, _, _), (_, q, _, _, _) in zip(tuned, fixed):
+        assert _close(p, q)
