@@ -51,9 +51,10 @@ def compile_kernels():
 
 
 kernel_objs = compile_kernels()
-# PDDL_SANITIZE=1: host code (bindings, runtime, io) with AddressSanitizer + UBSan for the CPU
-# test suite (scripts/sanitize_host.sh); device code is unaffected (it is compiled above).
-SAN = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"] if os.environ.get("PDDL_SANITIZE") else []
+# PDDL_SANITIZE=1 (UBSan) or =<list> (e.g. address,undefined): host code (bindings, runtime, io)
+# built with sanitizers for the CPU test suite (scripts/sanitize_host.sh); device code unaffected.
+_san = os.environ.get("PDDL_SANITIZE", "")
+SAN = ([f"-fsanitize={'undefined' if _san == '1' else _san}", "-fno-omit-frame-pointer", "-g"] if _san else [])
 HOST_CFLAGS = (["-O1"] if SAN else ["-O2", "-g0"]) + ["-std=c++17"] + SAN
 STRIP = [] if SAN else ["-Wl,--strip-debug"]
 host_srcs = [os.path.join("csrc", "bindings.cpp")] + sorted(glob.glob(os.path.join("csrc", "runtime", "*.cpp")))
@@ -75,7 +76,7 @@ setup(
         CppExtension(
             "_pddl_io",
             [os.path.join("csrc", "io", "imagenet_io.cpp")],
-            include_dirs=["/opt/conda/include"],
+            include_dirs=[os.path.join(ROOT, "csrc"), "/opt/conda/include"],
             library_dirs=["/opt/conda/lib"],
             libraries=["jpeg"],
             extra_link_args=["-Wl,-rpath,/opt/conda/lib"] + STRIP + SAN,

@@ -33,7 +33,7 @@ def _engines(B, crop, image_size):
     return L, he, te
 
 
-@pytest.mark.parametrize("crop,image_size", [(224, 224), (160, 224)])
+@pytest.mark.parametrize("crop,image_size", [(224, 224), (160, 224), (244, 224)])   # 244: Q1 up-size, odd grids
 def test_engine_matches_reference(crop, image_size):
     torch.manual_seed(0)
     B = 4
