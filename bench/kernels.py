@@ -86,7 +86,7 @@ def main():
         print(json.dumps(brow), flush=True)
         res.append(brow)
         del am, bm, gm
-        for kind, fn, knob, variants in (("igemm", fwd, "igemm_big", [0, 2]), ("wgrad", wg, "wgrad", [0])):
+        for kind, fn, knob, variants in (("igemm", fwd, "igemm_big", [0, 3]), ("wgrad", wg, "wgrad", [0])):
             t = {v: [] for v in variants}
             for _ in range(a.rounds):
                 for v in variants:

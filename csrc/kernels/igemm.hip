@@ -47,9 +47,10 @@ enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 // plus the dgrad ReLU bitmask) of the whole wave tile is loaded into registers before the
 // accumulators are staged through LDS, so its HBM latency overlaps the staging instead of
 // stalling every store iteration (short-K 1x1 layers are epilogue-bound).
-template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false>
+// WTM_: wave-tile rows (64, or 128 for the 256x256 tile: 8 waves as 2 x 4, 128x64 each).
+template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmParams p) {
-  constexpr int WTM = 64, WTN = 64;
+  constexpr int WTM = WTM_, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int WAVES_N = BN / WTN;
   static_assert((BM / WTM) * (BN / WTN) == NW, "wave grid must cover the block tile");
@@ -390,7 +391,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
 
 int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wave tiles)
 int g_igemm_big = 0;       // 8-wave 256x128 3-stage tile: 0 never (default: measured slower on every
-                           // ResNet-50 layer, kbench A/B), 1 heuristic, 2 always (Nn > 64)
+                           // ResNet-50 layer, kbench A/B), 1 heuristic, 2 always (Nn > 64);
+                           // 256x256 8-wave tile: 3 heuristic (Nn, K >= 256), 4 always (Nn > 128)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
 int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 layers with a residual / add
 
@@ -418,18 +420,23 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
 }
 
 // Tile configuration of a problem: 0 = 256x64 / 4 waves (Nn <= 64), 1 = 128x128 / 4 waves,
-// 2 = 256x128 / 8 waves / 3-stage ring (compute-bound: K >= 256 and >= 2 tiles per CU).
+// 2 = 256x128 / 8 waves / 3-stage ring, 3 = 256x256 / 8 waves of 128x64 / 2-stage (half the
+// LDS-DMA pieces per MFMA of the 128x128 tile; for wide, long-K layers).
 static int igemm_config(int M, int Nn, int K) {
   if (Nn <= 64) return 0;
+  if (g_igemm_big == 4 && Nn > 128) return 3;   // forced (equivalence tests)
+  if (g_igemm_big == 3 && Nn >= 256 && K >= 256 && (long)((M + 255) / 256) * ((Nn + 255) / 256) >= 256) return 3;
   const long big_tiles = (long)((M + 255) / 256) * ((Nn + 127) / 128);
   if (g_igemm_big == 2 || (g_igemm_big == 1 && K >= 256 && big_tiles >= 512)) return 2;
   return 1;
 }
 static int igemm_bm(int cfg) { return cfg == 1 ? 128 : 256; }
+static int igemm_wtm(int cfg) { return cfg == 3 ? 128 : 64; }
 
 int igemm_partial_rows(int M, int Nn, int K) {
-  const int BM = igemm_bm(igemm_config(M, Nn, K));
-  return ((M + BM - 1) / BM) * (BM / 64);
+  const int cfg = igemm_config(M, Nn, K);
+  const int BM = igemm_bm(cfg);
+  return ((M + BM - 1) / BM) * (BM / igemm_wtm(cfg));
 }
 
 const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
@@ -455,14 +462,14 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
     else IG_GO(BM_, BN_, NW_, NS_, AM_DUAL);                         \
   }
   const int cfg = igemm_config(p.M, p.Nn, p.K);
-  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : 128;
+  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : (cfg == 3 ? 256 : 128);
   const int nwg = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
   // PF where the prefetched operand exists for every element (forward residual; dgrad
   // residual-gradient without the stride-2 scatter).  Measured (bench/epilogue.py, b1024,
   // profiles/r1_epilogue_prefetch_ab.json): forward +3-20% on every stage; dgrad +10-14% for
   // K >= 256 but -8-10% for the single-stage K <= 128 tiles, whose occupancy the 24 extra
   // VGPRs cut from 3 to 2 waves per SIMD -- so dgrad uses it only on 2-stage tiles.
-  const bool pf = g_igemm_pf && am == AM_DIRECT && cfg != 2 &&
+  const bool pf = g_igemm_pf && am == AM_DIRECT && cfg <= 1 &&
                   ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && ns == 2));
   if (pf) {
 #define IG_PF(BM_, BN_, NS_) \
@@ -473,6 +480,13 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
       if (ns == 1) IG_PF(256, 64, 1); else IG_PF(256, 64, 2);
     }
 #undef IG_PF
+  } else if (cfg == 3) {
+#define IG_W(AM_) \
+  hipLaunchKernelGGL((igemm_kernel<256, 256, 8, 2, AM_, false, 128>), dim3(nwg), dim3(512), 0, stream, p)
+    if (am == AM_DIRECT) IG_W(AM_DIRECT);
+    else if (am == AM_HALO) IG_W(AM_HALO);
+    else IG_W(AM_DUAL);
+#undef IG_W
   } else if (cfg == 2) {
     IG_MODES(256, 128, 8, 3)
   } else if (cfg == 1) {

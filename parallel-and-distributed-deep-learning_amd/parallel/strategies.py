@@ -505,7 +505,7 @@ class _LocalReplicas:
             with torch.cuda.device(d):
                 o.step()
                 e.after_update()
-        out = stats[0].to(self.devices[0])
+        out = stats[0].to(self.devices[0]).clone()   # (the graphs' static stats buffers are reused)
         for s in stats[1:]:
             out = out + s.to(self.devices[0])
         return out

@@ -132,10 +132,12 @@ def test_igemm_dgrad(case):
     assert rel(cs, ref.sum((0, 1, 2))) < 1e-2
 
 
+@pytest.mark.parametrize("big", [2, 4])
 @pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual"])
-def test_igemm_big_tile_matches(kind):
-    """The 8-wave 256x128 3-stage configuration computes the same result (same k order)
-    as the 4-wave 128x128 one, including the fused epilogues."""
+def test_igemm_big_tile_matches(kind, big):
+    """The 8-wave 256x128 3-stage (knob 2) and 256x256 2-stage (knob 4) configurations compute
+    the same result (same k order) as the 4-wave 128x128 one, including the fused epilogues
+    and the per-wave column-sum rows."""
     torch.manual_seed(12)
     n, h, ho = 3, 14, 7
     if kind == "fwd3x3":
@@ -151,8 +153,8 @@ def test_igemm_big_tile_matches(kind):
         wt = rnd(256, 640, scale=0.05)
         mask = rnd(n, h, h, 256)
     outs = []
-    for big in (0, 2):
-        N().set_variant("igemm_big", big)
+    for knob in (0, big):
+        N().set_variant("igemm_big", knob)
         try:
             if kind == "fwd3x3":
                 y = torch.empty(n, h, h, 256, dtype=torch.bfloat16, device=dev)
