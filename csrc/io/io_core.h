@@ -209,8 +209,10 @@ class Pool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  // run fn(i) for i in [0, n) on the pool; rethrows the first error
+  // run fn(i) for i in [0, n) on the pool; rethrows the first error.  Calls from several
+  // threads are serialized (one job in flight).
   void run(int64_t n, const std::function<void(int64_t)>& fn) {
+    std::lock_guard<std::mutex> job(run_mu_);
     {
       std::lock_guard<std::mutex> lk(mu_);
       fn_ = &fn; n_ = n; next_.store(0); done_ = 0; err_.clear(); ++gen_;
@@ -250,7 +252,7 @@ class Pool {
     }
   }
   std::vector<std::thread> th_;
-  std::mutex mu_;
+  std::mutex run_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   bool stop_ = false;
   uint64_t gen_ = 0;

@@ -16,8 +16,10 @@
 //   * Readiness "negotiation" is static: buckets are issued strictly in id order on every rank
 //     and the bucket signature is all-reduced once at construction to prove all ranks agree
 //     (Horovod's controller exists to handle dynamic orders; ours is deterministic).
-//   * Stall watchdog: a thread flags any bucket queued but not issued within the timeout
-//     (a rank that stopped producing gradients) and `finish()` raises with a diagnostic.
+//   * Stall watchdog: a thread flags any bucket queued but not issued within the timeout, or
+//     issued but not completed within it (a peer that stopped producing gradients or never
+//     joined the collective), and the next `finish()` / `begin_step()` raises with a diagnostic
+//     (on a host-blocking backend `finish()` bounds its wait by the same timeout).
 //   * Timeline: chrome-trace JSON (QUEUED -> ALLREDUCE phases per bucket), like HOROVOD_TIMELINE.
 // The transport is the c10d ProcessGroup passed from Python: RCCL ("nccl") on GPU, gloo on CPU
 // (so the engine itself is exercised by the CPU multi-process tests).
@@ -83,6 +85,7 @@ class FusionEngine {
 
   void begin_step() {
     std::lock_guard<std::mutex> lk(mu_);
+    TORCH_CHECK(!stalled_, "pddl fusion: stall detected: ", stall_msg_);
     TORCH_CHECK(pending_.empty() && inflight_.empty(), "pddl fusion: begin_step with outstanding buckets");
     next_expected_ = 0;
     ++step_;
@@ -119,7 +122,18 @@ class FusionEngine {
       done.swap(inflight_);
     }
     for (auto& it : done) {
-      it.work->wait();
+      if (gpu_ || stall_s_ <= 0) {
+        it.work->wait();   // GPU: a stream-ordered wait, the host does not block here
+      } else {             // host-blocking backend: poll, so the watchdog's stall verdict can end the wait
+        while (!it.work->isCompleted()) {
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            TORCH_CHECK(!stalled_, "pddl fusion: stall detected: ", stall_msg_);
+          }
+          std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+        it.work->wait();   // completed: returns at once (and rethrows a collective error)
+      }
       it.t_done = now_us();
       if (average_ && world_ > 1) {
         auto sl = flat_.narrow(0, buckets_[it.bucket].first, buckets_[it.bucket].second);
@@ -164,6 +178,18 @@ class FusionEngine {
     double t_ready = 0, t_issue = 0, t_done = 0;
   };
 
+  struct Watch {
+    c10::intrusive_ptr<c10d::Work> work;
+    double t_issue;
+    int bucket;
+  };
+
+  void report_stall(const std::string& msg) {   // (mu_ held)
+    stall_msg_ = msg;
+    stalled_ = true;
+    fprintf(stderr, "[pddl stall inspector] %s\n", stall_msg_.c_str());
+  }
+
   void verify_signature() {
     // all ranks must agree on the bucket table (static negotiation)
     double sig = 0;
@@ -205,6 +231,7 @@ class FusionEngine {
         }
         issued_++;
         std::lock_guard<std::mutex> lk(mu_);
+        watch_.push_back({it.work, it.t_issue, it.bucket});
         inflight_.push_back(std::move(it));
         busy_ = false;
       } catch (const std::exception& e) {
@@ -228,9 +255,20 @@ class FusionEngine {
             os << "rank " << rank_ << ": bucket " << pending_.front().bucket << " queued for " << age
                << " s without being issued (" << pending_.size() << " pending, " << inflight_.size()
                << " in flight) - a peer rank is likely stuck or diverged";
-            stall_msg_ = os.str();
-            stalled_ = true;
-            fprintf(stderr, "[pddl stall inspector] %s\n", stall_msg_.c_str());
+            report_stall(os.str());
+          }
+        }
+        // issued collectives that never complete: a peer never joined (stream-ordered waits on
+        // the GPU do not block the host, so this is where a stuck peer becomes visible)
+        while (!watch_.empty() && watch_.front().work->isCompleted()) watch_.pop_front();
+        if (stall_s_ > 0 && !watch_.empty() && !stalled_) {
+          const double age = (now_us() - watch_.front().t_issue) * 1e-6;
+          if (age > stall_s_) {
+            std::ostringstream os;
+            os << "rank " << rank_ << ": all-reduce of bucket " << watch_.front().bucket << " issued " << age
+               << " s ago has not completed (" << watch_.size() << " outstanding) - a peer rank is likely stuck"
+               << " or diverged";
+            report_stall(os.str());
           }
         }
       }
@@ -250,6 +288,7 @@ class FusionEngine {
   std::condition_variable cv_;
   std::deque<Item> pending_;
   std::vector<Item> inflight_;
+  std::deque<Watch> watch_;
   bool stop_ = false, busy_ = false, stalled_ = false;
   std::string error_, stall_msg_;
   int next_expected_ = 0, step_ = 0;

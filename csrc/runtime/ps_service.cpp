@@ -105,9 +105,13 @@ struct Shm {
     close(fd);
     return ptr != MAP_FAILED;
   }
+  void unlink() {   // the mapping stays valid; the name disappears from /dev/shm
+    if (owner) shm_unlink(name.c_str());
+    owner = false;
+  }
   ~Shm() {
     if (ptr && ptr != MAP_FAILED) munmap(ptr, bytes);
-    if (owner) shm_unlink(name.c_str());
+    unlink();
   }
 };
 
@@ -249,6 +253,14 @@ class PSServer {
         }
         if (!any) {
           const double t = now_s();
+          if (!unlinked_) {   // every worker attached: drop the names (no /dev/shm leak on a crash)
+            bool all = true;
+            for (int w = 0; w < W_; ++w) all = all && ctrl_->slot[w].pid.load() > 0;
+            if (all) {
+              ctrl_shm_.unlink(); mb_shm_.unlink(); rx_shm_.unlink();
+              unlinked_ = true;
+            }
+          }
           if (t - last_check > 0.5) {   // a worker process that vanished counts as finished
             last_check = t;
             for (int w = 0; w < W_; ++w) {
@@ -282,6 +294,7 @@ class PSServer {
   std::thread thr_;
   std::atomic<bool> stop_{false};
   std::vector<int> dead_;
+  bool unlinked_ = false;
   std::string err_;
 };
 
