@@ -58,9 +58,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # (modulo: lets a rehearsal put several ranks on one GPU; one rank per GPU on a real node)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # PDDL_DIST_BACKEND=gloo only for rehearsing the multi-rank path on one GPU (RCCL refuses
+        # two ranks on the same device); the measured configuration is RCCL ("nccl")
+        backend = os.environ.get("PDDL_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)} if backend == "nccl" else {}))
     B = args.batch
     L = ParamLayout()
     eng = make_hip_engine(L, B, bn_mode=args.bn_mode, crop=args.crop, image_size=224)

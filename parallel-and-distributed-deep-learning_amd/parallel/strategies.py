@@ -105,6 +105,7 @@ class Strategy:
         want = self.cfg.device
         if want == "cpu" or (want == "auto" and not gpu_available()):
             return torch.device("cpu")
+        local_index %= torch.cuda.device_count()   # (rehearsals may put several ranks on one GPU)
         torch.cuda.set_device(local_index)
         return torch.device("cuda", local_index)
 
@@ -214,8 +215,10 @@ class _ProcessGroupMixin:
         self.info = info
         if not dist.is_initialized():
             backend = "nccl" if self.device.type == "cuda" else "gloo"
+            # PDDL_DIST_BACKEND=gloo: rehearse GPU ranks sharing one device (RCCL refuses that)
+            backend = os.environ.get("PDDL_DIST_BACKEND", backend)
             kw = {}
-            if self.device.type == "cuda":
+            if backend == "nccl":
                 kw["device_id"] = self.device
             dist.init_process_group(backend, init_method="env://", rank=info.rank, world_size=info.world_size, **kw)
 
