@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--knob", default="igemm_big", help="igemm knob to A/B (igemm_big, igemm_il, ...)")
+    ap.add_argument("--variants", default="0,3", help="comma-separated knob values")
     a = ap.parse_args()
     N = require_native()
     B = a.batch
@@ -86,7 +88,8 @@ def main():
         print(json.dumps(brow), flush=True)
         res.append(brow)
         del am, bm, gm
-        for kind, fn, knob, variants in (("igemm", fwd, "igemm_big", [0, 3]), ("wgrad", wg, "wgrad", [0])):
+        for kind, fn, knob, variants in (("igemm", fwd, a.knob, [int(v) for v in a.variants.split(",")]),
+                                          ("wgrad", wg, "wgrad", [0])):
             t = {v: [] for v in variants}
             for _ in range(a.rounds):
                 for v in variants:

@@ -378,6 +378,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm_deep") pddl::g_igemm_deep = v;
     else if (which == "igemm_big") pddl::g_igemm_big = v;
     else if (which == "igemm_pf") pddl::g_igemm_pf = v;
+    else if (which == "igemm_il") pddl::g_igemm_il = v;
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });

@@ -43,6 +43,10 @@ enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 //   NW = 4, NSTAGE 1/2: 2 blocks per CU, the next k-tile's LDS-DMA overlaps this tile's MFMAs.
 //   NW = 8 (256x128), NSTAGE 3: one 144 KiB block per CU, 2 waves per SIMD; a 3-deep LDS ring
 //   keeps two k-tiles in flight (counted vmcnt across a raw barrier) for compute-bound layers.
+//   NSTAGE 4: the 2-stage pipeline with the next tile's LDS-DMA issue spread over the MFMA
+//   groups (one piece per TN-MFMA group, pinned by sched barriers) instead of a burst of AI+BI
+//   issues at the top of the tile, during which the barrier-aligned waves of a SIMD all stall
+//   the matrix pipe together.
 // PF: the epilogue's per-element operand (forward residual / dgrad residual-gradient `add`,
 // plus the dgrad ReLU bitmask) of the whole wave tile is loaded into registers before the
 // accumulators are staged through LDS, so its HBM latency overlaps the staging instead of
@@ -54,13 +58,15 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int WAVES_N = BN / WTN;
   static_assert((BM / WTM) * (BN / WTN) == NW, "wave grid must cover the block tile");
-  static_assert(NSTAGE >= 1 && NSTAGE <= 3, "1- to 3-stage LDS pipeline");
+  static_assert(NSTAGE >= 1 && NSTAGE <= 4, "1- to 3-stage LDS pipeline (4: interleaved 2-stage)");
+  constexpr bool IL = NSTAGE == 4;
+  constexpr int NS = IL ? 2 : NSTAGE;   // LDS buffers
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // 1 KiB LDS-DMA pieces per wave per tile
   static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows must split evenly over the waves");
   constexpr int EPI_LD = WTN + 4;
   constexpr int EPI_BYTES = NW * 32 * EPI_LD * 4;
-  constexpr int SMEM = (NSTAGE * STAGE > EPI_BYTES) ? NSTAGE * STAGE : EPI_BYTES;
+  constexpr int SMEM = (NS * STAGE > EPI_BYTES) ? NS * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -117,12 +123,12 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
   // of source `src2`; a "window" tile (C * S == 64) spans all S taps of one r.
   int ld_r = 0, ld_s = 0, ld_c0 = 0, ld_src2 = 0, ld_k = 0;
   const bool window = p.C1 * p.S == 64 && p.C1 < 64;
-  auto load_tile = [&](int buf) {
-    const int C = ld_src2 ? p.C2 : p.C1;
-    const int delta = ((ld_r * p.W + ld_s) * C + ld_c0) * 2;   // bytes
+  // piece j (< AI: A rows, else B rows) of the current walk position into LDS buffer buf
+  auto tile_delta = [&]() { return ((ld_r * p.W + ld_s) * (ld_src2 ? p.C2 : p.C1) + ld_c0) * 2; };   // bytes
+  auto load_piece = [&](int buf, int j, int delta) {
     char* abase = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
+    if (j < AI) {
+      const int i = j;
       void __attribute__((address_space(3)))* dst = LDS_PTR(abase + (wave * AI + i) * 1024);
       if (AM == AM_HALO) {
         const int tap = ld_r * p.S + ld_s;
@@ -133,12 +139,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
       } else {
         buf_lds16(ra1, dst, a_o1[i], delta);
       }
+    } else {
+      const int i = j - AI;
+      buf_lds16(rb, LDS_PTR(abase + A_BYTES + (wave * BI + i) * 1024), b_o[i], ld_k * 2);
     }
-    char* bbase = abase + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < BI; ++i)
-      buf_lds16(rb, LDS_PTR(bbase + (wave * BI + i) * 1024), b_o[i], ld_k * 2);
-    // advance to the next k-tile
+  };
+  // advance the walk to the next k-tile
+  auto advance = [&]() {
+    const int C = ld_src2 ? p.C2 : p.C1;
     ld_k += 64;
     if (window && !ld_src2) {
       ++ld_r;
@@ -151,6 +159,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
     }
     if (AM == AM_DUAL && !ld_src2 && ld_k == p.K1) { ld_src2 = 1; ld_r = ld_s = ld_c0 = 0; }
   };
+  auto load_tile = [&](int buf) {
+    const int delta = tile_delta();
+#pragma unroll
+    for (int j = 0; j < AI + BI; ++j) load_piece(buf, j, delta);
+    advance();
+  };
+  constexpr int PPG = (AI + BI + 2 * TM - 1) / (2 * TM);   // IL: pieces issued per MFMA group
 
   v4f acc[TM][TN];
 #pragma unroll
@@ -178,9 +193,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
       cur = t % 3;
       if (t + 2 < KT) load_tile((t + 2) % 3);
     } else {
-      cur = NSTAGE == 2 ? (t & 1) : 0;
+      cur = NS == 2 ? (t & 1) : 0;
       if (NSTAGE == 2 && t + 1 < KT) load_tile(cur ^ 1);
     }
+    const bool il_next = IL && t + 1 < KT;
+    const int il_delta = IL ? tile_delta() : 0;
     const char* As = smem + cur * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -192,11 +209,21 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const v8bf*>(Bs + b_off + j * 16 * 128 + pos);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if (IL) {
+#pragma unroll
+          for (int q = 0; q < PPG; ++q) {
+            const int jp = (kh * TM + i) * PPG + q;
+            if (jp < AI + BI && il_next) load_piece(cur ^ 1, jp, il_delta);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
+    if (il_next) advance();
     if (NSTAGE == 1 && t + 1 < KT) {
       __syncthreads();            // every wave is done reading the single buffer
       load_tile(0);
@@ -395,6 +422,10 @@ int g_igemm_big = 0;       // 8-wave 256x128 3-stage tile: 0 never (default: mea
                            // 256x256 8-wave tile: 3 heuristic (Nn, K >= 256), 4 always (Nn > 128)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
 int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 layers with a residual / add
+int g_igemm_il = 0;        // 2-stage tiles issue the next tile's LDS-DMA interleaved with the MFMAs:
+                           // off (measured -3..-12% on the compute-bound layers, -2.5% end to end;
+                           // profiles/r1_kbench_b1024_interleaved_issue.json) -- the later issue
+                           // shortens each piece's latency window more than the burst costs
 
 static bool igemm_no_halo(const IgemmParams& p) {
   return p.pad == 0 && (p.Ho - 1) * p.stride + p.R <= p.H && (p.Wo - 1) * p.stride + p.S <= p.W;
@@ -450,6 +481,7 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   const int KT = p.K / 64;
   int ns = g_igemm_variant;
   if (ns == 0) ns = KT <= 2 ? 1 : 2;
+  const bool il = g_igemm_il && ns == 2;
   const int am = p.a2 ? AM_DUAL : (igemm_no_halo(p) ? AM_DIRECT : AM_HALO);
   // (explicit launches per instantiation: taking kernel addresses through a conditional
   // expression leaves the host stubs uninstantiated with this compiler)
@@ -475,9 +507,9 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
 #define IG_PF(BM_, BN_, NS_) \
   hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_DIRECT, true>), dim3(nwg), dim3(256), 0, stream, p)
     if (cfg == 1) {
-      if (ns == 1) IG_PF(128, 128, 1); else IG_PF(128, 128, 2);
+      if (ns == 1) IG_PF(128, 128, 1); else if (il) IG_PF(128, 128, 4); else IG_PF(128, 128, 2);
     } else {
-      if (ns == 1) IG_PF(256, 64, 1); else IG_PF(256, 64, 2);
+      if (ns == 1) IG_PF(256, 64, 1); else if (il) IG_PF(256, 64, 4); else IG_PF(256, 64, 2);
     }
 #undef IG_PF
   } else if (cfg == 3) {
@@ -490,9 +522,9 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   } else if (cfg == 2) {
     IG_MODES(256, 128, 8, 3)
   } else if (cfg == 1) {
-    if (ns == 1) IG_MODES(128, 128, 4, 1) else IG_MODES(128, 128, 4, 2)
+    if (ns == 1) IG_MODES(128, 128, 4, 1) else if (il) IG_MODES(128, 128, 4, 4) else IG_MODES(128, 128, 4, 2)
   } else {
-    if (ns == 1) IG_MODES(256, 64, 4, 1) else IG_MODES(256, 64, 4, 2)
+    if (ns == 1) IG_MODES(256, 64, 4, 1) else if (il) IG_MODES(256, 64, 4, 4) else IG_MODES(256, 64, 4, 2)
   }
 #undef IG_MODES
 #undef IG_GO

@@ -42,12 +42,22 @@ def _load():
             loader.exec_module(mod)
             sys.modules["_pddl_native"] = mod
             _native = mod
+            _apply_knobs(mod)
             return mod
         except Exception as e:  # pragma: no cover - reported by require_native
             _err = f"{path}: {e}"
     if _err is None:
         _err = "no _pddl_native*.so found (run `python pddl_build.py`)"
     return None
+
+
+def _apply_knobs(mod):
+    """PDDL_KNOBS="igemm_il=1,igemm_big=3": kernel tuning knobs for A/B runs of whole
+    programs (bench.py, the entry scripts) without code changes."""
+    spec = os.environ.get("PDDL_KNOBS", "").strip()
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        name, _, val = item.partition("=")
+        mod.set_variant(name.strip(), int(val))
 
 
 def native_available() -> bool:

@@ -132,12 +132,13 @@ def test_igemm_dgrad(case):
     assert rel(cs, ref.sum((0, 1, 2))) < 1e-2
 
 
-@pytest.mark.parametrize("big", [2, 4])
+@pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1)])
 @pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual"])
-def test_igemm_big_tile_matches(kind, big):
-    """The 8-wave 256x128 3-stage (knob 2) and 256x256 2-stage (knob 4) configurations compute
-    the same result (same k order) as the 4-wave 128x128 one, including the fused epilogues
-    and the per-wave column-sum rows."""
+def test_igemm_big_tile_matches(kind, knob, big):
+    """The 8-wave 256x128 3-stage (igemm_big 2) and 256x256 2-stage (igemm_big 4)
+    configurations, and the interleaved-issue 2-stage pipeline (igemm_il 1), compute the same
+    result (same k order) as the 4-wave 128x128 one, including the fused epilogues and the
+    per-wave column-sum rows."""
     torch.manual_seed(12)
     n, h, ho = 3, 14, 7
     if kind == "fwd3x3":
@@ -153,8 +154,8 @@ def test_igemm_big_tile_matches(kind, big):
         wt = rnd(256, 640, scale=0.05)
         mask = rnd(n, h, h, 256)
     outs = []
-    for knob in (0, big):
-        N().set_variant("igemm_big", knob)
+    for kv in (0, big):
+        N().set_variant(knob, kv)
         try:
             if kind == "fwd3x3":
                 y = torch.empty(n, h, h, 256, dtype=torch.bfloat16, device=dev)
@@ -176,7 +177,7 @@ def test_igemm_big_tile_matches(kind, big):
                           1, h, h, part, None)
                 outs.append(torch.cat([out.float().flatten(), _fold(part, rows, 256)]))
         finally:
-            N().set_variant("igemm_big", 0)
+            N().set_variant(knob, 0)
     assert rel(outs[1], outs[0]) < 1e-5
 
 

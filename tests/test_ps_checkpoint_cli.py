@@ -25,6 +25,7 @@ def _cfg(preset, **kw):
 def test_ps_async_job_runs_and_applies_every_step(impl, monkeypatch):
     from pddl.parallel.parameter_server import run_ps_job
     monkeypatch.setenv("PDDL_PS_IMPL", impl)
+    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "600")   # a loaded CI box must not look like a dead worker
     cfg = _cfg("ps", steps_per_epoch=6, validation_steps=1, batch_size=2, epochs=2)
     res = run_ps_job(cfg, num_ps=2, num_workers=2, return_results=True)
     ps = [r for r in res if r[0] == "ps"]
