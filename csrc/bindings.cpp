@@ -380,6 +380,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm_pf") pddl::g_igemm_pf = v;
     else if (which == "igemm_il") pddl::g_igemm_il = v;
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
+    else if (which == "pool") pddl::g_pool_variant = v;
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });
   m.def("igemm_partial_rows", &pddl::igemm_partial_rows);

@@ -292,9 +292,20 @@ def test_wgrad_dual_and_padded_k():
     assert rel(dw, ref) < 5e-3
 
 
-def test_maxpool_and_gap():
+@pytest.mark.parametrize("variant,h", [(0, 12), (0, 13), (1, 12), (1, 13), (2, 13), (3, 12), (3, 18)])
+def test_maxpool_and_gap(variant, h):
+    """Max pool (pad 1, 3x3/s2; strip / block kernels and the per-pixel ones) against
+    PyTorch, including odd sizes and a partial last strip, then GAP."""
     torch.manual_seed(6)
-    n, h, c = 2, 12, 64
+    N().set_variant("pool", variant)
+    try:
+        _maxpool_gap(h)
+    finally:
+        N().set_variant("pool", 0)
+
+
+def _maxpool_gap(h):
+    n, c = 2, 64
     x = torch.relu(torch.randn(n, h, h, c, device=dev)).to(torch.bfloat16)
     ho = (h + 2 - 3) // 2 + 1
     y = torch.empty(n, ho, ho, c, dtype=torch.bfloat16, device=dev)
