@@ -381,6 +381,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm_il") pddl::g_igemm_il = v;
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
     else if (which == "pool") pddl::g_pool_variant = v;
+    else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
+    else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });
   m.def("igemm_partial_rows", &pddl::igemm_partial_rows);

@@ -22,7 +22,15 @@
 namespace pddl {
 
 // ~8 blocks of 256 lanes per CU; lanes loop so their per-channel setup is amortized
-static int bn_grid(long n) { return (int)lmin((n + 255) / 256, 2048); }
+// Grid caps of the streaming BN kernels (bench/bn.py sweep at b256, profiles/r1_bn_kernels_b256.json):
+// 512 blocks of 256 lanes for < 4M channel groups, 1024 above (2048 was 1.2-2x slower on the
+// 7x7 / 14x14 layers); 0 = this heuristic, > 0 forces a cap.
+int g_bn_apply_blocks = 0;
+int g_bn_red_blocks = 0;        // bn_bwd_reduce block cap: 0 = heuristic (see the launcher)
+static int bn_grid(long n) {
+  const long cap = g_bn_apply_blocks > 0 ? g_bn_apply_blocks : (n >= (4L << 20) ? 1024 : 512);
+  return (int)lmin((n + 255) / 256, cap);
+}
 
 // ------------------------------------------------------------------------------ stats
 __global__ void bn_stats_kernel(const float* __restrict__ acc, const BnStatLayer* __restrict__ L, int training,
@@ -81,24 +89,40 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ z, const float* __res
     sa[e] = a[c0 + e]; sb[e] = b[c0 + e];
     ra[e] = a2 ? a2[c0 + e] : 1.f; rb[e] = a2 ? b2[c0 + e] : 0.f;
   }
-  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
-    float v[8];
-    unpack8(reinterpret_cast<const uint4*>(z)[t], v);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = v[e] * sa[e] + sb[e];
+  // two items per iteration, both loads issued before either is used (memory-level
+  // parallelism: one item per lane left these streaming kernels at ~3.4 TB/s)
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long t = t0; t < total; t += 2 * stride) {
+    const bool two = t + stride < total;
+    const uint4 zq0 = reinterpret_cast<const uint4*>(z)[t];
+    const uint4 zq1 = two ? reinterpret_cast<const uint4*>(z)[t + stride] : zq0;
+    uint4 rq0 = zq0, rq1 = zq0;
     if (r) {
-      float rv[8];
-      unpack8(reinterpret_cast<const uint4*>(r)[t], rv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += rv[e] * ra[e] + rb[e];
+      rq0 = reinterpret_cast<const uint4*>(r)[t];
+      rq1 = two ? reinterpret_cast<const uint4*>(r)[t + stride] : rq0;
     }
-    if (relu) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      float v[8];
+      unpack8(u ? zq1 : zq0, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * sa[e] + sb[e];
+      if (r) {
+        float rv[8];
+        unpack8(u ? rq1 : rq0, rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += rv[e] * ra[e] + rb[e];
+      }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      const uint4 pk = pack8(v);
+      const long tu = t + u * stride;
+      reinterpret_cast<uint4*>(y)[tu] = pk;
+      if (bits) bits[tu] = (uint8_t)pos_bits8(pk);
     }
-    const uint4 pk = pack8(v);
-    reinterpret_cast<uint4*>(y)[t] = pk;
-    if (bits) bits[t] = (uint8_t)pos_bits8(pk);
   }
 }
 
@@ -135,18 +159,26 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
 #pragma unroll
   for (int e = 0; e < 8; ++e) { mu[e] = mean[c0 + e]; mu2[e] = z2 ? mean2[c0 + e] : 0.f; }
   if (slot < RPI) {
-#pragma unroll 4
-    for (long row = r0 + slot; row < r1; row += RPI) {
-      const long o = row * G + cgi;
-      float gv[8], zv[8];
-      unpack8(reinterpret_cast<const uint4*>(g)[o], gv);
-      unpack8(reinterpret_cast<const uint4*>(z)[o], zv);
+    for (long row = r0 + slot; row < r1; row += 2 * RPI) {   // two rows in flight per lane
+      const bool two = row + RPI < r1;
+      const long o = row * G + cgi, o1 = two ? o + (long)RPI * G : o;
+      const uint4 gq0 = reinterpret_cast<const uint4*>(g)[o], gq1 = reinterpret_cast<const uint4*>(g)[o1];
+      const uint4 zq0 = reinterpret_cast<const uint4*>(z)[o], zq1 = reinterpret_cast<const uint4*>(z)[o1];
+      uint4 wq0 = zq0, wq1 = zq1;
+      if (z2) { wq0 = reinterpret_cast<const uint4*>(z2)[o]; wq1 = reinterpret_cast<const uint4*>(z2)[o1]; }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { s0[e] += gv[e]; s1[e] += gv[e] * (zv[e] - mu[e]); }
-      if (z2) {
-        unpack8(reinterpret_cast<const uint4*>(z2)[o], zv);
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        float gv[8], zv[8];
+        unpack8(u ? gq1 : gq0, gv);
+        unpack8(u ? zq1 : zq0, zv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s2[e] += gv[e] * (zv[e] - mu2[e]);
+        for (int e = 0; e < 8; ++e) { s0[e] += gv[e]; s1[e] += gv[e] * (zv[e] - mu[e]); }
+        if (z2) {
+          unpack8(u ? wq1 : wq0, zv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s2[e] += gv[e] * (zv[e] - mu2[e]);
+        }
       }
     }
   }
@@ -180,9 +212,12 @@ const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uin
                                  float* sgx2, hipStream_t s) {
   if (C % 8 || C > 2048) return "bn_bwd_reduce: C must be a multiple of 8 and <= 2048";
   const int G = C / 8, rpi = 256 / G;
-  // >= 8 row iterations per lane, <= 1024 blocks, and <= ~256K atomics per call
+  // >= 8 row iterations per lane
   long nb = M / ((long)rpi * 8);
-  const long cap = lmin(1024, 262144 / C);
+  // About one block per CU (bench/bn.py sweep, profiles/r1_bn_kernels_b256.json): more blocks
+  // only add per-block LDS folds and same-address atomics (2048 blocks ran the 56x56x64
+  // reduce at 3.2 TB/s, 256 blocks at 6.0); the largest layers take 512.
+  const long cap = g_bn_red_blocks > 0 ? g_bn_red_blocks : (M * C > (1L << 27) ? 512 : 256);
   nb = nb < 1 ? 1 : (nb > cap ? cap : nb);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((int)nb), dim3(256), 0, s, g, z, z2, mean, mean2, M, C, sg, sgx,
                      sg2, sgx2);
@@ -231,21 +266,36 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* g, cons
   float A[8], B[8], Cc[8], A2[8], B2[8], C2[8];
   load8(c1 + c0, A); load8(c1 + ldc + c0, B); load8(c1 + 2 * ldc + c0, Cc);
   if (z2) { load8(c2 + c0, A2); load8(c2 + ldc + c0, B2); load8(c2 + 2 * ldc + c0, C2); }
-  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
-    float gv[8], zv[8], o[8];
-    unpack8(reinterpret_cast<const uint4*>(g)[t], gv);
-    unpack8(reinterpret_cast<const uint4*>(z)[t], zv);
-    float o2[8];
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long t = t0; t < total; t += 2 * stride) {   // two items in flight per lane (see bn_apply)
+    const bool two = t + stride < total;
+    const uint4 gq0 = reinterpret_cast<const uint4*>(g)[t];
+    const uint4 zq0 = reinterpret_cast<const uint4*>(z)[t];
+    const uint4 gq1 = two ? reinterpret_cast<const uint4*>(g)[t + stride] : gq0;
+    const uint4 zq1 = two ? reinterpret_cast<const uint4*>(z)[t + stride] : zq0;
+    uint4 wq0 = zq0, wq1 = zq0;
     if (z2) {
-      float wv[8];
-      unpack8(reinterpret_cast<const uint4*>(z2)[t], wv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o2[e] = A2[e] * gv[e] + B2[e] * wv[e] + C2[e];
+      wq0 = reinterpret_cast<const uint4*>(z2)[t];
+      wq1 = two ? reinterpret_cast<const uint4*>(z2)[t + stride] : wq0;
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = A[e] * gv[e] + B[e] * zv[e] + Cc[e];
-    reinterpret_cast<uint4*>(dz)[t] = pack8(o);
-    if (z2) reinterpret_cast<uint4*>(dz2)[t] = pack8(o2);
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      float gv[8], zv[8], o[8];
+      unpack8(u ? gq1 : gq0, gv);
+      unpack8(u ? zq1 : zq0, zv);
+      const long tu = t + u * stride;
+      if (z2) {
+        float wv[8], o2[8];
+        unpack8(u ? wq1 : wq0, wv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o2[e] = A2[e] * gv[e] + B2[e] * wv[e] + C2[e];
+        reinterpret_cast<uint4*>(dz2)[tu] = pack8(o2);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = A[e] * gv[e] + B[e] * zv[e] + Cc[e];
+      reinterpret_cast<uint4*>(dz)[tu] = pack8(o);
+    }
   }
 }
 
