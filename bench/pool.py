@@ -60,6 +60,15 @@ def main():
                         "bwd_GBps": round(bb / b / 1e3)}
         print(json.dumps({"variant": v, **res[f"v{v}"]}), flush=True)
     N.set_variant("pool", 0)
+    for cap in (1024, 2048, 4096, 8192, 16384):   # grid cap sweep of the default kernels
+        N.set_variant("pool_blocks", cap)
+        rows = N.maxpool_bwd_partial_rows(B, H, H, C)
+        part = torch.empty(rows * C, device=dev)
+        f = statistics.median(timeit(lambda: N.maxpool_fwd(x, y, idx, bits)) for _ in range(a.rounds))
+        b = statistics.median(timeit(lambda: N.maxpool_bwd(gy, idx, None, gx, part)) for _ in range(a.rounds))
+        res[f"blocks{cap}"] = {"fwd_us": round(f, 1), "bwd_us": round(b, 1)}
+        print(json.dumps({"blocks": cap, **res[f"blocks{cap}"]}), flush=True)
+    N.set_variant("pool_blocks", 8192)
     same = all(torch.equal(p, q) for v in (0, 2, 3) for p, q in zip(outs[v], outs[1]))
     res["bitwise_equal"] = same
     print(json.dumps({"bitwise_equal": same}), flush=True)

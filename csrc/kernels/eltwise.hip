@@ -92,7 +92,9 @@ const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStre
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
-static int grid_for(long n) { return (int)lmin((n + 255) / 256, 8192); }
+int g_pool_blocks = 8192;   // grid cap of the pool / GAP kernels: 4096 -> 8192 -> 16384 blocks
+                            // measured 772 -> 742 -> 733 us (fwd), flat beyond (profiles/r1_pool_grid_sweep.log)
+static int grid_for(long n) { return (int)lmin((n + 255) / 256, g_pool_blocks); }
 
 // --------------------------------------------------------------------------- maxpool
 // Window of output (ho, wo) covers input rows 2ho-1 .. 2ho+1 (ZeroPadding2D(1) then 3x3/s2
