@@ -93,7 +93,8 @@ const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStre
 }
 
 int g_pool_blocks = 8192;   // grid cap of the pool / GAP kernels: 4096 -> 8192 -> 16384 blocks
-                            // measured 772 -> 742 -> 733 us (fwd), flat beyond (profiles/r1_pool_grid_sweep.log)
+                            // measured 772 -> 742 -> 733 us (fwd); 16384 not adopted (1%, twice the
+                            // backward colsum partial rows; profiles/r1_pool_grid_sweep.log)
 static int grid_for(long n) { return (int)lmin((n + 255) / 256, g_pool_blocks); }
 
 // --------------------------------------------------------------------------- maxpool
