@@ -384,6 +384,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;
+    else if (which == "colred_chunks") { TORCH_CHECK(v >= 1 && v <= 65535, "colred_chunks"); pddl::g_colred_chunks = v; }
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });
   m.def("igemm_partial_rows", &pddl::igemm_partial_rows);

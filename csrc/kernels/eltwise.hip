@@ -545,11 +545,13 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRe
     }
   }
 }
+int g_colred_chunks = 512;   // row chunks per layer (knob colred_chunks): train-BN b256 end to end
+                             // 16/32/64/128/512/1024/2048 chunks = 8.3k/9.3k/9.9k/10.2k/10.25k/10.0k/9.8k img/s
 const char* colsum_reduce_launch(const float* part, const ColRedLayer* layers_dev, int nlayers, float* colsum,
                                  hipStream_t s) {
   // 512 row chunks per layer: every CU gets work even for one large layer (chunks past a
   // small layer's rows exit at once); one atomic per column per chunk
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(512, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(g_colred_chunks, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
