@@ -128,6 +128,28 @@ int main() {
   }
   CHECK(caught);
 
+  // concurrent callers (serialized by the pool) writing plain, non-atomic per-call buffers that
+  // the caller reads after run() returns: the worker -> caller hand-off must order those
+  // writes (ThreadSanitizer checks it in scripts/sanitize_host.sh); decodes run on the pool as
+  // in the reader
+  std::vector<std::thread> callers;
+  std::atomic<int> bad{0};
+  for (int c = 0; c < 4; ++c)
+    callers.emplace_back([&, c] {
+      for (int rep = 0; rep < 20; ++rep) {
+        std::vector<int> vals(64, 0);
+        std::vector<uint8_t> imgs(8 * 24 * 24 * 3);
+        pool.run(64, [&](int64_t i) {
+          vals[i] = (int)i * (c + 1);
+          if (i < 8) decode_crop_pad(rgb.data(), rgb.size(), 24, imgs.data() + i * 24 * 24 * 3);
+        });
+        for (int i = 0; i < 64; ++i) bad += vals[i] != i * (c + 1);
+        for (int i = 1; i < 8; ++i) bad += std::memcmp(imgs.data(), imgs.data() + i * 24 * 24 * 3, 24 * 24 * 3) != 0;
+      }
+    });
+  for (auto& t : callers) t.join();
+  CHECK(bad.load() == 0);
+
   std::printf("io_core_test: %s (%d hostile JPEGs threw, %d decoded)\n", fails ? "FAILED" : "ok", threw, decoded);
   return fails ? 1 : 0;
 }

@@ -352,6 +352,10 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         device = torch.device("cuda", rank % n)
     else:
         device = torch.device("cpu")
+        # P + W role processes share the host's cores (the reference sizes the workers'
+        # inter-op threads against cpu_count, imagenet-resnet50-ps.py:43-46): split the intra-op
+        # pool instead of letting every role oversubscribe all cores
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
     impl = ps_impl()
     # the native data plane needs c10d only for control (barriers, the TCP store): gloo
     gpu_pg = use_gpu and impl == "c10d"

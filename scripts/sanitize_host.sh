@@ -11,6 +11,8 @@
 #  2. ASan + UBSan natively: csrc/tests/io_core_test.cpp drives the torch-free reader core
 #     (CRC32C, tf.Example parser, libjpeg decode + crop/pad, thread pool) including truncated
 #     and corrupted inputs.
+#  3. ThreadSanitizer natively: the same driver, whose pool section runs concurrent callers
+#     that hand plain (non-atomic) buffers from the decode workers back to the caller.
 #
 #   bash scripts/sanitize_host.sh [pytest -k expression]
 set -euo pipefail
@@ -23,6 +25,10 @@ mkdir -p "$OUT/lib" && ln -sf /opt/conda/lib/libjpeg.so.9 "$OUT/lib/libjpeg.so.9
 g++ -std=c++17 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -I csrc -I /opt/conda/include \
     csrc/tests/io_core_test.cpp "$OUT/lib/libjpeg.so.9" -Wl,-rpath,"$PWD/$OUT/lib" -lpthread -o "$OUT/io_core_test"
 ASAN_OPTIONS=detect_leaks=1:halt_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 "$OUT/io_core_test"
+echo "== TSan: io core"
+g++ -std=c++17 -O1 -g -fsanitize=thread -I csrc -I /opt/conda/include \
+    csrc/tests/io_core_test.cpp "$OUT/lib/libjpeg.so.9" -Wl,-rpath,"$PWD/$OUT/lib" -lpthread -o "$OUT/io_core_tsan"
+TSAN_OPTIONS=halt_on_error=1 "$OUT/io_core_tsan"
 echo "== UBSan: runtime + reader under the CPU tests"
 PDDL_SANITIZE=1 PDDL_BUILD_TEMP=/tmp/pddl_build_san python setup.py build_ext --build-lib "$OUT" \
     --build-temp /tmp/pddl_build_san > "$OUT/build.log" 2>&1 || { tail -30 "$OUT/build.log"; exit 1; }
