@@ -416,6 +416,7 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         if store.check(["lr"]):
             lr = float(store.get("lr").decode())
         acc = torch.zeros(3, dtype=torch.float64)
+        t_epoch = time.perf_counter()
         while True:
             t = _claim(store, spe, epoch)
             if t < 0:
@@ -444,15 +445,18 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         if widx == 0:
             alive = cl.num_workers - store.add("dead_workers", 0)
             _wait_count(store, f"epoch_end/{epoch}", alive)
+            dt = time.perf_counter() - t_epoch      # every worker's training steps, before validation
             n = max(1, store.add(f"acc/{epoch}/n", 0))
             logs = {"loss": store.add(f"acc/{epoch}/loss", 0) / 1e6 / n,
-                    "accuracy": store.add(f"acc/{epoch}/correct", 0) / n, "steps": store.add(f"done/{epoch}", 0)}
+                    "accuracy": store.add(f"acc/{epoch}/correct", 0) / n, "steps": store.add(f"done/{epoch}", 0),
+                    "images_per_sec": n / max(dt, 1e-9)}
             if cfg.validation_steps:
                 logs.update(_validate(cfg, eng, device))
             history.append(logs)
             print(f"Epoch {epoch + 1}/{cfg.epochs} - {logs['steps']}/{spe} steps - loss: {logs['loss']:.4f} - "
                   f"accuracy: {logs['accuracy']:.4f}" + (f" - val_loss: {logs['val_loss']:.4f}"
-                                                          if 'val_loss' in logs else ""), flush=True)
+                                                          if 'val_loss' in logs else "")
+                  + f" - {logs['images_per_sec']:.1f} img/s", flush=True)
             store.set(f"epoch_go/{epoch}", "1")
         else:
             _wait_key(store, f"epoch_go/{epoch}")

@@ -34,6 +34,7 @@ class Callback:
     def on_epoch_end(self, epoch, logs=None): ...
     def on_batch_begin(self, batch, logs=None): ...
     def on_batch_end(self, batch, logs=None): ...
+    def on_train_batches_end(self, epoch): ...   # after the epoch's last training step, before validation
 
 
 class ReduceLROnPlateau(Callback):
@@ -156,6 +157,7 @@ class ThroughputMeter(Callback):
 
     def on_epoch_begin(self, epoch, logs=None):
         self.t0 = None
+        self.t1 = None
         self.n = 0
 
     def on_batch_end(self, batch, logs=None):
@@ -166,10 +168,17 @@ class ThroughputMeter(Callback):
         elif batch + 1 > self.skip:
             self.n += self.trainer.global_batch
 
+    def on_train_batches_end(self, epoch):
+        if self.t0 is not None and self.n > 0:   # training steps only: validation is not timed
+            self.trainer.sync()
+            self.t1 = time.perf_counter()
+
     def on_epoch_end(self, epoch, logs=None):
         if self.t0 is not None and self.n > 0:
-            self.trainer.sync()
-            ips = self.n / (time.perf_counter() - self.t0)
+            if self.t1 is None:
+                self.trainer.sync()
+                self.t1 = time.perf_counter()
+            ips = self.n / (self.t1 - self.t0)
             self.history.append(ips)
             if logs is not None:
                 logs["images_per_sec"] = ips

@@ -111,6 +111,8 @@ class Trainer:
                     print(f"\r{step + 1}/{spe}", end="", flush=True)
             if cfg.verbose == 1 and st.is_chief:
                 print()
+            for cb in cbs:
+                cb.on_train_batches_end(epoch)
             # metric reduction across replicas happens BEFORE callbacks read logs (Q11)
             tot = st.reduce_metrics(torch.cat([acc, torch.tensor([float(n_seen)], dtype=torch.float64,
                                                                  device=acc.device)]))
