@@ -14,7 +14,8 @@ statistics, momentum 0.99, epsilon 1.001e-5) on the same MFMA kernels plus csrc/
                       (dz; dgamma, dbeta, dbias) -> wgrad(x, dz) and dgrad(dz, W^T)
   A projection block's BN3 and shortcut BN0 share one reduce and one apply pass (same g).
 
-Parity: tests/test_gpu_engine.py compares against models/reference.py (bn_mode="train").
+Parity: tests/test_gpu_bn_train.py compares against models/reference.py (bn_mode="train") and
+plain PyTorch fp32 references of every BN kernel.
 """
 from __future__ import annotations
 
