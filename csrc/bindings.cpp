@@ -11,6 +11,7 @@
 
 using torch::Tensor;
 using OptT = c10::optional<Tensor>;
+namespace py = pybind11;
 
 #define PCHECK(cond, msg) TORCH_CHECK(cond, "pddl: ", msg)
 
@@ -333,6 +334,10 @@ void register_fusion(pybind11::module& m);
 void register_loader(pybind11::module& m);
 void register_ps(pybind11::module& m);
 
+// Kernel launches release the GIL: replica threads (Mirrored / multi-GPU workers) then enqueue
+// their launch streams concurrently instead of serializing on the interpreter lock.
+#define REL py::call_guard<py::gil_scoped_release>()
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "pddl MI355X (gfx950) HIP kernels + native runtime (RCCL comm, fusion engine, loader)";
   register_rccl(m);
@@ -356,23 +361,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                (int)r.size(0), scatter ? 1 : 0, cur_stream()),
        "range_copy");
   });
-  m.def("igemm", &igemm);
-  m.def("igemm_bn", &igemm_impl);
-  m.def("bn_stats", &bn_stats);
-  m.def("bn_apply", &bn_apply);
-  m.def("bn_bwd_reduce", &bn_bwd_reduce);
-  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("igemm", &igemm, REL);
+  m.def("igemm_bn", &igemm_impl, REL);
+  m.def("bn_stats", &bn_stats, REL);
+  m.def("bn_apply", &bn_apply, REL);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce, REL);
+  m.def("bn_bwd_apply", &bn_bwd_apply, REL);
   m.attr("BNSTAT_LAYER_BYTES") = (int)sizeof(pddl::BnStatLayer);
-  m.def("wgrad", &wgrad);
-  m.def("stem_s2d", &stem_s2d);
-  m.def("stem_wgrad_fold", &stem_wgrad_fold);
-  m.def("maxpool_fwd", &maxpool_fwd);
-  m.def("maxpool_bwd", &maxpool_bwd);
-  m.def("gap_fwd", &gap_fwd);
-  m.def("gap_bwd", &gap_bwd);
-  m.def("colsum", &colsum);
-  m.def("softmax_xent", &softmax_xent);
-  m.def("colsum_reduce", &colsum_reduce);
+  m.def("wgrad", &wgrad, REL);
+  m.def("stem_s2d", &stem_s2d, REL);
+  m.def("stem_wgrad_fold", &stem_wgrad_fold, REL);
+  m.def("maxpool_fwd", &maxpool_fwd, REL);
+  m.def("maxpool_bwd", &maxpool_bwd, REL);
+  m.def("gap_fwd", &gap_fwd, REL);
+  m.def("gap_bwd", &gap_bwd, REL);
+  m.def("colsum", &colsum, REL);
+  m.def("softmax_xent", &softmax_xent, REL);
+  m.def("colsum_reduce", &colsum_reduce, REL);
   m.def("set_variant", [](const std::string& which, int v) {
     if (which == "igemm") pddl::g_igemm_variant = v;
     else if (which == "igemm_deep") pddl::g_igemm_deep = v;
@@ -390,16 +395,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("igemm_partial_rows", &pddl::igemm_partial_rows);
   m.def("maxpool_bwd_partial_rows", &pddl::maxpool_bwd_partial_rows);
   m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);
-  m.def("prep", &prep);
-  m.def("wgrad_finalize", &wgrad_finalize);
-  m.def("bn_grad", &bn_grad);
-  m.def("synth", &synth);
-  m.def("opt_hparams", &opt_hparams);
-  m.def("adam", &adam);
-  m.def("sgd", &sgd);
-  m.def("scale_", &scale_);
-  m.def("cast_bf16", &cast_bf16);
-  m.def("cast_f32", &cast_f32);
+  m.def("prep", &prep, REL);
+  m.def("wgrad_finalize", &wgrad_finalize, REL);
+  m.def("bn_grad", &bn_grad, REL);
+  m.def("synth", &synth, REL);
+  m.def("opt_hparams", &opt_hparams, REL);
+  m.def("adam", &adam, REL);
+  m.def("sgd", &sgd, REL);
+  m.def("scale_", &scale_, REL);
+  m.def("cast_bf16", &cast_bf16, REL);
+  m.def("cast_f32", &cast_f32, REL);
   m.attr("PREP_LAYER_BYTES") = (int)sizeof(pddl::PrepLayer);
   m.attr("FIN_LAYER_BYTES") = (int)sizeof(pddl::FinLayer);
   m.attr("BNGRAD_LAYER_BYTES") = (int)sizeof(pddl::BnGradLayer);

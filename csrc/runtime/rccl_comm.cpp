@@ -100,6 +100,21 @@ class RcclComm {
     nck(ncclGroupEnd(), "group end (all_reduce)");
   }
 
+  // Same, on explicit streams (one per local rank, e.g. the comm streams of a replica driver
+  // that overlaps bucket all-reduces with the next graph segment's compute).
+  void all_reduce_on(std::vector<Tensor> ts, const std::string& op, std::vector<int64_t> streams) {
+    check_local(ts);
+    TORCH_CHECK(streams.size() == ts.size(), "pddl rccl: one stream per local rank");
+    nck(ncclGroupStart(), "group start");
+    for (size_t i = 0; i < ts.size(); ++i) {
+      c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
+      nck(ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), comms_[i],
+                        reinterpret_cast<hipStream_t>(streams[i])),
+          "all_reduce");
+    }
+    nck(ncclGroupEnd(), "group end (all_reduce)");
+  }
+
   void broadcast(std::vector<Tensor> ts, int root) {
     check_local(ts);
     nck(ncclGroupStart(), "group start");
@@ -168,6 +183,8 @@ void register_rccl(py::module& m) {
       .def_static("init_all", [](std::vector<int> devs) { return std::make_shared<RcclComm>(devs); })
       .def_static("unique_id", &RcclComm::unique_id)
       .def("all_reduce", &RcclComm::all_reduce, py::arg("tensors"), py::arg("op") = "sum",
+           py::call_guard<py::gil_scoped_release>())
+      .def("all_reduce_on", &RcclComm::all_reduce_on, py::arg("tensors"), py::arg("op"), py::arg("streams"),
            py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &RcclComm::broadcast, py::arg("tensors"), py::arg("root") = 0,
            py::call_guard<py::gil_scoped_release>())

@@ -72,7 +72,7 @@ class TrainConfig:
     resume: Optional[str] = None
     metrics_jsonl: Optional[str] = None
     timeline: Optional[str] = None                 # chrome-trace JSON of the fusion engine
-    graphs: bool = False                           # capture the step in a HIP graph (single device)
+    graphs: Optional[bool] = None                  # HIP graphs: None = auto (on for Mirrored / local replicas)
     roctx: bool = False                            # roctx ranges per step phase (utils/profiling.py)
     max_steps: Optional[int] = None                # cap steps per epoch (smoke / bench)
 
@@ -152,6 +152,7 @@ def add_cli_args(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--metrics-jsonl", type=str, dest="metrics_jsonl")
     a("--timeline", type=str)
     a("--graphs", action="store_true", default=None)
+    a("--no-graphs", action="store_false", dest="graphs", default=None)
     a("--roctx", action="store_true", default=None)
     a("--verbose", type=int)
     return ap

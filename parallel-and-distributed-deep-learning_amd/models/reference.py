@@ -40,10 +40,33 @@ class ReferenceResNet50:
         self.L = layout
         self.bn_mode = bn_mode
         self.stats = None   # flat buffer holding the BN moving statistics (non-trainable)
+        self._bound = None  # (flat tensor, {name: view}) of the last bind()
+
+    def bind(self, params):
+        """Per-tensor views of a flat buffer through ONE `split`: autograd then concatenates
+        the per-tensor gradients once, instead of materialising a full-size zero gradient per
+        slice (214 x 25.6M floats per backward)."""
+        ents = sorted((e for e in self.L.entries.values() if e.offset + e.size <= params.numel()),
+                      key=lambda e: e.offset)
+        sizes, names, pos = [], [], 0
+        for e in ents:
+            if e.offset > pos:
+                sizes.append(e.offset - pos)
+                names.append(None)
+            sizes.append(e.size)
+            names.append(e)
+            pos = e.offset + e.size
+        if pos < params.numel():
+            sizes.append(params.numel() - pos)
+            names.append(None)
+        views = {e.name: t.view(e.shape) for e, t in zip(names, torch.split(params, sizes)) if e is not None}
+        self._bound = (params, views)
 
     def _w(self, params, layer, kind):
         if kind in ("moving_mean", "moving_variance") and self.stats is not None:
             return self.L.view(self.stats, layer, kind)
+        if self._bound is not None and self._bound[0] is params:
+            return self._bound[1][f"{layer}/{kind}:0"]
         return self.L.view(params, layer, kind)
 
     def _conv(self, params, x, c, pad_explicit=False):
@@ -126,6 +149,7 @@ class TorchEngine:
         # (a copy: BN statistics share the flat buffer and train-mode BN updates them in place)
         p = self.params[: self.L.n_trainable].clone().requires_grad_(True)
         self.model.stats = self.params
+        self.model.bind(p)
         x = preprocess(images.to(self.device), self.crop, True, flip, crop_offset)
         logits = self.model.logits(p, x, training=True)
         lab = labels.to(self.device)

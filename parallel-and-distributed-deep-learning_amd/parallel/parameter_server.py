@@ -234,9 +234,11 @@ class PSServer:
                     continue
                 finished = cl.store.check([f"fin/{w}"])
                 if not finished and now - last > timeout:
-                    cur = int(cl.store.get(f"cur/{w}").decode()) if cl.store.check([f"cur/{w}"]) else -1
+                    cur, ep = -1, -1
+                    if cl.store.check([f"cur/{w}"]):
+                        ep, cur = (int(x) for x in cl.store.get(f"cur/{w}").decode().split(":"))
                     if cur >= 0:
-                        cl.store.add("requeue", 1)
+                        cl.store.add(f"requeue/{ep}", 1)    # only the dead worker's epoch re-runs it
                     requeued.add(w)
                     cl.store.add("dead_workers", 1)
                     print(f"[coordinator] worker {w} missed heartbeats for {now - last:.1f}s: re-queued its "
@@ -318,18 +320,34 @@ class PSWorker:
             if hasattr(self, "cli"):
                 self.cli.stop()
             cl.store.set(f"fin/{cl.rank}", "1")
+            cl.store.add("fin_count", 1)
             return
         ctrl = torch.tensor([OP_STOP, 0.0], dtype=torch.float64, device=cl.device)
         for p in range(cl.num_ps):
             dist.send(ctrl, dst=p, group=cl.pair[(cl.rank, p)])
         cl.store.set(f"fin/{cl.rank}", "1")
+        cl.store.add("fin_count", 1)
+
+
+class _PSControl:
+    """The slice of the trainer the LR / stop callbacks drive (worker 0 of a PS job)."""
+
+    def __init__(self, lr: float):
+        self.lr = float(lr)
+        self.stop_training = False
+
+    def set_lr(self, lr: float):
+        self.lr = float(lr)
+
+    def log(self, msg: str):
+        print(msg, flush=True)
 
 
 def _claim(store, spe: int, epoch: int) -> int:
     """Claim the next step ticket of `epoch`; -1 when the epoch's steps are exhausted
     (re-queued tickets of dead workers extend the budget)."""
     t = store.add(f"claim/{epoch}", 1) - 1
-    budget = spe + store.add("requeue", 0)
+    budget = spe + store.add(f"requeue/{epoch}", 0)
     return t if t < budget else -1
 
 
@@ -408,8 +426,20 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     from .strategies import Augment
     aug = Augment(cfg, device, cfg.seed + 7919 * widx)
     history = []
-    stats_acc = torch.zeros(3, dtype=torch.float64)
     steps_done = 0
+    ctl = _PSControl(lr)
+    cbs = []
+    if widx == 0:
+        # the coordinator-side callbacks of the reference's fit (imagenet-resnet50-ps.py:139-140):
+        # decisions taken on worker 0's validation, published on the control plane
+        from ..train.callbacks import EarlyStopping, ReduceLROnPlateau
+        cbs = [ReduceLROnPlateau(monitor="val_loss", factor=cfg.reduce_lr_factor, patience=cfg.reduce_lr_patience,
+                                 min_lr=cfg.min_lr),
+               EarlyStopping(monitor="val_loss", min_delta=cfg.early_stop_min_delta,
+                             patience=cfg.early_stop_patience)]
+        for cb in cbs:
+            cb.set_trainer(ctl)
+            cb.on_train_begin()
     for epoch in range(cfg.epochs):
         if store.check(["stop"]):
             break
@@ -421,7 +451,7 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             t = _claim(store, spe, epoch)
             if t < 0:
                 break
-            store.set(f"cur/{rank}", str(t))
+            store.set(f"cur/{rank}", f"{epoch}:{t}")
             store.set(_hb_key(rank), str(time.time()))
             if fault_at is not None and steps_done == fault_at:
                 print(f"[worker {widx}] injected failure at step {steps_done}", flush=True)
@@ -433,7 +463,7 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             acc[:2] += s.detach().double().cpu()
             acc[2] += B
             worker._exchange(OP_PUSH, lr)
-            store.set(f"cur/{rank}", "-1")
+            store.set(f"cur/{rank}", f"{epoch}:-1")
             store.add(f"done/{epoch}", 1)
             steps_done += 1
         store.set(_hb_key(rank), str(time.time()))
@@ -452,6 +482,14 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
                     "images_per_sec": n / max(dt, 1e-9)}
             if cfg.validation_steps:
                 logs.update(_validate(cfg, eng, device))
+            for cb in cbs:
+                cb.on_epoch_end(epoch, logs)
+            if ctl.lr != lr:
+                lr = ctl.lr
+                store.set("lr", repr(lr))           # every worker picks it up at its next epoch
+            if ctl.stop_training:
+                store.set("stop", "1")
+            logs["lr"] = lr
             history.append(logs)
             print(f"Epoch {epoch + 1}/{cfg.epochs} - {logs['steps']}/{spe} steps - loss: {logs['loss']:.4f} - "
                   f"accuracy: {logs['accuracy']:.4f}" + (f" - val_loss: {logs['val_loss']:.4f}"
@@ -460,6 +498,12 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             store.set(f"epoch_go/{epoch}", "1")
         else:
             _wait_key(store, f"epoch_go/{epoch}")
+    if widx == 0 and cfg.save:
+        # the reference saves the PS-held variables (imagenet-resnet50-ps.py:145-148): wait until
+        # every live worker pushed its last step and stopped, then pull the final state
+        alive = cl.num_workers - store.add("dead_workers", 0)
+        _wait_count(store, "fin_count", alive - 1)
+        worker._exchange(OP_PULL, lr)
     worker.stop()
     if widx == 0 and cfg.save:
         from ..utils.checkpoint import save_keras_h5

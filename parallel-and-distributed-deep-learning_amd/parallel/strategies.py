@@ -145,8 +145,12 @@ class Strategy:
     def _pipe(self, split: str, batch: int, shards: int, index: int) -> Pipeline:
         cfg = self.cfg
         src = make_source(cfg.data, split, cfg)
+        # Real data is read in a fresh permutation every epoch (the reference's
+        # shuffle_files=True, imagenet-resnet50.py:31; folder sources list files class by
+        # class).  Every rank uses the same seed, so the shards of one epoch stay disjoint.
+        shuffle = split == "train" and cfg.data not in ("synthetic", "synthetic_fixed")
         return Pipeline(src, batch, num_shards=shards, shard_index=index, shard_by=cfg.shard_by,
-                        repeat=cfg.strategy == "ps", seed=cfg.seed)
+                        repeat=cfg.strategy == "ps", shuffle=shuffle, seed=cfg.seed)
 
     def train_pipeline(self) -> Pipeline:
         return self._pipe("train", self.per_replica_batch * self.local_replicas, self.world, self.rank)
@@ -213,7 +217,7 @@ class _ProcessGroupMixin:
         export_torch_env(info)
         self.rank, self.world = info.rank, info.world_size
         self.info = info
-        if not dist.is_initialized():
+        if not dist.is_initialized() and info.world_size > 1:   # (a 1-rank job needs no rendezvous)
             backend = "nccl" if self.device.type == "cuda" else "gloo"
             # PDDL_DIST_BACKEND=gloo: rehearse GPU ranks sharing one device (RCCL refuses that)
             backend = os.environ.get("PDDL_DIST_BACKEND", backend)
@@ -351,32 +355,57 @@ class MultiWorkerStrategy(HorovodStrategy):
     """MultiWorkerMirroredStrategy (imagenet-resnet50-multiworkers.py): SLURM-resolved worker
     processes (SlurmClusterResolver(port_base=12345)), element-wise DATA sharding, synchronous
     all-reduce.  With several GPUs per worker process (PDDL_LOCAL_GPUS=R, e.g. 2 procs x 4
-    GPUs), each process runs R replica threads and ONE native RCCL communicator spans all
-    P*R replicas (unique id exchanged through the c10d store)."""
+    GPUs, multiworkers.py:20-26), each process drives R local replicas and ONE native RCCL
+    communicator spans all P*R replicas (unique id exchanged through the c10d store).  On CPU
+    the same layout runs R CPU replicas per process with the cross-process sum over gloo (the
+    test double of that communicator)."""
     name = "multiworker"
 
     def __init__(self, cfg, local_gpus: Optional[int] = None):
         super().__init__(cfg, comm="bucket")
         self.req_local = int(os.environ.get("PDDL_LOCAL_GPUS", local_gpus or 1))
 
+    def _local_devices(self, info: ClusterInfo) -> list:
+        R = self.req_local
+        want_gpu = self.cfg.device == "cuda" or (self.cfg.device == "auto" and gpu_available())
+        if not want_gpu:
+            return ["cpu"] * R
+        if not gpu_available():
+            raise RuntimeError(f"PDDL_LOCAL_GPUS={R} with device={self.cfg.device!r} but no GPU is visible")
+        have = torch.cuda.device_count()
+        devs = [info.local_rank * R + i for i in range(R)]
+        if devs[-1] >= have:
+            if os.environ.get("PDDL_REHEARSE", "0") != "1":
+                raise RuntimeError(f"local rank {info.local_rank} needs GPUs {devs[0]}..{devs[-1]} "
+                                   f"(PDDL_LOCAL_GPUS={R}) but only {have} are visible")
+            devs = [d % have for d in devs]    # rehearsal: replicas share devices (no RCCL)
+        return devs
+
     def _build(self, trainer):
-        if self.req_local <= 1 or not gpu_available():
+        if self.req_local <= 1:
             return super()._build(trainer)
         info = resolve_cluster(port_base=self.cfg.port_base)
         R = self.req_local
+        devs = self._local_devices(info)
         self.local_replicas = R
-        devs = [info.local_rank * R + i for i in range(R)]
-        self.device = self._pick_device(devs[0])
         # control plane: gloo process group over the same rendezvous
         export_torch_env(info)
         self.rank, self.world = info.rank, info.world_size
-        if not dist.is_initialized():
+        if not dist.is_initialized() and self.world > 1:
             dist.init_process_group("gloo", init_method="env://", rank=info.rank, world_size=info.world_size)
         self.mirror = _LocalReplicas(self.cfg, devs, global_rank_base=self.rank * R, world_ranks=self.world * R)
         self.engine, self.opt = self.mirror.replicas[0]
+        self.device = self.mirror.devices[0]
 
     def _replicas(self):
         return self.mirror.replicas if hasattr(self, "mirror") else super()._replicas()
+
+    def reduce_metrics(self, t):
+        if hasattr(self, "mirror") and self.world > 1:
+            x = t.to("cpu", torch.float64)       # (the control group is gloo)
+            dist.all_reduce(x)
+            return x
+        return super().reduce_metrics(t)
 
     def train_step(self, images, labels):
         if not hasattr(self, "mirror"):
@@ -391,15 +420,28 @@ class MultiWorkerStrategy(HorovodStrategy):
 
 
 class _LocalReplicas:
-    """R model replicas in this process, one per GPU, driven by replica threads; gradients are
-    summed with ONE grouped RCCL all-reduce across every replica of the job (in-process
-    ncclCommInitAll for Mirrored, ncclCommInitRank over P processes for multi-worker).  On CPU
-    the replicas run sequentially and the reduction is an in-process sum (test double)."""
+    """R model replicas in this process, one per device; gradients are summed across every
+    replica of the job.
+
+    GPU (distinct devices): ONE native RCCL communicator (in-process ncclCommInitAll for
+    Mirrored, ncclCommInitRank over P processes for multi-worker).  By default every replica's
+    step is replayed from HIP graphs segmented at the gradient-bucket boundaries
+    (train/graph.py SegmentedStepGraphs): segment k on all devices, then the grouped all-reduce
+    of bucket k on per-device comm streams while segment k+1 computes, then a captured
+    optimizer graph per device -- so one host thread drives R GPUs with ~R*(nb+1) graph
+    launches per step (no per-kernel Python launch cost).  cfg.graphs=False (--no-graphs): eager
+    replica threads (launch bindings release the GIL) with the same bucket overlap.
+
+    CPU (and rehearsals with replicas sharing a device): replicas run in turn and the
+    reduction is an in-process sum, plus a gloo all-reduce across processes when replicas of
+    the job live in other processes (the multi-worker test double of the RCCL communicator)."""
 
     def __init__(self, cfg, devices: List, global_rank_base: int = 0, world_ranks: Optional[int] = None):
         self.cfg = cfg
         self.devices = [torch.device(d) if not isinstance(d, int) else torch.device("cuda", d) for d in devices]
         self.R = len(self.devices)
+        world_ranks = world_ranks or self.R
+        self.cross = world_ranks > self.R           # replicas of the job in other processes
         cap = max(cfg.batch_size, cfg.val_batch_size or 0)
         self.replicas = []
         self.augs = []
@@ -414,10 +456,10 @@ class _LocalReplicas:
             self.augs.append(Augment(cfg, d, cfg.seed + 7919 * (global_rank_base + i)))
         self.comm = None
         self.gpu = self.devices[0].type == "cuda"
-        if self.gpu:
+        distinct = len({str(d) for d in self.devices}) == self.R
+        if self.gpu and distinct:
             from ..ops.native import require_native
             N = require_native()
-            world_ranks = world_ranks or self.R
             if world_ranks == self.R:
                 self.comm = N.RcclComm.init_all([d.index for d in self.devices])
             else:
@@ -426,24 +468,95 @@ class _LocalReplicas:
                 dist.broadcast_object_list(obj, src=0)
                 self.comm = N.RcclComm(world_ranks, obj[0], [global_rank_base + i for i in range(self.R)],
                                        [d.index for d in self.devices])
+        self.graph_mode = (self.comm is not None and hasattr(self.replicas[0][0], "wbf")
+                           and (cfg.graphs if cfg.graphs is not None else True))
+        self.graphs = None
+        self.buckets = None
 
+    # ------------------------------------------------------------------ state
     def broadcast(self):
         if self.comm is not None:
             self.comm.broadcast([e.params for e, _ in self.replicas], 0)
             for k in self.replicas[0][1].state_tensors():
                 self.comm.broadcast([o.state_tensors()[k] for _, o in self.replicas], 0)
         else:
-            p0 = self.replicas[0][0].params
+            e0, o0 = self.replicas[0]
+            if self.cross:
+                dist.broadcast(e0.params, 0)
+                for t in o0.state_tensors().values():
+                    dist.broadcast(t, 0)
             for e, o in self.replicas[1:]:
-                e.params.copy_(p0)
+                e.params.copy_(e0.params)
                 for k, t in o.state_tensors().items():
-                    t.copy_(self.replicas[0][1].state_tensors()[k])
+                    t.copy_(o0.state_tensors()[k])
         for e, _ in self.replicas:
             e.after_update()
 
+    def _split(self, images, labels):
+        """Per-replica (images, labels) on each replica's device: a list (one pre-placed batch
+        per device) or one global batch split along dim 0."""
+        if isinstance(images, (list, tuple)):
+            assert len(images) == self.R and len(labels) == self.R
+            return [(im.to(d, non_blocking=True), lb.to(d, non_blocking=True))
+                    for im, lb, d in zip(images, labels, self.devices)]
+        B = images.shape[0] // self.R
+        return [(images[i * B:(i + 1) * B].to(d, non_blocking=True), labels[i * B:(i + 1) * B].to(d, non_blocking=True))
+                for i, d in enumerate(self.devices)]
+
+    def _sum_stats(self, stats):
+        out = stats[0].to(self.devices[0]).clone()
+        for s in stats[1:]:
+            out = out + s.to(self.devices[0])
+        return out
+
+    # ------------------------------------------------------------------ graphed step
+    def _capture(self, parts, global_batch: int):
+        from ..train.graph import SegmentedStepGraphs
+        eng0 = self.replicas[0][0]
+        self.buckets = eng0.L.buckets(self.cfg.bucket_mb)
+        B = parts[0][0].shape[0]
+        H, W = parts[0][0].shape[1:3]
+        self.graphs = []
+        for (eng, opt), d in zip(self.replicas, self.devices):
+            with torch.cuda.device(d):
+                g = SegmentedStepGraphs(eng, opt, B, (H, W), 1.0 / global_batch, self.buckets,
+                                        image_dtype=parts[0][0].dtype)
+                g.capture()
+                self.graphs.append(g)
+        self.comm_streams = [torch.cuda.Stream(device=d) for d in self.devices]
+        self.evs = [[torch.cuda.Event() for _ in self.devices] for _ in self.buckets]
+        self._gb = global_batch
+
+    def _graphed_step(self, parts, global_batch: int):
+        B = parts[0][0].shape[0]
+        if self.graphs is None or self.graphs[0].B != B or self._gb != global_batch:
+            out = self._eager_step(parts, global_batch)   # first step eager (lazy tables), then capture
+            self._capture(parts, global_batch)
+            return out
+        grads = [e.grads for e, _ in self.replicas]
+        cur = [torch.cuda.current_stream(d) for d in self.devices]
+        for r, (g, d) in enumerate(zip(self.graphs, self.devices)):
+            with torch.cuda.device(d):
+                flip, off = self.augs[r](B)
+                g.load(parts[r][0], parts[r][1], flip, off)
+        streams = [cs.cuda_stream for cs in self.comm_streams]
+        for k, (s, e) in enumerate(self.buckets):
+            for r, d in enumerate(self.devices):
+                with torch.cuda.device(d):
+                    self.graphs[r].replay_segment(k)
+                    self.evs[k][r].record(cur[r])
+                    self.comm_streams[r].wait_event(self.evs[k][r])
+            self.comm.all_reduce_on([gr[s:e] for gr in grads], "sum", streams)
+        for r, d in enumerate(self.devices):
+            with torch.cuda.device(d):
+                cur[r].wait_stream(self.comm_streams[r])
+                self.graphs[r].replay_optimizer()
+        return self._sum_stats([g.stats for g in self.graphs])
+
+    # ------------------------------------------------------------------ eager step
     def _overlap_setup(self):
-        """Bucketed all-reduce overlapped with backward (GPU): each replica thread records an
-        event when bucket i of its flat gradient is produced; once all R replicas have bucket
+        """Eager bucketed all-reduce overlapped with backward (GPU): each replica thread records
+        an event when bucket i of its flat gradient is produced; once all R replicas have bucket
         i, a comm thread makes per-device comm streams wait on those events and issues ONE
         grouped RCCL all-reduce of bucket i across the devices, while the replicas keep
         computing the earlier layers' gradients.  (TF's Mirrored all-reduces one pack after
@@ -469,59 +582,25 @@ class _LocalReplicas:
 
     def _comm_loop(self):
         grads = [e.grads for e, _ in self.replicas]
+        streams = [cs.cuda_stream for cs in self.comm_streams]
         for _ in range(len(self.buckets)):
             i = self._q.get()
             s, e = self.buckets[i]
-            for r, d in enumerate(self.devices):
+            for r in range(self.R):
                 self.comm_streams[r].wait_event(self._events[i][r])
-                torch.cuda.set_stream(self.comm_streams[r])     # thread-local current stream per device
-            self.comm.all_reduce([g[s:e] for g in grads], "sum")
+            self.comm.all_reduce_on([g[s:e] for g in grads], "sum", streams)
         self._done = []
-        for r, d in enumerate(self.devices):
+        for r in range(self.R):
             ev = torch.cuda.Event()
             ev.record(self.comm_streams[r])
             self._done.append(ev)
 
-    def _graphed_step(self, images, labels, global_batch: int):
-        """cfg.graphs: one HIP-graph replay of forward+backward per device, issued from this
-        thread (launch cost ~1 call per GPU instead of ~180 per replica thread), then ONE
-        grouped RCCL all-reduce of the flat gradients and the eager optimizer steps."""
-        from ..train.graph import GraphedTrainStep
+    def _eager_step(self, parts, global_batch: int):
         R = self.R
-        B = images.shape[0] // R
-        if not hasattr(self, "graphed") or self.graphed[0].B != B:
-            H, W = images.shape[1:3]
-            self.graphed = []
-            for i, d in enumerate(self.devices):
-                with torch.cuda.device(d):
-                    eng, opt = self.replicas[i]
-                    self.graphed.append(GraphedTrainStep(eng, opt, B, (H, W), 1.0 / global_batch,
-                                                         with_optimizer=False))
-        stats = []
-        for i, d in enumerate(self.devices):
-            with torch.cuda.device(d):
-                flip, off = self.augs[i](B)
-                stats.append(self.graphed[i](images[i * B:(i + 1) * B].to(d, non_blocking=True),
-                                             labels[i * B:(i + 1) * B].to(d, non_blocking=True), flip, off))
-        self.comm.all_reduce([e.grads for e, _ in self.replicas], "sum")
-        for (e, o), d in zip(self.replicas, self.devices):
-            with torch.cuda.device(d):
-                o.step()
-                e.after_update()
-        out = stats[0].to(self.devices[0]).clone()   # (the graphs' static stats buffers are reused)
-        for s in stats[1:]:
-            out = out + s.to(self.devices[0])
-        return out
-
-    def step(self, images, labels, global_batch: int):
-        if self.cfg.graphs and self.comm is not None:
-            return self._graphed_step(images, labels, global_batch)
-        R = self.R
-        B = images.shape[0] // R
         stats = [None] * R
         overlap = self.comm is not None and os.environ.get("PDDL_MIRROR_OVERLAP", "1") != "0"
         if overlap:
-            if not hasattr(self, "buckets"):
+            if not hasattr(self, "_q"):
                 self._overlap_setup()
             nb = len(self.buckets)
             self._events = [[None] * R for _ in range(nb)]
@@ -534,9 +613,8 @@ class _LocalReplicas:
             d = self.devices[i]
             if d.type == "cuda":
                 torch.cuda.set_device(d)
-            im = images[i * B:(i + 1) * B].to(d, non_blocking=True)
-            lb = labels[i * B:(i + 1) * B].to(d, non_blocking=True)
-            flip, off = self.augs[i](B)
+            im, lb = parts[i]
+            flip, off = self.augs[i](im.shape[0])
             kw = dict(bucket_cb=self._bucket_cb(i), buckets=self.buckets) if overlap else {}
             stats[i] = eng.forward_backward(im, lb, 1.0 / global_batch, flip=flip, crop_offset=off, **kw).clone()
 
@@ -556,19 +634,28 @@ class _LocalReplicas:
                 torch.cuda.current_stream(d).wait_event(self._done[r])
         elif self.comm is not None:
             self.comm.all_reduce(grads, "sum")
-        elif R > 1:
-            tot = grads[0].clone()
+        elif R > 1 or self.cross:
+            if self.gpu:
+                for d in {str(d) for d in self.devices}:
+                    torch.cuda.synchronize(torch.device(d))   # replicas on other threads / streams
+            tot = grads[0].clone() if R > 1 else grads[0]
             for g in grads[1:]:
-                tot += g
+                tot += g.to(tot.device)
+            if self.cross:
+                dist.all_reduce(tot)
             for g in grads:
-                g.copy_(tot)
+                if g is not tot:
+                    g.copy_(tot)
         for e, o in self.replicas:
             o.step()
             e.after_update()
-        out = stats[0].to(self.devices[0])
-        for s in stats[1:]:
-            out = out + s.to(self.devices[0])
-        return out
+        return self._sum_stats(stats)
+
+    def step(self, images, labels, global_batch: int):
+        parts = self._split(images, labels)
+        if self.graph_mode:
+            return self._graphed_step(parts, global_batch)
+        return self._eager_step(parts, global_batch)
 
 
 class MirroredStrategy(Strategy):

@@ -114,7 +114,8 @@ def test_single_strategy_train_mode_bn_on_hip():
 
 
 def test_mirrored_graphed_step_matches_eager():
-    """Mirrored with --graphs (per-device forward+backward graph replays from one thread)
+    """Mirrored with HIP graphs (default: per-device step segments split at the gradient
+    buckets, grouped all-reduce of bucket k between segment k and k+1, captured optimizer)
     follows the eager Mirrored trajectory."""
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
@@ -125,9 +126,43 @@ def test_mirrored_graphed_step_matches_eager():
         tr = Trainer(cfg, st)
         h = tr.fit(1, [], validation=False)
         res.append((h.history["loss"][0], st.engine.params.clone(), st.opt.iterations))
+        assert st.mirror.graph_mode == graphs
         if graphs:
-            assert st.mirror.graphed[0].graph is not None
+            g = st.mirror.graphs[0]
+            assert g.captured and len(g.segments) == len(st.mirror.buckets) >= 2
     (l0, p0, i0), (l1, p1, i1) = res
     assert i0 == i1 == 3
     assert abs(l0 - l1) <= 1e-3 * abs(l0)
     assert ((p0 - p1).norm() / p0.norm()).item() < 2e-3
+
+
+def _bench_json(args, env):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, **env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], cwd=root, env=e,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("strategy", ["horovod", "mirrored"])
+def test_bench_two_rank_rehearsal_on_one_gpu(strategy):
+    """bench.py --gpus 2 on one GPU (PDDL_REHEARSE=1: ranks share device 0, gloo instead of
+    RCCL): the multi-rank launch path runs end to end and reports n_gpus 2."""
+    out = _bench_json(["--gpus", "2", "--strategy", strategy, "--batch", "32", "--steps", "2", "--warmup", "1"],
+                      {"PDDL_REHEARSE": "1"})
+    assert out["n_gpus"] == 2 and out["config"]["replicas"] == 2 and out["rehearsal"] is True
+    assert out["value"] > 0 and out["final_loss"] == out["final_loss"]
+
+
+def test_bench_mirrored_one_gpu_graphed():
+    """The in-process Mirrored bench on 1 GPU runs RCCL + segmented HIP graphs."""
+    out = _bench_json(["--gpus", "1", "--strategy", "mirrored", "--batch", "64", "--steps", "3", "--warmup", "2"], {})
+    assert out["n_gpus"] == 1 and out["config"]["hip_graph"] is True and "rehearsal" not in out

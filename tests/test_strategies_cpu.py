@@ -30,34 +30,39 @@ def _train(preset, **kw):
     return st, hist
 
 
-def _rank_main(rank, world, port, preset, kw, q):
+def _rank_main(rank, world, port, preset, kw, q, env=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    os.environ.update(env or {})
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import pddl  # noqa
     st, hist = _train(preset, **kw)
     n = st.engine.L.n_trainable
-    q.put((rank, st.engine.params[:n].numpy().copy(), hist.history["loss"][0],
-           type(getattr(st, "fusion", None)).__name__, getattr(st, "bucket_mb", None)))
+    reps = [e.params[:n].numpy().copy() for e, _ in st._replicas()]
+    q.put((rank, reps[0], hist.history["loss"][0], type(getattr(st, "fusion", None)).__name__,
+           getattr(st, "bucket_mb", None), reps, st.num_replicas_in_sync))
     import torch.distributed as dist
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _spawn(world, preset, kw):
+def _spawn(world, preset, kw, env=None, full=False):
     from pddl.parallel.launch import pick_unused_port
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = pick_unused_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, world, port, preset, kw, q)) for r in range(world)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, preset, kw, q, env)) for r in range(world)]
     for p in ps:
         p.start()
     out = [q.get(timeout=600) for _ in range(world)]
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    return [(r, torch.from_numpy(p), l, f, mb) for r, p, l, f, mb in sorted(out, key=lambda t: t[0])]
+    out = sorted(out, key=lambda t: t[0])
+    if full:
+        return out
+    return [(r, torch.from_numpy(p), l, f, mb) for r, p, l, f, mb, _, _ in out]
 
 
 @pytest.fixture(scope="module")
@@ -66,8 +71,8 @@ def single_b4():
     return st.engine.params[:st.engine.L.n_trainable].clone(), hist.history["loss"][0]
 
 
-def _close(a, b):
-    return ((a - b).norm() / b.norm()).item() < 1e-5
+def _close(a, b, tol=1e-5):
+    return ((a - b).norm() / b.norm()).item() < tol
 
 
 def test_horovod_2_ranks_equals_single_global_batch(single_b4):
@@ -85,6 +90,32 @@ def test_multiworker_element_sharding_equals_single(single_b4):
     out = _spawn(2, "multiworker", dict(batch_size=2, val_batch_size=2))
     for _, p, _, _, _ in out:
         assert _close(p, ref)
+
+
+def test_multiworker_2_procs_x_2_replicas_equals_single(single_b4):
+    """The MWMS 2 workers x R GPUs layout (imagenet-resnet50-multiworkers.py:20-26) as its CPU
+    double: 2 processes x 2 local replicas (PDDL_LOCAL_GPUS=2), in-process sum + gloo sum across
+    processes standing in for the one RCCL communicator; global batch 4 = single b4."""
+    ref, ref_loss = single_b4
+    out = _spawn(2, "multiworker", dict(batch_size=1, val_batch_size=1), env={"PDDL_LOCAL_GPUS": "2"}, full=True)
+    for rank, _, loss, _, _, reps, nrep in out:
+        assert nrep == 4 and len(reps) == 2
+        for p in reps:   # batch-1 replicas sum in another order than one b4 conv: Adam amplifies
+            assert _close(torch.from_numpy(p), ref, 2e-4)   # the reassociation of tiny grads (~7e-5)
+    assert abs(out[0][2] - ref_loss) <= 1e-5 * abs(ref_loss)
+    for p in out[1][5]:          # every replica of every process holds the same weights
+        assert (torch.from_numpy(p) == torch.from_numpy(out[0][5][0])).all()
+
+
+def test_multiworker_local_gpus_refuses_missing_devices(monkeypatch):
+    """PDDL_LOCAL_GPUS>1 on a GPU request that cannot be honoured errors out (no silent fallback
+    to one replica)."""
+    from pddl.parallel.strategies import MultiWorkerStrategy
+    from pddl.parallel.launch import ClusterInfo
+    monkeypatch.setenv("PDDL_LOCAL_GPUS", "4")
+    st = MultiWorkerStrategy(_cfg("multiworker", device="cuda"))
+    with pytest.raises(RuntimeError, match="no GPU is visible|GPUs"):
+        st._local_devices(ClusterInfo())
 
 
 def test_mirrored_two_cpu_replicas_equals_single(single_b4, monkeypatch):
