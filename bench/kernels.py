@@ -41,8 +41,13 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--knob", default="igemm_big", help="igemm knob to A/B (igemm_big, igemm_il, ...)")
     ap.add_argument("--variants", default="0,3", help="comma-separated knob values")
+    ap.add_argument("--skip-lib", action="store_true", help="skip the MIOpen / hipBLASLt yardsticks")
+    ap.add_argument("--set", default="", help="extra knobs for every variant, e.g. igemm8_min_tiles=1")
     a = ap.parse_args()
     N = require_native()
+    for kv in filter(None, a.set.split(",")):
+        k, v = kv.split("=")
+        N.set_variant(k, int(v))
     B = a.batch
     dev = "cuda"
     res = []
@@ -73,20 +78,26 @@ def main():
         def mi_wg():
             torch.ops.aten.convolution_backward(gt, xt, wt, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
                                                 [False, True, False])
-        mrow = {"layer": name, "kernel": "miopen", "fwd_us": round(timeit(mi_fwd), 1), "wgrad_us": round(timeit(mi_wg), 1)}
-        print(json.dumps(mrow), flush=True)
-        res.append(mrow)
+        if not a.skip_lib:
+            mrow = {"layer": name, "kernel": "miopen", "fwd_us": round(timeit(mi_fwd), 1),
+                    "wgrad_us": round(timeit(mi_wg), 1)}
+            print(json.dumps(mrow), flush=True)
+            res.append(mrow)
         # hipBLASLt on the same-FLOP plain GEMMs (im2col'd A already in memory, no epilogue):
         # the library ceiling for these M / N / K
         M, K = B * Ho * Ho, R * R * C
+        if a.skip_lib:
+            M = 0
         am = torch.randn(M, K, device=dev).to(torch.bfloat16)
         bm = (torch.randn(K, Co, device=dev) * 0.05).to(torch.bfloat16)
         gm = torch.randn(M, Co, device=dev).to(torch.bfloat16)
-        f_us, w_us = timeit(lambda: torch.mm(am, bm)), timeit(lambda: torch.mm(gm.t(), am))
-        brow = {"layer": name, "kernel": "hipblaslt", "fwd_us": round(f_us, 1), "fwd_tflops": round(flops / f_us / 1e6, 1),
-                "wgrad_us": round(w_us, 1), "wgrad_tflops": round(flops / w_us / 1e6, 1)}
-        print(json.dumps(brow), flush=True)
-        res.append(brow)
+        if not a.skip_lib:
+            f_us, w_us = timeit(lambda: torch.mm(am, bm)), timeit(lambda: torch.mm(gm.t(), am))
+            brow = {"layer": name, "kernel": "hipblaslt", "fwd_us": round(f_us, 1),
+                    "fwd_tflops": round(flops / f_us / 1e6, 1), "wgrad_us": round(w_us, 1),
+                    "wgrad_tflops": round(flops / w_us / 1e6, 1)}
+            print(json.dumps(brow), flush=True)
+            res.append(brow)
         del am, bm, gm
         for kind, fn, knob, variants in (("igemm", fwd, a.knob, [int(v) for v in a.variants.split(",")]),
                                           ("wgrad", wg, "wgrad", [0])):

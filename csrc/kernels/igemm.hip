@@ -39,6 +39,197 @@ namespace pddl {
 //   AM_DUAL:   two AM_DIRECT sources concatenated along K (projection-block dgrad).
 enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 
+// Epilogue of one wave sub-tile of TM x TN 16x16 fragments at global rows [mb, mb + 16*TM)
+// and columns [nb, nb + 16*TN): fragments -> LDS (fp32, per-wave `stage` of 32 x (16*TN + 4))
+// -> 16-byte row stores with the fused FWD / F32 / DGRAD operations; the column sums (dgrad)
+// and batch statistics (train-mode BN forward) go to partial row `prow`.
+// PF: the per-element epilogue operand of the whole sub-tile is loaded into registers before
+// the accumulators are staged, so its HBM latency overlaps the staging.
+template <int TM, int TN, bool PF>
+__device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
+                                               float* stage, int lane) {
+  constexpr int WTN = 16 * TN;
+  constexpr int EPI_LD = WTN + 4;
+  const int HoWo = p.Ho * p.Wo;
+  constexpr int LPR = WTN / 8;   // lanes per row (8 columns each)
+  constexpr int RPI = 64 / LPR;  // rows per iteration
+  const int c8 = lane % LPR, rr = lane / LPR;
+  const int gn = nb + c8 * 8;
+  const bool col_ok = gn < p.Nn;
+  float sc[8], sh[8];
+  bool relu = p.relu != 0;
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  int ldo = p.ldo, col = gn;
+  bool seg0 = true;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // FWD stats: sum of squares
+  if (p.mode != EPI_DGRAD && col_ok) {
+    const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
+    const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
+    float4 a = s4[0], b = s4[1], c = h4[0], d = h4[1];
+    sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+    sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
+    if (p.out2 && gn >= p.n_split) {
+      out = reinterpret_cast<bf16_t*>(p.out2); ldo = p.ldo2; relu = p.relu2 != 0; col = gn - p.n_split;
+      seg0 = false;
+    }
+  }
+  constexpr int NIT = 32 / RPI;
+  uint4 pre[PF ? (TM / 2) * NIT : 1];
+  uint32_t pre_bits[PF ? TM / 2 : 1];
+  const bool pf_bits = PF && p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
+  if (PF) {
+    const bf16_t* src = p.mode == EPI_FWD ? p.res : p.add;
+    const int ldp = p.mode == EPI_FWD ? p.ld_res : p.ld_add;
+#pragma unroll
+    for (int pass = 0; pass < TM / 2; ++pass) {
+      pre_bits[pass] = 0;
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int gm = mb + pass * 32 + it * RPI + rr;
+        const bool ok = gm < p.M && col_ok;
+        pre[pass * NIT + it] = ok ? *reinterpret_cast<const uint4*>(src + (long)gm * ldp + gn) : make_uint4(0, 0, 0, 0);
+        if (pf_bits && ok) pre_bits[pass] |= (uint32_t)p.bits_mask[(long)gm * p.ld_bits_mask + (gn >> 3)] << (8 * it);
+      }
+    }
+  }
+#pragma unroll
+  for (int pass = 0; pass < TM / 2; ++pass) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          stage[(i2 * 16 + (lane >> 4) * 4 + jj) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 2 + i2][j][jj];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int rl = it * RPI + rr;
+      const int gm = mb + pass * 32 + rl;
+      if (gm < p.M && col_ok) {
+        const float4* sp = reinterpret_cast<const float4*>(stage + rl * EPI_LD + c8 * 8);
+        float4 q0 = sp[0], q1 = sp[1];
+        float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        if (p.mode == EPI_FWD) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
+          if (p.res) {
+            float rv[8];
+            uint4 r4;   // (if/else, not ?: -- an lvalue select would force `pre` into scratch)
+            if (PF) r4 = pre[pass * NIT + it];
+            else r4 = *reinterpret_cast<const uint4*>(p.res + (long)gm * p.ld_res + gn);
+            unpack8(r4, rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += rv[e];
+          }
+          if (relu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          const uint4 pk = pack8(v);
+          *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pk;
+          if (p.bits_out && seg0) {
+            p.bits_out[(long)gm * p.ld_bits_out + (col >> 3)] = (uint8_t)pos_bits8(pk);
+          }
+          if (p.stats) {   // batch statistics of exactly the values the BN-apply pass will read
+            float rv[8];
+            unpack8(pk, rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { csum[e] += rv[e]; csq[e] += rv[e] * rv[e]; }
+          }
+        } else if (p.mode == EPI_F32) {
+          float* o = reinterpret_cast<float*>(p.out) + (long)gm * p.ldo + gn;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
+          reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+          reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+        } else {  // EPI_DGRAD
+          long row = gm;
+          int n = 0, i = 0, j = 0;
+          if (p.up2) {
+            n = fdiv(gm, p.mg_howo); const int rem = gm - n * HoWo; i = fdiv(rem, p.mg_wo); j = rem - i * p.Wo;
+            row = ((long)n * p.Hf + 2 * i) * p.Wf + 2 * j;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            long rq = row;
+            if (q > 0) {
+              if (!p.up2) break;
+              const int hh = 2 * i + (q >> 1), ww = 2 * j + (q & 1);
+              if (hh >= p.Hf || ww >= p.Wf) continue;
+              rq = ((long)n * p.Hf + hh) * p.Wf + ww;
+            }
+            float w[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = (q == 0) ? v[e] : 0.f;
+            if (p.add) {
+              float av[8];
+              uint4 a4;
+              if (PF) a4 = pre[pass * NIT + it];
+              else a4 = *reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn);
+              unpack8(a4, av);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) w[e] += av[e];
+            }
+            if (p.mask) {
+              float mv[8];
+              unpack8(*reinterpret_cast<const uint4*>(p.mask + rq * p.ld_mask + gn), mv);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
+            } else if (p.bits_mask) {
+              uint32_t byte;
+              if (pf_bits) byte = (pre_bits[pass] >> (8 * it)) & 0xffu;
+              else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) csum[e] += w[e];
+            *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pack8(w);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // Fused per-channel column sums of the written gradient (BN beta / conv bias grads):
+  // fold the lanes that share columns, then each wave stores ONE partial row (plain
+  // stores; atomics from every workgroup onto the same 64-2048 addresses serialize).
+  // Rows are indexed (m-tile, wave-row); colsum_reduce folds them.
+  if (p.colsum) {
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
+    if (rr == 0 && col_ok) {
+      float4* dst = reinterpret_cast<float4*>(p.colsum + (long)prow * p.Nn + gn);
+      dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
+    }
+  }
+  // Train-mode BN: per-wave partial (sum, sum of squares) rows of the forward output, same
+  // row indexing as the column sums; colsum_reduce folds them and bn_stats finalizes.
+  if (p.stats) {
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        csum[e] += __shfl_xor(csum[e], o, 64);
+        csq[e] += __shfl_xor(csq[e], o, 64);
+      }
+    if (rr == 0 && col_ok) {
+      float* row = p.stats + (long)prow * 2 * p.Nn;
+      float4* d1 = reinterpret_cast<float4*>(row + gn);
+      float4* d2 = reinterpret_cast<float4*>(row + p.Nn + gn);
+      d1[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      d1[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
+      d2[0] = make_float4(csq[0], csq[1], csq[2], csq[3]);
+      d2[1] = make_float4(csq[4], csq[5], csq[6], csq[7]);
+    }
+  }
+}
+
 // Block tile BM x BN of NW waves, each wave a 64x64 tile of 16x16x32 MFMAs.
 //   NW = 4, NSTAGE 1/2: 2 blocks per CU, the next k-tile's LDS-DMA overlaps this tile's MFMAs.
 //   NW = 8 (256x128), NSTAGE 3: one 144 KiB block per CU, 2 waves per SIMD; a 3-deep LDS ring
@@ -236,184 +427,213 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
   if (NSTAGE == 3) __syncthreads();   // all fragment reads done before the epilogue reuses LDS
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
-  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
-  constexpr int LPR = WTN / 8;   // lanes per row (8 columns each)
-  constexpr int RPI = 64 / LPR;  // rows per iteration
-  const int c8 = lane % LPR, rr = lane / LPR;
-  const int gn = n0 + wn * WTN + c8 * 8;
-  const bool col_ok = gn < p.Nn;
-  float sc[8], sh[8];
-  bool relu = p.relu != 0;
-  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-  int ldo = p.ldo, col = gn;
-  bool seg0 = true;
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // FWD stats: sum of squares
-  if (p.mode != EPI_DGRAD && col_ok) {
-    const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
-    const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
-    float4 a = s4[0], b = s4[1], c = h4[0], d = h4[1];
-    sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
-    sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
-    if (p.out2 && gn >= p.n_split) {
-      out = reinterpret_cast<bf16_t*>(p.out2); ldo = p.ldo2; relu = p.relu2 != 0; col = gn - p.n_split;
-      seg0 = false;
-    }
-  }
-  constexpr int NIT = 32 / RPI;
-  uint4 pre[PF ? (TM / 2) * NIT : 1];
-  uint32_t pre_bits[PF ? TM / 2 : 1];
-  const bool pf_bits = PF && p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
-  if (PF) {
-    const bf16_t* src = p.mode == EPI_FWD ? p.res : p.add;
-    const int ldp = p.mode == EPI_FWD ? p.ld_res : p.ld_add;
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (WTN + 4));
+  igemm_epilogue<TM, TN, PF>(p, acc, m0 + wm * WTM, n0 + wn * WTN, tm * (BM / WTM) + wm, stage, lane);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// 8-phase 256x256 implicit GEMM (cdna_hip_programming.md §5 "The 256² 8-phase template",
+// T3+T4): 8 waves, one 128 KiB block per CU, BK = 64, two LDS buffers of four 16 KiB
+// half-tiles {A rows 0-127, B cols 0-127, B cols 128-255, A rows 128-255} ("parts" 0..3).
+//
+// Every K-tile is computed in 4 phases, one 128x128 block QUADRANT per phase in snake order
+// Q(0,0) Q(0,1) Q(1,1) Q(1,0); all 8 waves work on the phase's quadrant (wave (wm, wn) owns a
+// 64x32 sub-tile of every quadrant = 16 MFMAs 16x16x32 per phase), so a phase reads exactly
+// one A half and one B half, and the snake reuses the A (or B) fragments of the previous
+// phase: 12, 4, 8, 4 ds_read_b128 per phase.
+//
+// Staging runs LEAD = 5 half-tiles ahead of the phase counter (one half = 2 LDS-DMA pieces
+// per wave, issued by every phase), in first-use order (part 0, 1, 2, 3 of K-tile t are first
+// read in phases 0, 0, 1, 2 of t).  RAW: before the FIRST barrier of the phase preceding a
+// half's first use, each wave waits with a COUNTED vmcnt (2 x halves issued after it: 6 in
+// steady state, never 0 inside the loop); the raw s_barrier then publishes every wave's
+// pieces.  WAR: a half is restaged >= 1 phase after the phase that last read it (the
+// reading phase's lgkmcnt retires its ds_reads before that phase's second barrier).
+// STAGGER: the wave row wm = 1 (the second wave on every SIMD) runs one barrier behind, so
+// one wave's ds_reads / DMA issue overlap the other's MFMAs; the barrier rules above hold for
+// that offset because every wait sits one phase ahead of its first read.
+template <int AM, bool STAGGER>
+__global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
+  constexpr int BM = 256, BN = 256, HALF = 16384, BUF = 4 * HALF, LEAD = 5;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int mt = (p.M + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, mt * nt);
+  const int tn = wg % nt, tm = wg / nt;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int HoWo = p.Ho * p.Wo;
+  const int pix_total = p.N * p.H * p.W;
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(p.a1, pix_total * p.C1 * 2);
+  const __amdgpu_buffer_rsrc_t ra2 =
+      make_rsrc(AM == AM_DUAL ? p.a2 : p.a1, pix_total * (AM == AM_DUAL ? p.C2 : p.C1) * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
+  const int chunk_sw = (lane & 7) ^ ((lane >> 3) & 7);
+
+  // Rows this lane stages: A/B half h, piece i (of the wave's 2) -> tile row 128h + (2*wave+i)*8 + lane/8.
+  uint32_t a_o1[4], a_o2[4], a_taps[4], b_o[4];
 #pragma unroll
-    for (int pass = 0; pass < TM / 2; ++pass) {
-      pre_bits[pass] = 0;
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int gm = m0 + wm * WTM + pass * 32 + it * RPI + rr;
-        const bool ok = gm < p.M && col_ok;
-        pre[pass * NIT + it] = ok ? *reinterpret_cast<const uint4*>(src + (long)gm * ldp + gn) : make_uint4(0, 0, 0, 0);
-        if (pf_bits && ok) pre_bits[pass] |= (uint32_t)p.bits_mask[(long)gm * p.ld_bits_mask + (gn >> 3)] << (8 * it);
+  for (int hi = 0; hi < 4; ++hi) {
+    const int r = 128 * (hi >> 1) + (2 * wave + (hi & 1)) * 8 + (lane >> 3);
+    const int m = m0 + r;
+    a_o1[hi] = OOB_OFF; a_o2[hi] = OOB_OFF; a_taps[hi] = 0;
+    if (m < p.M) {
+      const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
+      const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
+      const int hi_ = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
+      const int pix = (n * p.H + hi_) * p.W + wi;
+      a_o1[hi] = (uint32_t)((pix * p.C1 + chunk_sw * 8) * 2);
+      if (AM == AM_DUAL) a_o2[hi] = (uint32_t)((pix * p.C2 + chunk_sw * 8) * 2);
+      if (AM == AM_HALO) {
+        uint32_t rows = 0, cols = 0, mk = 0;
+        for (int rr = 0; rr < p.R; ++rr) rows |= (uint32_t)((unsigned)(hi_ + rr) < (unsigned)p.H) << rr;
+        for (int ss = 0; ss < p.S; ++ss) cols |= (uint32_t)((unsigned)(wi + ss) < (unsigned)p.W) << ss;
+        for (int rr = 0; rr < p.R; ++rr) mk |= ((rows >> rr) & 1u) ? cols << (rr * p.S) : 0u;
+        a_taps[hi] = mk;
       }
     }
+    const int n = n0 + r;
+    b_o[hi] = (n < p.Nn) ? (uint32_t)((n * p.ldb + chunk_sw * 8) * 2) : OOB_OFF;
   }
+
+  // scalar k-walk of the NEXT K-tile to stage (same walk as igemm_kernel)
+  int ld_r = 0, ld_s = 0, ld_c0 = 0, ld_src2 = 0, ld_k = 0;
+  auto tile_delta = [&]() { return ((ld_r * p.W + ld_s) * (ld_src2 ? p.C2 : p.C1) + ld_c0) * 2; };
+  auto advance = [&]() {
+    const int C = ld_src2 ? p.C2 : p.C1;
+    ld_k += 64;
+    ld_c0 += 64;
+    if (ld_c0 == C) {
+      ld_c0 = 0;
+      if (++ld_s == p.S) { ld_s = 0; ++ld_r; }
+    }
+    if (AM == AM_DUAL && !ld_src2 && ld_k == p.K1) { ld_src2 = 1; ld_r = ld_s = ld_c0 = 0; }
+  };
+  const int KT = p.K / 64;
+  const int NH = 4 * KT;              // half-tiles of the whole K loop
+  // stage half-tile j = 4*kt + part (part: 0 A rows 0-127, 1 B cols 0-127, 2 B cols 128-255, 3 A rows 128-255)
+  auto stage_half = [&](int j, int part) {
+    char* base = smem + ((j >> 2) & 1) * BUF;
+    const int delta = tile_delta();
+    if (part == 0 || part == 3) {
+      const int h = part == 0 ? 0 : 1;
+      char* hb = base + (part == 0 ? 0 : 3) * HALF;
 #pragma unroll
-  for (int pass = 0; pass < TM / 2; ++pass) {
-#pragma unroll
-    for (int i2 = 0; i2 < 2; ++i2)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          stage[(i2 * 16 + (lane >> 4) * 4 + jj) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 2 + i2][j][jj];
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < 32 / RPI; ++it) {
-      const int rl = it * RPI + rr;
-      const int gm = m0 + wm * WTM + pass * 32 + rl;
-      if (gm < p.M && col_ok) {
-        const float4* sp = reinterpret_cast<const float4*>(stage + rl * EPI_LD + c8 * 8);
-        float4 q0 = sp[0], q1 = sp[1];
-        float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-        if (p.mode == EPI_FWD) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
-          if (p.res) {
-            float rv[8];
-            uint4 r4;   // (if/else, not ?: -- an lvalue select would force `pre` into scratch)
-            if (PF) r4 = pre[pass * NIT + it];
-            else r4 = *reinterpret_cast<const uint4*>(p.res + (long)gm * p.ld_res + gn);
-            unpack8(r4, rv);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += rv[e];
-          }
-          if (relu) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
-          const uint4 pk = pack8(v);
-          *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pk;
-          if (p.bits_out && seg0) {
-            p.bits_out[(long)gm * p.ld_bits_out + (col >> 3)] = (uint8_t)pos_bits8(pk);
-          }
-          if (p.stats) {   // batch statistics of exactly the values the BN-apply pass will read
-            float rv[8];
-            unpack8(pk, rv);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { csum[e] += rv[e]; csq[e] += rv[e] * rv[e]; }
-          }
-        } else if (p.mode == EPI_F32) {
-          float* o = reinterpret_cast<float*>(p.out) + (long)gm * p.ldo + gn;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
-          reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
-          reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
-        } else {  // EPI_DGRAD
-          long row = gm;
-          int n = 0, i = 0, j = 0;
-          if (p.up2) {
-            n = fdiv(gm, p.mg_howo); const int rem = gm - n * HoWo; i = fdiv(rem, p.mg_wo); j = rem - i * p.Wo;
-            row = ((long)n * p.Hf + 2 * i) * p.Wf + 2 * j;
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            long rq = row;
-            if (q > 0) {
-              if (!p.up2) break;
-              const int hh = 2 * i + (q >> 1), ww = 2 * j + (q & 1);
-              if (hh >= p.Hf || ww >= p.Wf) continue;
-              rq = ((long)n * p.Hf + hh) * p.Wf + ww;
-            }
-            float w[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) w[e] = (q == 0) ? v[e] : 0.f;
-            if (p.add) {
-              float av[8];
-              uint4 a4;
-              if (PF) a4 = pre[pass * NIT + it];
-              else a4 = *reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn);
-              unpack8(a4, av);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) w[e] += av[e];
-            }
-            if (p.mask) {
-              float mv[8];
-              unpack8(*reinterpret_cast<const uint4*>(p.mask + rq * p.ld_mask + gn), mv);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
-            } else if (p.bits_mask) {
-              uint32_t byte;
-              if (pf_bits) byte = (pre_bits[pass] >> (8 * it)) & 0xffu;
-              else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) csum[e] += w[e];
-            *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pack8(w);
-          }
+      for (int i = 0; i < 2; ++i) {
+        auto dst = LDS_PTR(hb + (2 * wave + i) * 1024);
+        const int hi = 2 * h + i;
+        if (AM == AM_HALO) {
+          const int tap = ld_r * p.S + ld_s;
+          const uint32_t off = ((a_taps[hi] >> tap) & 1u) ? a_o1[hi] + (uint32_t)delta : OOB_OFF;
+          buf_lds16(ra1, dst, off, 0);
+        } else if (AM == AM_DUAL && ld_src2) {
+          buf_lds16(ra2, dst, a_o2[hi], delta);
+        } else {
+          buf_lds16(ra1, dst, a_o1[hi], delta);
         }
       }
+    } else {
+      const int h = part == 1 ? 0 : 1;
+      char* hb = base + part * HALF;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) buf_lds16(rb, LDS_PTR(hb + (2 * wave + i) * 1024), b_o[2 * h + i], ld_k * 2);
     }
-    __syncthreads();
+    if (part == 3) advance();
+  };
+  // counted wait: half `need` complete while the halves issued after it (up to `last`) fly
+#define IG8_WAIT_BARRIER(need, last)                                                              \
+  {                                                                                               \
+    const int after_ = (last) - (need);                                                           \
+    if (after_ >= 3) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");                \
+    else if (after_ == 2) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");           \
+    else if (after_ == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");           \
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");                            \
   }
-  // Fused per-channel column sums of the written gradient (BN beta / conv bias grads):
-  // fold the lanes that share columns, then each wave stores ONE partial row (plain
-  // stores; atomics from every workgroup onto the same 64-2048 addresses serialize).
-  // Rows are indexed (m-tile, wave-row); colsum_reduce folds them.
-  if (p.colsum) {
+
+  v4f acc[2][2][4][2];
 #pragma unroll
-    for (int o = LPR; o < 64; o <<= 1)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
-    if (rr == 0 && col_ok) {
-      float4* dst = reinterpret_cast<float4*>(p.colsum + (long)(tm * (BM / WTM) + wm) * p.Nn + gn);
-      dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
-      dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
-    }
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: halves 0 .. LEAD-1, then halves 0 and 1 (phase 0's) landed and published
+#pragma unroll
+  for (int j = 0; j < LEAD; ++j)      // (unrolled: the part selects registers at compile time)
+    if (j < NH) stage_half(j, j & 3);
+  {
+    const int last = (LEAD < NH ? LEAD : NH) - 1;
+    IG8_WAIT_BARRIER(1, last)
   }
-  // Train-mode BN: per-wave partial (sum, sum of squares) rows of the forward output, same
-  // row indexing as the column sums; colsum_reduce folds them and bn_stats finalizes.
-  if (p.stats) {
+  if (STAGGER && wm == 1) asm volatile("s_barrier" ::: "memory");
+
+  v8bf af[2][4], bfr[2][2];
+  const int a_row = (wm * 64 + (lane & 15)) * 128;
+  const int b_row = (wn * 32 + (lane & 15)) * 128;
+  int pos[2];
 #pragma unroll
-    for (int o = LPR; o < 64; o <<= 1)
+  for (int kh = 0; kh < 2; ++kh) pos[kh] = (((kh * 4) + (lane >> 4)) ^ (lane & 7)) * 16;
+
+  for (int t = 0; t < KT; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        csum[e] += __shfl_xor(csum[e], o, 64);
-        csq[e] += __shfl_xor(csq[e], o, 64);
+    for (int q = 0; q < 4; ++q) {
+      const int qm = (q == 0 || q == 1) ? 0 : 1;
+      const int qn = (q == 0 || q == 3) ? 0 : 1;
+      const bool loadA = (q == 0 || q == 2), loadB = (q != 2);
+      if (loadB) {
+        const char* Bs = buf + (qn == 0 ? 1 : 2) * HALF + b_row;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) bfr[kh][j] = *reinterpret_cast<const v8bf*>(Bs + j * 16 * 128 + pos[kh]);
       }
-    if (rr == 0 && col_ok) {
-      float* row = p.stats + (long)(tm * (BM / WTM) + wm) * 2 * p.Nn;
-      float4* d1 = reinterpret_cast<float4*>(row + gn);
-      float4* d2 = reinterpret_cast<float4*>(row + p.Nn + gn);
-      d1[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
-      d1[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
-      d2[0] = make_float4(csq[0], csq[1], csq[2], csq[3]);
-      d2[1] = make_float4(csq[4], csq[5], csq[6], csq[7]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (loadA) {
+        const char* As = buf + (qm == 0 ? 0 : 3) * HALF + a_row;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) af[kh][i] = *reinterpret_cast<const v8bf*>(As + i * 16 * 128 + pos[kh]);
+      }
+      const int js = 4 * t + q + LEAD;                 // half staged by this phase
+      if (js < NH) stage_half(js, (q + LEAD) & 3);
+      const int last = (js < NH ? js : NH - 1);
+      // wait for the half(s) the NEXT phase reads first: q0 -> part 2 of t; q1 -> part 3 of t;
+      // q3 -> parts 0, 1 of t+1; q2 -> none (phase 3 re-reads A1 / B0)
+      if (q == 0) IG8_WAIT_BARRIER(4 * t + 2, last)
+      else if (q == 1) IG8_WAIT_BARRIER(4 * t + 3, last)
+      else if (q == 3 && t + 1 < KT) IG8_WAIT_BARRIER(4 * t + 5, last)
+      else asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kh][i], bfr[kh][j], acc[qm][qn][i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
     }
   }
+#undef IG8_WAIT_BARRIER
+  if (STAGGER && wm == 0) asm volatile("s_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave is done with the LDS tiles before the epilogue stages through them
+
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (32 + 4));
+  igemm_epilogue<4, 2, false>(p, acc[0][0], m0 + wm * 64, n0 + wn * 32, tm * 4 + wm, stage, lane);
+  igemm_epilogue<4, 2, false>(p, acc[0][1], m0 + wm * 64, n0 + 128 + wn * 32, tm * 4 + wm, stage, lane);
+  igemm_epilogue<4, 2, false>(p, acc[1][0], m0 + 128 + wm * 64, n0 + wn * 32, tm * 4 + 2 + wm, stage, lane);
+  igemm_epilogue<4, 2, false>(p, acc[1][1], m0 + 128 + wm * 64, n0 + 128 + wn * 32, tm * 4 + 2 + wm, stage, lane);
 }
 
 int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wave tiles)
@@ -422,6 +642,9 @@ int g_igemm_big = 0;       // 8-wave 256x128 3-stage tile: 0 never (default: mea
                            // 256x256 8-wave tile: 3 heuristic (Nn, K >= 256), 4 always (Nn > 128)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
 int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 layers with a residual / add
+int g_igemm8 = 0;          // 8-phase 256x256 kernel (igemm8_kernel) for Nn >= 256, K >= 256: 0 off,
+                           // 1 on, 2 on with the wave-row stagger
+int g_igemm8_min_tiles = 128;   // ... when the problem has at least this many 256x256 tiles
 int g_igemm_il = 0;        // 2-stage tiles issue the next tile's LDS-DMA interleaved with the MFMAs:
                            // off (measured -3..-12% on the compute-bound layers, -2.5% end to end;
                            // profiles/r1_kbench_b1024_interleaved_issue.json) -- the later issue
@@ -455,6 +678,9 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
 // LDS-DMA pieces per MFMA of the 128x128 tile; for wide, long-K layers).
 static int igemm_config(int M, int Nn, int K) {
   if (Nn <= 64) return 0;
+  if (g_igemm8 && Nn >= 256 && K >= 256 &&
+      (long)((M + 255) / 256) * ((Nn + 255) / 256) >= g_igemm8_min_tiles)
+    return 4;
   if (g_igemm_big == 4 && Nn > 128) return 3;   // forced (equivalence tests)
   if (g_igemm_big == 3 && Nn >= 256 && K >= 256 && (long)((M + 255) / 256) * ((Nn + 255) / 256) >= 256) return 3;
   const long big_tiles = (long)((M + 255) / 256) * ((Nn + 127) / 128);
@@ -462,7 +688,7 @@ static int igemm_config(int M, int Nn, int K) {
   return 1;
 }
 static int igemm_bm(int cfg) { return cfg == 1 ? 128 : 256; }
-static int igemm_wtm(int cfg) { return cfg == 3 ? 128 : 64; }
+static int igemm_wtm(int cfg) { return cfg == 3 ? 128 : 64; }   // (cfg 4: 64-row partial-row groups)
 
 int igemm_partial_rows(int M, int Nn, int K) {
   const int cfg = igemm_config(M, Nn, K);
@@ -494,7 +720,7 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
     else IG_GO(BM_, BN_, NW_, NS_, AM_DUAL);                         \
   }
   const int cfg = igemm_config(p.M, p.Nn, p.K);
-  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : (cfg == 3 ? 256 : 128);
+  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : (cfg >= 3 ? 256 : 128);
   const int nwg = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
   // PF where the prefetched operand exists for every element (forward residual; dgrad
   // residual-gradient without the stride-2 scatter).  Measured (bench/epilogue.py, b1024,
@@ -503,7 +729,17 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   // VGPRs cut from 3 to 2 waves per SIMD -- so dgrad uses it only on 2-stage tiles.
   const bool pf = g_igemm_pf && am == AM_DIRECT && cfg <= 1 &&
                   ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && ns == 2));
-  if (pf) {
+  if (cfg == 4) {
+#define IG_8(AM_)                                                                                         \
+  {                                                                                                       \
+    if (g_igemm8 == 2) hipLaunchKernelGGL((igemm8_kernel<AM_, true>), dim3(nwg), dim3(512), 0, stream, p); \
+    else hipLaunchKernelGGL((igemm8_kernel<AM_, false>), dim3(nwg), dim3(512), 0, stream, p);             \
+  }
+    if (am == AM_DIRECT) IG_8(AM_DIRECT)
+    else if (am == AM_HALO) IG_8(AM_HALO)
+    else IG_8(AM_DUAL)
+#undef IG_8
+  } else if (pf) {
 #define IG_PF(BM_, BN_, NS_) \
   hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_DIRECT, true>), dim3(nwg), dim3(256), 0, stream, p)
     if (cfg == 1) {

@@ -38,6 +38,7 @@ struct IgemmParams {
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
 int igemm_partial_rows(int M, int Nn, int K);        // rows of the partial column-sum buffer
+extern int g_igemm8, g_igemm8_min_tiles;
 extern int g_igemm_variant, g_igemm_deep, g_igemm_big, g_igemm_pf, g_igemm_il, g_wgrad_variant, g_pool_variant, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
 
 struct WgradParams {

@@ -55,7 +55,15 @@ def run(preset: str, argv: Optional[List[str]] = None, extra=None) -> int:
         # epoch assumption, Q9) -- printed by every worker, as there
         print("Steps per epoch: ", int((10000000 / strategy.num_replicas_in_sync) / strategy.world), flush=True)
     cbs = default_callbacks(cfg, strategy)
-    trainer.fit(cfg.epochs, cbs)
+    initial_epoch = 0
+    rs = getattr(strategy, "resume_state", None)
+    if rs:          # --resume of a periodic checkpoint: epochs, LR and callback state continue
+        initial_epoch = int(rs.get("epoch", 0))
+        trainer.set_lr(float(rs.get("lr", trainer.lr)))
+        trainer.resume_state = rs
+        if strategy.is_chief:
+            print(f"Resuming after epoch {initial_epoch} at lr {trainer.lr:.4g}", flush=True)
+    trainer.fit(cfg.epochs, cbs, initial_epoch=initial_epoch)
     if cfg.timeline and hasattr(strategy, "write_timeline"):
         strategy.write_timeline(cfg.timeline)
     if cfg.save:

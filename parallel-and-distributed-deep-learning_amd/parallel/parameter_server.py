@@ -134,7 +134,7 @@ class _Cluster:
         self.device = device
         self.is_ps = rank < num_ps
         self.impl = impl
-        self.store = dist.distributed_c10d._get_default_store()
+        self.store = _LockedStore(dist.distributed_c10d._get_default_store())
         if rank == 0:
             self.store.set("ps_job", f"{os.getpid():x}{int(time.time() * 1e3) & 0xffffff:06x}")
         self.job = self.store.get("ps_job").decode()
@@ -153,6 +153,62 @@ class _Cluster:
 
 def _hb_key(w):
     return f"hb/{w}"
+
+
+class _LockedStore:
+    """The c10d store shared by a role's main thread and its heartbeat thread."""
+
+    def __init__(self, store):
+        self._s = store
+        self._lock = threading.Lock()
+
+    def set(self, k, v):
+        with self._lock:
+            return self._s.set(k, v)
+
+    def get(self, k):
+        with self._lock:
+            return self._s.get(k)
+
+    def add(self, k, n):
+        with self._lock:
+            return self._s.add(k, n)
+
+    def check(self, keys):
+        with self._lock:
+            return self._s.check(keys)
+
+    def compare_set(self, k, expected, desired):
+        with self._lock:
+            return self._s.compare_set(k, expected, desired)
+
+
+class _Heartbeat:
+    """A worker's liveness beacon (the coordinator's worker-failure watch): a daemon thread
+    stamps `hb/<rank>` every period, so a worker that is waiting (an epoch barrier, worker 0's
+    validation, a drained ticket queue) is not mistaken for a dead one; a dead process stops
+    beating with its last thread."""
+
+    def __init__(self, store, rank: int, period: float):
+        self.store, self.rank, self.period = store, rank, period
+        self._stop = threading.Event()
+        self.beat()
+        self._th = threading.Thread(target=self._run, daemon=True)
+        self._th.start()
+
+    def beat(self):
+        self.store.set(_hb_key(self.rank), str(time.time()))
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            try:
+                self.beat()
+            except Exception:
+                return
+
+    def stop(self):
+        self._stop.set()
+        self._th.join(timeout=5)
 
 
 class PSServer:
@@ -343,12 +399,22 @@ class _PSControl:
         print(msg, flush=True)
 
 
-def _claim(store, spe: int, epoch: int) -> int:
-    """Claim the next step ticket of `epoch`; -1 when the epoch's steps are exhausted
-    (re-queued tickets of dead workers extend the budget)."""
-    t = store.add(f"claim/{epoch}", 1) - 1
-    budget = spe + store.add(f"requeue/{epoch}", 0)
-    return t if t < budget else -1
+def _claim(store, spe: int, epoch: int, rank: int) -> int:
+    """Claim the next step ticket of `epoch`; -1 while the epoch's tickets are exhausted
+    (re-queued tickets of dead workers extend the budget, so callers poll).  A claim is one
+    compare-and-set of "<next ticket>/<claimer>" -- a poll never consumes a ticket, and the
+    claimer id makes a lost race unambiguous."""
+    key = f"claim/{epoch}"
+    raw = store.compare_set(key, "", "0/-1").decode()       # creates the counter on first use
+    while True:
+        cur = int(raw.split("/")[0])
+        if cur >= spe + store.add(f"requeue/{epoch}", 0):
+            return -1
+        want = f"{cur + 1}/{rank}"
+        got = store.compare_set(key, raw, want).decode()
+        if got == want:
+            return cur
+        raw = got
 
 
 def _fault_step(rank_in_workers: int) -> Optional[int]:
@@ -422,6 +488,7 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     if cfg.max_steps:
         spe = min(spe, cfg.max_steps)
     fault_at = _fault_step(widx)
+    hb = _Heartbeat(store, rank, max(0.05, float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30")) / 6))
     it = pipe.iterate(device)
     from .strategies import Augment
     aug = Augment(cfg, device, cfg.seed + 7919 * widx)
@@ -448,11 +515,15 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         acc = torch.zeros(3, dtype=torch.float64)
         t_epoch = time.perf_counter()
         while True:
-            t = _claim(store, spe, epoch)
+            t = _claim(store, spe, epoch, rank)
             if t < 0:
-                break
+                # out of tickets: the epoch ends when every ticket is DONE; until then a ticket
+                # of a worker that died holding it may be re-queued by the coordinator
+                if store.add(f"done/{epoch}", 0) >= spe:
+                    break
+                time.sleep(0.02)
+                continue
             store.set(f"cur/{rank}", f"{epoch}:{t}")
-            store.set(_hb_key(rank), str(time.time()))
             if fault_at is not None and steps_done == fault_at:
                 print(f"[worker {widx}] injected failure at step {steps_done}", flush=True)
                 os._exit(17)
@@ -466,15 +537,13 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             store.set(f"cur/{rank}", f"{epoch}:-1")
             store.add(f"done/{epoch}", 1)
             steps_done += 1
-        store.set(_hb_key(rank), str(time.time()))
         # epoch end: worker 0 (coordinator-side logic) validates and runs the callbacks
         store.add(f"acc/{epoch}/loss", int(acc[0].item() * 1e6))
         store.add(f"acc/{epoch}/correct", int(acc[1].item()))
         store.add(f"acc/{epoch}/n", int(acc[2].item()))
         store.add(f"epoch_end/{epoch}", 1)
         if widx == 0:
-            alive = cl.num_workers - store.add("dead_workers", 0)
-            _wait_count(store, f"epoch_end/{epoch}", alive)
+            _wait_count(store, f"epoch_end/{epoch}", lambda: cl.num_workers - store.add("dead_workers", 0))
             dt = time.perf_counter() - t_epoch      # every worker's training steps, before validation
             n = max(1, store.add(f"acc/{epoch}/n", 0))
             logs = {"loss": store.add(f"acc/{epoch}/loss", 0) / 1e6 / n,
@@ -501,10 +570,10 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     if widx == 0 and cfg.save:
         # the reference saves the PS-held variables (imagenet-resnet50-ps.py:145-148): wait until
         # every live worker pushed its last step and stopped, then pull the final state
-        alive = cl.num_workers - store.add("dead_workers", 0)
-        _wait_count(store, "fin_count", alive - 1)
+        _wait_count(store, "fin_count", lambda: cl.num_workers - 1 - store.add("dead_workers", 0))
         worker._exchange(OP_PULL, lr)
     worker.stop()
+    hb.stop()
     if widx == 0 and cfg.save:
         from ..utils.checkpoint import save_keras_h5
         path = os.path.join(cfg.save_dir, cfg.checkpoint_name())
@@ -516,8 +585,10 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
 
 
 def _wait_count(store, key, n, timeout=600):
+    """Wait until counter `key` reaches n (an int, or a callable re-read every poll: the live
+    worker count drops when the coordinator declares a worker dead)."""
     t0 = time.time()
-    while store.add(key, 0) < n:
+    while store.add(key, 0) < (n() if callable(n) else n):
         if time.time() - t0 > timeout:
             raise TimeoutError(key)
         time.sleep(0.05)

@@ -128,10 +128,11 @@ class Strategy:
     def _load_initial_weights(self):
         w = self.cfg.weights
         if self.cfg.resume:
-            from ..utils.checkpoint import load_checkpoint
+            from ..utils.checkpoint import load_checkpoint, read_resume_state
             for eng, opt in self._replicas():
                 load_checkpoint(self.cfg.resume, eng, opt)
                 eng.after_update()
+            self.resume_state = read_resume_state(self.cfg.resume)
         elif w and w != "none":
             from ..utils.checkpoint import load_pretrained
             for eng, _ in self._replicas():
@@ -177,11 +178,11 @@ class Strategy:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
-    def save(self, trainer, path: str, include_optimizer: bool = True):
+    def save(self, trainer, path: str, include_optimizer: bool = True, progress: Optional[dict] = None):
         if not self.is_chief:
             return
         from ..utils.checkpoint import save_keras_h5
-        save_keras_h5(path, self.engine, self.opt if include_optimizer else None, self.cfg)
+        save_keras_h5(path, self.engine, self.opt if include_optimizer else None, self.cfg, progress=progress)
 
 
 class SingleStrategy(Strategy):

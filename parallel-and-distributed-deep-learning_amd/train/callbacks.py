@@ -35,6 +35,8 @@ class Callback:
     def on_batch_begin(self, batch, logs=None): ...
     def on_batch_end(self, batch, logs=None): ...
     def on_train_batches_end(self, epoch): ...   # after the epoch's last training step, before validation
+    def get_state(self): return None            # resumable state (--resume), JSON-serialisable
+    def set_state(self, state): ...
 
 
 class ReduceLROnPlateau(Callback):
@@ -50,6 +52,12 @@ class ReduceLROnPlateau(Callback):
 
     def on_train_begin(self, logs=None):
         self.best, self.wait, self.cooldown_counter = np.inf, 0, 0
+
+    def get_state(self):
+        return {"best": float(self.best), "wait": self.wait, "cooldown_counter": self.cooldown_counter}
+
+    def set_state(self, st):
+        self.best, self.wait, self.cooldown_counter = float(st["best"]), int(st["wait"]), int(st["cooldown_counter"])
 
     def on_epoch_end(self, epoch, logs=None):
         logs = logs or {}
@@ -85,6 +93,12 @@ class EarlyStopping(Callback):
 
     def on_train_begin(self, logs=None):
         self.best, self.wait, self.stopped_epoch = np.inf, 0, 0
+
+    def get_state(self):
+        return {"best": float(self.best), "wait": self.wait}
+
+    def set_state(self, st):
+        self.best, self.wait = float(st["best"]), int(st["wait"])
 
     def on_epoch_end(self, epoch, logs=None):
         cur = (logs or {}).get(self.monitor)
@@ -212,4 +226,4 @@ class ModelCheckpoint(Callback):
 
     def on_epoch_end(self, epoch, logs=None):
         if self.every and (epoch + 1) % self.every == 0:
-            self.trainer.save(self.path_fmt.format(epoch=epoch + 1), include_optimizer=True)
+            self.trainer.save(self.path_fmt.format(epoch=epoch + 1), include_optimizer=True, epoch=epoch + 1)

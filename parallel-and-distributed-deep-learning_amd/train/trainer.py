@@ -58,8 +58,16 @@ class Trainer:
         if self.strategy.is_chief:
             print(msg, flush=True)
 
-    def save(self, path: str, include_optimizer: bool = True):
-        self.strategy.save(self, path, include_optimizer=include_optimizer)
+    def progress(self, epochs_done: int) -> dict:
+        """What --resume needs beyond weights and optimizer slots: completed epochs, the
+        current LR (ReduceLROnPlateau / warmup may have moved it) and callback state."""
+        cbs = {type(cb).__name__: cb.get_state() for cb in getattr(self, "callbacks", [])
+               if cb.get_state() is not None}
+        return {"epoch": int(epochs_done), "lr": float(self.lr), "callbacks": cbs}
+
+    def save(self, path: str, include_optimizer: bool = True, epoch: Optional[int] = None):
+        prog = self.progress(epoch) if epoch is not None else None
+        self.strategy.save(self, path, include_optimizer=include_optimizer, progress=prog)
 
     # -- the loop
     def fit(self, epochs: int, callbacks: Optional[List[Callback]] = None, validation: bool = True,
@@ -68,6 +76,7 @@ class Trainer:
         cfg = self.cfg
         st = self.strategy
         cbs = list(callbacks or [])
+        self.callbacks = cbs
         for cb in cbs:
             cb.set_trainer(self)
         hist = History()
@@ -84,6 +93,12 @@ class Trainer:
                 vsteps = min(vsteps, cfg.max_steps)
         for cb in cbs:
             cb.on_train_begin()
+        rs = getattr(self, "resume_state", None)
+        if rs:                                    # --resume: continue the callbacks' bookkeeping
+            for cb in cbs:
+                cst = rs.get("callbacks", {}).get(type(cb).__name__)
+                if cst is not None:
+                    cb.set_state(cst)
         it = train_pipe.iterate(st.device, epoch=initial_epoch) if train_pipe.repeat else None
         for epoch in range(initial_epoch, epochs):
             if self.stop_training:

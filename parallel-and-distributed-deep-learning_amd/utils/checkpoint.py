@@ -172,7 +172,10 @@ def _from_keras(e, arr: np.ndarray) -> torch.Tensor:
     return a.contiguous().view(-1)
 
 
-def save_keras_h5(path: str, engine, optimizer=None, cfg=None) -> None:
+def save_keras_h5(path: str, engine, optimizer=None, cfg=None, progress: Optional[dict] = None) -> None:
+    """Keras HDF5 full-model layout.  `progress` (additive, for --resume): completed epochs,
+    current learning rate and LR/stop callback state, stored as the root attr `pddl_resume`
+    (JSON; Keras ignores unknown root attributes)."""
     L: ParamLayout = engine.L
     params = engine.params.detach().cpu()
     inner = keras_resnet50_layers(L)
@@ -214,6 +217,8 @@ def save_keras_h5(path: str, engine, optimizer=None, cfg=None) -> None:
         attrs.append(("", "training_config", json.dumps({
             "loss": "sparse_categorical_crossentropy", "metrics": [["accuracy"]], "weighted_metrics": None,
             "loss_weights": None, "optimizer_config": {"class_name": oname, "config": ocfg}})))
+    if progress is not None:
+        attrs.append(("", "pddl_resume", json.dumps(progress)))
     tmp = path + ".tmp"
     h5().write(tmp, datasets, attrs)
     os.replace(tmp, path)   # atomic: a crashed writer never leaves a torn checkpoint
@@ -295,3 +300,11 @@ def load_checkpoint(path: str, engine, optimizer=None) -> int:
         for k, v in st.items():
             v.copy_(host[k].to(v.device))
     return n
+
+
+def read_resume_state(path: str) -> Optional[dict]:
+    """The `progress` a periodic checkpoint was saved with (None for a plain Keras file)."""
+    raw = h5().read_attr(path, "", "pddl_resume")
+    if not raw:
+        return None
+    return json.loads(raw if isinstance(raw, str) else raw[0])

@@ -132,13 +132,15 @@ def test_igemm_dgrad(case):
     assert rel(cs, ref.sum((0, 1, 2))) < 1e-2
 
 
-@pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1)])
+@pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1), ("igemm8", 1),
+                                      ("igemm8", 2)])
 @pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual"])
 def test_igemm_big_tile_matches(kind, knob, big):
     """The 8-wave 256x128 3-stage (igemm_big 2) and 256x256 2-stage (igemm_big 4)
-    configurations, and the interleaved-issue 2-stage pipeline (igemm_il 1), compute the same
-    result (same k order) as the 4-wave 128x128 one, including the fused epilogues and the
-    per-wave column-sum rows."""
+    configurations, the interleaved-issue 2-stage pipeline (igemm_il 1) and the 8-phase
+    256x256 kernel (igemm8 1, with the wave-row stagger 2) compute the same result (same k
+    order) as the 4-wave 128x128 one, including the fused epilogues and the per-wave
+    column-sum rows."""
     torch.manual_seed(12)
     n, h, ho = 3, 14, 7
     if kind == "fwd3x3":
@@ -154,6 +156,7 @@ def test_igemm_big_tile_matches(kind, knob, big):
         wt = rnd(256, 640, scale=0.05)
         mask = rnd(n, h, h, 256)
     outs = []
+    N().set_variant("igemm8_min_tiles", 1)       # (tiny problems: let the 8-phase kernel take them)
     for kv in (0, big):
         N().set_variant(knob, kv)
         try:
@@ -178,7 +181,41 @@ def test_igemm_big_tile_matches(kind, knob, big):
                 outs.append(torch.cat([out.float().flatten(), _fold(part, rows, 256)]))
         finally:
             N().set_variant(knob, 0)
+    N().set_variant("igemm8_min_tiles", 128)
     assert rel(outs[1], outs[0]) < 1e-5
+
+
+@pytest.mark.parametrize("stagger", [1, 2])
+@pytest.mark.parametrize("case", [
+    # N, H, C, Cout, R, stride, pad   (conv4 / conv5 3x3, a strided 1x1 with tile overhang, long-K 1x1)
+    (4, 14, 256, 256, 3, 1, 1),
+    (5, 7, 512, 512, 3, 1, 1),
+    (3, 15, 512, 1280, 1, 2, 0),
+    (2, 9, 2048, 384, 1, 1, 0),
+])
+def test_igemm8_forward_vs_fp32(case, stagger):
+    """8-phase kernel against the fp32 conv reference on ResNet-50 stage-4/5 shapes (K up to
+    4608 = 72 K-tiles through the counted-vmcnt pipeline; M and N tails)."""
+    torch.manual_seed(21)
+    n, h, c, co, r, st, pad = case
+    x = rnd(n, h, h, c)
+    w = rnd(co, r, r, c, scale=0.03)
+    ho = (h + 2 * pad - r) // st + 1
+    scale = torch.rand(co, device=dev) + 0.5
+    shift = torch.randn(co, device=dev)
+    res = rnd(n, ho, ho, co)
+    out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
+    N().set_variant("igemm8_min_tiles", 1)
+    N().set_variant("igemm8", stagger)
+    try:
+        for _ in range(3):       # repeated launches: a pipeline race would show up as a changing result
+            N().igemm(x, None, h, h, r, r, st, pad, ho, ho, w.view(co, -1), 0, scale, shift, res, None, None, out, 1,
+                      None, 0, 0, 0, 0, 0, None, None)
+            ref = (conv_ref(x, w, st, pad) * scale + shift + res.float()).relu()
+            assert rel(out, ref) < 1e-2
+    finally:
+        N().set_variant("igemm8", 0)
+        N().set_variant("igemm8_min_tiles", 128)
 
 
 def test_igemm_dgrad_dual_source():

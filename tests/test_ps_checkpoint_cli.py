@@ -53,6 +53,37 @@ def test_ps_worker_failure_requeues_closure(impl, monkeypatch):
     assert ps[0][2] >= 6                                     # all 6 closures done despite the failure
 
 
+def test_ps_plateau_lowers_lr_and_early_stop_ends_job(monkeypatch):
+    """The coordinator runs ReduceLROnPlateau / EarlyStopping (imagenet-resnet50-ps.py:139-140)
+    on worker 0's val_loss and publishes the LR and the stop flag to every worker: a flat
+    val_loss (lr ~ 0) lowers the LR after `patience` epochs and stops the job early."""
+    from pddl.parallel.parameter_server import run_ps_job
+    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "600")
+    cfg = _cfg("ps", steps_per_epoch=2, validation_steps=1, batch_size=2, epochs=6, lr=1e-12, min_lr=1e-14,
+               reduce_lr_patience=1, early_stop_patience=3)
+    res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
+    wk = [r for r in res if r[0] == "worker"]
+    hist = [r for r in wk if r[3]][0][3]
+    assert len(hist) == 4                                    # EarlyStopping(patience=3) ended epoch 4 of 6
+    assert sum(r[2] for r in wk) == 4 * 2                    # no worker ran past the stop
+    lrs = [h["lr"] for h in hist]
+    assert lrs[0] == 1e-12 and lrs[1] < lrs[0] and lrs[-1] < lrs[1]
+
+
+def test_ps_final_checkpoint_holds_the_ps_state(tmp_path, monkeypatch):
+    """The saved file is the PS-resident state after every worker's last push (the reference
+    saves the PS variables, imagenet-resnet50-ps.py:145-148), not worker 0's last snapshot."""
+    from pddl.parallel.parameter_server import run_ps_job
+    from pddl.utils.checkpoint import read_keras_weights
+    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "600")
+    cfg = _cfg("ps", steps_per_epoch=4, batch_size=2, epochs=1, save=True, save_dir=str(tmp_path))
+    res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
+    ps = [r for r in res if r[0] == "ps"]
+    assert ps[0][2] == 4
+    w = read_keras_weights(str(tmp_path / cfg.checkpoint_name()))
+    assert "dense/kernel:0" in w and np.isfinite(w["dense/kernel:0"]).all()
+
+
 # ------------------------------------------------------------------ checkpoint
 def _engine():
     from pddl.models.reference import TorchEngine
@@ -144,3 +175,25 @@ def test_ps_script_cli(tmp_path):
     r = subprocess.run(args, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     assert "ImageNet-ResNet50_ImageNet_PS-reuse.h5" in os.listdir(tmp_path)
+
+
+def test_resume_continues_epochs_lr_and_callbacks(tmp_path):
+    """--resume of a periodic checkpoint restores weights + slots AND the progress (completed
+    epochs, current LR, ReduceLROnPlateau / EarlyStopping bookkeeping): the resumed run starts
+    at the next epoch with the LR the first run had reached."""
+    base = [sys.executable, os.path.join(ROOT, "imagenet-resnet50.py"), "--device", "cpu", "--max-steps", "1",
+            "--batch-size", "2", "--crop", "32", "--image-size", "32", "--save-dir", str(tmp_path),
+            "--validation-steps", "1", "--verbose", "2", "--checkpoint-every", "1", "--no-save"]
+    r = subprocess.run(base + ["--epochs", "2", "--lr", "0.0005"], capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    ck = tmp_path / "ckpt-002.h5"
+    from pddl.utils.checkpoint import read_resume_state
+    st = read_resume_state(str(ck))
+    assert st["epoch"] == 2 and st["lr"] == 0.0005
+    assert set(st["callbacks"]) >= {"ReduceLROnPlateau", "EarlyStopping"}
+    r = subprocess.run(base + ["--epochs", "3", "--resume", str(ck)], capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Resuming after epoch 2 at lr 0.0005" in r.stdout
+    assert "Epoch 3/3" in r.stdout and "Epoch 1/3" not in r.stdout and "lr: 0.0005" in r.stdout
