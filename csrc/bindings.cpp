@@ -395,6 +395,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });
   m.def("igemm_partial_rows", &pddl::igemm_partial_rows);
+  m.def("igemm_plan", [](int M, int Nn, int K) {
+    int cfg = 0, split = 0;
+    pddl::igemm_plan_query(M, Nn, K, &cfg, &split);
+    return std::make_pair(cfg, split);
+  });
   m.def("maxpool_bwd_partial_rows", &pddl::maxpool_bwd_partial_rows);
   m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);
   m.def("prep", &prep, REL);

@@ -39,6 +39,19 @@ namespace pddl {
 //   AM_DUAL:   two AM_DIRECT sources concatenated along K (projection-block dgrad).
 enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 
+// LDS bank swizzle of the [rows][128 B] operand tiles (the XOR involution is applied to the
+// DMA SOURCE chunk and to the ds_read_b128 address, cdna_hip_programming §5.4 rule 21).
+// ds_read_b128 serves 16 lanes (16 consecutive rows, same logical chunk) per 256-byte bank
+// row of two 128-byte LDS rows: slot = (row & 1) * 8 + (chunk ^ f(row)).  f(row) = (row >> 1) & 7
+// gives 8 distinct chunks to the 8 rows of each parity -> 16 distinct slots, conflict-free
+// (f(row) = row & 7 would put rows r and r + 8 on the same banks: 2-way conflicts).
+// sw_chunk: logical chunk carried by lane-linear position (lane & 7) of DMA piece `i` (pieces
+// are 8 rows, consecutive pieces of a wave alternate parity, so (row >> 1) & 7 =
+// 4 * (i & 1) + lane / 16).  sw_read: byte position of logical chunk kh * 4 + lane / 16 for
+// a lane reading row 16 * j + (lane & 15).
+__device__ __forceinline__ int sw_chunk(int lane, int i) { return (lane & 7) ^ ((4 * (i & 1) + (lane >> 4)) & 7); }
+__device__ __forceinline__ int sw_read(int lane, int kh) { return (((kh * 4) + (lane >> 4)) ^ ((lane >> 1) & 7)) * 16; }
+
 // Epilogue of one wave sub-tile of TM x TN 16x16 fragments at global rows [mb, mb + 16*TM)
 // and columns [nb, nb + 16*TN): fragments -> LDS (fp32, per-wave `stage` of 32 x (16*TN + 4))
 // -> 16-byte row stores with the fused FWD / F32 / DGRAD operations; the column sums (dgrad)
@@ -263,10 +276,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: M0 from SGPRs
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int mt = (p.M + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
+  const int mt = (p.M - p.m_begin + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, mt * nt);
   const int tn = wg % nt, tm = wg / nt;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = p.m_begin + tm * BM, n0 = tn * BN;
   const int HoWo = p.Ho * p.Wo;
 
   // Buffer descriptors (wave-uniform kernel arguments only, so no waterfall loops).
@@ -278,7 +291,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
 
   // Per-lane constant source chunk: LDS position (lane & 7) of row (lane >> 3) holds the
   // logical 16-byte chunk (lane & 7) ^ (row & 7).
-  const int chunk_sw = (lane & 7) ^ ((lane >> 3) & 7);
+  // LDS-DMA piece i of a wave holds rows 8*(piece) + lane/8 (piece parity = i & 1); its lane-linear
+  // 16-byte chunk (lane & 7) carries logical chunk (lane & 7) ^ ((row >> 1) & 7) (sw_chunk).
 
   // A-row bookkeeping (fixed over the k loop): byte offset of the row's tap (0, 0) in each
   // source (OOB_OFF for rows past M) and, for AM_HALO, the bitmask of its in-bounds taps.
@@ -292,8 +306,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
       const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
       const int hi = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
       const int pix = (n * p.H + hi) * p.W + wi;
-      a_o1[i] = (uint32_t)((pix * p.C1 + chunk_sw * 8) * 2);
-      if (AM == AM_DUAL) a_o2[i] = (uint32_t)((pix * p.C2 + chunk_sw * 8) * 2);
+      a_o1[i] = (uint32_t)((pix * p.C1 + sw_chunk(lane, i) * 8) * 2);
+      if (AM == AM_DUAL) a_o2[i] = (uint32_t)((pix * p.C2 + sw_chunk(lane, i) * 8) * 2);
       if (AM == AM_HALO) {
         uint32_t rows = 0, cols = 0, mk = 0;
         for (int r = 0; r < p.R; ++r) rows |= (uint32_t)((unsigned)(hi + r) < (unsigned)p.H) << r;
@@ -307,7 +321,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     const int n = n0 + (wave * BI + i) * 8 + (lane >> 3);
-    b_o[i] = (n < p.Nn) ? (uint32_t)((n * p.ldb + chunk_sw * 8) * 2) : OOB_OFF;
+    b_o[i] = (n < p.Nn) ? (uint32_t)((n * p.ldb + sw_chunk(lane, i) * 8) * 2) : OOB_OFF;
   }
 
   // k-tile walk state (scalar): the next tile to load is tap (r, s), channels [c0, c0 + 64)
@@ -393,7 +407,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
-      const int pos = (((kh * 4) + (lane >> 4)) ^ (lane & 7)) * 16;
+      const int pos = sw_read(lane, kh);
       v8bf af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const v8bf*>(As + a_off + i * 16 * 128 + pos);
@@ -428,7 +442,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmPa
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (WTN + 4));
-  igemm_epilogue<TM, TN, PF>(p, acc, m0 + wm * WTM, n0 + wn * WTN, tm * (BM / WTM) + wm, stage, lane);
+  igemm_epilogue<TM, TN, PF>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, stage, lane);
 }
 
 
@@ -460,17 +474,18 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int mt = (p.M + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
+  const int mt = (p.M - p.m_begin + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, mt * nt);
   const int tn = wg % nt, tm = wg / nt;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = p.m_begin + tm * BM, n0 = tn * BN;
   const int HoWo = p.Ho * p.Wo;
   const int pix_total = p.N * p.H * p.W;
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(p.a1, pix_total * p.C1 * 2);
   const __amdgpu_buffer_rsrc_t ra2 =
       make_rsrc(AM == AM_DUAL ? p.a2 : p.a1, pix_total * (AM == AM_DUAL ? p.C2 : p.C1) * 2);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
-  const int chunk_sw = (lane & 7) ^ ((lane >> 3) & 7);
+  // LDS-DMA piece i of a wave holds rows 8*(piece) + lane/8 (piece parity = i & 1); its lane-linear
+  // 16-byte chunk (lane & 7) carries logical chunk (lane & 7) ^ ((row >> 1) & 7) (sw_chunk).
 
   // Rows this lane stages: A/B half h, piece i (of the wave's 2) -> tile row 128h + (2*wave+i)*8 + lane/8.
   uint32_t a_o1[4], a_o2[4], a_taps[4], b_o[4];
@@ -484,8 +499,8 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
       const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
       const int hi_ = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
       const int pix = (n * p.H + hi_) * p.W + wi;
-      a_o1[hi] = (uint32_t)((pix * p.C1 + chunk_sw * 8) * 2);
-      if (AM == AM_DUAL) a_o2[hi] = (uint32_t)((pix * p.C2 + chunk_sw * 8) * 2);
+      a_o1[hi] = (uint32_t)((pix * p.C1 + sw_chunk(lane, hi) * 8) * 2);
+      if (AM == AM_DUAL) a_o2[hi] = (uint32_t)((pix * p.C2 + sw_chunk(lane, hi) * 8) * 2);
       if (AM == AM_HALO) {
         uint32_t rows = 0, cols = 0, mk = 0;
         for (int rr = 0; rr < p.R; ++rr) rows |= (uint32_t)((unsigned)(hi_ + rr) < (unsigned)p.H) << rr;
@@ -495,7 +510,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
       }
     }
     const int n = n0 + r;
-    b_o[hi] = (n < p.Nn) ? (uint32_t)((n * p.ldb + chunk_sw * 8) * 2) : OOB_OFF;
+    b_o[hi] = (n < p.Nn) ? (uint32_t)((n * p.ldb + sw_chunk(lane, hi) * 8) * 2) : OOB_OFF;
   }
 
   // scalar k-walk of the NEXT K-tile to stage (same walk as igemm_kernel)
@@ -577,7 +592,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
   const int b_row = (wn * 32 + (lane & 15)) * 128;
   int pos[2];
 #pragma unroll
-  for (int kh = 0; kh < 2; ++kh) pos[kh] = (((kh * 4) + (lane >> 4)) ^ (lane & 7)) * 16;
+  for (int kh = 0; kh < 2; ++kh) pos[kh] = sw_read(lane, kh);
 
   for (int t = 0; t < KT; ++t) {
     const char* buf = smem + (t & 1) * BUF;
@@ -630,10 +645,11 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
   __syncthreads();   // every wave is done with the LDS tiles before the epilogue stages through them
 
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (32 + 4));
-  igemm_epilogue<4, 2, false>(p, acc[0][0], m0 + wm * 64, n0 + wn * 32, tm * 4 + wm, stage, lane);
-  igemm_epilogue<4, 2, false>(p, acc[0][1], m0 + wm * 64, n0 + 128 + wn * 32, tm * 4 + wm, stage, lane);
-  igemm_epilogue<4, 2, false>(p, acc[1][0], m0 + 128 + wm * 64, n0 + wn * 32, tm * 4 + 2 + wm, stage, lane);
-  igemm_epilogue<4, 2, false>(p, acc[1][1], m0 + 128 + wm * 64, n0 + 128 + wn * 32, tm * 4 + 2 + wm, stage, lane);
+  const int pr = p.prow_begin + tm * 4;
+  igemm_epilogue<4, 2, false>(p, acc[0][0], m0 + wm * 64, n0 + wn * 32, pr + wm, stage, lane);
+  igemm_epilogue<4, 2, false>(p, acc[0][1], m0 + wm * 64, n0 + 128 + wn * 32, pr + wm, stage, lane);
+  igemm_epilogue<4, 2, false>(p, acc[1][0], m0 + 128 + wm * 64, n0 + wn * 32, pr + 2 + wm, stage, lane);
+  igemm_epilogue<4, 2, false>(p, acc[1][1], m0 + 128 + wm * 64, n0 + 128 + wn * 32, pr + 2 + wm, stage, lane);
 }
 
 int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wave tiles)
@@ -642,8 +658,9 @@ int g_igemm_big = 0;       // 8-wave 256x128 3-stage tile: 0 never (default: mea
                            // 256x256 8-wave tile: 3 heuristic (Nn, K >= 256), 4 always (Nn > 128)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
 int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 layers with a residual / add
-int g_igemm8 = 0;          // 8-phase 256x256 kernel (igemm8_kernel) for Nn >= 256, K >= 256: 0 off,
-                           // 1 on, 2 on with the wave-row stagger
+int g_igemm8 = 2;          // 8-phase 256x256 kernel (igemm8_kernel) for Nn >= 256, K >= 256, Nn < 4K:
+                           // 0 off, 1 on, 2 on with the wave-row stagger (default: b1024 end to end
+                           // 18.82k -> 19.00k img/s; stagger beats 1 on every layer, kbench)
 int g_igemm8_min_tiles = 128;   // ... when the problem has at least this many 256x256 tiles
 int g_igemm_il = 0;        // 2-stage tiles issue the next tile's LDS-DMA interleaved with the MFMAs:
                            // off (measured -3..-12% on the compute-bound layers, -2.5% end to end;
@@ -678,7 +695,11 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
 // LDS-DMA pieces per MFMA of the 128x128 tile; for wide, long-K layers).
 static int igemm_config(int M, int Nn, int K) {
   if (Nn <= 64) return 0;
-  if (g_igemm8 && Nn >= 256 && K >= 256 &&
+  // 8-phase 256x256 for wide, long-K GEMMs -- not the expansion 1x1s (Nn >= 4K: conv3 forward,
+  // conv1 dgrad), whose short K loop is dominated by an epilogue that streams a residual /
+  // residual gradient: measured 30-40% slower there than the 2-block 128x128 tile with the
+  // epilogue-operand prefetch (per-layer A/B, profiles/r2_igemm8_per_layer_ab.txt)
+  if (g_igemm8 && Nn >= 256 && K >= 256 && Nn < 4 * K &&
       (long)((M + 255) / 256) * ((Nn + 255) / 256) >= g_igemm8_min_tiles)
     return 4;
   if (g_igemm_big == 4 && Nn > 128) return 3;   // forced (equivalence tests)
@@ -690,11 +711,56 @@ static int igemm_config(int M, int Nn, int K) {
 static int igemm_bm(int cfg) { return cfg == 1 ? 128 : 256; }
 static int igemm_wtm(int cfg) { return cfg == 3 ? 128 : 64; }   // (cfg 4: 64-row partial-row groups)
 
-int igemm_partial_rows(int M, int Nn, int K) {
-  const int cfg = igemm_config(M, Nn, K);
+static int igemm_rows_of(int cfg, int m) {
   const int BM = igemm_bm(cfg);
-  return ((M + BM - 1) / BM) * (BM / igemm_wtm(cfg));
+  return ((m + BM - 1) / BM) * (BM / igemm_wtm(cfg));
 }
+
+static int num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// Launch plan: rows [0, split) with `cfg`, rows [split, M) with the 128x128 tile.  The 8-phase
+// kernel runs one 256x256 block per CU, so its tiles come in rounds of #CUs; a last round
+// that fills at most half of the chip is handed to the 4x finer 128x128 tile (2 blocks per
+// CU) instead of leaving CUs idle for a whole 256x256 tile time (b1024 stage 4: 784 tiles on
+// 256 CUs = 3 full rounds + 16 tiles).
+struct IgemmPlan { int cfg, split; };
+static IgemmPlan igemm_plan(int M, int Nn, int K) {
+  IgemmPlan pl{igemm_config(M, Nn, K), M};
+  if (pl.cfg != 4) return pl;
+  const int nt = (Nn + 255) / 256, mt = (M + 255) / 256;
+  const long T = (long)mt * nt, C = num_cus();
+  const long F = T / C, r = T % C;
+  // the tail's 4r 128x128 tiles fit one round (2 per CU) when 2r <= C: it then costs about one
+  // 128x128 tile time instead of a whole 256x256 round; a bigger tail runs as a full round
+  if (r == 0 || 2 * r > C) return pl;
+  if (F == 0) { pl.cfg = 1; return pl; }
+  const long full_m_tiles = (F * C) / nt;
+  pl.split = (int)lmin((long)M, full_m_tiles * 256);
+  return pl;
+}
+
+void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split) {
+  const IgemmPlan pl = igemm_plan(M, Nn, K);
+  *cfg = pl.cfg;
+  *split = pl.split;
+}
+
+int igemm_partial_rows(int M, int Nn, int K) {
+  const IgemmPlan pl = igemm_plan(M, Nn, K);
+  return igemm_rows_of(pl.cfg, pl.split) + (pl.split < M ? igemm_rows_of(1, M - pl.split) : 0);
+}
+
+static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream);
 
 const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   const char* why = nullptr;
@@ -702,6 +768,24 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   IgemmParams p = p_in;
   p.mg_howo = fdiv_magic(p.Ho * p.Wo);
   p.mg_wo = fdiv_magic(p.Wo);
+  p.m_begin = 0;
+  p.prow_begin = 0;
+  const IgemmPlan pl = igemm_plan(p.M, p.Nn, p.K);
+  if (pl.split < p.M) {
+    IgemmParams head = p, tail = p;
+    head.M = pl.split;
+    tail.m_begin = pl.split;
+    tail.prow_begin = igemm_rows_of(pl.cfg, pl.split);
+    igemm_launch_cfg(head, pl.cfg, stream);
+    igemm_launch_cfg(tail, 1, stream);
+  } else {
+    igemm_launch_cfg(p, pl.cfg, stream);
+  }
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) {
   // Pipeline depth by K: short K (<= 2 k-tiles) is memory-bound -> single LDS stage for
   // twice the resident blocks (variant knob for A/B timing: 0 = heuristic, 1/2 = forced).
   const int KT = p.K / 64;
@@ -719,9 +803,8 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
     else if (am == AM_HALO) IG_GO(BM_, BN_, NW_, NS_, AM_HALO);      \
     else IG_GO(BM_, BN_, NW_, NS_, AM_DUAL);                         \
   }
-  const int cfg = igemm_config(p.M, p.Nn, p.K);
   const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : (cfg >= 3 ? 256 : 128);
-  const int nwg = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
+  const int nwg = ((p.M - p.m_begin + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
   // PF where the prefetched operand exists for every element (forward residual; dgrad
   // residual-gradient without the stride-2 scatter).  Measured (bench/epilogue.py, b1024,
   // profiles/r1_epilogue_prefetch_ab.json): forward +3-20% on every stage; dgrad +10-14% for
@@ -764,8 +847,6 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   }
 #undef IG_MODES
 #undef IG_GO
-  hipError_t e = hipGetLastError();
-  return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
 }  // namespace pddl

@@ -35,9 +35,12 @@ struct IgemmParams {
   float* stats;                                     // FWD: per-wave partial [rows][2*Nn]: sum | sum of squares
                                                     //      of the stored outputs (train-mode BN batch statistics)
   uint64_t mg_howo, mg_wo;                          // set by igemm_launch: magic divisors (fdiv)
+  int m_begin, prow_begin;                          // set by igemm_launch: this launch covers GEMM rows
+                                                    // [m_begin, M); its partial rows start at prow_begin
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
 int igemm_partial_rows(int M, int Nn, int K);        // rows of the partial column-sum buffer
+void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split);   // tile config; rows >= split: 128x128 tail
 extern int g_igemm8, g_igemm8_min_tiles;
 extern int g_igemm_variant, g_igemm_deep, g_igemm_big, g_igemm_pf, g_igemm_il, g_wgrad_variant, g_pool_variant, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
 

@@ -1,6 +1,6 @@
 """Per-layer breakdown of one training step from a rocprofv3 kernel trace.
 
-    python scripts/analyze_trace.py gpurun_out/prof/run_kernel_trace.csv [batch] [crop]
+    python scripts/analyze_trace.py gpurun_out/prof/run_kernel_trace.csv [batch] [crop] [knobs]
 
 Pairs the last complete step's dispatches with the engine's fixed launch schedule and
 prints time, TFLOP/s and effective GB/s per launch.
@@ -19,7 +19,7 @@ def schedule(B, crop):
     H2 = (H1 + 2 - 3) // 2 + 1
     ev = []
     ev.append(("stem_s2d", "stem", 0, B * H1 * H1 * 4 * 32))
-    ev.append(("igemm", "conv1 fwd", 2 * B * H1 * H1 * 256 * 64, B * H1 * H1 * 64 * 2))
+    ev.append(("igemm", "conv1 fwd", 2 * B * H1 * H1 * 256 * 64, B * H1 * H1 * 64 * 2, (B * H1 * H1, 64, 256)))
     ev.append(("maxpool_fwd", "pool", 0, B * (H1 * H1 + H2 * H2) * 64 * 2))
     H = H2
     geo = []
@@ -28,25 +28,26 @@ def schedule(B, crop):
         Ho = (H - 1) // b.stride + 1
         M = B * Ho * Ho
         n1 = 5 * f if b.proj else f
-        ev.append(("igemm", f"{b.name} c1{'+c0' if b.proj else ''} fwd", 2 * M * cin * n1, (B * H * H * cin + M * n1) * 2))
-        ev.append(("igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2))
-        ev.append(("igemm", f"{b.name} c3 fwd", 2 * M * f * 4 * f, (M * f + 2 * M * 4 * f) * 2))
+        ev.append(("igemm", f"{b.name} c1{'+c0' if b.proj else ''} fwd", 2 * M * cin * n1, (B * H * H * cin + M * n1) * 2,
+                   (M, n1, cin)))
+        ev.append(("igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2, (M, f, 9 * f)))
+        ev.append(("igemm", f"{b.name} c3 fwd", 2 * M * f * 4 * f, (M * f + 2 * M * 4 * f) * 2, (M, 4 * f, f)))
         geo.append((b, H, Ho))
         H = Ho
     ev.append(("gap_fwd", "gap", 0, B * H * H * 2048 * 2))
-    ev.append(("igemm", "dense fwd", 2 * B * 2048 * 1000, 0))
+    ev.append(("igemm", "dense fwd", 2 * B * 2048 * 1000, 0, (B, 1000, 2048)))
     ev.append(("softmax", "xent", 0, 0))
     ev.append(("wgrad", "dense wgrad", 2 * B * 2048 * 1000, 0))
     ev.append(("colsum", "dense", 0, 0))
-    ev.append(("igemm", "dense dgrad", 2 * B * 2048 * 1000, 0))
+    ev.append(("igemm", "dense dgrad", 2 * B * 2048 * 1000, 0, (B, 2048, 1024)))
     ev.append(("gap_bwd", "gap", 0, 0))
     for b, H, Ho in reversed(geo):
         f, cin = b.filters, b.cin
         M = B * Ho * Ho
         ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * M * f * 4 * f, (M * f + M * 4 * f) * 2))
-        ev.append(("igemm", f"{b.name} c3 dgrad", 2 * M * f * 4 * f, (M * 4 * f + 2 * M * f) * 2))
+        ev.append(("igemm", f"{b.name} c3 dgrad", 2 * M * f * 4 * f, (M * 4 * f + 2 * M * f) * 2, (M, f, 4 * f)))
         ev.append(("wgrad", f"{b.name} c2 wgrad", 2 * M * 9 * f * f, 2 * M * f * 2))
-        ev.append(("igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2))
+        ev.append(("igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2, (M, f, 9 * f)))
         n1 = 5 * f if b.proj else f
         if b.proj:   # conv1 and the shortcut conv: one wgrad launch per gradient source
             ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * f, (M * f + B * H * H * cin) * 2))
@@ -54,7 +55,7 @@ def schedule(B, crop):
         else:
             ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * n1, (M * n1 + B * H * H * cin) * 2))
         ev.append(("wgrad_finalize", b.name, 0, 0))
-        ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2))
+        ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2, (M, cin, n1)))
     ev.append(("maxpool_bwd", "pool", 0, 0))
     ev.append(("wgrad", "conv1 wgrad", 2 * B * H1 * H1 * 256 * 64, 0))
     ev.append(("stem_wgrad_fold", "fold", 0, 0))
@@ -71,30 +72,46 @@ def main():
     path = sys.argv[1]
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     crop = int(sys.argv[3]) if len(sys.argv) > 3 else 224
+    knobs = sys.argv[4] if len(sys.argv) > 4 else ""   # the run's PDDL_KNOBS (changes the launch plan)
     rows = [r for r in csv.DictReader(open(path))]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
     ev = schedule(B, crop)
-    # find start of last complete step: last stem_im2col such that len(ev) rows follow
+    # a split launch (8-phase kernel for full rounds + 128x128 tail) is two dispatches of one layer
+    try:
+        from pddl.ops.native import require_native
+        for knob in filter(None, knobs.split(",")):
+            k, v = knob.split("=")
+            require_native().set_variant(k, int(v))
+        plan = require_native().igemm_plan
+    except Exception:   # no native module: unsplit schedule
+        plan = None
+    nd = [2 if (e[0] == "igemm" and plan is not None and plan(*e[4])[1] < e[4][0]) else 1 for e in ev]
+    need = sum(nd)
     starts = [i for i, r in enumerate(rows) if "stem_s2d" in r["Kernel_Name"]]
     st = None
     for s in reversed(starts):
-        if s + len(ev) <= len(rows):
+        if s + need <= len(rows):
             st = s
             break
-    seg = rows[st:st + len(ev)]
+    seg = rows[st:st + need]
     tot = 0
     agg = {}
-    for (kind, name, flops, byts), r in zip(ev, seg):
-        kn = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pddl::", "")
+    k = 0
+    for e, n in zip(ev, nd):
+        kind, name, flops, byts = e[:4]
+        rs = seg[k:k + n]
+        k += n
+        kn = " + ".join(r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pddl::", "")[:22] for r in rs)
         assert kind.split("_")[0] in kn, (kind, kn)
-        t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+        t = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rs)
         tot += t
         k2 = kind + (" fwd" if "fwd" in name and kind == "igemm" else " dgrad" if "dgrad" in name else "")
         agg[k2] = agg.get(k2, 0) + t
         tf = flops / t / 1e12 if flops else 0
         gb = byts / t / 1e9 if byts else 0
-        print(f"{t*1e6:9.1f} us  {tf:7.1f} TF/s  {gb:7.0f} GB/s  grid={r['Grid_Size_X']:>8}  {kn[:28]:28s} {name}")
+        grid = "+".join(r["Grid_Size_X"] for r in rs)
+        print(f"{t*1e6:9.1f} us  {tf:7.1f} TF/s  {gb:7.0f} GB/s  grid={grid:>16}  {kn[:40]:40s} {name}")
     print(f"step total {tot*1e3:.2f} ms")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1]):
         print(f"  {k:24s} {v*1e3:8.3f} ms")

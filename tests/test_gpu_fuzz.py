@@ -2,7 +2,8 @@
 hypothesis draws batch / spatial / channel / kernel / stride combinations (channels multiples
 of 64 as the kernels require, odd spatial sizes like the 244 / 160 crops produce) and every
 draw is compared with an fp32 PyTorch reference of the same op.  Includes the residual and
-residual-gradient epilogues, so both prefetch variants are exercised (knob igemm_pf)."""
+residual-gradient epilogues, so both prefetch variants are exercised (knob igemm_pf), and the
+8-phase 256x256 kernel is forced onto tiny problems (igemm8_min_tiles=1) on half the draws."""
 import pytest
 import torch
 
@@ -36,9 +37,14 @@ conv = st.tuples(
 )
 
 
+def _k8(on):
+    N().set_variant("igemm8", 2 if on else 0)
+    N().set_variant("igemm8_min_tiles", 1 if on else 128)
+
+
 @settings(max_examples=25, deadline=None, derandomize=True)
-@given(conv, st.booleans(), st.integers(0, 1))
-def test_igemm_forward_fuzz(case, with_res, pf):
+@given(conv, st.booleans(), st.integers(0, 1), st.booleans())
+def test_igemm_forward_fuzz(case, with_res, pf, k8):
     n, h, c, co, (r, s, pad) = case
     ho = (h + 2 * pad - r) // s + 1
     if ho < 1:
@@ -51,11 +57,14 @@ def test_igemm_forward_fuzz(case, with_res, pf):
     res = rnd(n, ho, ho, co) if with_res else None
     out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
     N().set_variant("igemm_pf", pf)
+    _k8(k8)
     try:
         N().igemm(x, None, h, h, r, r, s, pad, ho, ho, w.view(co, -1), 0, sc, sh, res, None, None, out, 1, None, 0,
                   0, 0, 0, 0, None, None)
     finally:
         N().set_variant("igemm_pf", 1)
+        _k8(True)
+        N().set_variant("igemm8_min_tiles", 128)
     ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s,
                                      padding=pad).permute(0, 2, 3, 1) * sc + sh
     if with_res:
@@ -65,8 +74,8 @@ def test_igemm_forward_fuzz(case, with_res, pf):
 
 
 @settings(max_examples=25, deadline=None, derandomize=True)
-@given(conv, st.integers(0, 1))
-def test_igemm_dgrad_and_wgrad_fuzz(case, pf):
+@given(conv, st.integers(0, 1), st.booleans())
+def test_igemm_dgrad_and_wgrad_fuzz(case, pf, k8):
     n, cin_h, cin, co, (r, s, pad) = case
     h = cin_h
     ho = (h + 2 * pad - r) // s + 1
@@ -80,11 +89,14 @@ def test_igemm_dgrad_and_wgrad_fuzz(case, pf):
     wt = w.float().flip(1).flip(2).permute(3, 1, 2, 0).contiguous().to(torch.bfloat16)   # [cin][R][S][co]
     out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
     N().set_variant("igemm_pf", pf)
+    _k8(k8)
     try:
         N().igemm(g, None, ho, ho, r, r, 1, r - 1 - pad, ho, ho, wt.view(cin, -1), 1, None, None, None, mask, add,
                   out, 0, None, 0, 0, 1 if s == 2 else 0, h, h, None, None)
     finally:
         N().set_variant("igemm_pf", 1)
+        _k8(True)
+        N().set_variant("igemm8_min_tiles", 128)
     ref = torch.nn.grad.conv2d_input((n, cin, h, h), w.float().permute(0, 3, 1, 2), g.float().permute(0, 3, 1, 2),
                                      stride=s, padding=pad)
     ref = (ref.permute(0, 2, 3, 1) + add.float()) * (mask.float() > 0)

@@ -157,6 +157,7 @@ def test_igemm_big_tile_matches(kind, knob, big):
         mask = rnd(n, h, h, 256)
     outs = []
     N().set_variant("igemm8_min_tiles", 1)       # (tiny problems: let the 8-phase kernel take them)
+    N().set_variant("igemm8", 0)                 # baseline: the 128x128 tile
     for kv in (0, big):
         N().set_variant(knob, kv)
         try:
@@ -182,7 +183,35 @@ def test_igemm_big_tile_matches(kind, knob, big):
         finally:
             N().set_variant(knob, 0)
     N().set_variant("igemm8_min_tiles", 128)
+    N().set_variant("igemm8", 2)
     assert rel(outs[1], outs[0]) < 1e-5
+
+
+@pytest.mark.parametrize("stagger", [1, 2])
+def test_igemm8_round_split_dgrad_colsum(stagger):
+    """A problem whose 256x256 tiles leave a partial last round (300 tiles on 256 CUs) runs the
+    full rounds on the 8-phase kernel and the M-tail on the 128x128 tile (two launches, one
+    partial-row table): output and fused column sums equal the single-kernel result."""
+    torch.manual_seed(23)
+    n, h, cin, co = 3, 160, 256, 256            # M = 76800 rows = 300 x 256
+    g = rnd(n, h, h, co)
+    wt = rnd(cin, co, scale=0.05)
+    add, mask = rnd(n, h, h, cin), rnd(n, h, h, cin)
+    outs = []
+    for kv in (0, stagger):
+        N().set_variant("igemm8", kv)
+        try:
+            out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
+            rows = N().igemm_partial_rows(n * h * h, cin, co)
+            part = torch.full((rows * cin,), float("nan"), device=dev)
+            N().igemm(g, None, h, h, 1, 1, 1, 0, h, h, wt, 1, None, None, None, mask, add, out, 0, None, 0, 0, 0, 0, 0,
+                      part, None)
+            outs.append((out.float(), _fold(part, rows, cin), rows))
+        finally:
+            N().set_variant("igemm8", 2)
+    (o0, c0, r0), (o1, c1, r1) = outs
+    assert r0 == r1 == 1200          # (both tilings keep 4 partial rows per 256 GEMM rows)
+    assert rel(o1, o0) < 1e-5 and rel(c1, c0) < 1e-4
 
 
 @pytest.mark.parametrize("stagger", [1, 2])
@@ -214,7 +243,7 @@ def test_igemm8_forward_vs_fp32(case, stagger):
             ref = (conv_ref(x, w, st, pad) * scale + shift + res.float()).relu()
             assert rel(out, ref) < 1e-2
     finally:
-        N().set_variant("igemm8", 0)
+        N().set_variant("igemm8", 2)
         N().set_variant("igemm8_min_tiles", 128)
 
 
