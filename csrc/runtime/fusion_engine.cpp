@@ -20,12 +20,21 @@
 //     issued but not completed within it (a peer that stopped producing gradients or never
 //     joined the collective), and the next `finish()` / `begin_step()` raises with a diagnostic
 //     (on a host-blocking backend `finish()` bounds its wait by the same timeout).
-//   * Timeline: chrome-trace JSON (QUEUED -> ALLREDUCE phases per bucket), like HOROVOD_TIMELINE.
+//   * Timeline: chrome-trace JSON like HOROVOD_TIMELINE.  On the GPU every phase is stamped
+//     with HIP events, not host clocks: READY (the compute stream finished the bucket's
+//     kernels), ALLREDUCE (the side stream passed its wait for READY and issued the RCCL
+//     kernel -> the collective finished, as the side stream observes it), placed on the host
+//     time axis through a reference event recorded at begin_step.  Host QUEUED spans (bucket
+//     handed over -> collective enqueued) are kept beside them.
+//   * Wire dtype: "bf16" casts each bucket to bf16 on the side stream (a HIP kernel), reduces
+//     the half-size message (48.8 MiB instead of 97.6 MiB per step for ResNet-50) and casts
+//     the sum back before the optimizer reads it (Horovod's fp16 compression analogue).
 // The transport is the c10d ProcessGroup passed from Python: RCCL ("nccl") on GPU, gloo on CPU
 // (so the engine itself is exercised by the CPU multi-process tests).
 #include <torch/extension.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
+#include "kernels/kernels.h"
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/HIPEvent.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -53,18 +62,40 @@ double now_us() {
 struct TimelineEvent {
   int bucket;
   int64_t bytes;
-  double t_ready, t_issue, t_done;
+  double t_ready, t_issue, t_done;          // host clock (us)
+  double g_ready = -1, g_start = -1, g_end = -1;   // GPU event times on the host axis (us), -1: none
   int step;
+};
+
+// A timing-enabled HIP event (at::cuda::CUDAEvent defaults to timing disabled).
+struct TimedEvent {
+  hipEvent_t ev = nullptr;
+  TimedEvent() { TORCH_CHECK(hipEventCreate(&ev) == hipSuccess, "pddl fusion: hipEventCreate"); }
+  ~TimedEvent() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
+  TimedEvent(const TimedEvent&) = delete;
+  TimedEvent& operator=(const TimedEvent&) = delete;
+  void record(hipStream_t s) { TORCH_CHECK(hipEventRecord(ev, s) == hipSuccess, "pddl fusion: hipEventRecord"); }
+  // ms from `ref` to this event (both must have completed)
+  double since(const TimedEvent& ref) const {
+    float ms = 0.f;
+    (void)hipEventSynchronize(ev);
+    return hipEventElapsedTime(&ms, ref.ev, ev) == hipSuccess ? (double)ms : -1.0;
+  }
 };
 
 class FusionEngine {
  public:
   FusionEngine(py::object pg_obj, Tensor flat, std::vector<std::pair<int64_t, int64_t>> buckets, double stall_s,
-               bool average, int rank)
+               bool average, int rank, const std::string& wire)
       : flat_(flat), buckets_(std::move(buckets)), stall_s_(stall_s), average_(average), rank_(rank) {
     pg_ = py::cast<c10::intrusive_ptr<c10d::ProcessGroup>>(pg_obj);
     world_ = pg_->getSize();
     gpu_ = flat_.is_cuda();
+    TORCH_CHECK(wire == "fp32" || wire == "bf16", "pddl fusion: wire dtype fp32 or bf16");
+    TORCH_CHECK(flat_.scalar_type() == torch::kFloat32 && flat_.is_contiguous(), "pddl fusion: fp32 flat gradients");
+    if (wire == "bf16") lowp_ = torch::empty({flat_.numel()}, flat_.options().dtype(torch::kBFloat16));
     if (gpu_) side_ = c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, flat_.device().index());
     verify_signature();
     worker_ = std::thread([this] { run(); });
@@ -89,6 +120,11 @@ class FusionEngine {
     TORCH_CHECK(pending_.empty() && inflight_.empty(), "pddl fusion: begin_step with outstanding buckets");
     next_expected_ = 0;
     ++step_;
+    if (gpu_ && timeline_on_) {   // the step's GPU time origin, pinned to the host clock
+      step_ref_ = std::make_shared<TimedEvent>();
+      step_ref_host_ = now_us();
+      step_ref_->record(compute_stream());
+    }
   }
 
   void bucket_ready(int i) {
@@ -99,6 +135,12 @@ class FusionEngine {
     if (gpu_) {
       it.event = std::make_shared<at::cuda::CUDAEvent>();
       it.event->record(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()));
+      if (timeline_on_ && step_ref_) {
+        it.ref = step_ref_;
+        it.ref_host = step_ref_host_;
+        it.g_ready = std::make_shared<TimedEvent>();
+        it.g_ready->record(compute_stream());
+      }
     }
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -122,7 +164,10 @@ class FusionEngine {
       done.swap(inflight_);
     }
     for (auto& it : done) {
-      if (gpu_ || stall_s_ <= 0) {
+      if (gpu_ && it.done) {
+        // bf16 wire: the side stream cast the sum back after the collective; wait for that
+        it.done->block(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()));
+      } else if (gpu_ || stall_s_ <= 0) {
         it.work->wait();   // GPU: a stream-ordered wait, the host does not block here
       } else {             // host-blocking backend: poll, so the watchdog's stall verdict can end the wait
         while (!it.work->isCompleted()) {
@@ -135,48 +180,91 @@ class FusionEngine {
         it.work->wait();   // completed: returns at once (and rethrows a collective error)
       }
       it.t_done = now_us();
+      if (!gpu_ && lowp_.defined()) {   // host backend, bf16 wire: widen the reduced bucket
+        auto sl = flat_.narrow(0, buckets_[it.bucket].first, buckets_[it.bucket].second);
+        sl.copy_(lowp_.narrow(0, buckets_[it.bucket].first, buckets_[it.bucket].second));
+      }
       if (average_ && world_ > 1) {
         auto sl = flat_.narrow(0, buckets_[it.bucket].first, buckets_[it.bucket].second);
         sl.div_(world_);
       }
       if (timeline_on_) {
         std::lock_guard<std::mutex> lk(tl_mu_);
-        timeline_.push_back({it.bucket, buckets_[it.bucket].second * (int64_t)flat_.element_size(), it.t_ready,
-                             it.t_issue, it.t_done, step_});
+        TimelineEvent e{it.bucket, buckets_[it.bucket].second * (lowp_.defined() ? 2 : 4), it.t_ready, it.t_issue,
+                        it.t_done};
+        e.step = step_;
+        timeline_.push_back(e);
+        if (it.ref) tl_gpu_.push_back({timeline_.size() - 1, it.ref, it.ref_host, it.g_ready, it.g_start, it.g_end});
       }
     }
   }
 
   void set_timeline(bool on) { timeline_on_ = on; }
+  // Chrome-trace JSON.  GPU: READY (instant) and ALLREDUCE (span) from HIP events; host:
+  // QUEUED spans.  CPU backends: QUEUED and ALLREDUCE from the host clock.
   std::string timeline_json() {
     std::lock_guard<std::mutex> lk(tl_mu_);
+    resolve_gpu_times();
     std::ostringstream os;
     os << std::fixed << std::setprecision(1) << "[";
     bool first = true;
     for (auto& e : timeline_) {
-      auto emit = [&](const char* name, double t0, double t1) {
+      auto emit = [&](const char* name, double t0, double t1, const char* clock) {
         if (!first) os << ",\n";
         first = false;
-        os << "{\"name\":\"" << name << "\",\"cat\":\"bucket" << e.bucket << "\",\"ph\":\"X\",\"ts\":" << t0
-           << ",\"dur\":" << (t1 - t0) << ",\"pid\":" << rank_ << ",\"tid\":" << e.bucket
-           << ",\"args\":{\"bytes\":" << e.bytes << ",\"step\":" << e.step << "}}";
+        os << "{\"name\":\"" << name << "\",\"cat\":\"bucket" << e.bucket << "\",\"ph\":\"" << (t1 < t0 ? "i" : "X")
+           << "\",\"ts\":" << t0;
+        if (t1 >= t0) os << ",\"dur\":" << (t1 - t0);
+        else os << ",\"s\":\"t\"";
+        os << ",\"pid\":" << rank_ << ",\"tid\":" << e.bucket << ",\"args\":{\"bytes\":" << e.bytes
+           << ",\"step\":" << e.step << ",\"clock\":\"" << clock << "\"}}";
       };
-      emit("QUEUED", e.t_ready, e.t_issue);
-      emit("ALLREDUCE", e.t_issue, e.t_done);
+      emit("QUEUED", e.t_ready, e.t_issue, "host");
+      if (e.g_start >= 0) {
+        emit("READY", e.g_ready, -1e300, "gpu");
+        emit("ALLREDUCE", e.g_start, e.g_end, "gpu");
+      } else {
+        emit("ALLREDUCE", e.t_issue, e.t_done, "host");
+      }
     }
     os << "]";
     return os.str();
   }
   int world() const { return world_; }
+  std::string wire() const { return lowp_.defined() ? "bf16" : "fp32"; }
   int64_t issued() const { return issued_.load(); }
 
  private:
   struct Item {
     int bucket = 0;
-    std::shared_ptr<at::cuda::CUDAEvent> event;
+    std::shared_ptr<at::cuda::CUDAEvent> event;   // compute stream passed the bucket's kernels
+    std::shared_ptr<at::cuda::CUDAEvent> done;    // bf16 wire: side stream finished the cast back
     c10::intrusive_ptr<c10d::Work> work;
     double t_ready = 0, t_issue = 0, t_done = 0;
+    std::shared_ptr<TimedEvent> ref, g_ready, g_start, g_end;   // timeline (GPU)
+    double ref_host = 0;
   };
+  struct GpuStamp {
+    size_t idx;
+    std::shared_ptr<TimedEvent> ref;
+    double ref_host;
+    std::shared_ptr<TimedEvent> ready, start, end;
+  };
+
+  hipStream_t compute_stream() const {
+    return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()).stream();
+  }
+
+  // GPU stamps -> host time axis: t = host time of the step's reference event + elapsed (tl_mu_ held)
+  void resolve_gpu_times() {
+    for (auto& g : tl_gpu_) {
+      auto& e = timeline_[g.idx];
+      e.g_ready = g.ref_host + 1e3 * g.ready->since(*g.ref);
+      e.g_start = g.ref_host + 1e3 * g.start->since(*g.ref);
+      e.g_end = g.ref_host + 1e3 * g.end->since(*g.ref);
+    }
+    tl_gpu_.clear();
+  }
 
   struct Watch {
     c10::intrusive_ptr<c10d::Work> work;
@@ -218,14 +306,45 @@ class FusionEngine {
         busy_ = true;
       }
       try {
-        auto sl = flat_.narrow(0, buckets_[it.bucket].first, buckets_[it.bucket].second);
-        std::vector<Tensor> v{sl};
+        const int64_t b0 = buckets_[it.bucket].first, bn = buckets_[it.bucket].second;
+        auto sl = flat_.narrow(0, b0, bn);
         if (gpu_) {
           c10::hip::HIPStreamGuardMasqueradingAsCUDA g(*side_);
+          const hipStream_t ss = side_->stream();
           it.event->block(*side_);
+          if (it.g_ready) {
+            it.g_start = std::make_shared<TimedEvent>();
+            it.g_start->record(ss);
+          }
+          std::vector<Tensor> v{sl};
+          if (lowp_.defined()) {
+            auto lo = lowp_.narrow(0, b0, bn);
+            const char* err = pddl::cast_bf16_launch(sl.data_ptr<float>(), reinterpret_cast<uint16_t*>(lo.data_ptr()),
+                                                     bn, ss);
+            TORCH_CHECK(err == nullptr, "pddl fusion: cast: ", err ? err : "");
+            v = {lo};
+          }
           it.t_issue = now_us();
           it.work = pg_->allreduce(v);
+          if (lowp_.defined() || it.g_ready) it.work->wait();   // side stream: after the collective
+          if (lowp_.defined()) {
+            const char* err = pddl::cast_f32_launch(reinterpret_cast<const uint16_t*>(v[0].data_ptr()),
+                                                    sl.data_ptr<float>(), bn, ss);
+            TORCH_CHECK(err == nullptr, "pddl fusion: cast: ", err ? err : "");
+            it.done = std::make_shared<at::cuda::CUDAEvent>();
+            it.done->record(*side_);
+          }
+          if (it.g_ready) {
+            it.g_end = std::make_shared<TimedEvent>();
+            it.g_end->record(ss);
+          }
         } else {
+          std::vector<Tensor> v{sl};
+          if (lowp_.defined()) {
+            auto lo = lowp_.narrow(0, b0, bn);
+            lo.copy_(sl);
+            v = {lo};
+          }
           it.t_issue = now_us();
           it.work = pg_->allreduce(v);
         }
@@ -297,15 +416,20 @@ class FusionEngine {
   bool timeline_on_ = false;
   std::mutex tl_mu_;
   std::vector<TimelineEvent> timeline_;
+  std::vector<GpuStamp> tl_gpu_;
+  std::shared_ptr<TimedEvent> step_ref_;
+  double step_ref_host_ = 0;
+  Tensor lowp_;   // bf16 wire buffer (undefined: fp32 wire)
 };
 
 }  // namespace
 
 void register_fusion(py::module& m) {
   py::class_<FusionEngine, std::shared_ptr<FusionEngine>>(m, "FusionEngine")
-      .def(py::init<py::object, Tensor, std::vector<std::pair<int64_t, int64_t>>, double, bool, int>(),
+      .def(py::init<py::object, Tensor, std::vector<std::pair<int64_t, int64_t>>, double, bool, int,
+                    const std::string&>(),
            py::arg("process_group"), py::arg("flat"), py::arg("buckets"), py::arg("stall_timeout_s") = 60.0,
-           py::arg("average") = false, py::arg("rank") = 0)
+           py::arg("average") = false, py::arg("rank") = 0, py::arg("wire") = "fp32")
       .def("begin_step", &FusionEngine::begin_step)
       .def("bucket_ready", &FusionEngine::bucket_ready)
       .def("finish", &FusionEngine::finish, py::call_guard<py::gil_scoped_release>())
@@ -313,5 +437,6 @@ void register_fusion(py::module& m) {
       .def("set_timeline", &FusionEngine::set_timeline)
       .def("timeline_json", &FusionEngine::timeline_json)
       .def_property_readonly("world", &FusionEngine::world)
-      .def_property_readonly("issued", &FusionEngine::issued);
+      .def_property_readonly("issued", &FusionEngine::issued)
+      .def_property_readonly("wire", [](const FusionEngine& f) { return f.wire(); });
 }

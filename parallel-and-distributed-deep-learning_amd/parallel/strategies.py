@@ -282,7 +282,7 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
                 if native_available():
                     self.fusion = require_native().FusionEngine(
                         dist.group.WORLD, self.engine.grads, [(s, e - s) for s, e in self.buckets],
-                        float(os.environ.get("PDDL_STALL_TIMEOUT", "60")), False, self.rank)
+                        float(os.environ.get("PDDL_STALL_TIMEOUT", "60")), False, self.rank, self.cfg.grad_dtype)
                     if self.cfg.timeline:
                         self.fusion.set_timeline(True)
             if self.fusion is None:

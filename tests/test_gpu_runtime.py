@@ -29,20 +29,34 @@ def test_fusion_engine_over_rccl_process_group():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(pick_unused_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        g = torch.randn(10000, device="cuda")
-        ref = g.clone()
-        fe = require_native().FusionEngine(dist.group.WORLD, g, [(0, 4000), (4000, 6000)], 10.0, False, 0)
-        fe.set_timeline(True)
-        for _ in range(3):
-            fe.begin_step()
-            g.mul_(1.0)              # kernel on the compute stream the buckets depend on
-            fe.bucket_ready(0)
-            fe.bucket_ready(1)
-            fe.finish()
-        torch.cuda.synchronize()
-        assert torch.equal(g, ref) and fe.issued == 6
-        assert '"ALLREDUCE"' in fe.timeline_json()
-        fe.shutdown()
+        import json
+        for wire in ("fp32", "bf16"):
+            g = torch.randn(10000, device="cuda")
+            ref = g.clone()
+            fe = require_native().FusionEngine(dist.group.WORLD, g, [(0, 4000), (4000, 6000)], 10.0, False, 0, wire)
+            fe.set_timeline(True)
+            for _ in range(3):
+                fe.begin_step()
+                g.mul_(1.0)              # kernel on the compute stream the buckets depend on
+                fe.bucket_ready(0)
+                g[4000:].mul_(1.0)       # bucket 1 completes later
+                fe.bucket_ready(1)
+                fe.finish()
+            torch.cuda.synchronize()
+            assert fe.issued == 6 and fe.wire == wire
+            if wire == "fp32":
+                assert torch.equal(g, ref)
+            else:   # one rank: the bf16 round trip is the only change
+                assert torch.equal(g, ref.to(torch.bfloat16).float())
+            # GPU-stamped timeline: every ALLREDUCE span starts after its bucket's READY event
+            ev = json.loads(fe.timeline_json())
+            ready = {(e["args"]["step"], e["tid"]): e["ts"] for e in ev if e["name"] == "READY"}
+            spans = [e for e in ev if e["name"] == "ALLREDUCE"]
+            assert len(spans) == 6 and len(ready) == 6
+            for e in spans:
+                assert e["args"]["clock"] == "gpu" and e["dur"] >= 0
+                assert e["ts"] >= ready[(e["args"]["step"], e["tid"])] - 1.0   # (us rounding)
+            fe.shutdown()
     finally:
         dist.destroy_process_group()
 

@@ -138,3 +138,21 @@ def test_horovod_bucket_autotune_picks_one_size_and_matches_fixed(monkeypatch):
     assert tuned[0][4] in (8.0, 16.0, 32.0, 64.0) and tuned[0][4] == tuned[1][4]
     for (_, p, _, _, _), (_, q, _, _, _) in zip(tuned, fixed):
         assert _close(p, q)
+
+
+def test_horovod_bf16_wire_close_to_fp32():
+    """--grad-dtype bf16: the FusionEngine reduces bf16 buckets (half the bytes on the wire)
+    and widens the sum back; the trajectory stays within bf16 rounding of the fp32 run."""
+    from pddl.models.reference import TorchEngine
+    from pddl.models.resnet50 import ParamLayout
+    kw = dict(batch_size=2, lr=1e-3, lr_scale_by_size=False, warmup_epochs=0, shard_by="batch")
+    fp32 = _spawn(2, "horovod", dict(kw, grad_dtype="fp32"))
+    bf16 = _spawn(2, "horovod", dict(kw, grad_dtype="bf16"))
+    e0 = TorchEngine(ParamLayout(), 1, crop=32)
+    e0.init(seed=5)
+    p0 = e0.params[:e0.L.n_trainable]
+    assert bf16[0][3] == "FusionEngine"
+    upd = (fp32[0][1] - p0).norm()
+    assert upd > 0
+    assert ((bf16[0][1] - fp32[0][1]).norm() / upd).item() < 0.05
+    assert torch.equal(bf16[0][1], bf16[1][1])        # both ranks applied the same reduced gradient
