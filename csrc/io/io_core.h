@@ -169,7 +169,10 @@ inline void decode_crop_pad(const uint8_t* buf, size_t n, int S, uint8_t* out) {
   std::memset(out, 0, (size_t)S * S * 3);
   row.resize((size_t)W * C);
   const bool adobe_inverted = cmyk && ci.saw_Adobe_marker;
-  while ((int)ci.output_scanline < H) {
+  // rows past the crop window are never needed: stop there and abort the decompressor (the
+  // center crop of a 375-row ImageNet image leaves ~20% of the rows undecoded)
+  const int y_end = cy + ch;
+  while ((int)ci.output_scanline < y_end) {
     const int y = (int)ci.output_scanline;
     JSAMPROW rp = row.data();
     jpeg_read_scanlines(&ci, &rp, 1);
@@ -190,7 +193,8 @@ inline void decode_crop_pad(const uint8_t* buf, size_t n, int S, uint8_t* out) {
       }
     }
   }
-  jpeg_finish_decompress(&ci);
+  if ((int)ci.output_scanline < H) jpeg_abort_decompress(&ci);
+  else jpeg_finish_decompress(&ci);
   jpeg_destroy_decompress(&ci);
 }
 

@@ -26,12 +26,23 @@ import torch
 
 
 class ImageSource:
+    """A source either generates batches on the device (`fetch`, host = False) or loads them
+    into host memory (`fetch_host` -> pinned uint8 images + int64 labels, host = True: decode /
+    gather on native thread pools with the GIL released), which the pipeline's prefetch stage
+    runs ahead of the training thread and copies to the device asynchronously."""
     num_examples: int
     image_size: int
     num_classes: int
+    host = False
+
+    def fetch_host(self, idx: np.ndarray) -> Tuple[torch.Tensor, torch.Tensor]:
+        raise NotImplementedError
 
     def fetch(self, idx: np.ndarray, device) -> Tuple[torch.Tensor, torch.Tensor]:
-        raise NotImplementedError
+        if not self.host:
+            raise NotImplementedError
+        img, lab = self.fetch_host(idx)
+        return img.to(device, non_blocking=True), lab.to(device, non_blocking=True)
 
 
 class SyntheticImageNet(ImageSource):
@@ -107,17 +118,20 @@ class RecordsImageNet(ImageSource):
                 self._loader = np.memmap(self.path, dtype=np.uint8, mode="r").reshape(self.num_examples, -1)
         return self._loader
 
-    def fetch(self, idx: np.ndarray, device):
+    host = True
+
+    def fetch_host(self, idx: np.ndarray):
         ld = self._native()
         S = self.image_size
         if isinstance(ld, np.memmap):
-            host = torch.from_numpy(np.ascontiguousarray(ld[idx]))
+            buf = torch.from_numpy(np.ascontiguousarray(ld[idx]))
         else:
-            host = torch.empty((len(idx), self.row), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
-            ld.gather(torch.from_numpy(np.asarray(idx, dtype=np.int64)), host)
-        img = host.view(len(idx), S, S, 3).to(device, non_blocking=True)
-        lab = torch.from_numpy(self.labels[idx]).to(device, non_blocking=True)
-        return img, lab
+            buf = torch.empty((len(idx), self.row), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+            ld.gather(torch.from_numpy(np.asarray(idx, dtype=np.int64)), buf)
+        lab = torch.from_numpy(self.labels[idx])
+        if torch.cuda.is_available():
+            lab = lab.pin_memory()
+        return buf.view(len(idx), S, S, 3), lab
 
 
 def write_records(root: str, split: str, images: np.ndarray, labels: np.ndarray) -> None:
@@ -175,8 +189,17 @@ class Pipeline:
                 return
             epoch += 1
 
-    def iterate(self, device, epoch: int = 0, prefetch: int = 2):
-        """Yields (images, labels) on `device`; fetches run one batch ahead."""
+    def iterate(self, device, epoch: int = 0, prefetch: int = 3):
+        """Yields (images, labels) on `device`, tf.data `prefetch` semantics.
+
+        Host sources: a producer thread decodes / gathers up to `prefetch` batches ahead of the
+        consumer into pinned memory (native code, GIL released), and the host->device copy of
+        batch i+1 is issued on a side stream before batch i is handed out; the consumer's
+        stream waits on the copy's event (stream-ordered, the training thread never decodes
+        nor blocks on a copy).  Device sources (synthetic) generate on the GPU in order."""
+        if getattr(self.source, "host", False):
+            yield from _PrefetchIter(self, torch.device(device), epoch, max(1, prefetch))
+            return
         it = self.batches(epoch)
         pending = []
         for idx in it:
@@ -185,6 +208,87 @@ class Pipeline:
                 yield pending.pop(0)
         while pending:
             yield pending.pop(0)
+
+
+class _PrefetchIter:
+    """Producer thread (host decode k batches ahead) + async H2D one batch ahead."""
+
+    _END = object()
+
+    def __init__(self, pipe: "Pipeline", device: torch.device, epoch: int, depth: int):
+        import queue
+        import threading
+        self.q = queue.Queue(maxsize=depth)
+        self.stop = threading.Event()
+        self.device = device
+        self.cuda = device.type == "cuda"
+        self.copy_stream = torch.cuda.Stream(device=device) if self.cuda else None
+        self.th = threading.Thread(target=self._produce, args=(pipe, epoch), daemon=True,
+                                   name="pddl-prefetch")
+        self.th.start()
+
+    def _put(self, item) -> bool:
+        import queue
+        while not self.stop.is_set():
+            try:
+                self.q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _produce(self, pipe, epoch):
+        try:
+            for idx in pipe.batches(epoch):
+                if self.stop.is_set() or not self._put(pipe.source.fetch_host(idx)):
+                    return
+            self._put(self._END)
+        except BaseException as e:   # surfaced on the consumer thread
+            self._put(e)
+
+    def _to_device(self, hb):
+        img, lab = hb
+        if not self.cuda:
+            return img, lab, None
+        with torch.cuda.stream(self.copy_stream):
+            di = img.to(self.device, non_blocking=True)
+            dl = lab.to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        return di, dl, ev
+
+    def _hand_out(self, item):
+        di, dl, ev = item
+        if ev is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            di.record_stream(cur)     # the copy stream's allocation is used on the compute stream
+            dl.record_stream(cur)
+        return di, dl
+
+    def __iter__(self):
+        pending = None
+        try:
+            while True:
+                item = self.q.get()
+                if item is self._END:
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                nxt = self._to_device(item)       # batch i+1's copy starts before batch i is used
+                if pending is not None:
+                    yield self._hand_out(pending)
+                pending = nxt
+            if pending is not None:
+                yield self._hand_out(pending)
+        finally:
+            self.stop.set()
+            while not self.q.empty():
+                try:
+                    self.q.get_nowait()
+                except Exception:
+                    break
+            self.th.join(timeout=5)
 
 
 def make_source(spec: str, split: str, cfg) -> ImageSource:

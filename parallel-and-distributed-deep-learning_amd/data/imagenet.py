@@ -73,11 +73,14 @@ class TFDSImageNet(ImageSource):
         self.image_size = image_size
         self.num_classes = num_classes
 
-    def fetch(self, idx: np.ndarray, device):
+    host = True
+
+    def fetch_host(self, idx: np.ndarray):
+        """Decode into pinned host buffers (native thread pool, GIL released)."""
         n = len(idx)
         img, lab = _host_batch(n, self.image_size)
         self.reader.fetch(torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)), img, lab)
-        return img.to(device, non_blocking=True), lab.to(device, non_blocking=True)
+        return img, lab
 
 
 class JpegFolderImageNet(ImageSource):
@@ -104,12 +107,14 @@ class JpegFolderImageNet(ImageSource):
         self.image_size = image_size
         self.num_classes = num_classes
 
-    def fetch(self, idx: np.ndarray, device):
+    host = True
+
+    def fetch_host(self, idx: np.ndarray):
         n = len(idx)
         img, lab = _host_batch(n, self.image_size)
         self.reader.fetch([self.files[i] for i in idx], img)
         lab.copy_(torch.from_numpy(self.labels[np.asarray(idx)]))
-        return img.to(device, non_blocking=True), lab.to(device, non_blocking=True)
+        return img, lab
 
 
 # ------------------------------------------------------------------ writing (tests, subsets)
