@@ -29,12 +29,15 @@
 //   * Wire dtype: "bf16" casts each bucket to bf16 on the side stream (a HIP kernel), reduces
 //     the half-size message (48.8 MiB instead of 97.6 MiB per step for ResNet-50) and casts
 //     the sum back before the optimizer reads it (Horovod's fp16 compression analogue).
-// The transport is the c10d ProcessGroup passed from Python: RCCL ("nccl") on GPU, gloo on CPU
+// The threads, queues and stall inspector live in runtime/fusion_core.h (torch-free, run
+// natively under ThreadSanitizer by csrc/tests/fusion_core_test.cpp); this file adds the
+// transport.  The transport is the c10d ProcessGroup passed from Python: RCCL ("nccl") on GPU, gloo on CPU
 // (so the engine itself is exercised by the CPU multi-process tests).
 #include <torch/extension.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
 #include "kernels/kernels.h"
+#include "runtime/fusion_core.h"
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/HIPEvent.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -85,8 +88,27 @@ struct TimedEvent {
   }
 };
 
+// c10d::Work as the core's in-flight handle
+struct C10dWork : pddl::FusionWork {
+  c10::intrusive_ptr<c10d::Work> w;
+  explicit C10dWork(c10::intrusive_ptr<c10d::Work> w_) : w(std::move(w_)) {}
+  bool completed() override { return w->isCompleted(); }
+};
+
+// Per-bucket transport state carried through the core.
+struct Payload {
+  std::shared_ptr<at::cuda::CUDAEvent> event;   // compute stream passed the bucket's kernels
+  std::shared_ptr<at::cuda::CUDAEvent> done;    // bf16 wire: side stream finished the cast back
+  c10::intrusive_ptr<c10d::Work> work;
+  std::shared_ptr<TimedEvent> ref, g_ready, g_start, g_end;   // timeline (GPU)
+  double ref_host = 0;
+};
+
 class FusionEngine {
  public:
+  using Core = pddl::FusionCore<Payload>;
+  using Item = Core::Item;
+
   FusionEngine(py::object pg_obj, Tensor flat, std::vector<std::pair<int64_t, int64_t>> buckets, double stall_s,
                bool average, int rank, const std::string& wire)
       : flat_(flat), buckets_(std::move(buckets)), stall_s_(stall_s), average_(average), rank_(rank) {
@@ -98,28 +120,17 @@ class FusionEngine {
     if (wire == "bf16") lowp_ = torch::empty({flat_.numel()}, flat_.options().dtype(torch::kBFloat16));
     if (gpu_) side_ = c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, flat_.device().index());
     verify_signature();
-    worker_ = std::thread([this] { run(); });
-    watchdog_ = std::thread([this] { watch(); });
+    core_ = std::make_unique<Core>((int)buckets_.size(), stall_s_, rank_, [this](Item& it) { issue(it); });
+    core_->start();
   }
   ~FusionEngine() { shutdown(); }
 
   void shutdown() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (stop_) return;
-      stop_ = true;
-    }
-    cv_.notify_all();
-    if (worker_.joinable()) worker_.join();
-    if (watchdog_.joinable()) watchdog_.join();
+    if (core_) core_->shutdown();
   }
 
   void begin_step() {
-    std::lock_guard<std::mutex> lk(mu_);
-    TORCH_CHECK(!stalled_, "pddl fusion: stall detected: ", stall_msg_);
-    TORCH_CHECK(pending_.empty() && inflight_.empty(), "pddl fusion: begin_step with outstanding buckets");
-    next_expected_ = 0;
-    ++step_;
+    core_->begin_step();
     if (gpu_ && timeline_on_) {   // the step's GPU time origin, pinned to the host clock
       step_ref_ = std::make_shared<TimedEvent>();
       step_ref_host_ = now_us();
@@ -128,56 +139,37 @@ class FusionEngine {
   }
 
   void bucket_ready(int i) {
-    TORCH_CHECK(i >= 0 && i < (int)buckets_.size(), "pddl fusion: bad bucket id");
     Item it;
     it.bucket = i;
     it.t_ready = now_us();
     if (gpu_) {
-      it.event = std::make_shared<at::cuda::CUDAEvent>();
-      it.event->record(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()));
+      it.payload.event = std::make_shared<at::cuda::CUDAEvent>();
+      it.payload.event->record(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()));
       if (timeline_on_ && step_ref_) {
-        it.ref = step_ref_;
-        it.ref_host = step_ref_host_;
-        it.g_ready = std::make_shared<TimedEvent>();
-        it.g_ready->record(compute_stream());
+        it.payload.ref = step_ref_;
+        it.payload.ref_host = step_ref_host_;
+        it.payload.g_ready = std::make_shared<TimedEvent>();
+        it.payload.g_ready->record(compute_stream());
       }
     }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      TORCH_CHECK(i == next_expected_, "pddl fusion: buckets must become ready in order (got ", i, ", expected ",
-                  next_expected_, ")");
-      ++next_expected_;
-      pending_.push_back(std::move(it));
-    }
-    cv_.notify_all();
+    core_->ready(std::move(it));
   }
 
   // Wait until every queued bucket has been issued, then make the caller's current stream wait
   // for the collectives (stream-ordered on GPU, host-blocking on gloo).
   void finish() {
-    std::vector<Item> done;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [this] { return (pending_.empty() && !busy_) || stalled_ || stop_ || !error_.empty(); });
-      TORCH_CHECK(error_.empty(), "pddl fusion: collective failed: ", error_);
-      TORCH_CHECK(!stalled_, "pddl fusion: stall detected: ", stall_msg_);
-      done.swap(inflight_);
-    }
+    std::vector<Item> done = core_->drain();
+    const int step = core_->step();
     for (auto& it : done) {
-      if (gpu_ && it.done) {
+      Payload& pl = it.payload;
+      if (gpu_ && pl.done) {
         // bf16 wire: the side stream cast the sum back after the collective; wait for that
-        it.done->block(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()));
+        pl.done->block(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(flat_.device().index()));
       } else if (gpu_ || stall_s_ <= 0) {
-        it.work->wait();   // GPU: a stream-ordered wait, the host does not block here
+        pl.work->wait();   // GPU: a stream-ordered wait, the host does not block here
       } else {             // host-blocking backend: poll, so the watchdog's stall verdict can end the wait
-        while (!it.work->isCompleted()) {
-          {
-            std::lock_guard<std::mutex> lk(mu_);
-            TORCH_CHECK(!stalled_, "pddl fusion: stall detected: ", stall_msg_);
-          }
-          std::this_thread::sleep_for(std::chrono::microseconds(200));
-        }
-        it.work->wait();   // completed: returns at once (and rethrows a collective error)
+        core_->wait_polling(it);
+        pl.work->wait();   // completed: returns at once (and rethrows a collective error)
       }
       it.t_done = now_us();
       if (!gpu_ && lowp_.defined()) {   // host backend, bf16 wire: widen the reduced bucket
@@ -192,9 +184,9 @@ class FusionEngine {
         std::lock_guard<std::mutex> lk(tl_mu_);
         TimelineEvent e{it.bucket, buckets_[it.bucket].second * (lowp_.defined() ? 2 : 4), it.t_ready, it.t_issue,
                         it.t_done};
-        e.step = step_;
+        e.step = step;
         timeline_.push_back(e);
-        if (it.ref) tl_gpu_.push_back({timeline_.size() - 1, it.ref, it.ref_host, it.g_ready, it.g_start, it.g_end});
+        if (pl.ref) tl_gpu_.push_back({timeline_.size() - 1, pl.ref, pl.ref_host, pl.g_ready, pl.g_start, pl.g_end});
       }
     }
   }
@@ -232,18 +224,9 @@ class FusionEngine {
   }
   int world() const { return world_; }
   std::string wire() const { return lowp_.defined() ? "bf16" : "fp32"; }
-  int64_t issued() const { return issued_.load(); }
+  int64_t issued() const { return core_->issued(); }
 
  private:
-  struct Item {
-    int bucket = 0;
-    std::shared_ptr<at::cuda::CUDAEvent> event;   // compute stream passed the bucket's kernels
-    std::shared_ptr<at::cuda::CUDAEvent> done;    // bf16 wire: side stream finished the cast back
-    c10::intrusive_ptr<c10d::Work> work;
-    double t_ready = 0, t_issue = 0, t_done = 0;
-    std::shared_ptr<TimedEvent> ref, g_ready, g_start, g_end;   // timeline (GPU)
-    double ref_host = 0;
-  };
   struct GpuStamp {
     size_t idx;
     std::shared_ptr<TimedEvent> ref;
@@ -266,18 +249,6 @@ class FusionEngine {
     tl_gpu_.clear();
   }
 
-  struct Watch {
-    c10::intrusive_ptr<c10d::Work> work;
-    double t_issue;
-    int bucket;
-  };
-
-  void report_stall(const std::string& msg) {   // (mu_ held)
-    stall_msg_ = msg;
-    stalled_ = true;
-    fprintf(stderr, "[pddl stall inspector] %s\n", stall_msg_.c_str());
-  }
-
   void verify_signature() {
     // all ranks must agree on the bucket table (static negotiation)
     double sig = 0;
@@ -294,105 +265,52 @@ class FusionEngine {
     TORCH_CHECK(mx == sig && mn == sig, "pddl fusion: ranks disagree on the gradient bucket layout");
   }
 
-  void run() {
-    while (true) {
-      Item it;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
-        if (stop_) return;
-        it = std::move(pending_.front());
-        pending_.pop_front();
-        busy_ = true;
+  // The core's worker thread: enqueue the collective of one ready bucket.
+  void issue(Item& it) {
+    Payload& pl = it.payload;
+    const int64_t b0 = buckets_[it.bucket].first, bn = buckets_[it.bucket].second;
+    auto sl = flat_.narrow(0, b0, bn);
+    if (gpu_) {
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(*side_);
+      const hipStream_t ss = side_->stream();
+      pl.event->block(*side_);
+      if (pl.g_ready) {
+        pl.g_start = std::make_shared<TimedEvent>();
+        pl.g_start->record(ss);
       }
-      try {
-        const int64_t b0 = buckets_[it.bucket].first, bn = buckets_[it.bucket].second;
-        auto sl = flat_.narrow(0, b0, bn);
-        if (gpu_) {
-          c10::hip::HIPStreamGuardMasqueradingAsCUDA g(*side_);
-          const hipStream_t ss = side_->stream();
-          it.event->block(*side_);
-          if (it.g_ready) {
-            it.g_start = std::make_shared<TimedEvent>();
-            it.g_start->record(ss);
-          }
-          std::vector<Tensor> v{sl};
-          if (lowp_.defined()) {
-            auto lo = lowp_.narrow(0, b0, bn);
-            const char* err = pddl::cast_bf16_launch(sl.data_ptr<float>(), reinterpret_cast<uint16_t*>(lo.data_ptr()),
-                                                     bn, ss);
-            TORCH_CHECK(err == nullptr, "pddl fusion: cast: ", err ? err : "");
-            v = {lo};
-          }
-          it.t_issue = now_us();
-          it.work = pg_->allreduce(v);
-          if (lowp_.defined() || it.g_ready) it.work->wait();   // side stream: after the collective
-          if (lowp_.defined()) {
-            const char* err = pddl::cast_f32_launch(reinterpret_cast<const uint16_t*>(v[0].data_ptr()),
-                                                    sl.data_ptr<float>(), bn, ss);
-            TORCH_CHECK(err == nullptr, "pddl fusion: cast: ", err ? err : "");
-            it.done = std::make_shared<at::cuda::CUDAEvent>();
-            it.done->record(*side_);
-          }
-          if (it.g_ready) {
-            it.g_end = std::make_shared<TimedEvent>();
-            it.g_end->record(ss);
-          }
-        } else {
-          std::vector<Tensor> v{sl};
-          if (lowp_.defined()) {
-            auto lo = lowp_.narrow(0, b0, bn);
-            lo.copy_(sl);
-            v = {lo};
-          }
-          it.t_issue = now_us();
-          it.work = pg_->allreduce(v);
-        }
-        issued_++;
-        std::lock_guard<std::mutex> lk(mu_);
-        watch_.push_back({it.work, it.t_issue, it.bucket});
-        inflight_.push_back(std::move(it));
-        busy_ = false;
-      } catch (const std::exception& e) {
-        std::lock_guard<std::mutex> lk(mu_);
-        error_ = e.what();
-        busy_ = false;
+      std::vector<Tensor> v{sl};
+      if (lowp_.defined()) {
+        auto lo = lowp_.narrow(0, b0, bn);
+        const char* err = pddl::cast_bf16_launch(sl.data_ptr<float>(), reinterpret_cast<uint16_t*>(lo.data_ptr()),
+                                                 bn, ss);
+        TORCH_CHECK(err == nullptr, "pddl fusion: cast: ", err ? err : "");
+        v = {lo};
       }
-      cv_.notify_all();
+      it.t_issue = now_us();
+      pl.work = pg_->allreduce(v);
+      if (lowp_.defined() || pl.g_ready) pl.work->wait();   // side stream: after the collective
+      if (lowp_.defined()) {
+        const char* err = pddl::cast_f32_launch(reinterpret_cast<const uint16_t*>(v[0].data_ptr()),
+                                                sl.data_ptr<float>(), bn, ss);
+        TORCH_CHECK(err == nullptr, "pddl fusion: cast: ", err ? err : "");
+        pl.done = std::make_shared<at::cuda::CUDAEvent>();
+        pl.done->record(*side_);
+      }
+      if (pl.g_ready) {
+        pl.g_end = std::make_shared<TimedEvent>();
+        pl.g_end->record(ss);
+      }
+    } else {
+      std::vector<Tensor> v{sl};
+      if (lowp_.defined()) {
+        auto lo = lowp_.narrow(0, b0, bn);
+        lo.copy_(sl);
+        v = {lo};
+      }
+      it.t_issue = now_us();
+      pl.work = pg_->allreduce(v);
     }
-  }
-
-  void watch() {
-    while (true) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        if (cv_.wait_for(lk, std::chrono::milliseconds(200), [this] { return stop_; })) return;
-        if (stall_s_ > 0 && !pending_.empty()) {
-          const double age = (now_us() - pending_.front().t_ready) * 1e-6;
-          if (age > stall_s_ && !stalled_) {
-            std::ostringstream os;
-            os << "rank " << rank_ << ": bucket " << pending_.front().bucket << " queued for " << age
-               << " s without being issued (" << pending_.size() << " pending, " << inflight_.size()
-               << " in flight) - a peer rank is likely stuck or diverged";
-            report_stall(os.str());
-          }
-        }
-        // issued collectives that never complete: a peer never joined (stream-ordered waits on
-        // the GPU do not block the host, so this is where a stuck peer becomes visible)
-        while (!watch_.empty() && watch_.front().work->isCompleted()) watch_.pop_front();
-        if (stall_s_ > 0 && !watch_.empty() && !stalled_) {
-          const double age = (now_us() - watch_.front().t_issue) * 1e-6;
-          if (age > stall_s_) {
-            std::ostringstream os;
-            os << "rank " << rank_ << ": all-reduce of bucket " << watch_.front().bucket << " issued " << age
-               << " s ago has not completed (" << watch_.size() << " outstanding) - a peer rank is likely stuck"
-               << " or diverged";
-            report_stall(os.str());
-          }
-        }
-      }
-      cv_.notify_all();
-    }
+    it.work = std::make_shared<C10dWork>(pl.work);
   }
 
   Tensor flat_;
@@ -403,16 +321,7 @@ class FusionEngine {
   int rank_, world_ = 1;
   bool gpu_ = false;
   c10::optional<c10::hip::HIPStreamMasqueradingAsCUDA> side_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<Item> pending_;
-  std::vector<Item> inflight_;
-  std::deque<Watch> watch_;
-  bool stop_ = false, busy_ = false, stalled_ = false;
-  std::string error_, stall_msg_;
-  int next_expected_ = 0, step_ = 0;
-  std::atomic<int64_t> issued_{0};
-  std::thread worker_, watchdog_;
+  std::unique_ptr<Core> core_;
   bool timeline_on_ = false;
   std::mutex tl_mu_;
   std::vector<TimelineEvent> timeline_;

@@ -1,0 +1,130 @@
+// Control-plane protocol of the parameter-server data plane (ps_service.cpp),
+// free of torch and HIP so ThreadSanitizer can drive it natively (csrc/tests/ps_protocol_test.cpp
+// runs the service loop and several clients as threads over one segment).
+//
+// One control segment per PS (POSIX shared memory across processes) with a slot per worker.
+// A request is: the worker writes its gradient into its mailbox and the learning rate into the
+// slot (plain stores), then publishes `req_seq` with RELEASE; the service loop ACQUIREs
+// `req_seq`, applies the update, writes the fresh shard into the worker's receive buffer
+// (plain stores) and publishes `done_seq` with RELEASE; the worker ACQUIREs `done_seq` before
+// reading the receive buffer.  Those two release/acquire pairs are the only ordering the
+// plain mailbox / receive-buffer traffic relies on.  (GPU roles: the mailbox and receive
+// buffers are HIP-IPC device memory written by kernels and peer copies, fenced by a stream
+// synchronize before the release store.)
+#pragma once
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace pddl {
+namespace ps {
+
+constexpr uint64_t kMagic = 0x5044444c50535631ull;   // "PDDLPSV1"
+constexpr int kMaxWorkers = 64;
+constexpr int kIpcHandleBytes = 64;                  // hipIpcMemHandle_t
+enum { OP_PUSH = 0, OP_PULL = 1, OP_STOP = 2 };
+
+struct alignas(128) WorkerSlot {
+  std::atomic<uint64_t> req_seq;
+  std::atomic<uint64_t> done_seq;
+  std::atomic<int32_t> op;
+  std::atomic<int32_t> rx_ready;
+  std::atomic<int32_t> pid;
+  float lr;                                    // plain: published by req_seq
+  unsigned char rx_handle[kIpcHandleBytes];    // worker receive buffer (GPU roles); published by rx_ready
+};
+
+struct PSCtrl {
+  uint64_t magic;
+  int64_t n;            // shard elements (padded to a multiple of 4)
+  int32_t workers;
+  int32_t gpu;          // 1: data in GPU memory (IPC), 0: shared memory
+  std::atomic<int32_t> ready;
+  std::atomic<uint64_t> updates;
+  unsigned char mailbox_handle[kIpcHandleBytes];
+  WorkerSlot slot[kMaxWorkers];
+};
+
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Service loop of one PS: serve every worker's requests in arrival order until each has sent
+// OP_STOP or vanished.  apply(w, lr): the update of worker w's mailbox; snapshot(w): the fresh
+// shard into w's receive buffer; idle(): called when no request was pending (housekeeping);
+// alive(pid): false once a worker process is gone (polled every 0.5 s while idle).
+template <class Apply, class Snapshot, class Idle, class Alive>
+void serve(PSCtrl* ctrl, int W, const std::atomic<bool>& stop, Apply apply, Snapshot snapshot, Idle idle,
+           Alive alive, std::vector<int>* dead) {
+  std::vector<uint64_t> seen(W, 0);
+  std::vector<char> finished(W, 0);
+  int n_done = 0;
+  double last_check = now_s();
+  while (n_done < W && !stop.load()) {
+    bool any = false;
+    for (int w = 0; w < W; ++w) {
+      if (finished[w]) continue;
+      WorkerSlot& s = ctrl->slot[w];
+      const uint64_t r = s.req_seq.load(std::memory_order_acquire);
+      if (r == seen[w]) continue;
+      any = true;
+      seen[w] = r;
+      const int op = s.op.load(std::memory_order_relaxed);
+      if (op == OP_STOP) {
+        finished[w] = 1;
+        ++n_done;
+      } else {
+        if (op == OP_PUSH) {
+          apply(w, s.lr);
+          ctrl->updates.fetch_add(1);
+        }
+        snapshot(w);
+      }
+      s.done_seq.store(r, std::memory_order_release);
+    }
+    if (!any) {
+      idle();
+      const double t = now_s();
+      if (t - last_check > 0.5) {   // a worker process that vanished counts as finished
+        last_check = t;
+        for (int w = 0; w < W; ++w) {
+          const int pid = ctrl->slot[w].pid.load();
+          if (!finished[w] && pid > 0 && !alive(pid)) {
+            finished[w] = 1;
+            ++n_done;
+            if (dead) dead->push_back(w);
+          }
+        }
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+}
+
+// Client side: publish request `seq` (after the mailbox / lr writes) ...
+inline void post(WorkerSlot& s, uint64_t seq, int op, float lr) {
+  s.lr = lr;
+  s.op.store(op, std::memory_order_relaxed);
+  s.req_seq.store(seq, std::memory_order_release);
+}
+
+// ... and wait for its completion (then the receive buffer holds the fresh shard).
+inline void wait_done(WorkerSlot& s, uint64_t seq, double timeout_s, int p) {
+  const double t0 = now_s();
+  int spins = 0;
+  while (s.done_seq.load(std::memory_order_acquire) != seq) {
+    if (++spins > 64) {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if (now_s() - t0 >= timeout_s)
+        throw std::runtime_error("pddl ps client: parameter server " + std::to_string(p) + " did not answer within " +
+                                 std::to_string(timeout_s) + " s (PS failure aborts the job)");
+    }
+  }
+}
+
+}  // namespace ps
+}  // namespace pddl

@@ -17,6 +17,8 @@
 //     (unbounded staleness, as the reference's asynchronous coordinator).
 //   * CPU roles (tests, `--device cpu`): the same protocol with the mailboxes and receive
 //     buffers in shared memory and a host Adam loop.
+//   * The request / completion protocol and the service loop are in runtime/ps_protocol.h
+//     (torch-free; ThreadSanitizer drives it natively: csrc/tests/ps_protocol_test.cpp).
 //   * Failure handling: a worker that dies never bumps its sequence number again (its
 //     half-written mailbox is never applied); the service loop treats a vanished worker pid
 //     as finished, and the coordinator re-queues its closure (parameter_server.py).  A worker
@@ -41,36 +43,22 @@
 #include <vector>
 
 #include "kernels/kernels.h"
+#include "runtime/ps_protocol.h"
 
 namespace py = pybind11;
 using torch::Tensor;
 
 namespace {
 
-constexpr uint64_t kMagic = 0x5044444c50535631ull;   // "PDDLPSV1"
-constexpr int kMaxWorkers = 64;
-enum { OP_PUSH = 0, OP_PULL = 1, OP_STOP = 2 };
-
-struct alignas(128) WorkerSlot {
-  std::atomic<uint64_t> req_seq;
-  std::atomic<uint64_t> done_seq;
-  std::atomic<int32_t> op;
-  std::atomic<int32_t> rx_ready;
-  std::atomic<int32_t> pid;
-  float lr;
-  hipIpcMemHandle_t rx_handle;   // worker receive buffer (GPU roles)
-};
-
-struct PSCtrl {
-  uint64_t magic;
-  int64_t n;            // shard elements (padded to a multiple of 4)
-  int32_t workers;
-  int32_t gpu;          // 1: data in GPU memory (IPC), 0: shared memory
-  std::atomic<int32_t> ready;
-  std::atomic<uint64_t> updates;
-  hipIpcMemHandle_t mailbox_handle;
-  WorkerSlot slot[kMaxWorkers];
-};
+using pddl::ps::kMagic;
+using pddl::ps::kMaxWorkers;
+using pddl::ps::PSCtrl;
+using pddl::ps::WorkerSlot;
+using pddl::ps::OP_PUSH;
+using pddl::ps::OP_PULL;
+using pddl::ps::OP_STOP;
+using pddl::ps::now_s;
+static_assert(sizeof(hipIpcMemHandle_t) == pddl::ps::kIpcHandleBytes, "IPC handle size");
 
 void hck(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, "pddl ps ", what, ": ", hipGetErrorString(e)); }
 void kck(const char* err, const char* what) { TORCH_CHECK(err == nullptr, "pddl ps ", what, ": ", err ? err : ""); }
@@ -115,10 +103,6 @@ struct Shm {
   }
 };
 
-double now_s() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 // ------------------------------------------------------------------------------ server
 class PSServer {
  public:
@@ -145,7 +129,9 @@ class PSServer {
       hck(hipMemcpy(params_, host.data_ptr<float>(), n_real_ * sizeof(float), hipMemcpyHostToDevice), "init copy");
       hck(hipMalloc(&mailbox_, (size_t)W_ * n_ * sizeof(float)), "malloc mailbox");
       hck(hipMemset(mailbox_, 0, (size_t)W_ * n_ * sizeof(float)), "memset mailbox");
-      hck(hipIpcGetMemHandle(&ctrl_->mailbox_handle, mailbox_), "ipc handle");
+      hipIpcMemHandle_t mh;
+      hck(hipIpcGetMemHandle(&mh, mailbox_), "ipc handle");
+      std::memcpy(ctrl_->mailbox_handle, &mh, sizeof(mh));
       hck(hipDeviceSynchronize(), "init sync");
       rx_ptr_.assign(W_, nullptr);
     } else {
@@ -214,7 +200,9 @@ class PSServer {
       if (!rx_ptr_[w]) {
         TORCH_CHECK(s.rx_ready.load(std::memory_order_acquire) == 1, "worker ", w, " has no receive buffer");
         void* ptr = nullptr;
-        hck(hipIpcOpenMemHandle(&ptr, s.rx_handle, hipIpcMemLazyEnablePeerAccess), "open rx handle");
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, s.rx_handle, sizeof(h));
+        hck(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "open rx handle");
         rx_ptr_[w] = static_cast<float*>(ptr);
       }
       hck(hipMemcpyAsync(rx_ptr_[w], params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
@@ -226,53 +214,19 @@ class PSServer {
   void serve() {
     try {
       if (dev_ >= 0) hck(hipSetDevice(dev_), "set device");
-      std::vector<uint64_t> seen(W_, 0);
-      std::vector<char> finished(W_, 0);
-      int n_done = 0;
-      double last_check = now_s();
-      while (n_done < W_ && !stop_.load()) {
-        bool any = false;
-        for (int w = 0; w < W_; ++w) {
-          if (finished[w]) continue;
-          WorkerSlot& s = ctrl_->slot[w];
-          const uint64_t r = s.req_seq.load(std::memory_order_acquire);
-          if (r == seen[w]) continue;
-          any = true;
-          seen[w] = r;
-          const int op = s.op.load(std::memory_order_relaxed);
-          if (op == OP_STOP) {
-            finished[w] = 1; ++n_done;
-          } else {
-            if (op == OP_PUSH) {
-              apply_adam(w, s.lr);
-              ctrl_->updates.fetch_add(1);
-            }
-            send_snapshot(w);
-          }
-          s.done_seq.store(r, std::memory_order_release);
-        }
-        if (!any) {
-          const double t = now_s();
-          if (!unlinked_) {   // every worker attached: drop the names (no /dev/shm leak on a crash)
-            bool all = true;
-            for (int w = 0; w < W_; ++w) all = all && ctrl_->slot[w].pid.load() > 0;
-            if (all) {
-              ctrl_shm_.unlink(); mb_shm_.unlink(); rx_shm_.unlink();
-              unlinked_ = true;
-            }
-          }
-          if (t - last_check > 0.5) {   // a worker process that vanished counts as finished
-            last_check = t;
-            for (int w = 0; w < W_; ++w) {
-              const int pid = ctrl_->slot[w].pid.load();
-              if (!finished[w] && pid > 0 && kill(pid, 0) != 0 && errno == ESRCH) {
-                finished[w] = 1; ++n_done; dead_.push_back(w);
+      pddl::ps::serve(
+          ctrl_, W_, stop_, [this](int w, float lr) { apply_adam(w, lr); }, [this](int w) { send_snapshot(w); },
+          [this] {
+            if (!unlinked_) {   // every worker attached: drop the names (no /dev/shm leak on a crash)
+              bool all = true;
+              for (int w = 0; w < W_; ++w) all = all && ctrl_->slot[w].pid.load() > 0;
+              if (all) {
+                ctrl_shm_.unlink(); mb_shm_.unlink(); rx_shm_.unlink();
+                unlinked_ = true;
               }
             }
-          }
-          std::this_thread::sleep_for(std::chrono::microseconds(20));
-        }
-      }
+          },
+          [](int pid) { return !(kill(pid, 0) != 0 && errno == ESRCH); }, &dead_);
       if (dev_ >= 0) hipStreamSynchronize(stream_);
     } catch (const std::exception& e) {
       err_ = e.what();
@@ -345,14 +299,18 @@ class PSClient {
       WorkerSlot& s = r.ctrl->slot[w_];
       r.seq = s.done_seq.load();
       if (dev_ >= 0) {
-        hck(hipIpcOpenMemHandle(&r.mb_base, r.ctrl->mailbox_handle, hipIpcMemLazyEnablePeerAccess), "open mailbox");
+        hipIpcMemHandle_t mh;
+        std::memcpy(&mh, r.ctrl->mailbox_handle, sizeof(mh));
+        hck(hipIpcOpenMemHandle(&r.mb_base, mh, hipIpcMemLazyEnablePeerAccess), "open mailbox");
         r.mailbox = static_cast<float*>(r.mb_base) + (size_t)w_ * r.n;
         void* rx = nullptr;
         hck(hipMalloc(&rx, r.n * sizeof(float)), "malloc rx");
         hck(hipMemset(rx, 0, r.n * sizeof(float)), "memset rx");
         hck(hipDeviceSynchronize(), "rx sync");
         r.rx = static_cast<float*>(rx);
-        hck(hipIpcGetMemHandle(&s.rx_handle, r.rx), "rx handle");
+        hipIpcMemHandle_t rh;
+        hck(hipIpcGetMemHandle(&rh, r.rx), "rx handle");
+        std::memcpy(s.rx_handle, &rh, sizeof(rh));
         s.rx_ready.store(1, std::memory_order_release);
         auto opts = torch::TensorOptions().dtype(torch::kUInt8);
         Tensor hrows = torch::empty({(int64_t)(r.host_rows.size() * sizeof(pddl::RangeRow))}, opts);
@@ -403,12 +361,7 @@ class PSClient {
       }
     }
     if (dev_ >= 0 && push) hck(hipStreamSynchronize(st), "sync push");   // peer writes complete + visible
-    for (Remote& r : rem_) {
-      WorkerSlot& s = r.ctrl->slot[w_];
-      s.lr = (float)lr;
-      s.op.store(push ? OP_PUSH : OP_PULL, std::memory_order_relaxed);
-      s.req_seq.store(++r.seq, std::memory_order_release);
-    }
+    for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], ++r.seq, push ? OP_PUSH : OP_PULL, (float)lr);
     for (size_t p = 0; p < rem_.size(); ++p) {
       Remote& r = rem_[p];
       wait_done(r, (int)p);
@@ -424,27 +377,12 @@ class PSClient {
     }
   }
   void stop() {
-    for (Remote& r : rem_) {
-      WorkerSlot& s = r.ctrl->slot[w_];
-      s.op.store(OP_STOP, std::memory_order_relaxed);
-      s.req_seq.store(++r.seq, std::memory_order_release);
-    }
+    for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], ++r.seq, OP_STOP, 0.f);
     for (size_t p = 0; p < rem_.size(); ++p) wait_done(rem_[p], (int)p);
   }
 
  private:
-  void wait_done(Remote& r, int p) {
-    WorkerSlot& s = r.ctrl->slot[w_];
-    const double t0 = now_s();
-    int spins = 0;
-    while (s.done_seq.load(std::memory_order_acquire) != r.seq) {
-      if (++spins > 64) {
-        std::this_thread::sleep_for(std::chrono::microseconds(20));
-        TORCH_CHECK(now_s() - t0 < timeout_, "pddl ps client: parameter server ", p, " did not answer within ",
-                    timeout_, " s (PS failure aborts the job)");
-      }
-    }
-  }
+  void wait_done(Remote& r, int p) { pddl::ps::wait_done(r.ctrl->slot[w_], r.seq, timeout_, p); }
 
   int w_, dev_;
   double timeout_;

@@ -33,12 +33,44 @@ def preprocess(images: torch.Tensor, crop: int, training: bool, flip: Optional[t
     return x
 
 
-class ReferenceResNet50:
-    """Functional ResNet-50 over a flat parameter buffer (fp32, any device)."""
+class _RoundBF16(torch.autograd.Function):
+    """bf16 storage point: the value AND the gradient flowing back through it are rounded to
+    bf16 (where the HIP engine stores an activation / writes a dgrad output in bf16)."""
 
-    def __init__(self, layout: ParamLayout, bn_mode: str = "frozen"):
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+class _RoundGradBF16(torch.autograd.Function):
+    """Identity forward, bf16-rounded gradient (fp32 logits whose gradient is stored in bf16)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+class ReferenceResNet50:
+    """Functional ResNet-50 over a flat parameter buffer (fp32, any device).
+
+    bf16_points=True: the fp32 math with the HIP engine's bf16 storage points (models/engine.py)
+    -- the preprocessed input, every fused conv+BN(+residual)+ReLU output, the GAP output, conv
+    weights (straight-through: the weight gradient stays fp32), and the gradients stored at those
+    points on the way back (dlogits, dpooled, every dgrad output) -- so an engine-vs-reference
+    comparison measures accumulation order, not bf16 storage."""
+
+    def __init__(self, layout: ParamLayout, bn_mode: str = "frozen", bf16_points: bool = False):
         self.L = layout
         self.bn_mode = bn_mode
+        self.bf16 = bf16_points
         self.stats = None   # flat buffer holding the BN moving statistics (non-trainable)
         self._bound = None  # (flat tensor, {name: view}) of the last bind()
 
@@ -69,8 +101,13 @@ class ReferenceResNet50:
             return self._bound[1][f"{layer}/{kind}:0"]
         return self.L.view(params, layer, kind)
 
+    def _q(self, x):
+        return _RoundBF16.apply(x) if self.bf16 else x
+
     def _conv(self, params, x, c, pad_explicit=False):
         w = self._w(params, c.name, "kernel").permute(0, 3, 1, 2)
+        if self.bf16:
+            w = w + (w.to(torch.bfloat16).float() - w).detach()
         b = self._w(params, c.name, "bias")
         pad = 0 if pad_explicit else c.pad
         return F.conv2d(x, w, b, stride=c.stride, padding=pad)
@@ -96,25 +133,30 @@ class ReferenceResNet50:
     def features(self, params, x, training=True):
         L = self.L
         s = L.stem
-        x = F.pad(x, (3, 3, 3, 3))
-        x = F.relu(self._bn(params, self._conv(params, x, s, pad_explicit=True), s, training))
+        q = self._q
+        x = q(F.pad(x, (3, 3, 3, 3)))
+        x = q(F.relu(self._bn(params, self._conv(params, x, s, pad_explicit=True), s, training)))
         x = F.pad(x, (1, 1, 1, 1))
         x = F.max_pool2d(x, 3, 2)
         for b in L.blocks:
             c = b.convs
             if b.proj:
-                sc = self._bn(params, self._conv(params, x, c["0"]), c["0"], training)
+                sc = q(self._bn(params, self._conv(params, x, c["0"]), c["0"], training))
             else:
                 sc = x
-            y = F.relu(self._bn(params, self._conv(params, x, c["1"]), c["1"], training))
-            y = F.relu(self._bn(params, self._conv(params, y, c["2"]), c["2"], training))
+            y = q(F.relu(self._bn(params, self._conv(params, x, c["1"]), c["1"], training)))
+            y = q(F.relu(self._bn(params, self._conv(params, y, c["2"]), c["2"], training)))
             y = self._bn(params, self._conv(params, y, c["3"]), c["3"], training)
-            x = F.relu(y + sc)
-        return x.mean(dim=(2, 3))
+            x = q(F.relu(y + sc))
+        return q(x.mean(dim=(2, 3)))
 
     def logits(self, params, x, training=True):
         f = self.features(params, x, training)
-        return f @ self._w(params, "dense", "kernel").t() + self._w(params, "dense", "bias")
+        w = self._w(params, "dense", "kernel")
+        if self.bf16:
+            w = w + (w.to(torch.bfloat16).float() - w).detach()
+        out = f @ w.t() + self._w(params, "dense", "bias")
+        return _RoundGradBF16.apply(out) if self.bf16 else out
 
 
 class TorchEngine:
@@ -125,14 +167,14 @@ class TorchEngine:
     """
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, device="cpu", bn_mode="frozen",
-                 num_classes: int = 1000):
+                 num_classes: int = 1000, bf16_points: bool = False):
         self.L = layout
         self.device = torch.device(device)
         self.batch = batch
         self.crop = crop
         self.params = torch.zeros(layout.total, dtype=torch.float32, device=self.device)
         self.grads = torch.zeros(layout.n_trainable, dtype=torch.float32, device=self.device)
-        self.model = ReferenceResNet50(layout, bn_mode)
+        self.model = ReferenceResNet50(layout, bn_mode, bf16_points=bf16_points)
         self.num_classes = num_classes
         self._leaf = None
 

@@ -13,6 +13,15 @@
 #     and corrupted inputs.
 #  3. ThreadSanitizer natively: the same driver, whose pool section runs concurrent callers
 #     that hand plain (non-atomic) buffers from the decode workers back to the caller.
+#  4. ThreadSanitizer + ASan/UBSan natively over the concurrent runtime cores (a libtorch
+#     Python process cannot run under TSan here): csrc/tests/fusion_core_test.cpp drives the
+#     fusion engine's worker / watchdog / caller threads (runtime/fusion_core.h) with a fake
+#     network completing collectives at random delays and a hung collective for the stall
+#     inspector; csrc/tests/ps_protocol_test.cpp runs the PS service loop against 4 worker
+#     threads over one control segment (runtime/ps_protocol.h), whose plain mailbox / receive
+#     buffer traffic is ordered only by the protocol's release / acquire sequence numbers.
+#     TSan uses ROCm's clang runtime: GCC 11's libtsan does not intercept
+#     pthread_cond_clockwait (std::condition_variable::wait_for) and reports a false "double lock".
 #
 #   bash scripts/sanitize_host.sh [pytest -k expression]
 set -euo pipefail
@@ -29,6 +38,16 @@ echo "== TSan: io core"
 g++ -std=c++17 -O1 -g -fsanitize=thread -I csrc -I /opt/conda/include \
     csrc/tests/io_core_test.cpp "$OUT/lib/libjpeg.so.9" -Wl,-rpath,"$PWD/$OUT/lib" -lpthread -o "$OUT/io_core_tsan"
 TSAN_OPTIONS=halt_on_error=1 "$OUT/io_core_tsan"
+CLANG=${CLANG:-/opt/rocm/llvm/bin/clang++}
+for t in fusion_core ps_protocol; do
+  echo "== TSan: $t"
+  "$CLANG" -std=c++17 -O1 -g -fsanitize=thread -I csrc "csrc/tests/${t}_test.cpp" -lpthread -o "$OUT/${t}_tsan"
+  TSAN_OPTIONS=halt_on_error=1 "$OUT/${t}_tsan"
+  echo "== ASan+UBSan: $t"
+  g++ -std=c++17 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -I csrc "csrc/tests/${t}_test.cpp" \
+      -lpthread -o "$OUT/${t}_asan"
+  ASAN_OPTIONS=detect_leaks=1:halt_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 "$OUT/${t}_asan"
+done
 echo "== UBSan: runtime + reader under the CPU tests"
 PDDL_SANITIZE=1 PDDL_BUILD_TEMP=/tmp/pddl_build_san python setup.py build_ext --build-lib "$OUT" \
     --build-temp /tmp/pddl_build_san > "$OUT/build.log" 2>&1 || { tail -30 "$OUT/build.log"; exit 1; }
