@@ -339,6 +339,16 @@ class PSClient {
   // push (op 0): send this worker's gradients, receive the updated shards; pull (op 1):
   // receive only.  Writes the received shards into `params` (flat).
   void exchange(Tensor grads, Tensor params, double lr, bool push) {
+    begin(grads, params, lr, push);
+    end(params);
+  }
+
+  // Split form, so a worker can overlap the round trip with its next step (the PS applies the
+  // update and snapshots the shard while the worker computes): begin() packs the gradients into
+  // the PS mailboxes and publishes the requests; end() waits for every PS and unpacks the fresh
+  // shards into `params`.  The mailbox is not touched again before end() returned.
+  void begin(Tensor grads, Tensor params, double lr, bool push) {
+    TORCH_CHECK(!in_flight_, "pddl ps: begin() while an exchange is in flight");
     TORCH_CHECK(params.is_contiguous() && params.scalar_type() == torch::kFloat32, "pddl ps: flat fp32 params");
     TORCH_CHECK((dev_ >= 0) == params.is_cuda(), "pddl ps: params on the worker's device");
     TORCH_CHECK(params.numel() >= flat_end_ && (!push || grads.numel() >= flat_end_),
@@ -362,6 +372,16 @@ class PSClient {
     }
     if (dev_ >= 0 && push) hck(hipStreamSynchronize(st), "sync push");   // peer writes complete + visible
     for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], ++r.seq, push ? OP_PUSH : OP_PULL, (float)lr);
+    in_flight_ = true;
+  }
+
+  void end(Tensor params) {
+    TORCH_CHECK(in_flight_, "pddl ps: end() without begin()");
+    TORCH_CHECK(params.is_contiguous() && params.scalar_type() == torch::kFloat32 && params.numel() >= flat_end_,
+                "pddl ps: flat fp32 params");
+    hipStream_t st = nullptr;
+    if (dev_ >= 0) st = at::hip::getCurrentHIPStream(dev_).stream();
+    in_flight_ = false;
     for (size_t p = 0; p < rem_.size(); ++p) {
       Remote& r = rem_[p];
       wait_done(r, (int)p);
@@ -376,7 +396,10 @@ class PSClient {
       }
     }
   }
+  bool in_flight() const { return in_flight_; }
+
   void stop() {
+    TORCH_CHECK(!in_flight_, "pddl ps: stop() while an exchange is in flight");
     for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], ++r.seq, OP_STOP, 0.f);
     for (size_t p = 0; p < rem_.size(); ++p) wait_done(rem_[p], (int)p);
   }
@@ -386,6 +409,7 @@ class PSClient {
 
   int w_, dev_;
   double timeout_;
+  bool in_flight_ = false;
   int64_t flat_end_ = 0;
   std::vector<Remote> rem_;
 };
@@ -407,5 +431,8 @@ void register_ps(py::module& m) {
            py::arg("job"), py::arg("ranges"), py::arg("worker"), py::arg("device"), py::arg("timeout_s") = 120.0,
            py::call_guard<py::gil_scoped_release>())
       .def("exchange", &PSClient::exchange, py::call_guard<py::gil_scoped_release>())
+      .def("begin", &PSClient::begin, py::call_guard<py::gil_scoped_release>())
+      .def("end", &PSClient::end, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("in_flight", &PSClient::in_flight)
       .def("stop", &PSClient::stop, py::call_guard<py::gil_scoped_release>());
 }

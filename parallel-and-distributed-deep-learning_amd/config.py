@@ -64,6 +64,7 @@ class TrainConfig:
     port_base: int = 12345                         # SlurmClusterResolver(port_base=12345) (multiworkers.py:16)
     min_shard_bytes: int = 256 << 10               # MinSizePartitioner (ps.py:77)
     shard_by: str = "batch"                        # hvd: batch-then-shard (hvd.py:77-78); mwms: element DATA
+    ps_overlap: bool = True                        # PS: a worker's push/pull round trip overlaps its next step
     # device / output
     device: str = "auto"                           # auto | cpu | cuda
     save: bool = True
@@ -155,6 +156,8 @@ def add_cli_args(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--no-graphs", action="store_false", dest="graphs", default=None)
     a("--roctx", action="store_true", default=None)
     a("--verbose", type=int)
+    a("--ps-sync", action="store_false", dest="ps_overlap", default=None,
+      help="PS: block on every push/pull round trip (no overlap with the next step)")
     return ap
 
 

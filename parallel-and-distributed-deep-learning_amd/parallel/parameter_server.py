@@ -20,6 +20,9 @@ MI355X-native design:
     peer-copies the fresh shard back (CPU roles: the same protocol in shared memory);
     PDDL_PS_IMPL=c10d selects the portable fallback: one 2-rank process group per
     (worker, PS) pair with RCCL / gloo send/recv served from Python threads;
+  * a worker's push / pull round trip overlaps its next step (cfg.ps_overlap, default; the
+    step then reads parameters one round trip older -- the reference's asynchronous PS has
+    unbounded staleness anyway); --ps-sync restores the blocking exchange per step;
   * control plane (closure scheduling, heartbeats, LR broadcast, stop) is the c10d TCPStore:
     a worker claims step tickets; the coordinator re-queues the ticket of a worker that misses
     its heartbeats (ClusterCoordinator's closure re-queue); PDDL_FAULT=kill_worker:<i>@<step>
@@ -347,15 +350,34 @@ class PSWorker:
         self.packed = [torch.empty(n, dtype=torch.float32, device=cl.device) for n in cl.sizes]
         self.widx = cl.rank - cl.num_ps
 
+    def _client(self):
+        if not hasattr(self, "cli"):
+            from ..ops.native import require_native
+            cl = self.cl
+            dev = cl.device.index if cl.device.type == "cuda" else -1
+            self.cli = require_native().PSClient(cl.job, cl.ranges, self.widx, dev,
+                                                 float(os.environ.get("PDDL_PS_TIMEOUT", "120")))
+        return self.cli
+
+    def exchange_begin(self, lr: float):
+        """Overlapped push (native data plane): pack + publish the gradients and return; the PS
+        applies them and snapshots the shard while this worker computes its next step, whose
+        forward therefore reads the parameters of the previous round trip (one more step of
+        staleness; the reference's async PS already has unbounded staleness, ps.py:80-84)."""
+        if self.cl.impl == "native":
+            self._client().begin(self.engine.grads, self.engine.params, lr, True)
+        else:
+            self._exchange(OP_PUSH, lr)
+
+    def exchange_end(self):
+        if self.cl.impl == "native" and self._client().in_flight:
+            self.cli.end(self.engine.params)
+            self.engine.after_update()
+
     def _exchange(self, op: float, lr: float):
         cl = self.cl
         if cl.impl == "native":
-            if not hasattr(self, "cli"):
-                from ..ops.native import require_native
-                dev = cl.device.index if cl.device.type == "cuda" else -1
-                self.cli = require_native().PSClient(cl.job, cl.ranges, self.widx, dev,
-                                                     float(os.environ.get("PDDL_PS_TIMEOUT", "120")))
-            self.cli.exchange(self.engine.grads, self.engine.params, lr, op == OP_PUSH)
+            self._client().exchange(self.engine.grads, self.engine.params, lr, op == OP_PUSH)
             self.engine.after_update()
             return
         ctrl = torch.tensor([op, lr], dtype=torch.float64, device=cl.device)
@@ -533,10 +555,15 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off)
             acc[:2] += s.detach().double().cpu()
             acc[2] += B
-            worker._exchange(OP_PUSH, lr)
+            if cfg.ps_overlap:
+                worker.exchange_end()            # the previous push's fresh parameters
+                worker.exchange_begin(lr)        # this push flies while the next step computes
+            else:
+                worker._exchange(OP_PUSH, lr)
             store.set(f"cur/{rank}", f"{epoch}:-1")
             store.add(f"done/{epoch}", 1)
             steps_done += 1
+        worker.exchange_end()                    # drain the last overlapped push of the epoch
         # epoch end: worker 0 (coordinator-side logic) validates and runs the callbacks
         store.add(f"acc/{epoch}/loss", int(acc[0].item() * 1e6))
         store.add(f"acc/{epoch}/correct", int(acc[1].item()))
