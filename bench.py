@@ -5,6 +5,7 @@
     python bench.py --gpus 8                          # spawns 8 rank processes (Horovod-style)
     python bench.py --gpus 8 --strategy mirrored      # ONE process drives 8 GPUs (in-process RCCL)
     python bench.py --gpus 8 --strategy multiworker --local-gpus 4   # 2 processes x 4 GPUs
+    python bench.py --gpus 8 --strategy ps --ps 2      # async parameter server: 2 PS + 6 workers
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8        # what the driver runs: 1 rank per GPU
 
@@ -19,6 +20,8 @@ scaling).  The step is the SAME strategy code the entry scripts run (parallel/st
   mirrored     imagenet-resnet50-mirror.py: 1 process, R GPUs, native RcclComm (ncclCommInitAll),
                per-device HIP-graph segments with grouped bucket all-reduces between them.
   multiworker  imagenet-resnet50-multiworkers.py: P processes x R GPUs in one RCCL communicator.
+  ps           imagenet-resnet50-ps.py: P parameter servers + W workers (roles are processes),
+               asynchronous push/pull over the native HIP-IPC data plane.
 
 The full training step (preprocess, forward, backward, all-reduce, optimizer, weight re-prep)
 is inside the timed region: W untimed warmup steps, then K timed steps bracketed by a barrier
@@ -50,7 +53,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1, help="total GPUs (ranks x local GPUs) of the job")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--strategy", default="horovod", choices=["horovod", "mirrored", "multiworker"])
+    ap.add_argument("--strategy", default="horovod", choices=["horovod", "mirrored", "multiworker", "ps"])
+    ap.add_argument("--ps", type=int, default=None, help="ps: parameter-server roles (default gpus // 4, >= 1)")
     ap.add_argument("--local-gpus", type=int, default=1, help="multiworker: GPUs per worker process")
     # Per-GPU batch sized for 288 GB HBM3E (BASELINE north star): 1024 is the largest batch whose
     # biggest activation (conv1 output, 1.6 GB) stays inside the kernels' 31-bit buffer offsets.
@@ -265,11 +269,62 @@ def run(args):
     return 0
 
 
+def run_ps(args):
+    """BASELINE config 5: asynchronous parameter server (imagenet-resnet50-ps.py) with P PS roles
+    and W = gpus - P workers, one GPU each, the native HIP-IPC data plane over xGMI.  One
+    untimed warmup epoch, then a timed epoch of `steps` worker steps claimed by the workers
+    asynchronously; value = aggregate worker images/sec of the timed epoch (worker 0's clock
+    over every worker's training steps, parameter_server.py)."""
+    import pddl  # noqa: F401
+    from pddl.config import make_config
+    from pddl.parallel.parameter_server import run_ps_job
+    n_ps = args.ps if args.ps is not None else max(1, args.gpus // 4)
+    n_w = args.gpus - n_ps
+    if n_w < 1:
+        fail(f"--gpus {args.gpus} leaves no worker next to {n_ps} parameter server(s)")
+    if args.device == "cuda" and not rehearsing():
+        have = visible_gpus()
+        if have < args.gpus:
+            fail(f"--gpus {args.gpus} but only {have} GPU(s) are visible")
+    cfg = make_config("ps", batch_size=args.batch, crop=args.crop, image_size=args.image_size,
+                      optimizer="adam", lr=1e-3, bn_mode=args.bn_mode, device=args.device, data="synthetic",
+                      steps_per_epoch=args.steps, validation_steps=0, epochs=2, save=False, verbose=0,
+                      train_images=max(1_281_167, args.steps * args.batch), num_ps=n_ps, num_workers=n_w)
+    t0 = time.perf_counter()
+    res = run_ps_job(cfg, num_ps=n_ps, num_workers=n_w, return_results=True)
+    wall = time.perf_counter() - t0
+    hist = [r[3] for r in res if r[0] == "worker" and r[3]]
+    if not hist or len(hist[0]) < 2:
+        fail("parameter-server job returned no timed epoch")
+    ep = hist[0][1]
+    ips = ep["images_per_sec"]
+    print(json.dumps({
+        "metric": METRIC, "value": round(ips, 2), "unit": "images/sec", "n_gpus": args.gpus, "steps": args.steps,
+        "warmup": args.steps, "ms_per_step": round(args.batch * n_w / ips * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if args.device == "cpu" else "bf16",
+        "data": f"synthetic (uint8 3x{args.image_size}x{args.image_size}, random labels, random-init weights)",
+        "config": {"model": "ResNet-50 Keras-v1 (25,636,712 params, random init)", "global_batch": args.batch * n_w,
+                   "per_gpu_batch": args.batch, "seq_len": None, "image_size": args.crop,
+                   "parallelism": f"ps{n_ps}+w{n_w}", "strategy":
+                   f"async parameter server: {n_ps} PS + {n_w} workers, native HIP-IPC push/pull, PS-side fused Adam",
+                   "replicas": n_w, "optimizer": "adam", "bn": args.bn_mode, "hip_graph": False,
+                   "device": "cpu" if args.device == "cpu" else "MI355X",
+                   "note": "ms_per_step = one synchronous-equivalent step of all workers; warmup = one untimed epoch"},
+        "per_gpu_images_per_sec": round(ips / n_w, 2), "steps_timed_epoch": ep.get("steps"),
+        "job_wall_s": round(wall, 1), **({"rehearsal": True} if rehearsing() else {}),
+    }), flush=True)
+    return 0
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     if args.gpus < 1:
         fail("--gpus must be >= 1")
+    if args.strategy == "ps":
+        if "WORLD_SIZE" in os.environ:
+            fail("--strategy ps spawns its own P + W role processes; do not launch it with torchrun")
+        return run_ps(args)
     torchrun = "WORLD_SIZE" in os.environ
     if not torchrun and args.gpus > 1 and args.strategy != "mirrored":
         if args.device == "cuda" and not rehearsing():

@@ -587,10 +587,11 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
                 store.set("stop", "1")
             logs["lr"] = lr
             history.append(logs)
-            print(f"Epoch {epoch + 1}/{cfg.epochs} - {logs['steps']}/{spe} steps - loss: {logs['loss']:.4f} - "
-                  f"accuracy: {logs['accuracy']:.4f}" + (f" - val_loss: {logs['val_loss']:.4f}"
-                                                          if 'val_loss' in logs else "")
-                  + f" - {logs['images_per_sec']:.1f} img/s", flush=True)
+            if cfg.verbose:
+                print(f"Epoch {epoch + 1}/{cfg.epochs} - {logs['steps']}/{spe} steps - loss: {logs['loss']:.4f} - "
+                      f"accuracy: {logs['accuracy']:.4f}" + (f" - val_loss: {logs['val_loss']:.4f}"
+                                                              if 'val_loss' in logs else "")
+                      + f" - {logs['images_per_sec']:.1f} img/s", flush=True)
             store.set(f"epoch_go/{epoch}", "1")
         else:
             _wait_key(store, f"epoch_go/{epoch}")

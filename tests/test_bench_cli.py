@@ -60,3 +60,14 @@ def test_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *SMALL], cwd=ROOT, env=e,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "rank(s)" in r.stderr
+
+
+def test_cpu_parameter_server_bench():
+    """--strategy ps: P PS + W worker role processes (BASELINE config 5's layout, here 1 + 2 on CPU),
+    one JSON line with the aggregate worker images/sec of the timed epoch."""
+    r = _bench("--gpus", "3", "--strategy", "ps", "--ps", "1", "--device", "cpu", "--steps", "4", "--batch", "2",
+               "--image-size", "32")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json(r)
+    assert out["n_gpus"] == 3 and out["config"]["parallelism"] == "ps1+w2" and out["steps_timed_epoch"] == 4
+    assert out["value"] > 0
