@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--knob", default="igemm_big", help="igemm knob to A/B (igemm_big, igemm_il, ...)")
     ap.add_argument("--variants", default="0,3", help="comma-separated knob values")
+    ap.add_argument("--wgrad-knob", default="wgrad8", help="wgrad knob to A/B")
+    ap.add_argument("--wgrad-variants", default="0,2", help="comma-separated wgrad knob values")
     ap.add_argument("--skip-lib", action="store_true", help="skip the MIOpen / hipBLASLt yardsticks")
     ap.add_argument("--set", default="", help="extra knobs for every variant, e.g. igemm8_min_tiles=1")
     a = ap.parse_args()
@@ -100,7 +102,8 @@ def main():
             res.append(brow)
         del am, bm, gm
         for kind, fn, knob, variants in (("igemm", fwd, a.knob, [int(v) for v in a.variants.split(",")]),
-                                          ("wgrad", wg, "wgrad", [0])):
+                                          ("wgrad", wg, a.wgrad_knob,
+                                           [int(v) for v in a.wgrad_variants.split(",")])):
             t = {v: [] for v in variants}
             for _ in range(a.rounds):
                 for v in variants:

@@ -716,8 +716,8 @@ static int igemm_rows_of(int cfg, int m) {
   return ((m + BM - 1) / BM) * (BM / igemm_wtm(cfg));
 }
 
-static int num_cus() {
-  static int cached[64] = {0};
+int num_cus() {
+  static int cached[64] = {0};   // (per device; a benign race writes the same value)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
   if (!cached[dev]) {

@@ -35,6 +35,16 @@ __device__ __forceinline__ int tr_swz128(int row) { return (((row >> 1) & 1) | (
 
 // BM = 128: 2x2 waves, wave tile 64 (co) x 64 (k).  BM = 64 (Cout = 64 layers: the stem and
 // stage 2): 1x4 waves, wave tile 64 x 32, gradient tile with 128-byte rows.
+// ds_read_b64_tr_b16 as inline asm: the builtin form makes the compiler drain every LDS-DMA
+// load in flight (vmcnt(0)) before each transposed read, which serialises the staging pipeline;
+// the asm form is invisible to its wait insertion, so the kernel waits itself (lgkmcnt(0) before
+// the MFMAs that consume the fragments).
+__device__ __forceinline__ v4bf tr_read(const char* p) {
+  v4bf r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
+  return r;
+}
+
 template <bool FAST, int BM, int NSTAGE>  // NSTAGE: LDS buffers (the loop is written for 2)
 __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split, const int2* __restrict__ rowinfo) {
   constexpr int G_BYTES = 64 * BM * 2;        // 64 m-rows x BM bf16
@@ -170,21 +180,19 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ch = wm * 8 + i * 2 + (pp >> 1);
-        v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) v4bf*)(gb + goff[0] + ((ch ^ gsw[0]) << 4)));
-        v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) v4bf*)(gb + goff[1] + ((ch ^ gsw[1]) << 4)));
+        v4bf lo = tr_read(gb + goff[0] + ((ch ^ gsw[0]) << 4));
+        v4bf hi = tr_read(gb + goff[1] + ((ch ^ gsw[1]) << 4));
         af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int ch = wn * (WTN / 8) + j * 2 + (pp >> 1);
-        v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) v4bf*)(xb + roff[0] + ((ch ^ rsw[0]) << 4)));
-        v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (__attribute__((address_space(3))) v4bf*)(xb + roff[1] + ((ch ^ rsw[1]) << 4)));
+        v4bf lo = tr_read(xb + roff[0] + ((ch ^ rsw[0]) << 4));
+        v4bf hi = tr_read(xb + roff[1] + ((ch ^ rsw[1]) << 4));
         bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the asm fragment reads)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -223,6 +231,271 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// 8-phase 256 (co) x 256 (k) weight gradient: the igemm8_kernel schedule (igemm.hip) on the
+// transposed-operand GEMM.  8 waves, one 128 KiB block per CU; per 64-row m-tile four 16 KiB
+// half-tiles {G cols 0-127, X cols 0-127, X cols 128-255, G cols 128-255} ([64 m][128] bf16,
+// tr_swz-swizzled rows) staged LEAD = 5 halves ahead with counted vmcnt and raw barriers; each
+// m-tile is reduced in 4 phases over the 128x128 output quadrants in snake order (every wave
+// owns a 64 (co) x 32 (k) sub-tile of each quadrant: 16 MFMAs per phase), fragments read with
+// ds_read_b64_tr_b16 as in wgrad_kernel.  The m reduction is split over workgroups sized to one
+// block per CU and the fp32 partial tiles are added with row-contiguous atomics.  The generic
+// (padded / strided) gather decodes each row's im2col geometry arithmetically (magic-number
+// division) when its m-tile is staged: an ordinary global load of a row table would make the
+// compiler drain the LDS-DMA queue (vmcnt(0)) at its first use.
+// Host-computed im2col stepping of wgrad8_kernel's generic gather (64 rows per m-tile).
+struct Wg8Geom {
+  uint64_t mg_howo, mg_wo;   // magic divisors for the starting row of a split
+  int dho, dwo, dpix;        // 64 rows as (output rows, output cols) and the tap-(0,0) pixel delta
+  int carry_w, carry_h;      // pixel delta of a column -> row carry and of a row -> image carry
+  uint32_t row_unit;         // bit r*S for every kernel row r
+};
+
+template <bool FAST, bool STAGGER>
+__global__ void __launch_bounds__(512, 1) wgrad8_kernel(WgradParams p, int m_per_split, Wg8Geom geo, int probe) {
+  constexpr int HALF = 16384, BUF = 4 * HALF, LEAD = 5;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tco = (p.Cout + 255) / 256, tk = (p.K + 255) / 256, ntiles = tco * tk;
+  const int splits = (p.M + m_per_split - 1) / m_per_split;
+  const int wg = xcd_remap(blockIdx.x, ntiles * splits);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int co0 = (tile % tco) * 256, k0 = (tile / tco) * 256;
+  const int mbeg = split * m_per_split;
+  const int mend = min(p.M, mbeg + m_per_split);
+  const int nit = (mend - mbeg + 63) / 64;
+  if (nit <= 0) return;   // (block-uniform, before any barrier)
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.g, p.M * p.ldg * 2);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, FAST ? p.M * p.ldx * 2 : p.N * p.H * p.W * p.C * 2);
+
+  // staging lanes: piece i of a half covers m-rows (2*wave + i)*4 .. +3, 16 chunks per row
+  const int lrow = lane >> 4, lpos = lane & 15;
+  int prow[2], pch[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    prow[i] = (2 * wave + i) * 4 + lrow;
+    pch[i] = lpos ^ tr_swz(prow[i]);
+  }
+  uint32_t g_off[2][2], x_off[2][2], x_bit[2][2];
+  int x_delta2[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = co0 + 128 * h + pch[i] * 8;
+      g_off[h][i] = co >= p.Cout ? OOB_OFF : (uint32_t)((prow[i] * p.ldg + co) * 2);
+      const int kc = k0 + 128 * h + pch[i] * 8;
+      x_off[h][i] = (FAST && kc < p.K) ? (uint32_t)((prow[i] * p.ldx + kc) * 2) : OOB_OFF;
+      const int kk = k0 + 128 * h + (pch[i] >> 3) * 64;   // the lane's 64-column sub-half
+      const int rs = kk / p.C, c0 = kk - rs * p.C, r = rs / p.S, s = rs - r * p.S;
+      x_delta2[h][i] = ((r * p.W + s) * p.C + c0 + (pch[i] & 7) * 8) * 2;
+      x_bit[h][i] = kk < p.K ? 1u << (r * p.S + s) : 0u;   // the lane's tap in a row's valid-tap mask
+    }
+  // generic gather: each lane stages 2 rows of every m-tile (m = mb + prow[i]).  Their im2col
+  // geometry -- output position (ho, wo) and the input pixel of tap (0, 0) -- advances by 64
+  // rows per m-tile with mixed-radix carries (host-computed steps, no divisions or full-rate
+  // multiplies in the loop); the valid-tap mask follows from the window's clipped row / column
+  // ranges: (column bits) x (row-start bits of the valid rows).
+  int gho[2] = {0, 0}, gwo[2] = {0, 0}, gpix[2] = {0, 0};
+  int rpix2[2] = {0, 0};
+  uint32_t rmask[2] = {0u, 0u};
+  if (!FAST) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = mbeg + prow[i];
+      const int n = fdiv(m, geo.mg_howo), rem = m - n * p.Ho * p.Wo;
+      gho[i] = fdiv(rem, geo.mg_wo);
+      gwo[i] = rem - gho[i] * p.Wo;
+      gpix[i] = (n * p.H + gho[i] * p.stride - p.pad) * p.W + gwo[i] * p.stride - p.pad;
+    }
+  }
+  auto row_geometry = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int hi = __mul24(gho[i], p.stride) - p.pad, wi = __mul24(gwo[i], p.stride) - p.pad;
+      const int rmin = max(0, -hi), rmax = min(p.R, p.H - hi);
+      const int cmin = max(0, -wi), cmax = min(p.S, p.W - wi);
+      const uint32_t cols = (cmax > cmin) ? (~0u >> (32 - cmax)) & ~((1u << cmin) - 1u) : 0u;
+      const uint32_t rows = (rmax > rmin) ? geo.row_unit & (~0u >> (32 - rmax * p.S)) & ~((1u << (rmin * p.S)) - 1u) : 0u;
+      rmask[i] = mb + prow[i] < mend ? cols * rows : 0u;
+      rpix2[i] = __mul24(gpix[i], 2 * p.C);
+      // advance to the next m-tile (64 rows)
+      gwo[i] += geo.dwo;
+      gho[i] += geo.dho;
+      gpix[i] += geo.dpix;
+      if (gwo[i] >= p.Wo) { gwo[i] -= p.Wo; gho[i] += 1; gpix[i] += geo.carry_w; }
+      if (gho[i] >= p.Ho) { gho[i] -= p.Ho; gpix[i] += geo.carry_h; }
+    }
+  };
+  const int NH = 4 * nit;
+  // half-tile j = 4 t + part of m-tile t: part 0 G cols 0-127, 1 X cols 0-127, 2 X cols 128-255,
+  // 3 G cols 128-255 (first read in phases 0, 0, 1, 2 of the tile, as in igemm8_kernel)
+  auto stage_half = [&](int j, int part) {
+    const int mb = mbeg + (j >> 2) * 64;
+    char* base = smem + ((j >> 2) & 1) * BUF;
+    const bool full = mb + 64 <= mend;
+    if (part == 0 || part == 3) {
+      const int h = part == 0 ? 0 : 1;
+      char* hb = base + (part == 0 ? 0 : 3) * HALF;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t off = (full || mb + prow[i] < mend) ? g_off[h][i] : OOB_OFF;
+        buf_lds16(rg, LDS_PTR(hb + (2 * wave + i) * 1024), off, mb * p.ldg * 2);
+      }
+    } else {
+      const int h = part == 1 ? 0 : 1;
+      char* hb = base + part * HALF;
+      if (!FAST && part == 1) row_geometry(mb);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (FAST) {
+          const bool mok = full || mb + prow[i] < mend;
+          buf_lds16(rx, LDS_PTR(hb + (2 * wave + i) * 1024), mok ? x_off[h][i] : OOB_OFF, mb * p.ldx * 2);
+        } else {
+          const uint32_t off = (rmask[i] & x_bit[h][i]) ? (uint32_t)(rpix2[i] + x_delta2[h][i]) : OOB_OFF;
+          buf_lds16(rx, LDS_PTR(hb + (2 * wave + i) * 1024), off, 0);
+        }
+      }
+    }
+  };
+#define WG8_WAIT_BARRIER(need, last)                                                              \
+  {                                                                                               \
+    const int after_ = (last) - (need);                                                           \
+    if (after_ >= 3) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");                \
+    else if (after_ == 2) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");           \
+    else if (after_ == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");           \
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");                            \
+  }
+
+  v4f acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int j = 0; j < LEAD; ++j)
+    if (j < NH) stage_half(j, j & 3);
+  {
+    const int last = (LEAD < NH ? LEAD : NH) - 1;
+    WG8_WAIT_BARRIER(1, last)
+  }
+  if (STAGGER && wm == 1) asm volatile("s_barrier" ::: "memory");
+
+  // fragment-read geometry (T10): group G = lane>>4 reads m-rows 8G + 4h + q, q = (lane&15)>>2,
+  // columns 4p..4p+3 of its 8-column chunk, p = lane&3
+  const int Gq = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  int roff[2][2], rsw[2][2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int row = kh * 32 + 8 * Gq + 4 * h2 + qq;
+      roff[kh][h2] = row * 256 + (pp & 1) * 8;
+      rsw[kh][h2] = tr_swz(row);
+    }
+  v8bf af[2][4], bfr[2][2];
+  for (int t = 0; t < nit; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int qm = (q == 0 || q == 1) ? 0 : 1;
+      const int qn = (q == 0 || q == 3) ? 0 : 1;
+      const bool loadA = (q == 0 || q == 2), loadB = (q != 2);
+      if (loadB) {
+        const char* Xs = buf + (qn == 0 ? 1 : 2) * HALF;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int ch = wn * 4 + j * 2 + (pp >> 1);
+            v4bf lo = tr_read(Xs + roff[kh][0] + ((ch ^ rsw[kh][0]) << 4));
+            v4bf hi = tr_read(Xs + roff[kh][1] + ((ch ^ rsw[kh][1]) << 4));
+            bfr[kh][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (loadA) {
+        const char* Gs = buf + (qm == 0 ? 0 : 3) * HALF;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int ch = wm * 8 + i * 2 + (pp >> 1);
+            v4bf lo = tr_read(Gs + roff[kh][0] + ((ch ^ rsw[kh][0]) << 4));
+            v4bf hi = tr_read(Gs + roff[kh][1] + ((ch ^ rsw[kh][1]) << 4));
+            af[kh][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+      }
+      const int js = 4 * t + q + LEAD;
+      if (js < NH) stage_half(js, (q + LEAD) & 3);
+      const int last = (js < NH ? js : NH - 1);
+      if (q == 0) WG8_WAIT_BARRIER(4 * t + 2, last)
+      else if (q == 1) WG8_WAIT_BARRIER(4 * t + 3, last)
+      else if (q == 3 && t + 1 < nit) WG8_WAIT_BARRIER(4 * t + 5, last)
+      else asm volatile("s_barrier" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the asm fragment reads)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kh][i], bfr[kh][j], acc[qm][qn][i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+  }
+#undef WG8_WAIT_BARRIER
+  if (STAGGER && wm == 0) asm volatile("s_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (probe & 1) {   // (timing probe only: main loop without the atomic epilogue)
+    if (acc[0][0][0][0][0] == 12345.f && acc[1][1][3][1][3] == 54321.f) p.dw[tid] = 0.f;
+    return;
+  }
+
+  // epilogue: per quadrant, the wave's 64 x 32 partial tile through LDS (2 passes of 32 rows),
+  // then row-contiguous atomics: 2 rows of 32 floats (2 x 128 B) per wave instruction
+  constexpr int EPI_LD = 36;
+  float* stage = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
+  const int rsub = lane >> 5, cl = lane & 31;
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn) {
+      const int kcol = k0 + qn * 128 + wn * 32 + cl;
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              stage[(i2 * 16 + (lane >> 4) * 4 + jj) * EPI_LD + j * 16 + (lane & 15)] = acc[qm][qn][pass * 2 + i2][j][jj];
+        __syncthreads();
+        if (kcol < p.K) {
+          for (int r = 0; r < 32; r += 2) {
+            const int co = co0 + qm * 128 + wm * 64 + pass * 32 + r + rsub;
+            if (co < p.Cout) unsafeAtomicAdd(p.dw + (long)co * p.ld_dw + kcol, stage[(r + rsub) * EPI_LD + cl]);
+          }
+        }
+        __syncthreads();
+      }
+    }
+}
+
 // rowinfo[m] = {(n*H + ho*stride - pad)*W + wo*stride - pad, bit (r*S + s) set iff tap (r, s)
 // of output row m reads inside the image}.
 __global__ void rowinfo_kernel(int2* __restrict__ out, int M, int Ho, int Wo, int H, int W, int stride, int pad,
@@ -259,6 +532,8 @@ static const int2* rowinfo_for(const WgradParams& p, hipStream_t stream, const c
 }
 
 int g_wgrad_variant = 0;   // A/B knob (unused: one pipeline depth remains)
+int g_wgrad8 = 1;          // 8-phase 256x256 wgrad8_kernel for Cout >= 256, K >= 256: 0 off, 1 on, 2 with the
+                           // wave-row stagger (measured slower here); +8 (probe): skip the atomic epilogue
 
 static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream);
 
@@ -289,6 +564,40 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
   if ((fast ? (long)p.M * p.ldx : (long)p.N * p.H * p.W * p.C) * 2 >= (1L << 31) ||
       (long)p.M * p.ldg * 2 >= (1L << 31))
     return "wgrad: operand too large for 31-bit buffer offsets";
+  if (g_wgrad8 && p.Cout >= 256 && p.K >= 256 && !window && p.splits <= 0 &&
+      (fast || ((long)p.N * p.H * p.W < (1L << 22) && 2L * p.C < (1L << 23)))) {
+    // one 256x256 block per CU: split the m reduction so tiles x splits ~ one round of CUs,
+    // each split at least 16 m-tiles (1024 rows)
+    const int cus = num_cus();
+    const int nt8 = ((p.Cout + 255) / 256) * ((p.K + 255) / 256);
+    int sp = (cus + nt8 / 2) / nt8;
+    const int cap = (p.M + 1023) / 1024;
+    if (sp > cap) sp = cap;
+    if (sp < 1) sp = 1;
+    int mps = ((p.M + sp - 1) / sp + 63) / 64 * 64;
+    sp = (p.M + mps - 1) / mps;
+    Wg8Geom geo{};
+    geo.mg_howo = fdiv_magic(p.Ho * p.Wo);
+    geo.mg_wo = fdiv_magic(p.Wo);
+    {
+      const int HoWo = p.Ho * p.Wo, dn = 64 / HoWo, rem = 64 % HoWo;
+      geo.dho = rem / p.Wo;
+      geo.dwo = rem % p.Wo;
+      geo.dpix = dn * p.H * p.W + geo.dho * p.stride * p.W + geo.dwo * p.stride;
+      geo.carry_w = p.stride * p.W - p.Wo * p.stride;
+      geo.carry_h = p.H * p.W - p.Ho * p.stride * p.W;
+      for (int r = 0; r < p.R; ++r) geo.row_unit |= 1u << (r * p.S);
+    }
+    if ((g_wgrad8 & 7) == 2) {
+      if (fast) hipLaunchKernelGGL((wgrad8_kernel<true, true>), dim3(nt8 * sp), dim3(512), 0, stream, p, mps, geo, g_wgrad8 >> 3);
+      else hipLaunchKernelGGL((wgrad8_kernel<false, true>), dim3(nt8 * sp), dim3(512), 0, stream, p, mps, geo, g_wgrad8 >> 3);
+    } else {
+      if (fast) hipLaunchKernelGGL((wgrad8_kernel<true, false>), dim3(nt8 * sp), dim3(512), 0, stream, p, mps, geo, g_wgrad8 >> 3);
+      else hipLaunchKernelGGL((wgrad8_kernel<false, false>), dim3(nt8 * sp), dim3(512), 0, stream, p, mps, geo, g_wgrad8 >> 3);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? nullptr : hipGetErrorString(e);
+  }
   const int BM = p.Cout <= 64 ? 64 : 128;
   const int ntiles = ((p.Cout + BM - 1) / BM) * ((p.K + 127) / 128);
   int splits = p.splits;

@@ -358,6 +358,41 @@ def test_wgrad_dual_and_padded_k():
     assert rel(dw, ref) < 5e-3
 
 
+@pytest.mark.parametrize("stagger", [1, 2])
+@pytest.mark.parametrize("case", [
+    (4, 14, 1024, 256, 1, 1, 0),     # 1x1 s1 (direct rows), K = 1024
+    (8, 14, 256, 256, 3, 1, 1),      # 3x3 pad 1: arithmetic im2col gather, 9 taps
+    (4, 14, 256, 256, 3, 2, 1),      # 3x3 s2 (v1.5 downsampling conv2)
+    (4, 14, 512, 1024, 1, 2, 0),     # 1x1 s2 projection: gather path with one tap
+    (3, 11, 264, 320, 1, 1, 0),      # M, Cout and K tails of the 256x256 tile
+    (32, 14, 256, 512, 1, 1, 0),     # several m splits per tile
+])
+def test_wgrad8_vs_fp32(case, stagger):
+    """8-phase 256x256 weight-gradient kernel against the fp32 reference and the 128-wide
+    kernel, repeated (a staging race would show up as a changing result)."""
+    torch.manual_seed(31)
+    n, h, cin, co, r, st, pad = case
+    ho = (h + 2 * pad - r) // st + 1
+    x = rnd(n, h, h, cin)
+    g = rnd(n, ho, ho, co)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (co, cin, r, r),
+                                      g.float().permute(0, 3, 1, 2), stride=st, padding=pad)
+    ref = ref.permute(0, 2, 3, 1).reshape(co, -1)
+    outs = []
+    try:
+        for kv in (0, stagger, stagger, stagger):
+            N().set_variant("wgrad8", kv)
+            dw = torch.zeros(co, r * r * cin, device=dev)
+            N().wgrad(x, h, h, r, r, st, pad, ho, ho, g, None, 0, dw, r * r * cin, 0)
+            assert rel(dw, ref) < 5e-3
+            outs.append(dw)
+    finally:
+        N().set_variant("wgrad8", 1)
+    for o in outs[1:]:
+        assert rel(o, outs[0]) < 1e-4
+    assert rel(outs[2], outs[1]) < 1e-5
+
+
 @pytest.mark.parametrize("variant,h", [(0, 12), (0, 13), (1, 12), (1, 13), (2, 13), (3, 12), (3, 18)])
 def test_maxpool_and_gap(variant, h):
     """Max pool (pad 1, 3x3/s2; strip / block kernels and the per-pixel ones) against
