@@ -88,26 +88,50 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
     }
   }
   constexpr int NIT = 32 / RPI;
-  uint4 pre[PF ? (TM / 2) * NIT : 1];
-  uint32_t pre_bits[PF ? TM / 2 : 1];
-  const bool pf_bits = PF && p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
-  if (PF) {
-    const bf16_t* src = p.mode == EPI_FWD ? p.res : p.add;
-    const int ldp = p.mode == EPI_FWD ? p.ld_res : p.ld_add;
+  // The per-element operand (forward residual / dgrad `add` + ReLU bits) is loaded ahead of
+  // the stores that consume it: PF for the whole sub-tile before the staging, otherwise one
+  // 32-row pass at a time at the top of the pass.  (Loaded inside the store loop, each load
+  // would wait behind the previous iteration's store -- `out` may alias `add` as far as the
+  // compiler knows -- and the pass would pay NIT serialised HBM round trips.)
+  uint4 pre[PF ? (TM / 2) * NIT : NIT];
+  uint32_t pre_bits[PF ? (TM / 2) * NIT : NIT];
+  const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
+  const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
+  const bf16_t* pre_src = p.mode == EPI_FWD ? p.res : p.add;
+  const int pre_ld = p.mode == EPI_FWD ? p.ld_res : p.ld_add;
+  // Branch-free loads (row and column clamped into the tensor, the value zeroed afterwards):
+  // under an exec branch the compiler completes each load (and everything issued before it)
+  // inside the branch, which serialises the prefetch into one HBM round trip per row.
+  // Both loads are issued whenever either operand is in use (an unused one reads the output
+  // tensor's first element) so that neither sits under a uniform branch either.
+  const int gn_c = col_ok ? gn : 0;
+  const bf16_t* psrc = pre_on ? pre_src : reinterpret_cast<const bf16_t*>(p.out);
+  const long pld = pre_on ? pre_ld : 0;
+  const int pcol = pre_on ? gn_c : 0;
+  const uint8_t* bsrc = pf_bits ? p.bits_mask : reinterpret_cast<const uint8_t*>(p.out);
+  const long bld = pf_bits ? p.ld_bits_mask : 0;
+  const int bcol = pf_bits ? (gn_c >> 3) : 0;
+  auto prefetch = [&](int pass, uint4* dst, uint32_t* bits) {
 #pragma unroll
-    for (int pass = 0; pass < TM / 2; ++pass) {
-      pre_bits[pass] = 0;
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int gm = mb + pass * 32 + it * RPI + rr;
-        const bool ok = gm < p.M && col_ok;
-        pre[pass * NIT + it] = ok ? *reinterpret_cast<const uint4*>(src + (long)gm * ldp + gn) : make_uint4(0, 0, 0, 0);
-        if (pf_bits && ok) pre_bits[pass] |= (uint32_t)p.bits_mask[(long)gm * p.ld_bits_mask + (gn >> 3)] << (8 * it);
-      }
+    for (int it = 0; it < NIT; ++it) {
+      const int gm = mb + pass * 32 + it * RPI + rr;
+      const bool ok = gm < p.M && col_ok;
+      const long gr = gm < p.M ? gm : p.M - 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + pcol);
+      const uint32_t b = bsrc[gr * bld + bcol];
+      dst[it] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
+      bits[it] = (ok && pf_bits) ? b : 0u;
     }
+  };
+  if (PF && (pre_on || pf_bits)) {
+#pragma unroll
+    for (int pass = 0; pass < TM / 2; ++pass) prefetch(pass, pre + pass * NIT, pre_bits + pass * NIT);
   }
 #pragma unroll
   for (int pass = 0; pass < TM / 2; ++pass) {
+    if (!PF && (pre_on || pf_bits)) prefetch(pass, pre, pre_bits);
+    const uint4* ppre = PF ? pre + pass * NIT : pre;
+    const uint32_t* pbits = PF ? pre_bits + pass * NIT : pre_bits;
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -129,9 +153,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
           for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
           if (p.res) {
             float rv[8];
-            uint4 r4;   // (if/else, not ?: -- an lvalue select would force `pre` into scratch)
-            if (PF) r4 = pre[pass * NIT + it];
-            else r4 = *reinterpret_cast<const uint4*>(p.res + (long)gm * p.ld_res + gn);
+            const uint4 r4 = ppre[it];
             unpack8(r4, rv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += rv[e];
@@ -178,8 +200,8 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
             for (int e = 0; e < 8; ++e) w[e] = (q == 0) ? v[e] : 0.f;
             if (p.add) {
               float av[8];
-              uint4 a4;
-              if (PF) a4 = pre[pass * NIT + it];
+              uint4 a4;   // (if/else, not ?: -- an lvalue select would force `pre` into scratch)
+              if (!p.up2) a4 = ppre[it];
               else a4 = *reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn);
               unpack8(a4, av);
 #pragma unroll
@@ -192,7 +214,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
               for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
             } else if (p.bits_mask) {
               uint32_t byte;
-              if (pf_bits) byte = (pre_bits[pass] >> (8 * it)) & 0xffu;
+              if (pf_bits) byte = pbits[it];
               else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
@@ -811,7 +833,7 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
   // K >= 256 but -8-10% for the single-stage K <= 128 tiles, whose occupancy the 24 extra
   // VGPRs cut from 3 to 2 waves per SIMD -- so dgrad uses it only on 2-stage tiles.
   const bool pf = g_igemm_pf && am == AM_DIRECT && cfg <= 1 &&
-                  ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && ns == 2));
+                  ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && (ns == 2 || g_igemm_pf == 2)));
   if (cfg == 4) {
 #define IG_8(AM_)                                                                                         \
   {                                                                                                       \

@@ -16,10 +16,12 @@ from pddl.ops.native import require_native   # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", choices=["wgrad", "fwd"], default="wgrad")
+    ap.add_argument("--op", choices=["wgrad", "fwd", "fwdres", "dgrad_add"], default="wgrad")
     ap.add_argument("--shape", default="1024,14,256,256,3,1,1", help="N,H,Cin,Cout,R,stride,pad")
     ap.add_argument("--set", default="", help="knobs, e.g. wgrad8=1,igemm8=2")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--drop", default="", help="dgrad_add: comma list of fused operands to leave out "
+                    "(bits, add, colsum) to price each one")
     a = ap.parse_args()
     N = require_native()
     for kv in filter(None, a.set.split(",")):
@@ -34,13 +36,30 @@ def main():
     dw = torch.zeros(co, r * r * c, device=dev)
     y = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
     sc, sh = torch.ones(co, device=dev), torch.zeros(co, device=dev)
+    res = torch.randn(n, ho, ho, co, device=dev).to(torch.bfloat16)
+    # dgrad of a 1x1 conv c -> co as the engine runs it (c1 of a bottleneck): g [n,ho,ho,co] ->
+    # dx [n,h,h,c] with the residual-gradient add, ReLU bitmask and fused column sums
+    gd = torch.randn(n, ho, ho, co, device=dev).to(torch.bfloat16)
+    wdt = (torch.randn(c, co, device=dev) * 0.05).to(torch.bfloat16)
+    add = torch.randn(n, h, h, c, device=dev).to(torch.bfloat16)
+    bits = torch.randint(0, 255, (n, h, h, c // 8), dtype=torch.uint8, device=dev)
+    dx = torch.empty(n, h, h, c, dtype=torch.bfloat16, device=dev)
+    part = torch.empty(N.igemm_partial_rows(n * h * h, c, co) * c, device=dev) if a.op == "dgrad_add" else None
 
     def step():
         if a.op == "wgrad":
             N.wgrad(x, h, h, r, r, st, pad, ho, ho, g, None, 0, dw, r * r * c, 0)
-        else:
+        elif a.op == "fwd":
             N.igemm(x, None, h, h, r, r, st, pad, ho, ho, w, 0, sc, sh, None, None, None, y, 1, None, 0, 0, 0, 0, 0,
                     None, None)
+        elif a.op == "fwdres":
+            N.igemm(x, None, h, h, r, r, st, pad, ho, ho, w, 0, sc, sh, res, None, None, y, 1, None, 0, 0, 0, 0, 0,
+                    None, None)
+        else:
+            drop = a.drop.split(",")
+            N.igemm(gd, None, h, h, 1, 1, 1, 0, h, h, wdt, 1, None, None, None, None if "bits" in drop else bits,
+                    None if "add" in drop else add, dx, 0, None, 0, 0, 0, 0, 0, None if "colsum" in drop else part,
+                    None)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
@@ -52,7 +71,7 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.iters
     flops = 2.0 * n * ho * ho * co * r * r * c
-    print(json.dumps({"op": a.op, "shape": a.shape, "set": a.set, "us": round(us, 1),
+    print(json.dumps({"op": a.op, "shape": a.shape, "set": a.set, "drop": a.drop, "us": round(us, 1),
                       "tflops": round(flops / us / 1e6, 1)}), flush=True)
 
 
