@@ -67,13 +67,15 @@ def parse(argv=None):
                     help="frozen = the reference's training=False BN (folded); train = batch statistics")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="fp32: the reference's precision on the fp32-MFMA HIP convolutions (models/engine_f32.py)")
     ap.add_argument("--graph", type=int, default=None,
                     help="HIP graphs: 1 GPU = whole step; mirrored = per-device segments (default on)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: BASELINE config 1 plumbing (fp32 PyTorch reference engine, gloo ranks)")
     args = ap.parse_args(argv)
     if args.batch is None:
-        args.batch = 32 if args.device == "cpu" else 1024
+        args.batch = 32 if args.device == "cpu" else (256 if args.precision == "fp32" else 1024)
     if args.crop is None:
         args.crop = args.image_size
     return args
@@ -139,7 +141,7 @@ def build_cfg(args, strategy):
                        image_size=args.image_size, optimizer=args.optimizer,
                        lr=1e-3 if args.optimizer == "adam" else 0.1, bn_mode=args.bn_mode,
                        bucket_mb=args.bucket_mb, grad_dtype=args.grad_dtype, device=args.device,
-                       graphs=graphs, data="synthetic_fixed", seed=0)
+                       graphs=graphs, data="synthetic_fixed", seed=0, precision=args.precision)
 
 
 def run(args):
@@ -246,7 +248,7 @@ def run(args):
             "metric": METRIC, "value": round(ips, 2), "unit": "images/sec", "n_gpus": args.gpus,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32" if cpu else "bf16",
+            "dtype": "fp32" if cpu else args.precision,
             "data": f"synthetic (uint8 3x{S}x{S}, random labels, random-init weights)",
             "config": {"model": "ResNet-50 Keras-v1 (25,636,712 params, random init)", "global_batch": total,
                        "per_gpu_batch": B, "seq_len": None, "image_size": args.crop,

@@ -202,6 +202,39 @@ void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
   ok(pddl::wgrad_launch(p, cur_stream()), "wgrad");
 }
 
+// fp32 convolution (reference precision): y[N,Ho,Wo,Cout] = conv(x[N,H,W,C], w[Cout, R*S*C]) (+ bias)
+void conv_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tensor w, OptT bias, Tensor y) {
+  pddl::ConvF32Params p{};
+  PCHECK(x.is_contiguous() && x.dim() == 4 && w.is_contiguous() && y.is_contiguous() && y.dim() == 4,
+         "conv_f32: contiguous NHWC x / y and [Cout, K] w");
+  p.x = f32p(x); p.N = (int)x.size(0); p.H = (int)x.size(1); p.W = (int)x.size(2); p.C = (int)x.size(3);
+  p.R = (int)R; p.S = (int)S; p.stride = (int)stride; p.pad = (int)pad;
+  p.Ho = (int)y.size(1); p.Wo = (int)y.size(2); p.M = p.N * p.Ho * p.Wo;
+  PCHECK(y.size(0) == p.N && p.Ho == (p.H + 2 * p.pad - p.R) / p.stride + 1 &&
+         p.Wo == (p.W + 2 * p.pad - p.S) / p.stride + 1, "conv_f32: output shape");
+  p.w = f32p(w); p.Cout = (int)w.size(0); p.K = (int)w.size(1);
+  PCHECK(y.size(3) == p.Cout && p.K == p.R * p.S * p.C, "conv_f32: weight shape");
+  if (bias.has_value()) { PCHECK(bias->numel() == p.Cout, "conv_f32: bias"); p.bias = f32p(*bias); }
+  p.y = f32p(y);
+  ok(pddl::conv_f32_launch(p, cur_stream()), "conv_f32");
+}
+
+// dw[Cout, R*S*C] += sum_m dy[m, Cout] * im2col(x)[m, :]
+void wgrad_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tensor dy, Tensor dw) {
+  pddl::ConvF32Params p{};
+  PCHECK(x.is_contiguous() && x.dim() == 4 && dy.is_contiguous() && dy.dim() == 4 && dw.is_contiguous(),
+         "wgrad_f32: contiguous NHWC x / dy and [Cout, K] dw");
+  p.x = f32p(x); p.N = (int)x.size(0); p.H = (int)x.size(1); p.W = (int)x.size(2); p.C = (int)x.size(3);
+  p.R = (int)R; p.S = (int)S; p.stride = (int)stride; p.pad = (int)pad;
+  p.Ho = (int)dy.size(1); p.Wo = (int)dy.size(2); p.M = p.N * p.Ho * p.Wo;
+  PCHECK(dy.size(0) == p.N && p.Ho == (p.H + 2 * p.pad - p.R) / p.stride + 1 &&
+         p.Wo == (p.W + 2 * p.pad - p.S) / p.stride + 1, "wgrad_f32: gradient shape");
+  p.Cout = (int)dy.size(3); p.K = p.R * p.S * p.C;
+  PCHECK(dw.size(0) == p.Cout && dw.numel() == (int64_t)p.Cout * p.K, "wgrad_f32: dw shape");
+  p.y = f32p(dy); p.dw = f32p(dw);
+  ok(pddl::wgrad_f32_launch(p, cur_stream()), "wgrad_f32");
+}
+
 void stem_s2d(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_t oy, int64_t ox, Tensor out,
               OptT crop_dev) {
   pddl::StemParams p{};
@@ -369,6 +402,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply, REL);
   m.attr("BNSTAT_LAYER_BYTES") = (int)sizeof(pddl::BnStatLayer);
   m.def("wgrad", &wgrad, REL);
+  m.def("conv_f32", &conv_f32, REL);
+  m.def("wgrad_f32", &wgrad_f32, REL);
   m.def("stem_s2d", &stem_s2d, REL);
   m.def("stem_wgrad_fold", &stem_wgrad_fold, REL);
   m.def("maxpool_fwd", &maxpool_fwd, REL);

@@ -1,0 +1,276 @@
+// fp32 convolution on the fp32 matrix cores (v_mfma_f32_16x16x4_f32) for the reference's
+// precision (imagenet-resnet50.py:56-62 builds and trains the Keras model in float32 with no
+// mixed-precision policy).  NHWC activations, OHWI weights, fp32 accumulate AND fp32 operands.
+//
+//   conv_f32_kernel:   y[m][n] = sum_k im2col(x)[m][k] * w[n][k] (+ bias[n])   (forward, and the
+//                      data gradient as a forward conv of dy with flipped/transposed weights)
+//   wgrad_f32_kernel:  dw[n][k] += sum_m dy[m][n] * im2col(x)[m][k]           (weight gradient,
+//                      m split over workgroups, fp32 atomics into dw)
+//
+// Both: 256 threads = 4 waves as 2 x 2 wave tiles of 32 x 32 (2 x 2 MFMA tiles), block tile
+// 64 x 64, reduction step 16.  The 16x16x4 fp32 MFMA takes ONE operand element per lane
+// (row lane % 16, reduction index lane / 16); the reduction order inside a 16-step is free, so
+// lane group g owns reduction indices 4g .. 4g+3 and reads its four MFMA operands with one
+// ds_read_b128 from a [row][16 (+4 pad)] LDS image.  Global loads for step t+1 are issued into
+// registers before step t's MFMAs and stored to the other LDS buffer after them: one barrier per
+// step.  VEC: C % 4 == 0, so a 4-wide reduction chunk is 4 channels of one tap (float4 gathers);
+// otherwise (the 3-channel stem) elements are gathered one by one.
+#include "common.h"
+#include "kernels.h"
+
+namespace pddl {
+
+namespace {
+constexpr int F_BM = 64, F_BN = 64, F_BK = 16, F_LD = F_BK + 4;   // LDS row: 16 floats + 4 pad
+
+__device__ __forceinline__ v4f mfma4(const float4& a, const float4& b, v4f c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+  return c;
+}
+
+// im2col element / 4-chunk of row geometry (n, hi0 = ho*stride - pad, wi0) at reduction index k
+template <bool VEC>
+__device__ __forceinline__ float4 gather4(const ConvF32Params& p, int n, int hi0, int wi0, bool mok, int k,
+                                          int S, int C) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!mok) return v;
+  if (VEC) {
+    if (k < p.K) {
+      const int rs = k / C, c = k - rs * C, r = rs / S, s = rs - r * S;
+      const int hi = hi0 + r, wi = wi0 + s;
+      if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+        v = *reinterpret_cast<const float4*>(p.x + ((long)(n * p.H + hi) * p.W + wi) * C + c);
+    }
+  } else {
+    float e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      e[q] = 0.f;
+      const int kk = k + q;
+      if (kk < p.K) {
+        const int rs = kk / C, c = kk - rs * C, r = rs / S, s = rs - r * S;
+        const int hi = hi0 + r, wi = wi0 + s;
+        if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+          e[q] = p.x[((long)(n * p.H + hi) * p.W + wi) * C + c];
+      }
+    }
+    v = make_float4(e[0], e[1], e[2], e[3]);
+  }
+  return v;
+}
+}  // namespace
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) conv_f32_kernel(ConvF32Params p) {
+  __shared__ __attribute__((aligned(16))) float As[2][F_BM * F_LD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][F_BN * F_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int mt = (p.M + F_BM - 1) / F_BM, nt = (p.Cout + F_BN - 1) / F_BN;
+  const int wg = xcd_remap(blockIdx.x, mt * nt);
+  const int tn = wg % nt, tm = wg / nt;
+  const int m0 = tm * F_BM, n0 = tn * F_BN;
+  // loader: thread -> (row tid/4, reduction chunk (tid%4)*4) of both tiles
+  const int lrow = tid >> 2, lk = (tid & 3) * 4;
+  const int m = m0 + lrow;
+  const bool mok = m < p.M;
+  int n = 0, hi0 = 0, wi0 = 0;
+  if (mok) {
+    n = fdiv(m, p.mg_howo);
+    const int rem = m - n * p.Ho * p.Wo, ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
+    hi0 = ho * p.stride - p.pad;
+    wi0 = wo * p.stride - p.pad;
+  }
+  const int wrow = n0 + lrow;
+  const bool wok = wrow < p.Cout;
+  auto load_b = [&](int k) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (wok) {
+      if (VEC) {
+        if (k < p.K) v = *reinterpret_cast<const float4*>(p.w + (long)wrow * p.K + k);
+      } else {
+        float e[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) e[q] = (k + q < p.K) ? p.w[(long)wrow * p.K + k + q] : 0.f;
+        v = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+    return v;
+  };
+  v4f acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int nk = (p.K + F_BK - 1) / F_BK;
+  float4 ra = gather4<VEC>(p, n, hi0, wi0, mok, lk, p.S, p.C);
+  float4 rb = load_b(lk);
+  *reinterpret_cast<float4*>(&As[0][lrow * F_LD + lk]) = ra;
+  *reinterpret_cast<float4*>(&Bs[0][lrow * F_LD + lk]) = rb;
+  __syncthreads();
+  const int fr = lane & 15, g = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) {
+      ra = gather4<VEC>(p, n, hi0, wi0, mok, (t + 1) * F_BK + lk, p.S, p.C);
+      rb = load_b((t + 1) * F_BK + lk);
+    }
+    float4 af[2], bf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      af[i] = *reinterpret_cast<const float4*>(&As[cur][(wm * 32 + i * 16 + fr) * F_LD + 4 * g]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      bf[j] = *reinterpret_cast<const float4*>(&Bs[cur][(wn * 32 + j * 16 + fr) * F_LD + 4 * g]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(af[i], bf[j], acc[i][j]);
+    if (t + 1 < nk) {
+      *reinterpret_cast<float4*>(&As[cur ^ 1][lrow * F_LD + lk]) = ra;
+      *reinterpret_cast<float4*>(&Bs[cur ^ 1][lrow * F_LD + lk]) = rb;
+    }
+    __syncthreads();
+  }
+  // D fragment: lane holds rows 4g .. 4g+3 of column lane % 16
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 32 + j * 16 + fr;
+    if (col >= p.Cout) continue;
+    const float b = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wm * 32 + i * 16 + 4 * g + e;
+        if (row < p.M) p.y[(long)row * p.Cout + col] = acc[i][j][e] + b;
+      }
+  }
+}
+
+// dw[n][k] += sum over this workgroup's m range of dy[m][n] * im2col(x)[m][k]
+template <bool VEC>
+__global__ void __launch_bounds__(256) wgrad_f32_kernel(ConvF32Params p, int m_per_split) {
+  __shared__ __attribute__((aligned(16))) float Gs[2][F_BM * F_LD];   // [n][m]
+  __shared__ __attribute__((aligned(16))) float Xs[2][F_BN * F_LD];   // [k][m]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tnn = (p.Cout + F_BM - 1) / F_BM, tkk = (p.K + F_BN - 1) / F_BN, ntiles = tnn * tkk;
+  const int splits = (p.M + m_per_split - 1) / m_per_split;
+  const int wg = xcd_remap(blockIdx.x, ntiles * splits);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int n0 = (tile % tnn) * F_BM, k0 = (tile / tnn) * F_BN;
+  const int mbeg = split * m_per_split, mend = min(p.M, mbeg + m_per_split);
+  // loader: thread -> (m row tid/16 of the 16-row step, 4 columns (tid%16)*4) of both tiles
+  const int lm = tid >> 4, lc = (tid & 15) * 4;
+  const int gcol = n0 + lc;
+  const int kq = k0 + lc;
+  auto load = [&](int mb, float4& gv, float4& xv) {
+    const int mm = mb + lm;
+    const bool ok = mm < mend;
+    gv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok && gcol < p.Cout) gv = *reinterpret_cast<const float4*>(p.y + (long)mm * p.Cout + gcol);
+    int n = 0, hi0 = 0, wi0 = 0;
+    if (ok) {
+      n = fdiv(mm, p.mg_howo);
+      const int rem = mm - n * p.Ho * p.Wo, ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
+      hi0 = ho * p.stride - p.pad;
+      wi0 = wo * p.stride - p.pad;
+    }
+    xv = gather4<VEC>(p, n, hi0, wi0, ok, kq, p.S, p.C);
+  };
+  auto store = [&](int buf, const float4& gv, const float4& xv) {   // transposed: [col][m]
+    Gs[buf][(lc + 0) * F_LD + lm] = gv.x;
+    Gs[buf][(lc + 1) * F_LD + lm] = gv.y;
+    Gs[buf][(lc + 2) * F_LD + lm] = gv.z;
+    Gs[buf][(lc + 3) * F_LD + lm] = gv.w;
+    Xs[buf][(lc + 0) * F_LD + lm] = xv.x;
+    Xs[buf][(lc + 1) * F_LD + lm] = xv.y;
+    Xs[buf][(lc + 2) * F_LD + lm] = xv.z;
+    Xs[buf][(lc + 3) * F_LD + lm] = xv.w;
+  };
+  v4f acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (mend - mbeg + F_BK - 1) / F_BK;
+  if (nsteps <= 0) return;   // (block-uniform, before any barrier)
+  float4 gv, xv;
+  load(mbeg, gv, xv);
+  store(0, gv, xv);
+  __syncthreads();
+  const int fr = lane & 15, g = lane >> 4;
+  for (int t = 0; t < nsteps; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nsteps) load(mbeg + (t + 1) * F_BK, gv, xv);
+    float4 af[2], bf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      af[i] = *reinterpret_cast<const float4*>(&Gs[cur][(wm * 32 + i * 16 + fr) * F_LD + 4 * g]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      bf[j] = *reinterpret_cast<const float4*>(&Xs[cur][(wn * 32 + j * 16 + fr) * F_LD + 4 * g]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(af[i], bf[j], acc[i][j]);
+    if (t + 1 < nsteps) store(cur ^ 1, gv, xv);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = k0 + wn * 32 + j * 16 + fr;
+    if (col >= p.K) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = n0 + wm * 32 + i * 16 + 4 * g + e;
+        if (row < p.Cout) unsafeAtomicAdd(p.dw + (long)row * p.K + col, acc[i][j][e]);
+      }
+  }
+}
+
+static const char* check_f32(const ConvF32Params& p) {
+  if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "conv_f32: empty problem";
+  if (p.K != p.R * p.S * p.C) return "conv_f32: K must be R*S*C";
+  if ((long)p.N * p.H * p.W * p.C >= (1L << 31) || (long)p.M * p.Cout >= (1L << 31))
+    return "conv_f32: tensor too large for 32-bit row indexing";
+  return nullptr;
+}
+
+const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
+  if (const char* e = check_f32(p)) return e;
+  p.mg_howo = fdiv_magic(p.Ho * p.Wo);
+  p.mg_wo = fdiv_magic(p.Wo);
+  const int grid = ((p.M + F_BM - 1) / F_BM) * ((p.Cout + F_BN - 1) / F_BN);
+  if (p.C % 4 == 0) hipLaunchKernelGGL(conv_f32_kernel<true>, dim3(grid), dim3(256), 0, stream, p);
+  else hipLaunchKernelGGL(conv_f32_kernel<false>, dim3(grid), dim3(256), 0, stream, p);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
+  if (const char* e = check_f32(p)) return e;
+  if (p.Cout % 4) return "wgrad_f32: Cout must be a multiple of 4";
+  p.mg_howo = fdiv_magic(p.Ho * p.Wo);
+  p.mg_wo = fdiv_magic(p.Wo);
+  const int ntiles = ((p.Cout + F_BM - 1) / F_BM) * ((p.K + F_BN - 1) / F_BN);
+  // ~4 workgroups per CU, each reducing at least 256 rows of m
+  int splits = (4 * num_cus() + ntiles - 1) / ntiles;
+  const int cap = (p.M + 255) / 256;
+  if (splits > cap) splits = cap;
+  if (splits < 1) splits = 1;
+  int mps = ((p.M + splits - 1) / splits + F_BK - 1) / F_BK * F_BK;
+  splits = (p.M + mps - 1) / mps;
+  if (p.C % 4 == 0) hipLaunchKernelGGL(wgrad_f32_kernel<true>, dim3(ntiles * splits), dim3(256), 0, stream, p, mps);
+  else hipLaunchKernelGGL(wgrad_f32_kernel<false>, dim3(ntiles * splits), dim3(256), 0, stream, p, mps);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+}  // namespace pddl

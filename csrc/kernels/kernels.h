@@ -57,6 +57,19 @@ struct WgradParams {
 };
 const char* wgrad_launch(const WgradParams& p, hipStream_t stream);
 
+// ---- fp32 convolution on the fp32 matrix cores (conv_f32.hip): the reference-precision path ----
+struct ConvF32Params {
+  const float* x; int N, H, W, C;      // NHWC input (im2col source)
+  int R, S, stride, pad, Ho, Wo, M;    // M = N * Ho * Wo
+  const float* w; const float* bias;   // forward: w [Cout][K] (OHWI), optional bias [Cout]
+  int Cout, K;                         // K = R * S * C
+  float* y;                            // forward: output [M][Cout]; wgrad: the output gradient (read)
+  float* dw;                           // wgrad: [Cout][K], accumulated with atomics
+  uint64_t mg_howo, mg_wo;             // (set by the launchers)
+};
+const char* conv_f32_launch(ConvF32Params p, hipStream_t stream);
+const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream);
+
 // ---- elementwise / reduction kernels (eltwise.hip) ----
 struct StemParams {
   const void* in; int in_u8;          // [B, Hin, Win, 3] uint8 or fp32 (0..255)

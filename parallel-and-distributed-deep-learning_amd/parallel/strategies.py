@@ -37,13 +37,18 @@ def gpu_available() -> bool:
 
 
 def build_engine(cfg, device: torch.device, cap: int):
-    """HIP engine (bf16 MFMA kernels; frozen or train-mode BN) on a GPU; the fp32 PyTorch
-    reference engine on CPU (config 1 of BASELINE.json: CPU plumbing) or for precision=fp32."""
+    """On a GPU: the bf16 HIP engine (bf16 MFMA kernels; frozen or train-mode BN), or for
+    precision=fp32 the reference-precision engine on the fp32-MFMA HIP convolutions
+    (models/engine_f32.py).  On CPU: the fp32 PyTorch reference engine (config 1 of
+    BASELINE.json: CPU plumbing)."""
     L = ParamLayout(cfg.num_classes)
     if device.type == "cuda" and cfg.precision == "bf16":
         from ..models.engine import make_hip_engine
         return make_hip_engine(L, cap, bn_mode=cfg.bn_mode, crop=cfg.crop, image_size=cfg.image_size,
                                device=device, num_classes=cfg.num_classes)
+    if device.type == "cuda":
+        from ..models.engine_f32 import HipF32Engine
+        return HipF32Engine(L, cap, crop=cfg.crop, device=device, bn_mode=cfg.bn_mode, num_classes=cfg.num_classes)
     from ..models.reference import TorchEngine
     return TorchEngine(L, cap, crop=cfg.crop, device=device, bn_mode=cfg.bn_mode, num_classes=cfg.num_classes)
 
