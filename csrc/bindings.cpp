@@ -422,6 +422,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm8") pddl::g_igemm8 = v;
     else if (which == "igemm8_min_tiles") pddl::g_igemm8_min_tiles = v;
     else if (which == "wgrad8") pddl::g_wgrad8 = v;
+    else if (which == "igemm8_expand") pddl::g_igemm8_expand = v;
+    else if (which == "igemm_ns1_kt") pddl::g_igemm_ns1_kt = v;
+    else if (which == "igemm8_min_n") pddl::g_igemm8_min_n = v;
+    else if (which == "wgrad1") pddl::g_wgrad1 = v;
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
     else if (which == "pool") pddl::g_pool_variant = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;

@@ -39,6 +39,11 @@ namespace pddl {
 //   AM_DUAL:   two AM_DIRECT sources concatenated along K (projection-block dgrad).
 enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 
+// Blocks per CU the 4-wave tiles are register-budgeted for (launch-bounds minimum).
+#ifndef IGEMM_MIN_BLOCKS
+#define IGEMM_MIN_BLOCKS 2
+#endif
+
 // LDS bank swizzle of the [rows][128 B] operand tiles (the XOR involution is applied to the
 // DMA SOURCE chunk and to the ds_read_b128 address, cdna_hip_programming §5.4 rule 21).
 // ds_read_b128 serves 16 lanes (16 consecutive rows, same logical chunk) per 256-byte bank
@@ -279,7 +284,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 // stalling every store iteration (short-K 1x1 layers are epilogue-bound).
 // WTM_: wave-tile rows (64, or 128 for the 256x256 tile: 8 waves as 2 x 4, 128x64 each).
 template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64>
-__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) igemm_kernel(IgemmParams p) {
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParams p) {
   constexpr int WTM = WTM_, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int WAVES_N = BN / WTN;
@@ -683,6 +688,13 @@ int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 lay
 int g_igemm8 = 2;          // 8-phase 256x256 kernel (igemm8_kernel) for Nn >= 256, K >= 256, Nn < 4K:
                            // 0 off, 1 on, 2 on with the wave-row stagger (default: b1024 end to end
                            // 18.82k -> 19.00k img/s; stagger beats 1 on every layer, kbench)
+int g_igemm_ns1_kt = 1000; // single-stage tile for K <= 64 * this (default: every K).  b1024 end to
+                           // end 2/4/8/16/36 -> 20.11k/20.42k/20.53k/20.76k/20.87k img/s: three
+                           // resident single-buffer blocks per CU overlap each other's load and MFMA
+                           // phases better than one block's double buffer does
+int g_igemm8_expand = 0;
+int g_igemm8_min_n = 512;  // ... and only for GEMM widths Nn >= this (with single-stage 128x128
+                           // tiles the 8-phase kernel wins only the stage-5 layers, kbench)  // A/B: also run the expansion 1x1s (Nn >= 4K) on the 8-phase kernel
 int g_igemm8_min_tiles = 128;   // ... when the problem has at least this many 256x256 tiles
 int g_igemm_il = 0;        // 2-stage tiles issue the next tile's LDS-DMA interleaved with the MFMAs:
                            // off (measured -3..-12% on the compute-bound layers, -2.5% end to end;
@@ -721,7 +733,7 @@ static int igemm_config(int M, int Nn, int K) {
   // conv1 dgrad), whose short K loop is dominated by an epilogue that streams a residual /
   // residual gradient: measured 30-40% slower there than the 2-block 128x128 tile with the
   // epilogue-operand prefetch (per-layer A/B, profiles/r2_igemm8_per_layer_ab.txt)
-  if (g_igemm8 && Nn >= 256 && K >= 256 && Nn < 4 * K &&
+  if (g_igemm8 && Nn >= g_igemm8_min_n && K >= 256 && (Nn < 4 * K || g_igemm8_expand) &&
       (long)((M + 255) / 256) * ((Nn + 255) / 256) >= g_igemm8_min_tiles)
     return 4;
   if (g_igemm_big == 4 && Nn > 128) return 3;   // forced (equivalence tests)
@@ -812,7 +824,7 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
   // twice the resident blocks (variant knob for A/B timing: 0 = heuristic, 1/2 = forced).
   const int KT = p.K / 64;
   int ns = g_igemm_variant;
-  if (ns == 0) ns = KT <= 2 ? 1 : 2;
+  if (ns == 0) ns = KT <= g_igemm_ns1_kt ? 1 : 2;
   const bool il = g_igemm_il && ns == 2;
   const int am = p.a2 ? AM_DUAL : (igemm_no_halo(p) ? AM_DIRECT : AM_HALO);
   // (explicit launches per instantiation: taking kernel addresses through a conditional

@@ -45,7 +45,10 @@ __device__ __forceinline__ v4bf tr_read(const char* p) {
   return r;
 }
 
-template <bool FAST, int BM, int NSTAGE>  // NSTAGE: LDS buffers (the loop is written for 2)
+// NSTAGE: LDS buffers.  2: the next m-tile's LDS-DMA overlaps this tile's MFMAs; 1: load ->
+// compute -> load in one buffer at half the LDS, so more blocks share a CU and overlap each
+// other's phases instead (measured faster on the short / narrow layers, knob wgrad1).
+template <bool FAST, int BM, int NSTAGE>
 __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_split, const int2* __restrict__ rowinfo) {
   constexpr int G_BYTES = 64 * BM * 2;        // 64 m-rows x BM bf16
   constexpr int X_BYTES = 64 * 256;           // 64 m-rows x 128 bf16
@@ -55,7 +58,9 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   constexpr int TN = WTN / 16;
   constexpr int EPI_LD = WTN + 4;
   constexpr int GI = G_BYTES / 4096;          // 1 KiB G pieces per wave
-  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
+  constexpr int EPI_BYTES = 4 * 32 * EPI_LD * 4;
+  constexpr int SMEM = NSTAGE * STAGE > EPI_BYTES ? NSTAGE * STAGE : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -161,8 +166,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
     __syncthreads();
   }
   for (int it = 0; it < nit; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
+    const int cur = NSTAGE == 2 ? (it & 1) : 0;
+    if (NSTAGE == 2 && it + 1 < nit) load_tile(mbeg + (it + 1) * 64, cur ^ 1);
     const char* gb = smem + cur * STAGE;
     const char* xb = gb + G_BYTES;
 #pragma unroll
@@ -198,6 +203,10 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (NSTAGE == 1 && it + 1 < nit) {
+      __syncthreads();            // every wave is done reading the single buffer
+      load_tile(mbeg + (it + 1) * 64, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -532,6 +541,7 @@ static const int2* rowinfo_for(const WgradParams& p, hipStream_t stream, const c
 }
 
 int g_wgrad_variant = 0;   // A/B knob (unused: one pipeline depth remains)
+int g_wgrad1 = 1;          // single-LDS-stage 128-wide wgrad kernel (see wgrad_kernel; 0: 2-stage)
 int g_wgrad8 = 1;          // 8-phase 256x256 wgrad8_kernel for Cout >= 256, K >= 256: 0 off, 1 on, 2 with the
                            // wave-row stagger (measured slower here); +8 (probe): skip the atomic epilogue
 
@@ -625,11 +635,19 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
     ri = rowinfo_for(p, stream, &why);
     if (!ri) return why;
   }
-#define WG_LAUNCH(F_, BM_) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, 2>), dim3(nwg), dim3(256), 0, stream, p, mps, ri);
-  if (BM == 64) {
-    if (fast) WG_LAUNCH(true, 64) else WG_LAUNCH(false, 64)
+#define WG_LAUNCH(F_, BM_, NS_) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, NS_>), dim3(nwg), dim3(256), 0, stream, p, mps, ri);
+  if (g_wgrad1) {
+    if (BM == 64) {
+      if (fast) WG_LAUNCH(true, 64, 1) else WG_LAUNCH(false, 64, 1)
+    } else {
+      if (fast) WG_LAUNCH(true, 128, 1) else WG_LAUNCH(false, 128, 1)
+    }
   } else {
-    if (fast) WG_LAUNCH(true, 128) else WG_LAUNCH(false, 128)
+    if (BM == 64) {
+      if (fast) WG_LAUNCH(true, 64, 2) else WG_LAUNCH(false, 64, 2)
+    } else {
+      if (fast) WG_LAUNCH(true, 128, 2) else WG_LAUNCH(false, 128, 2)
+    }
   }
 #undef WG_LAUNCH
   hipError_t e = hipGetLastError();

@@ -78,8 +78,12 @@ def test_engine_matches_bf16_point_reference_within_its_noise_floor(crop, image_
     few % through the bf16 roundings downstream (the SAME reference run on the CPU instead of
     the GPU differs from itself by 2.5 % median, 3.7 % max per tensor: scripts/parity_noise.py,
     profiles/r2_parity_noise_floor.txt).  So each tensor is bounded by that measured floor:
-    engine error <= 2 x (GPU-vs-CPU reference error) + 0.5 %, which a mis-scaled bias / BN
-    parameter (error ~100 %) cannot pass, unlike the fixed 15 % bound above."""
+    engine error <= 3 x (GPU-vs-CPU reference error) + 0.5 %, which a mis-scaled bias / BN
+    parameter (error ~100 %) cannot pass, unlike the fixed 15 % bound above; and across tensors
+    the engine's median error is at most 1.5 x the floor's.  (The factor 3 covers the engine's
+    own run-to-run spread: its weight gradients are summed with fp32 atomics in no fixed order,
+    which moves a cancellation-heavy BN-gamma gradient -- a dot product of W and dW -- by ~1 %
+    between runs, e.g. 3.3 % against a 1.1 % floor in one run and within 2x in the next.)"""
     from pddl.models.reference import TorchEngine
     torch.manual_seed(0)
     B = 4
@@ -99,15 +103,22 @@ def test_engine_matches_bf16_point_reference_within_its_noise_floor(crop, image_
     class _Cpu:
         grads = tc.grads.cuda()
     floor = {n: r for r, n in _grad_errors(L, _Cpu, te)}
-    over = [(n, round(r, 4), round(floor[n], 4)) for r, n in _grad_errors(L, he, te) if r > 2 * floor[n] + 0.005]
+    errs = _grad_errors(L, he, te)
+    over = [(n, round(r, 4), round(floor[n], 4)) for r, n in errs if r > 3 * floor[n] + 0.005]
     assert not over, over[:8]
+    med = lambda v: sorted(v)[len(v) // 2]   # noqa: E731
+    assert med([r for r, _ in errs]) <= 1.5 * med(list(floor.values())), (med([r for r, _ in errs]),
+                                                                           med(list(floor.values())))
 
 
 def test_engine_loss_trajectory_20_steps():
     """20 Adam steps on one fixed batch (the reference's training step, imagenet-resnet50.py:62-67):
-    the HIP engine's loss trajectory follows the bf16-point reference's step by step, within the
-    divergence the same reference shows against itself run on the CPU (small accumulation-order
-    differences grow through 20 nonlinear Adam steps for any implementation)."""
+    the HIP engine's loss trajectory tracks the bf16-point reference run on the CPU as closely as
+    the SAME reference run on the GPU does.  Past the first few steps the trajectory is chaotic
+    (the loss oscillates 2.1-3.0 while Adam memorises the batch), so small accumulation-order
+    differences grow to a few % for any implementation -- the GPU reference (MIOpen, itself not
+    run-to-run deterministic) deviates from the CPU one by up to ~4 % per step -- and the bound is
+    relative to that spread: mean deviation <= 2 x the reference's own + 1 %, worst step < 10 %."""
     from pddl.models.reference import TorchEngine
     from pddl.train.optim import make_optimizer
     torch.manual_seed(0)
@@ -128,11 +139,12 @@ def test_engine_loss_trajectory_20_steps():
                 he.after_update()
     lh, lt, lc = traj
     assert lh[-1] < 0.5 * lh[0] and lt[-1] < 0.5 * lt[0], (lh, lt)       # both learn the batch
-    dev_e = [abs(a - b) / abs(b) for a, b in zip(lh, lt)]                # engine vs reference
-    dev_r = [abs(c - b) / abs(b) for c, b in zip(lc, lt)]                # reference vs itself (CPU)
-    # the step-by-step divergence is chaotic for any implementation (the CPU reference alone
-    # drifts ~1 % from the GPU one within a few steps): bound the worst step and the mean
-    assert max(dev_e) < 0.05 and sum(dev_e) / len(dev_e) < max(0.02, 3 * sum(dev_r) / len(dev_r)), (dev_e, dev_r)
+    dev_e = [abs(a - c) / abs(c) for a, c in zip(lh, lc)]                # engine vs CPU reference
+    dev_r = [abs(b - c) / abs(c) for b, c in zip(lt, lc)]                # GPU reference vs CPU reference
+    print("losses engine / reference / cpu reference:", [(round(a, 4), round(b, 4), round(c, 4))
+                                                        for a, b, c in zip(lh, lt, lc)])
+    assert max(dev_e[:4]) < 2e-3, dev_e[:4]                                # before the chaotic phase
+    assert max(dev_e) < 0.10 and sum(dev_e) / len(dev_e) <= 2 * sum(dev_r) / len(dev_r) + 0.01, (dev_e, dev_r)
 
 
 def test_engine_trains():

@@ -40,6 +40,7 @@ conv = st.tuples(
 def _k8(on):
     N().set_variant("igemm8", 2 if on else 0)
     N().set_variant("igemm8_min_tiles", 1 if on else 128)
+    N().set_variant("igemm8_min_n", 256 if on else 512)
 
 
 @settings(max_examples=25, deadline=None, derandomize=True)
@@ -65,6 +66,7 @@ def test_igemm_forward_fuzz(case, with_res, pf, k8):
         N().set_variant("igemm_pf", 1)
         _k8(True)
         N().set_variant("igemm8_min_tiles", 128)
+    N().set_variant("igemm8_min_n", 512)
     ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s,
                                      padding=pad).permute(0, 2, 3, 1) * sc + sh
     if with_res:
@@ -97,6 +99,7 @@ def test_igemm_dgrad_and_wgrad_fuzz(case, pf, k8):
         N().set_variant("igemm_pf", 1)
         _k8(True)
         N().set_variant("igemm8_min_tiles", 128)
+    N().set_variant("igemm8_min_n", 512)
     ref = torch.nn.grad.conv2d_input((n, cin, h, h), w.float().permute(0, 3, 1, 2), g.float().permute(0, 3, 1, 2),
                                      stride=s, padding=pad)
     ref = (ref.permute(0, 2, 3, 1) + add.float()) * (mask.float() > 0)

@@ -133,7 +133,7 @@ def test_igemm_dgrad(case):
 
 
 @pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1), ("igemm8", 1),
-                                      ("igemm8", 2)])
+                                      ("igemm8", 2), ("igemm", 2)])
 @pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual"])
 def test_igemm_big_tile_matches(kind, knob, big):
     """The 8-wave 256x128 3-stage (igemm_big 2) and 256x256 2-stage (igemm_big 4)
@@ -156,7 +156,8 @@ def test_igemm_big_tile_matches(kind, knob, big):
         wt = rnd(256, 640, scale=0.05)
         mask = rnd(n, h, h, 256)
     outs = []
-    N().set_variant("igemm8_min_tiles", 1)       # (tiny problems: let the 8-phase kernel take them)
+    N().set_variant("igemm8_min_tiles", 1)
+    N().set_variant("igemm8_min_n", 256)       # (tiny problems: let the 8-phase kernel take them)
     N().set_variant("igemm8", 0)                 # baseline: the 128x128 tile
     for kv in (0, big):
         N().set_variant(knob, kv)
@@ -183,6 +184,7 @@ def test_igemm_big_tile_matches(kind, knob, big):
         finally:
             N().set_variant(knob, 0)
     N().set_variant("igemm8_min_tiles", 128)
+    N().set_variant("igemm8_min_n", 512)
     N().set_variant("igemm8", 2)
     assert rel(outs[1], outs[0]) < 1e-5
 
@@ -198,6 +200,7 @@ def test_igemm8_round_split_dgrad_colsum(stagger):
     wt = rnd(cin, co, scale=0.05)
     add, mask = rnd(n, h, h, cin), rnd(n, h, h, cin)
     outs = []
+    N().set_variant("igemm8_min_n", 256)
     for kv in (0, stagger):
         N().set_variant("igemm8", kv)
         try:
@@ -209,6 +212,7 @@ def test_igemm8_round_split_dgrad_colsum(stagger):
             outs.append((out.float(), _fold(part, rows, cin), rows))
         finally:
             N().set_variant("igemm8", 2)
+    N().set_variant("igemm8_min_n", 512)
     (o0, c0, r0), (o1, c1, r1) = outs
     assert r0 == r1 == 1200          # (both tilings keep 4 partial rows per 256 GEMM rows)
     assert rel(o1, o0) < 1e-5 and rel(c1, c0) < 1e-4
@@ -235,6 +239,7 @@ def test_igemm8_forward_vs_fp32(case, stagger):
     res = rnd(n, ho, ho, co)
     out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
     N().set_variant("igemm8_min_tiles", 1)
+    N().set_variant("igemm8_min_n", 256)
     N().set_variant("igemm8", stagger)
     try:
         for _ in range(3):       # repeated launches: a pipeline race would show up as a changing result
@@ -245,6 +250,7 @@ def test_igemm8_forward_vs_fp32(case, stagger):
     finally:
         N().set_variant("igemm8", 2)
         N().set_variant("igemm8_min_tiles", 128)
+        N().set_variant("igemm8_min_n", 512)
 
 
 def test_igemm_dgrad_dual_source():
@@ -329,6 +335,26 @@ def test_wgrad(case):
                                       g.float().permute(0, 3, 1, 2), stride=st, padding=pad)
     ref = ref.permute(0, 2, 3, 1).reshape(co, -1)
     assert rel(dw, ref) < 5e-3
+
+
+@pytest.mark.parametrize("case", WG_CASES)
+def test_wgrad_single_stage_matches_double(case):
+    """The single-LDS-stage 128-wide wgrad (default, knob wgrad1=1) equals the 2-stage one."""
+    torch.manual_seed(6)
+    n, h, cin, co, r, st, pad = case
+    ho = (h + 2 * pad - r) // st + 1
+    x = rnd(n, h, h, cin)
+    g = rnd(n, ho, ho, co)
+    outs = []
+    try:
+        for kv in (0, 1):
+            N().set_variant("wgrad1", kv)
+            dw = torch.zeros(co, r * r * cin, device=dev)
+            N().wgrad(x, h, h, r, r, st, pad, ho, ho, g, None, 0, dw, r * r * cin, 0)
+            outs.append(dw)
+    finally:
+        N().set_variant("wgrad1", 1)
+    assert rel(outs[1], outs[0]) < 1e-5
 
 
 def test_wgrad_dual_and_padded_k():
