@@ -89,7 +89,12 @@ void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, 
   if (mode == pddl::EPI_F32) p.out = f32p(out); else p.out = bfpm(out);
   p.ldo = ld(out);
   p.relu = (int)relu;
-  if (out2.has_value()) { p.out2 = bfpm(*out2); p.ldo2 = ld(*out2); }
+  if (out2.has_value()) {
+    p.out2 = bfpm(*out2); p.ldo2 = ld(*out2);
+    if (mode == pddl::EPI_DGRAD)   // dgrad: compact copy of the stride-2 scatter's rows
+      PCHECK(up2 && out2->numel() / std::max<int64_t>(1, out2->size(-1)) >= p.M && out2->size(-1) >= p.Nn,
+             "dgrad out2 is the compact [N*Ho*Wo][Nn] copy of an up2 scatter");
+  }
   p.relu2 = (int)relu2; p.n_split = (int)n_split;
   p.up2 = (int)up2; p.Hf = (int)Hf; p.Wf = (int)Wf;
   p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;

@@ -226,7 +226,12 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) csum[e] += w[e];
-            *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pack8(w);
+            const uint4 pk = pack8(w);
+            *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pk;
+            // compact copy of the stride-2 positions (the only nonzero rows of the scatter):
+            // the consumers of a downsampling block's input gradient run at a quarter of M on it
+            if (q == 0 && p.up2 && p.out2)
+              *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out2) + (long)gm * p.ldo2 + gn) = pk;
           }
         }
       }

@@ -226,6 +226,16 @@ class HipEngine:
         self.gbuf = [torch.empty(outer, **bf), torch.empty(outer, **bf)]
         self.g1buf = torch.empty(inner, **bf)
         self.g2buf = torch.empty(inner, **bf)
+        # compact (stride-2 grid) copies of the output gradient / conv2-output gradient of every
+        # block feeding a downsampling block (see _s2_fed)
+        gc, g2c = 1, 1
+        for bi in self._s2_fed():
+            b = L.blocks[bi]
+            Hc = self.geo[b.name][1] // 2 + self.geo[b.name][1] % 2
+            gc = max(gc, B * Hc * Hc * 4 * b.filters)
+            g2c = max(g2c, B * Hc * Hc * b.filters)
+        self.gcbuf = torch.empty(gc, **bf)
+        self.g2cbuf = torch.empty(g2c, **bf)
         self.pooled = torch.empty(B, 2048, **bf)
         self.logits = torch.empty(B, self.num_classes, dtype=torch.float32, device=dev)
         self.dlogits = torch.zeros(B, self.ncls_pad, **bf)
@@ -234,6 +244,14 @@ class HipEngine:
         self.cap = B
         self._cred = {}
         self.colpart = torch.empty(self._colred(B)[2], dtype=torch.float32, device=dev)
+
+    def _s2_fed(self):
+        """Blocks whose output feeds a stride-2 projection block (ResNet v1 downsamples in the
+        first 1x1 conv and the shortcut, both reading only the even rows / columns): their output
+        gradient is zero off the stride-2 grid, so their conv3 weight / data gradients and conv2
+        weight gradient run on the compact quarter (conv2_block3, conv3_block4, conv4_block6)."""
+        bl = self.L.blocks
+        return {bi for bi in range(len(bl) - 1) if bl[bi + 1].proj and bl[bi + 1].stride == 2}
 
     def _colred(self, B):
         """Partial column-sum regions of every fused producer for batch B:
@@ -249,13 +267,18 @@ class HipEngine:
             rows.append(struct.pack(_CRED_FMT, off, nrows, C, self.ch[layer], 0))
             off += nrows * C
         blocks = L.blocks
+        s2 = self._s2_fed()
         add(blocks[-1].convs["3"].name, B, 2048)                              # gap_bwd
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
             H, Ho = self.geo[b.name]
             M = B * Ho * Ho
             f = b.filters
-            add(b.convs["2"].name, N.igemm_partial_rows(M, f, 4 * f), f)          # c3 dgrad -> g2
+            Mc = M
+            if bi in s2:       # c3 dgrad runs on the compact stride-2 grid
+                Hc = Ho // 2 + Ho % 2
+                Mc = B * Hc * Hc
+            add(b.convs["2"].name, N.igemm_partial_rows(Mc, f, 4 * f), f)         # c3 dgrad -> g2
             add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)          # c2 dgrad -> g1
             if bi > 0:                                                           # c1 dgrad -> g_out(prev)
                 add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin, 5 * f if b.proj else f), b.cin)
@@ -399,6 +422,7 @@ class HipEngine:
         def part(layer):
             return cp[coffs[layer]:]
         N.gap_bwd(dpooled, x5, gout, part(blocks[-1].convs["3"].name))
+        s2 = self._s2_fed()
         # ---- blocks (column sums of every produced gradient are fused into its producer)
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
@@ -417,13 +441,24 @@ class HipEngine:
             y1, y2 = a["y1"][:B], a["y2"][:B]
             gout = self.gbuf[cur][: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
             c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
-            # conv3
-            N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)
             g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
-            N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m, None,
-                    g2, 0, None, 0, 0, 0, 0, 0, part(c2n), None)
-            # conv2 (3x3)
-            N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
+            if bi in s2:
+                # gout is zero off the stride-2 grid (the next block reads only even rows /
+                # columns); its compact copy `gc` came from that block's dgrad epilogue
+                Hc = Ho // 2 + Ho % 2
+                gc = self.gcbuf[: B * Hc * Hc * 4 * f].view(B, Hc, Hc, 4 * f)
+                g2c = self.g2cbuf[: B * Hc * Hc * f].view(B, Hc, Hc, f)
+                N.wgrad(y2, Ho, Ho, 1, 1, 2, 0, Hc, Hc, gc, None, 0, self._gview(c3n, 4 * f, f), f, 0)
+                N.igemm(gc, None, Hc, Hc, 1, 1, 1, 0, Hc, Hc, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
+                        None, g2, 0, g2c, 0, 0, 1, Ho, Ho, part(c2n), None)
+                N.wgrad(y1, Ho, Ho, 3, 3, 2, 1, Hc, Hc, g2c, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
+            else:
+                # conv3
+                N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)
+                N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
+                        None, g2, 0, None, 0, 0, 0, 0, 0, part(c2n), None)
+                # conv2 (3x3)
+                N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
             g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
             N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1m, None,
                     g1, 0, None, 0, 0, 0, 0, 0, part(c1n), None)
@@ -433,8 +468,11 @@ class HipEngine:
             if b.proj:
                 N.wgrad(x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0)
                 N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
+                gxc = None
+                if bi - 1 in s2:   # compact copy for the previous block's stride-2-grid passes
+                    gxc = self.gcbuf[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
                 N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, 5 * f), 1, None, None, None,
-                        mask_in, None, gx, 0, None, 0, 0, 1 if b.stride == 2 else 0, H, H, cs_in, None)
+                        mask_in, None, gx, 0, gxc, 0, 0, 1 if b.stride == 2 else 0, H, H, cs_in, None)
                 last = L.entry(b.convs["0"].name, "kernel")
             else:
                 N.wgrad(x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0)
