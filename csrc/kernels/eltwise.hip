@@ -358,23 +358,220 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t*
     }
   }
 }
+// Row-streaming forms (pool = 4): a wave owns WL = 64 / (C/8) output columns x all channel
+// groups of one image and walks the output rows top to bottom.  Every input row is fetched
+// once per wave (the per-output forms fetch the row shared by two vertically adjacent windows
+// twice, and the two fetches land on different XCDs because neighbouring workgroups are
+// dispatched round-robin over the 8 L2s), so the HBM traffic is one read of the input plus the
+// outputs.  Forward: the horizontal 3-max (value + tap) of input row 2ho+1 is the bottom row of
+// window ho and the top row of window ho+1, so it is carried to the next iteration; rows are
+// combined top to bottom with strict '>' and taps left to right within a row, which keeps the
+// first maximum in scan order (the per-output forms' tie rule).
+template <int CG>
+__global__ void __launch_bounds__(256) maxpool_fwd_stream_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                                 uint8_t* __restrict__ idx, uint8_t* __restrict__ bits,
+                                                                 int B, int H, int W, int Ho, int Wo) {
+  constexpr int C = CG * 8, WL = 64 / CG;
+  const int lane = threadIdx.x & 63, g = lane % CG, wl = lane / CG;
+  const int bands = (Wo + WL - 1) / WL;
+  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= B * bands) return;
+  const int b = wid / bands, wo = (wid - b * bands) * WL + wl;
+  if (wo >= Wo) return;
+  const bf16_t* xb = x + (long)b * H * W * C + g * 8;
+  const int wi0 = 2 * wo - 1;
+  // raw taps of input row hi, columns wi0 .. wi0 + 2: branch-free loads (address clamped into
+  // the image, zero padding selected afterwards) so the next rows' loads can be issued ahead
+  bool col_ok[3];
+  int wcl[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int wi = wi0 + s;
+    col_ok[s] = wi >= 0 && wi < W;
+    wcl[s] = wi < 0 ? 0 : (wi >= W ? W - 1 : wi);
+  }
+  auto fetch = [&](int hi, uint4 (&r)[3]) {
+    const bool row_ok = hi >= 0 && hi < H;
+    const int hc = hi < 0 ? 0 : (hi >= H ? H - 1 : hi);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const uint4 v = *reinterpret_cast<const uint4*>(xb + ((long)hc * W + wcl[s]) * C);
+      r[s] = (row_ok && col_ok[s]) ? v : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // horizontal max + first-max tap of one fetched row
+  auto hmax = [&](const uint4 (&r)[3], float (&hv)[8], uint32_t (&hs)[8]) {
+    float t[3][8];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) unpack8(r[s], t[s]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = t[0][e];
+      uint32_t s = 0;
+      if (t[1][e] > v) { v = t[1][e]; s = 1; }
+      if (t[2][e] > v) { v = t[2][e]; s = 2; }
+      hv[e] = v; hs[e] = s;
+    }
+  };
+  float tv[8];
+  uint32_t ts[8];
+  uint4 r1[3], r2[3];
+  fetch(-1, r1);
+  hmax(r1, tv, ts);   // the padding row above window 0
+  fetch(0, r1);
+  fetch(1, r2);
+  for (int ho = 0; ho < Ho; ++ho) {
+    float mv[8], bv[8];
+    uint32_t ms[8], bs[8];
+    hmax(r1, mv, ms);
+    hmax(r2, bv, bs);
+    if (ho + 1 < Ho) {   // rows of the next window in flight while this one is reduced and stored
+      fetch(2 * ho + 2, r1);
+      fetch(2 * ho + 3, r2);
+    }
+    float best[8];
+    uint32_t code[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = tv[e]; code[e] = ts[e];
+      if (mv[e] > best[e]) { best[e] = mv[e]; code[e] = 3 + ms[e]; }
+      if (bv[e] > best[e]) { best[e] = bv[e]; code[e] = 6 + bs[e]; }
+      tv[e] = bv[e]; ts[e] = bs[e];   // row 2ho+1 is the top row of window ho+1
+    }
+    const long o = (((long)b * Ho + ho) * Wo + wo) * C + g * 8;
+    const uint4 yv = pack8(best);
+    *reinterpret_cast<uint4*>(y + o) = yv;
+    if (bits) bits[o >> 3] = (uint8_t)pos_bits8(yv);
+    *reinterpret_cast<uint2*>(idx + o) =
+        make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
+                   code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24));
+  }
+}
+
+// Backward, same wave shape: the lane owns input columns 2p, 2p+1 of one channel group and
+// walks input row pairs (2q, 2q+1).  Exactly outputs (q..q+1, p..p+1) route gradient into the
+// 2x2 block (row 2q: output row q tap r = 1; row 2q+1: output row q tap 2 and row q+1 tap 0;
+// columns likewise), and output row q+1's (gy, idx) are carried as the next pair's row q, so
+// every (gy, idx) row is read once per wave (the neighbour column p+1 comes from L1).
+template <int CG>
+__global__ void __launch_bounds__(256) maxpool_bwd_stream_kernel(const bf16_t* __restrict__ gy,
+                                                                 const uint8_t* __restrict__ idx,
+                                                                 const bf16_t* __restrict__ xmask,
+                                                                 bf16_t* __restrict__ gx, int B, int H, int W,
+                                                                 int Ho, int Wo, float* __restrict__ colsum) {
+  constexpr int C = CG * 8, WL = 64 / CG;
+  const int lane = threadIdx.x & 63, g = lane % CG, wl = lane / CG;
+  const int Wq = (W + 1) / 2, Hq = (H + 1) / 2;
+  const int bands = (Wq + WL - 1) / WL;
+  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= B * bands) return;   // (whole waves: the colsum row of such a wave is never read)
+  const int b = wid / bands, p = (wid - b * bands) * WL + wl;
+  float cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (p < Wq) {
+    // raw (gy, idx) of output row ho at columns p, p + 1: branch-free loads (address clamped,
+    // zero gradient / no-match taps outside the output) so the row after next is in flight
+    // while this pair is scattered
+    const bool okp1 = p + 1 < Wo;
+    const int wo1 = okp1 ? p + 1 : Wo - 1;
+    auto orow = [&](int ho, uint4 (&gr)[2], uint2 (&ir)[2]) {
+      const bool rok = ho < Ho;
+      const long rb = ((long)b * Ho + (rok ? ho : Ho - 1)) * Wo;
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const long o = (rb + (d ? wo1 : p)) * C + g * 8;
+        const uint4 gv = *reinterpret_cast<const uint4*>(gy + o);
+        const uint2 iv = *reinterpret_cast<const uint2*>(idx + o);
+        const bool ok = rok && (d == 0 || okp1);
+        gr[d] = ok ? gv : make_uint4(0, 0, 0, 0);
+        ir[d] = ok ? iv : make_uint2(0xffffffffu, 0xffffffffu);   // matches no tap
+      }
+    };
+    auto tap = [](const uint2& iv, int e) { return ((e < 4 ? iv.x : iv.y) >> (8 * (e & 3))) & 0xffu; };
+    uint4 gq[2], gq1[2];   // output rows q and q + 1
+    uint2 iq[2], iq1[2];
+    orow(0, gq, iq);
+    orow(1, gq1, iq1);
+    for (int q = 0; q < Hq; ++q) {
+      float ga[8], gb[8], gc[8], gd[8];   // (q, p), (q, p+1), (q+1, p), (q+1, p+1)
+      unpack8(gq[0], ga); unpack8(gq[1], gb); unpack8(gq1[0], gc); unpack8(gq1[1], gd);
+      const uint2 ia = iq[0], ib = iq[1], ic = iq1[0], id = iq1[1];
+      gq[0] = gq1[0]; gq[1] = gq1[1]; iq[0] = iq1[0]; iq[1] = iq1[1];
+      if (q + 1 < Hq) orow(q + 2, gq1, iq1);
+      float acc[2][2][8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t ta = tap(ia, e), tb = tap(ib, e), tc = tap(ic, e), td = tap(id, e);
+        // input (2q + a, 2p + c): from output (q, p) tap (a + 1, c + 1); (q, p+1) tap (a + 1, 0)
+        // for c = 1; (q+1, p) tap (0, c + 1) for a = 1; (q+1, p+1) tap (0, 0) for a = c = 1
+        acc[0][0][e] = ta == 4u ? ga[e] : 0.f;
+        acc[0][1][e] = (ta == 5u ? ga[e] : 0.f) + (tb == 3u ? gb[e] : 0.f);
+        acc[1][0][e] = (ta == 7u ? ga[e] : 0.f) + (tc == 1u ? gc[e] : 0.f);
+        acc[1][1][e] = (ta == 8u ? ga[e] : 0.f) + (tb == 6u ? gb[e] : 0.f) + (tc == 2u ? gc[e] : 0.f) +
+                       (td == 0u ? gd[e] : 0.f);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int h = 2 * q + a, w = 2 * p + c;
+          if (h >= H || w >= W) continue;
+          const long o = (((long)b * H + h) * W + w) * C + g * 8;
+          if (xmask) {
+            float mv[8];
+            unpack8(*reinterpret_cast<const uint4*>(xmask + o), mv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[a][c][e] = mv[e] > 0.f ? acc[a][c][e] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += acc[a][c][e];
+          *reinterpret_cast<uint4*>(gx + o) = pack8(acc[a][c]);
+        }
+    }
+  }
+  if (colsum) {   // one partial row of C sums per wave
+#pragma unroll
+    for (int o = CG; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], o, 64);
+    if (wl == 0) {
+      float4* dst = reinterpret_cast<float4*>(colsum + (long)wid * C + g * 8);
+      dst[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      dst[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+    }
+  }
+}
+
 // Max-pool kernels (bench/pool.py, b1024 @ 112x112x64; profiles/r1_pool_ab.json):
 //   0 = per-output forward (740 us) + 2x2-block backward (628 us, was 827 us per input pixel)
 //   1 = per-output forward + per-input-pixel backward
 //   2 / 3 = 2- / 4-output strip forward (796 / 1000 us: the register-held strip costs more
 //           occupancy than the saved re-reads return) + block backward
-int g_pool_variant = 0;
+//   4 = row-streaming forward and backward (one wave per image x column band)
+int g_pool_variant = 4;
+static bool pool_stream(int C) { return g_pool_variant == 4 && (C == 64 || C == 128 || C == 256); }
+static long pool_stream_waves(int B, int cols, int C) {
+  const int WL = 64 / (C / 8);
+  return (long)B * ((cols + WL - 1) / WL);
+}
 static long pool_bwd_items(int B, int H, int W, int C) {
   return g_pool_variant == 1 ? (long)B * H * W * C / 8 : (long)B * ((H + 1) / 2) * ((W + 1) / 2) * C / 8;
 }
-int maxpool_bwd_partial_rows(int B, int H, int W, int C) { return grid_for(pool_bwd_items(B, H, W, C)) * 4; }
+int maxpool_bwd_partial_rows(int B, int H, int W, int C) {
+  if (pool_stream(C)) return (int)pool_stream_waves(B, (W + 1) / 2, C);
+  return grid_for(pool_bwd_items(B, H, W, C)) * 4;
+}
 
 const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, uint8_t* bits, int B, int H, int W, int C, int Ho,
                                int Wo, hipStream_t s) {
   if (C % 8) return "maxpool: C % 8";
   if ((long)B * H * W * C / 8 >= (1L << 31) - (1L << 24)) return "maxpool: too many elements for 32-bit indexing";
   if (Ho != (H - 1) / 2 + 1 || Wo != (W - 1) / 2 + 1) return "maxpool: output must be the pad-1 3x3/s2 size";
-  if (g_pool_variant <= 1) {
+  if (pool_stream(C)) {
+    const int grid = (int)((pool_stream_waves(B, Wo, C) + 3) / 4);
+#define POOL_F(CG_) hipLaunchKernelGGL(maxpool_fwd_stream_kernel<CG_>, dim3(grid), dim3(256), 0, s, x, y, idx, bits, B, H, W, Ho, Wo)
+    if (C == 64) POOL_F(8); else if (C == 128) POOL_F(16); else POOL_F(32);
+#undef POOL_F
+  } else if (g_pool_variant <= 1) {
     const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic(Wo), fdiv_magic(Ho)};
     hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)B * Ho * Wo * C / 8)), dim3(256), 0, s, x, y, idx,
                        bits, B, H, W, C, Ho, Wo, dv);
@@ -398,7 +595,13 @@ const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uin
   if ((long)B * H * W * C / 8 >= (1L << 31) - (1L << 24)) return "maxpool: too many elements for 32-bit indexing";
   if (Ho != (H - 1) / 2 + 1 || Wo != (W - 1) / 2 + 1) return "maxpool: output must be the pad-1 3x3/s2 size";
   const int grid = grid_for(pool_bwd_items(B, H, W, C));
-  if (g_pool_variant == 1) {
+  if (pool_stream(C)) {
+    const int sgrid = (int)((pool_stream_waves(B, (W + 1) / 2, C) + 3) / 4);
+#define POOL_B(CG_) \
+  hipLaunchKernelGGL(maxpool_bwd_stream_kernel<CG_>, dim3(sgrid), dim3(256), 0, s, gy, idx, xmask, gx, B, H, W, Ho, Wo, colsum)
+    if (C == 64) POOL_B(8); else if (C == 128) POOL_B(16); else POOL_B(32);
+#undef POOL_B
+  } else if (g_pool_variant == 1) {
     const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic(W), fdiv_magic(H)};
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, s, gy, idx, xmask, gx, B, H, W, C, Ho, Wo,
                        colsum, dv);

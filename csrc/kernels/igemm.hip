@@ -701,6 +701,7 @@ int g_igemm8_expand = 0;
 int g_igemm8_min_n = 512;  // ... and only for GEMM widths Nn >= this (with single-stage 128x128
                            // tiles the 8-phase kernel wins only the stage-5 layers, kbench)  // A/B: also run the expansion 1x1s (Nn >= 4K) on the 8-phase kernel
 int g_igemm8_min_tiles = 128;   // ... when the problem has at least this many 256x256 tiles
+int g_igemm_n64 = 1;       // see igemm_config (1: conv2_block1 c1+c0 fwd 831 -> 765 us; 2: no further gain)
 int g_igemm_il = 0;        // 2-stage tiles issue the next tile's LDS-DMA interleaved with the MFMAs:
                            // off (measured -3..-12% on the compute-bound layers, -2.5% end to end;
                            // profiles/r1_kbench_b1024_interleaved_issue.json) -- the later issue
@@ -734,6 +735,11 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
 // LDS-DMA pieces per MFMA of the 128x128 tile; for wide, long-K layers).
 static int igemm_config(int M, int Nn, int K) {
   if (Nn <= 64) return 0;
+  // A/B knob: 256x64 tiles for widths that are not a multiple of 128 (1: conv2_block1's
+  // c1 + shortcut, Nn = 320, whose third 128-column tile is half empty) or for every short-K
+  // (K = 64) layer (2)
+  if (g_igemm_n64 == 1 && Nn % 128 && Nn % 64 == 0) return 0;
+  if (g_igemm_n64 == 2 && K <= 64 && Nn % 64 == 0) return 0;
   // 8-phase 256x256 for wide, long-K GEMMs -- not the expansion 1x1s (Nn >= 4K: conv3 forward,
   // conv1 dgrad), whose short K loop is dominated by an epilogue that streams a residual /
   // residual gradient: measured 30-40% slower there than the 2-block 128x128 tile with the

@@ -1,6 +1,6 @@
 """Per-layer breakdown of one training step from a rocprofv3 kernel trace.
 
-    python scripts/analyze_trace.py gpurun_out/prof/run_kernel_trace.csv [batch] [crop] [knobs]
+    python scripts/analyze_trace.py gpurun_out/prof/run_kernel_trace.csv [batch=1024] [crop=224] [knobs]
 
 Pairs the last complete step's dispatches with the engine's fixed launch schedule and
 prints time, TFLOP/s and effective GB/s per launch.
@@ -41,12 +41,17 @@ def schedule(B, crop):
     ev.append(("colsum", "dense", 0, 0))
     ev.append(("igemm", "dense dgrad", 2 * B * 2048 * 1000, 0, (B, 2048, 1024)))
     ev.append(("gap_bwd", "gap", 0, 0))
-    for b, H, Ho in reversed(geo):
+    blocks = L.blocks
+    s2 = {i for i in range(len(blocks) - 1) if blocks[i + 1].proj and blocks[i + 1].stride == 2}
+    for bi in range(len(geo) - 1, -1, -1):
+        b, H, Ho = geo[bi]
         f, cin = b.filters, b.cin
         M = B * Ho * Ho
-        ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * M * f * 4 * f, (M * f + M * 4 * f) * 2))
-        ev.append(("igemm", f"{b.name} c3 dgrad", 2 * M * f * 4 * f, (M * 4 * f + 2 * M * f) * 2, (M, f, 4 * f)))
-        ev.append(("wgrad", f"{b.name} c2 wgrad", 2 * M * 9 * f * f, 2 * M * f * 2))
+        # blocks feeding a stride-2 block: conv3 wgrad/dgrad and conv2 wgrad on the compact quarter
+        Mc = B * (Ho // 2 + Ho % 2) ** 2 if bi in s2 else M
+        ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * Mc * f * 4 * f, (Mc * f + Mc * 4 * f) * 2))
+        ev.append(("igemm", f"{b.name} c3 dgrad", 2 * Mc * f * 4 * f, (Mc * 4 * f + Mc * f + M * f) * 2, (Mc, f, 4 * f)))
+        ev.append(("wgrad", f"{b.name} c2 wgrad", 2 * Mc * 9 * f * f, (Mc + M) * f * 2))
         ev.append(("igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2, (M, f, 9 * f)))
         n1 = 5 * f if b.proj else f
         if b.proj:   # conv1 and the shortcut conv: one wgrad launch per gradient source
@@ -70,7 +75,7 @@ def schedule(B, crop):
 
 def main():
     path = sys.argv[1]
-    B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
     crop = int(sys.argv[3]) if len(sys.argv) > 3 else 224
     knobs = sys.argv[4] if len(sys.argv) > 4 else ""   # the run's PDDL_KNOBS (changes the launch plan)
     rows = [r for r in csv.DictReader(open(path))]

@@ -419,20 +419,22 @@ def test_wgrad8_vs_fp32(case, stagger):
     assert rel(outs[2], outs[1]) < 1e-5
 
 
-@pytest.mark.parametrize("variant,h", [(0, 12), (0, 13), (1, 12), (1, 13), (2, 13), (3, 12), (3, 18)])
-def test_maxpool_and_gap(variant, h):
-    """Max pool (pad 1, 3x3/s2; strip / block kernels and the per-pixel ones) against
-    PyTorch, including odd sizes and a partial last strip, then GAP."""
+@pytest.mark.parametrize("variant,h,c", [(0, 12, 64), (0, 13, 64), (1, 12, 64), (1, 13, 64), (2, 13, 64),
+                                         (3, 12, 64), (3, 18, 64), (4, 12, 64), (4, 13, 64), (4, 35, 64),
+                                         (4, 13, 128), (4, 18, 256)])
+def test_maxpool_and_gap(variant, h, c):
+    """Max pool (pad 1, 3x3/s2; row-streaming, strip / block kernels and the per-pixel ones)
+    against PyTorch, including odd sizes, partial column bands and a partial last strip, then GAP."""
     torch.manual_seed(6)
     N().set_variant("pool", variant)
     try:
-        _maxpool_gap(h)
+        _maxpool_gap(h, c)
     finally:
-        N().set_variant("pool", 0)
+        N().set_variant("pool", 4)
 
 
-def _maxpool_gap(h):
-    n, c = 2, 64
+def _maxpool_gap(h, c):
+    n = 2
     x = torch.relu(torch.randn(n, h, h, c, device=dev)).to(torch.bfloat16)
     ho = (h + 2 - 3) // 2 + 1
     y = torch.empty(n, ho, ho, c, dtype=torch.bfloat16, device=dev)
