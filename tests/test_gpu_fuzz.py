@@ -110,3 +110,39 @@ def test_igemm_dgrad_and_wgrad_fuzz(case, pf, k8):
     wref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (co, cin, r, r), g.float().permute(0, 3, 1, 2),
                                        stride=s, padding=pad).permute(0, 2, 3, 1).reshape(co, -1)
     assert rel(dw, wref) < 5e-3
+
+
+@pytest.mark.parametrize("n,h,c,r,s,pad", [(2, 13, 64, 3, 1, 1), (3, 19, 128, 1, 1, 0), (1, 9, 256, 1, 2, 0),
+                                           (4, 17, 64, 3, 1, 1), (2, 28, 64, 1, 1, 0)])
+def test_igemm_n64_tiles(n, h, c, r, s, pad):
+    """GEMM width 64 (the 256x64 tile): forward with residual and dgrad with add + mask, M tails
+    included.  (A 512x64 tile of 128x64 wave tiles was measured 4x slower -- register spills.)"""
+    co = 64
+    ho = (h + 2 * pad - r) // s + 1
+    torch.manual_seed(n * 100 + h + c)
+    x = rnd(n, h, h, c)
+    w = rnd(co, r, r, c, scale=0.05)
+    sc = torch.rand(co, device=dev) + 0.5
+    sh = torch.randn(co, device=dev)
+    res = rnd(n, ho, ho, co)
+    out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
+    N().igemm(x, None, h, h, r, r, s, pad, ho, ho, w.view(co, -1), 0, sc, sh, res, None, None, out, 1, None, 0,
+              0, 0, 0, 0, None, None)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s,
+                                     padding=pad).permute(0, 2, 3, 1) * sc + sh
+    assert rel(out, torch.relu(ref + res.float())) < 1e-2
+    # dgrad of a conv with Cin = 64 (GEMM width 64): g [n, ho, ho, c'] -> [n, h, h, 64]
+    if s == 1:
+        cp = c
+        g = rnd(n, ho, ho, cp)
+        w2 = rnd(cp, r, r, co, scale=0.05)
+        add = rnd(n, h, h, co)
+        mask = rnd(n, h, h, co)
+        wt = w2.float().flip(1).flip(2).permute(3, 1, 2, 0).contiguous().to(torch.bfloat16)
+        gx = torch.empty(n, h, h, co, dtype=torch.bfloat16, device=dev)
+        N().igemm(g, None, ho, ho, r, r, 1, r - 1 - pad, ho, ho, wt.view(co, -1), 1, None, None, None, mask, add,
+                  gx, 0, None, 0, 0, 0, h, h, None, None)
+        ref = torch.nn.grad.conv2d_input((n, co, h, h), w2.float().permute(0, 3, 1, 2),
+                                         g.float().permute(0, 3, 1, 2), stride=1, padding=pad)
+        ref = (ref.permute(0, 2, 3, 1) + add.float()) * (mask.float() > 0)
+        assert rel(gx, ref) < 1e-2
