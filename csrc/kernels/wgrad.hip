@@ -541,7 +541,10 @@ static const int2* rowinfo_for(const WgradParams& p, hipStream_t stream, const c
 }
 
 int g_wgrad_variant = 0;   // A/B knob (unused: one pipeline depth remains)
-int g_wgrad1 = 1;          // single-LDS-stage 128-wide wgrad kernel (see wgrad_kernel; 0: 2-stage)
+int g_wgrad1 = 1;          // LDS stages of the 128/64-wide wgrad kernel: 1 = single stage except the
+                           // long-reduction direct layers (1x1 / stem window, M >= 2M rows: stage-2
+                           // 1x1s -4..-12 %, stem -8 %, 3x3 and stage 3+ +8..+13 % with 2 stages;
+                           // per-layer A/B at b1024), 0 = 2 stages everywhere, 2 = single everywhere
 int g_wgrad8 = 1;          // 8-phase 256x256 wgrad8_kernel for Cout >= 256, K >= 256: 0 off, 1 on, 2 with the
                            // wave-row stagger (measured slower here); +8 (probe): skip the atomic epilogue
 
@@ -636,7 +639,8 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
     if (!ri) return why;
   }
 #define WG_LAUNCH(F_, BM_, NS_) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, NS_>), dim3(nwg), dim3(256), 0, stream, p, mps, ri);
-  if (g_wgrad1) {
+  const bool one_stage = g_wgrad1 == 2 || (g_wgrad1 == 1 && !((fast || window) && p.M >= (1 << 21)));
+  if (one_stage) {
     if (BM == 64) {
       if (fast) WG_LAUNCH(true, 64, 1) else WG_LAUNCH(false, 64, 1)
     } else {

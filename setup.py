@@ -28,6 +28,9 @@ ARCH = os.environ.get("PDDL_OFFLOAD_ARCH", "gfx950")
 TEMP = os.environ.get("PDDL_BUILD_TEMP", os.path.join(os.environ.get("TMPDIR", "/tmp"), "pddl_build_temp"))
 HIPCC = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
 HIP_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=fast", "-fPIC", "-I" + os.path.join(ROOT, "csrc")]
+# A/B builds of compile-time kernel parameters, e.g. PDDL_HIP_DEFINES="-DIGEMM_MIN_BLOCKS_1=4"
+# (use a separate PDDL_BUILD_TEMP: objects are rebuilt on source changes only)
+HIP_FLAGS += os.environ.get("PDDL_HIP_DEFINES", "").split()
 
 
 def compile_kernels():
