@@ -1,16 +1,17 @@
-# ad-hoc GPU A/B session (edited per experiment); every step bounded, chained with &&
+# ad-hoc GPU session (edited per experiment); every step bounded, chained with &&
 set -o pipefail
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
-SO=parallel-and-distributed-deep-learning_amd/_pddl_native.cpython-310-x86_64-linux-gnu.so
-prof() {  # name knobs
-  PDDL_KNOBS=$2 timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/ab/prof_$1 -o run --output-format csv -- python bench.py --steps 4 --warmup 2 > gpurun_out/ab/prof_$1.log 2>&1
-}
-bench() { PDDL_KNOBS=$2 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ab/bench_$1.log 2>&1; }
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q -k "wgrad" --timeout 120 > gpurun_out/ab/wgtest.log 2>&1 && \
-bench def "" && prof def "" && cp ab_so/minb4.so $SO && bench minb4 "" && prof minb4 "" && \
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fuzz.py -x -q --timeout 120 > gpurun_out/ab/minb4_tests.log 2>&1
+b() { local n=$1; shift; timeout -k 10 300 python bench.py "$@" > gpurun_out/ab/$n.log 2>&1; }
+p() { local n=$1; shift; timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/ab/prof_$n -o run --output-format csv -- python bench.py --steps 4 --warmup 2 "$@" > gpurun_out/ab/prof_$n.log 2>&1; }
+PDDL_REHEARSE=1 b reh_hvd --gpus 2 --batch 256 --steps 5 --warmup 2 && \
+PDDL_REHEARSE=1 b reh_mir --gpus 2 --strategy mirrored --batch 256 --steps 5 --warmup 2 && \
+b bntrain --bn-mode train --steps 10 --warmup 3 && \
+b fp32 --precision fp32 --steps 10 --warmup 3 && \
+b c160 --batch 256 --image-size 160 --steps 20 --warmup 5 && \
+b c244 --batch 256 --image-size 244 --steps 20 --warmup 5 && \
+b c224 --batch 256 --steps 20 --warmup 5 && \
+p c160 --batch 256 --image-size 160 && p c244 --batch 256 --image-size 244
 rc=$?
-tail -n 2 gpurun_out/ab/wgtest.log gpurun_out/ab/minb4_tests.log
-grep -h '"value"' gpurun_out/ab/bench_*.log | cut -c1-200
+grep -h '"value"' gpurun_out/ab/*.log | cut -c1-260
 exit $rc
