@@ -58,7 +58,8 @@ def parse(argv=None):
     ap.add_argument("--local-gpus", type=int, default=1, help="multiworker: GPUs per worker process")
     # Per-GPU batch sized for 288 GB HBM3E (BASELINE north star): 1024 is the largest batch whose
     # biggest activation (conv1 output, 1.6 GB) stays inside the kernels' 31-bit buffer offsets.
-    # Measured on 1 MI355X: b128 13.5k, b256 15.4k, b512 16.9k, b1024 18.3k images/s.
+    # Measured on 1 MI355X (round 1): b128 13.5k, b256 15.4k, b512 16.9k, b1024 18.3k images/s;
+    # round 2: b256 16.8k, b1024 22.1-22.5k.
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 1024; CPU 32)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--crop", type=int, default=None, help="network input (default = image size)")
@@ -262,6 +263,8 @@ def run(args):
             "per_gpu_images_per_sec": round(ips / args.gpus, 2),
             "final_loss": round(loss, 4),
         }
+        if not cpu:   # HBM footprint of the step (torch caching allocator, device of rank 0)
+            out["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(local_devs[0]) / 1e9, 2)
         if rehearsing():
             out["rehearsal"] = True
         print(json.dumps(out), flush=True)

@@ -43,7 +43,8 @@ int old(const OptT& t) { return t.has_value() ? ld(*t) : 0; }
 void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
                 int64_t Ho, int64_t Wo, Tensor b, int64_t mode, OptT scale, OptT shift, OptT res, OptT mask,
                 OptT add, Tensor out, int64_t relu, OptT out2, int64_t relu2, int64_t n_split, int64_t up2,
-                int64_t Hf, int64_t Wf, OptT colsum, OptT bits_out, OptT stats) {
+                int64_t Hf, int64_t Wf, OptT colsum, OptT bits_out, OptT stats, OptT bn_z = c10::nullopt,
+                OptT bn_mean = c10::nullopt) {
   pddl::IgemmParams p{};
   PCHECK(a1.is_contiguous(), "A source must be contiguous NHWC");
   p.a1 = bfp(a1);
@@ -100,10 +101,19 @@ void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, 
   p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;
   if (p.colsum)
     PCHECK(colsum->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn, p.K) * p.Nn, "colsum partial buffer too short");
+  if (bn_z.has_value()) {
+    PCHECK(mode == pddl::EPI_DGRAD && stats.has_value() && bn_mean.has_value() && !up2,
+           "bn_z: fused BN-backward sums of a dgrad (stats rows, bn_mean; no stride-2 scatter)");
+    PCHECK(bn_z->scalar_type() == torch::kBFloat16 && ld(*bn_z) == ld(out) &&
+               bn_z->numel() / std::max<int64_t>(1, bn_z->size(-1)) >= p.M && bn_mean->numel() >= p.Nn,
+           "bn_z must be bf16 [M][ldo] like the output, bn_mean [Nn]");
+    p.bn_z = bfp(*bn_z);
+    p.bn_mean = f32p(*bn_mean);
+  }
   if (stats.has_value()) {
-    PCHECK(mode == pddl::EPI_FWD, "BN statistics are a forward-epilogue output");
+    PCHECK(mode == pddl::EPI_FWD || p.bn_z, "BN statistics are a forward-epilogue output (or a bn_z dgrad)");
     p.stats = f32p(*stats);
-    PCHECK(stats->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn, p.K) * 2 * p.Nn,
+    PCHECK(stats->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn, p.K, p.bn_z != nullptr) * 2 * p.Nn,
            "stats partial buffer too short");
   }
   const int64_t rows_out = up2 ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
@@ -440,7 +450,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "colred_chunks") { TORCH_CHECK(v >= 1 && v <= 65535, "colred_chunks"); pddl::g_colred_chunks = v; }
     else TORCH_CHECK(false, "unknown kernel knob ", which);
   });
-  m.def("igemm_partial_rows", &pddl::igemm_partial_rows);
+  m.def("igemm_partial_rows", [](int M, int Nn, int K, bool bnz) { return pddl::igemm_partial_rows(M, Nn, K, bnz); },
+        py::arg("M"), py::arg("Nn"), py::arg("K"), py::arg("bnz") = false);
   m.def("igemm_plan", [](int M, int Nn, int K) {
     int cfg = 0, split = 0;
     pddl::igemm_plan_query(M, Nn, K, &cfg, &split);

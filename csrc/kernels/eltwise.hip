@@ -719,7 +719,9 @@ const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, 
 }
 
 // Fold partial column-sum rows: grid (row chunks, layers).  A block = RL row-lanes x C
-// columns (C <= 256) reduced through LDS, then one atomic per column per block.
+// columns (C <= 256) reduced through LDS, then one atomic per column per block.  A layer may
+// fold a column range of wider rows (ColRedLayer::pad = row stride): the (sum g | sum g*(z-mu))
+// halves of a fused BN-backward dgrad land in two separate accumulators.
 __global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRedLayer* __restrict__ L,
                                      float* __restrict__ colsum) {
   __shared__ float red[256];
@@ -728,12 +730,13 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRe
   const int r0 = (int)((long)l.rows * blockIdx.x / chunks), r1 = (int)((long)l.rows * (blockIdx.x + 1) / chunks);
   if (r0 >= r1) return;
   const int t = threadIdx.x;
+  const long ld = l.pad > 0 ? l.pad : l.C;   // row stride (pad > 0: one column range of wider rows)
   if (l.C <= 256) {
     const int RL = 256 / l.C;
     const int c = t % l.C, rl = t / l.C;
     float s = 0.f;
     if (rl < RL)
-      for (int r = r0 + rl; r < r1; r += RL) s += part[l.part + (long)r * l.C + c];
+      for (int r = r0 + rl; r < r1; r += RL) s += part[l.part + (long)r * ld + c];
     red[t] = s;
     __syncthreads();
     if (t < l.C) {
@@ -743,7 +746,7 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRe
   } else {
     for (int c = t; c < l.C; c += blockDim.x) {
       float s = 0.f;
-      for (int r = r0; r < r1; ++r) s += part[l.part + (long)r * l.C + c];
+      for (int r = r0; r < r1; ++r) s += part[l.part + (long)r * ld + c];
       unsafeAtomicAdd(colsum + l.out + c, s);
     }
   }

@@ -63,7 +63,7 @@ __device__ __forceinline__ int sw_read(int lane, int kh) { return (((kh * 4) + (
 // and batch statistics (train-mode BN forward) go to partial row `prow`.
 // PF: the per-element epilogue operand of the whole sub-tile is loaded into registers before
 // the accumulators are staged, so its HBM latency overlaps the staging.
-template <int TM, int TN, bool PF>
+template <int TM, int TN, bool PF, bool BNZ = false>
 __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
                                                float* stage, int lane) {
   constexpr int WTN = 16 * TN;
@@ -80,10 +80,13 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
   int ldo = p.ldo, col = gn;
   bool seg0 = true;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // FWD stats: sum of squares
-  if (p.mode != EPI_DGRAD && col_ok) {
-    const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
-    const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
+  float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // FWD stats: sum of squares; DGRAD: sum g*(z-mu)
+  // sc: FWD / F32 scale, or (BNZ: DGRAD + bn_z) the batch mean of the BN whose output
+  // gradient this is.  BNZ is a separate kernel instantiation: the fused sums cost the
+  // default kernels' register budget 30 VGPRs (occupancy 3 -> 2) when compiled in.
+  if ((p.mode != EPI_DGRAD || BNZ) && col_ok) {
+    const float4* s4 = reinterpret_cast<const float4*>((p.mode == EPI_DGRAD ? p.bn_mean : p.scale) + gn);
+    const float4* h4 = reinterpret_cast<const float4*>((p.mode == EPI_DGRAD ? p.bn_mean : p.shift) + gn);
     float4 a = s4[0], b = s4[1], c = h4[0], d = h4[1];
     sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
     sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
@@ -224,9 +227,19 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
             }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) csum[e] += w[e];
             const uint4 pk = pack8(w);
+            if constexpr (BNZ) {
+              // train-mode BN backward reduction fused here (stats rows; no up2): sums of exactly
+              // the stored bf16 gradient, as bn_bwd_apply will read it
+              float zv[8], wr[8];
+              unpack8(*reinterpret_cast<const uint4*>(p.bn_z + rq * p.ldo + gn), zv);
+              unpack8(pk, wr);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) { csum[e] += wr[e]; csq[e] += wr[e] * (zv[e] - sc[e]); }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) csum[e] += w[e];
+            }
             *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pk;
             // compact copy of the stride-2 positions (the only nonzero rows of the scatter):
             // the consumers of a downsampling block's input gradient run at a quarter of M on it
@@ -254,7 +267,8 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
     }
   }
   // Train-mode BN: per-wave partial (sum, sum of squares) rows of the forward output, same
-  // row indexing as the column sums; colsum_reduce folds them and bn_stats finalizes.
+  // row indexing as the column sums; colsum_reduce folds them and bn_stats finalizes.  In a
+  // dgrad with bn_z the rows are (sum g, sum g*(z - mean)) for bn_bwd_apply.
   if (p.stats) {
 #pragma unroll
     for (int o = LPR; o < 64; o <<= 1)
@@ -288,7 +302,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 // accumulators are staged through LDS, so its HBM latency overlaps the staging instead of
 // stalling every store iteration (short-K 1x1 layers are epilogue-bound).
 // WTM_: wave-tile rows (64, or 128 for the 256x256 tile: 8 waves as 2 x 4, 128x64 each).
-template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64>
+template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64, bool BNZ = false>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParams p) {
   constexpr int WTM = WTM_, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -474,7 +488,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (WTN + 4));
-  igemm_epilogue<TM, TN, PF>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, stage, lane);
+  igemm_epilogue<TM, TN, PF, BNZ>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, stage,
+                                  lane);
 }
 
 
@@ -722,6 +737,9 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
   if (!igemm_no_halo(p) && p.R * p.S > 32) { *why = "padded convs support at most 32 taps"; return false; }
   if (p.Nn % 8 || p.ldb % 8 || p.ldo % 8) { *why = "N / ldb / ldo must be multiples of 8"; return false; }
   if (p.M <= 0 || p.Nn <= 0 || p.K <= 0) { *why = "empty problem"; return false; }
+  if (p.bn_z && (p.mode != EPI_DGRAD || p.a2 || p.up2 || !p.stats)) {
+    *why = "bn_z: fused BN-backward sums need a single-source dgrad without scatter, with stats rows"; return false;
+  }
   if ((long)p.M * p.Ho * p.Wo >= (1L << 40)) { *why = "too many output rows for the magic-number row decode"; return false; }
   // buffer offsets are 32-bit byte offsets with 0x80000000 reserved as "out of range"
   if ((long)p.N * p.H * p.W * (p.C1 > p.C2 ? p.C1 : p.C2) * 2 >= (1L << 31) || (long)p.Nn * p.ldb * 2 >= (1L << 31)) {
@@ -779,8 +797,12 @@ int num_cus() {
 // CU) instead of leaving CUs idle for a whole 256x256 tile time (b1024 stage 4: 784 tiles on
 // 256 CUs = 3 full rounds + 16 tiles).
 struct IgemmPlan { int cfg, split; };
-static IgemmPlan igemm_plan(int M, int Nn, int K) {
+static IgemmPlan igemm_plan(int M, int Nn, int K, bool bnz = false) {
   IgemmPlan pl{igemm_config(M, Nn, K), M};
+  if (bnz) {   // fused BN-backward sums: only the 4-wave single-stage tiles carry that epilogue
+    if (pl.cfg != 0) pl.cfg = 1;
+    return pl;
+  }
   if (pl.cfg != 4) return pl;
   const int nt = (Nn + 255) / 256, mt = (M + 255) / 256;
   const long T = (long)mt * nt, C = num_cus();
@@ -800,8 +822,8 @@ void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split) {
   *split = pl.split;
 }
 
-int igemm_partial_rows(int M, int Nn, int K) {
-  const IgemmPlan pl = igemm_plan(M, Nn, K);
+int igemm_partial_rows(int M, int Nn, int K, bool bnz) {
+  const IgemmPlan pl = igemm_plan(M, Nn, K, bnz);
   return igemm_rows_of(pl.cfg, pl.split) + (pl.split < M ? igemm_rows_of(1, M - pl.split) : 0);
 }
 
@@ -815,7 +837,7 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   p.mg_wo = fdiv_magic(p.Wo);
   p.m_begin = 0;
   p.prow_begin = 0;
-  const IgemmPlan pl = igemm_plan(p.M, p.Nn, p.K);
+  const IgemmPlan pl = igemm_plan(p.M, p.Nn, p.K, p.bn_z != nullptr);
   if (pl.split < p.M) {
     IgemmParams head = p, tail = p;
     head.M = pl.split;
@@ -857,7 +879,16 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
   // VGPRs cut from 3 to 2 waves per SIMD -- so dgrad uses it only on 2-stage tiles.
   const bool pf = g_igemm_pf && am == AM_DIRECT && cfg <= 1 &&
                   ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && (ns == 2 || g_igemm_pf == 2)));
-  if (cfg == 4) {
+  if (p.bn_z) {   // (igemm_check: DGRAD, no dual source; plan: cfg 0 / 1)
+#define IG_Z(BM_, BN_, AM_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, 1, AM_, false, 64, true>), dim3(nwg), dim3(256), 0, stream, p)
+    if (cfg == 0) {
+      if (am == AM_DIRECT) IG_Z(256, 64, AM_DIRECT); else IG_Z(256, 64, AM_HALO);
+    } else {
+      if (am == AM_DIRECT) IG_Z(128, 128, AM_DIRECT); else IG_Z(128, 128, AM_HALO);
+    }
+#undef IG_Z
+  } else if (cfg == 4) {
 #define IG_8(AM_)                                                                                         \
   {                                                                                                       \
     if (g_igemm8 == 2) hipLaunchKernelGGL((igemm8_kernel<AM_, true>), dim3(nwg), dim3(512), 0, stream, p); \

@@ -34,12 +34,16 @@ struct IgemmParams {
   const uint8_t* bits_mask; int ld_bits_mask;       // DGRAD: multiply by the bit instead of (mask > 0)
   float* stats;                                     // FWD: per-wave partial [rows][2*Nn]: sum | sum of squares
                                                     //      of the stored outputs (train-mode BN batch statistics)
+                                                    // DGRAD (with bn_z): sum g | sum g * (z - bn_mean) of the
+                                                    //      stored gradient (train-mode BN backward reduction)
+  const uint16_t* bn_z; const float* bn_mean;       // DGRAD: the BN input z ([rows][ldo]) and its batch mean
   uint64_t mg_howo, mg_wo;                          // set by igemm_launch: magic divisors (fdiv)
   int m_begin, prow_begin;                          // set by igemm_launch: this launch covers GEMM rows
                                                     // [m_begin, M); its partial rows start at prow_begin
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
-int igemm_partial_rows(int M, int Nn, int K);        // rows of the partial column-sum buffer
+int igemm_partial_rows(int M, int Nn, int K, bool bnz = false);   // rows of the partial column-sum buffer
+                                                    // (bnz: a launch with the fused BN-backward sums)
 void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split);   // tile config; rows >= split: 128x128 tail
 extern int g_igemm8, g_igemm8_min_tiles, g_igemm8_expand, g_igemm8_min_n, g_igemm_ns1_kt, g_wgrad8, g_wgrad1;
 int num_cus();   // compute units of the current device (cached)
@@ -99,7 +103,7 @@ const char* gap_bwd_launch(const uint16_t* gp, int ldgp, const uint16_t* ymask, 
 const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, hipStream_t s);
 // Partial column sums written by the fused producers (igemm dgrad, maxpool_bwd, gap_bwd):
 // colsum[l.out + c] += sum_t part[l.part + t * C + c] for every layer of the table.
-struct ColRedLayer { long part; int rows, C, out; int pad; };
+struct ColRedLayer { long part; int rows, C, out; int pad; };   // pad > 0: row stride (floats)
 const char* colsum_reduce_launch(const float* part, const ColRedLayer* layers_dev, int nlayers, float* colsum,
                                  hipStream_t s);
 int maxpool_bwd_partial_rows(int B, int H, int W, int C);

@@ -11,7 +11,9 @@ statistics, momentum 0.99, epsilon 1.001e-5) on the same MFMA kernels plus csrc/
                       -> bn_apply: y = relu(bn(z) [+ x | + bn0(z0)]) + ReLU bitmask
   backward, per conv: (dgrad of the next conv applies the ReLU bitmask, adds the residual
                       gradient) -> bn_bwd_reduce (sum g, sum g*(z - mean)) -> bn_bwd_apply
-                      (dz; dgamma, dbeta, dbias) -> wgrad(x, dz) and dgrad(dz, W^T)
+                      (dz; dgamma, dbeta, dbias) -> wgrad(x, dz) and dgrad(dz, W^T);
+                      for BN1 / BN2 (fed by the conv2 / conv3 dgrads) the two sums are fused
+                      into the dgrad epilogue (it reads z instead of a separate pass over g, z)
   A projection block's BN3 and shortcut BN0 share one reduce and one apply pass (same g).
 
 Parity: tests/test_gpu_bn_train.py compares against models/reference.py (bn_mode="train") and
@@ -56,6 +58,8 @@ class HipEngineBNTrain(HipEngine):
         self.bcoef = torch.zeros(3 * self.nch, **f32)   # backward (A, B, C) per channel
         # zeroed per step: forward (sum, sum^2) of every igemm launch | backward sum g | sum g*(z-mean)
         self.bws = torch.zeros(off + 2 * self.nch, **f32)
+        self._bws_off = off
+        self._bwd_tabs = {}
         self.acc = self.bws[:off]
         self.bsg = self.bws[off:off + self.nch]
         self.bsgx = self.bws[off + self.nch:off + 2 * self.nch]
@@ -124,6 +128,11 @@ class HipEngineBNTrain(HipEngine):
                 col += c.cout
             st = self._stat_table(items, count=float(M))
             res[key] = (cred, st, len(items), max(c.cout for c in convs[key]), M)
+        for b in L.blocks:   # fused BN-backward dgrads (c3 -> g2, c2 -> g1): [rows][2 * f]
+            H, Ho = self.geo[b.name]
+            M, f = B * Ho * Ho, b.filters
+            for K in (4 * f, 9 * f):
+                max_part = max(max_part, N.igemm_partial_rows(M, f, K, True) * 2 * f)
         res["_max_part"] = max_part
         self._stat_cache[B] = res
         return res
@@ -158,7 +167,7 @@ class HipEngineBNTrain(HipEngine):
         ch = self.ch[key]
         N.igemm_bn(x, None, H, W, R, S, stride, pad, Ho, Wo, self._wf(key, nn, K), 0, self.scale[ch:], self.shift[ch:],
                    None, None, None, out, 0, out2, 0, n_split, 0, 0, 0, None, None,
-                   self.partial if training else None)
+                   self.partial if training else None, None, None)
         if training:
             cred, st, nst, maxc, _ = tabs[key]
             N.colsum_reduce(self.partial, cred, 1, self.acc)
@@ -242,6 +251,30 @@ class HipEngineBNTrain(HipEngine):
             N.bn_bwd_apply(g, z, z2, self._bn_layer(c, M), self._bn_layer(c2, M), self.params, self.bn_mean,
                            self.bn_inv, self.bsg, self.bsgx, out, out2, self.grads, self.bcoef)
 
+    def _dgrad_bn_bwd(self, g_in, Ho, R, pad, w, mask, g, z, c, M):
+        """g = dgrad(g_in) * mask with the BN-backward sums (sum g, sum g*(z - mean)) of conv `c`'s
+        BN fused into the dgrad epilogue (stats rows folded into bsg / bsgx: no bn_bwd_reduce
+        pass over g and z), then dz = bn_bwd_apply(g, z) in place."""
+        N = self.N
+        f = c.cout
+        N.igemm_bn(g_in, None, Ho, Ho, R, R, 1, pad, Ho, Ho, w, 1, None, None, None, mask, None, g, 0, None, 0, 0,
+                   0, 0, 0, None, None, self.partial, z, self._chs(self.bn_mean, c))
+        key = (c.name, M)
+        tab = self._bwd_tabs.get(key)
+        if tab is None:
+            rows = N.igemm_partial_rows(M, f, w.shape[1], True)
+            o = self._bws_off + self.ch[c.name]
+            tab = self._dev_table([struct.pack("<q4i", 0, rows, f, o, 2 * f),
+                                   struct.pack("<q4i", f, rows, f, o + self.nch, 2 * f)])
+            self._bwd_tabs[key] = tab
+        N.colsum_reduce(self.partial, tab, 2, self.bws)
+        self._bn_bwd_apply(g, z, c, M, g)
+
+    def _bn_bwd_apply(self, g, z, c, M, out):
+        """dz from g once bsg / bsgx of conv `c`'s BN hold (sum g, sum g*(z - mean))."""
+        self.N.bn_bwd_apply(g, z, None, self._bn_layer(c, M), [], self.params, self.bn_mean, self.bn_inv, self.bsg,
+                            self.bsgx, out, None, self.grads, self.bcoef)
+
     def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0),
                          bucket_cb: Optional[Callable[[int], None]] = None, buckets=None):
         N, L = self.N, self.L
@@ -307,15 +340,11 @@ class HipEngineBNTrain(HipEngine):
             # conv3
             N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, dz3, None, 0, self._gview(c3c.name, 4 * f, f), f, 0)
             g2 = self.g2buf[: M * f].view(B, Ho, Ho, f)
-            N.igemm(dz3, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3c.name, f, 4 * f), 1, None, None, None, y2m,
-                    None, g2, 0, None, 0, 0, 0, 0, 0, None, None)
-            self._bn_bwd(g2, z["2"], c2c, M, g2)
+            self._dgrad_bn_bwd(dz3, Ho, 1, 0, self._wdv(c3c.name, f, 4 * f), y2m, g2, z["2"], c2c, M)
             # conv2 (3x3)
             N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2c.name, f, 9 * f), 9 * f, 0)
             g1 = self.g1buf[: M * f].view(B, Ho, Ho, f)
-            N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2c.name, f, 9 * f), 1, None, None, None, y1m,
-                    None, g1, 0, None, 0, 0, 0, 0, 0, None, None)
-            self._bn_bwd(g1, z["1"], c1c, M, g1)
+            self._dgrad_bn_bwd(g2, Ho, 3, 1, self._wdv(c2c.name, f, 9 * f), y1m, g1, z["1"], c1c, M)
             # conv1 (+ conv0)
             nxt = 1 - cur
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)

@@ -42,13 +42,46 @@ def test_igemm_stats_epilogue(case):
     rows = nat.igemm_partial_rows(M, co, K)
     part = torch.full((rows * 2 * co,), float("nan"), device=dev)
     nat.igemm_bn(x, None, h, h, r, r, st, pad, ho, ho, w.view(co, -1), 0, ones, bias, None, None, None, out, 0, None,
-                 0, 0, 0, 0, 0, None, None, part)
+                 0, 0, 0, 0, 0, None, None, part, None, None)
     acc = torch.zeros(2 * co, device=dev)
     tab = torch.frombuffer(bytearray(struct.pack("<q4i", 0, rows, 2 * co, 0, 0)), dtype=torch.uint8).to(dev)
     nat.colsum_reduce(part, tab, 1, acc)
     y = out.float().view(M, co)
     assert rel(acc[:co], y.sum(0)) < 1e-4
     assert rel(acc[co:], (y * y).sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("case", [(2, 14, 64, 64, 1, 0), (3, 9, 128, 64, 3, 1), (2, 7, 512, 256, 1, 0),
+                                  (1, 5, 2048, 512, 1, 0)])
+def test_dgrad_fused_bn_backward_sums(case):
+    """dgrad epilogue with bn_z: partial rows (sum g, sum g*(z - mean)) of the stored, masked
+    gradient, folded by two strided colsum_reduce layers into separate accumulators."""
+    torch.manual_seed(3)
+    n, h, co, cin, r, pad = case   # conv cin -> co; its dgrad has GEMM width cin
+    nat = N()
+    g_in = rnd(n, h, h, co)
+    w = rnd(co, r, r, cin, scale=0.05)
+    wt = w.float().flip(1).flip(2).permute(3, 1, 2, 0).contiguous().to(torch.bfloat16)   # [cin][R][S][co]
+    mask = rnd(n, h, h, cin)
+    z = rnd(n, h, h, cin, scale=2.0, shift=0.5)
+    mean = torch.randn(cin, device=dev) * 0.3
+    out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
+    M, K = n * h * h, r * r * co
+    rows = nat.igemm_partial_rows(M, cin, K, True)
+    part = torch.full((rows * 2 * cin,), float("nan"), device=dev)
+    nat.igemm_bn(g_in, None, h, h, r, r, 1, r - 1 - pad, h, h, wt.view(cin, -1), 1, None, None, None, mask, None, out,
+                 0, None, 0, 0, 0, 0, 0, None, None, part, z, mean)
+    ref = torch.nn.grad.conv2d_input((n, cin, h, h), w.float().permute(0, 3, 1, 2), g_in.float().permute(0, 3, 1, 2),
+                                     padding=pad).permute(0, 2, 3, 1) * (mask.float() > 0)
+    assert rel(out, ref) < 1e-2
+    acc = torch.zeros(2 * cin + 7, device=dev)
+    tab = torch.frombuffer(bytearray(struct.pack("<q4i", 0, rows, cin, 0, 2 * cin) +
+                                     struct.pack("<q4i", cin, rows, cin, cin + 7, 2 * cin)),
+                           dtype=torch.uint8).to(dev)
+    nat.colsum_reduce(part, tab, 2, acc)
+    gv, zv = out.float().view(M, cin), z.float().view(M, cin)
+    assert rel(acc[:cin], gv.sum(0)) < 1e-4
+    assert rel(acc[cin + 7:], (gv * (zv - mean)).sum(0)) < 1e-4
 
 
 def _stat_table(C, count, ch, offs):
@@ -185,6 +218,13 @@ def test_train_bn_engine_matches_reference(crop, image_size):
         orig(g, z, c, M, out, z2, c2, out2)
         rec.append((c.name, gin, z.clone(), out.clone(), None if z2 is None else (c2.name, z2.clone(), out2.clone())))
     he._bn_bwd = spy
+    orig_apply = he._bn_bwd_apply   # BN1 / BN2: sums fused into the dgrad epilogue, then the apply
+
+    def spy_apply(g, z, c, M, out):
+        gin = g.clone()
+        orig_apply(g, z, c, M, out)
+        rec.append((c.name, gin, z.clone(), out.clone(), None))
+    he._bn_bwd_apply = spy_apply
     s_h = he.forward_backward(img, lab, 1.0 / B, flip=flip, crop_offset=off).clone()
     s_t = te.forward_backward(img, lab, 1.0 / B, flip=flip, crop_offset=off)
     torch.cuda.synchronize()
