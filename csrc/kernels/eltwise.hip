@@ -64,10 +64,66 @@ __global__ void stem_s2d_kernel(StemParams p, int npix, uint64_t mg_ws, uint64_t
   }
 }
 
+// Row form for uint8 identity / crop input (modes 0 and 2, the training path): one block per
+// s2d row (b, i) stages the two preprocessed source rows 2i-3, 2i-2 through LDS with
+// coalesced 4-byte loads (the per-pixel form issues 12 scattered byte loads per thread and
+// ran at 1.8 TB/s), then thread j assembles s2d pixel j (flip applied on the LDS read).
+// Bitwise equal to the per-pixel form (same (float)u8 * scale -> bf16).
+constexpr int STEM_ROW_MAXW = 1024;   // preprocessed width the LDS row buffer holds
+__global__ void __launch_bounds__(128) stem_s2d_rows_kernel(StemParams p) {
+  __shared__ uint32_t rowbuf[2][(STEM_ROW_MAXW * 3) / 4 + 2];
+  if (p.crop_dev) { p.oy = p.crop_dev[0]; p.ox = p.crop_dev[1]; }
+  const int i = blockIdx.x % p.Hs, b = blockIdx.x / p.Hs;
+  const int oy = p.mode == 2 ? p.oy : 0, ox = p.mode == 2 ? p.ox : 0;
+  const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
+  int shift[2];
+  bool rok[2];
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy) {
+    const int y = 2 * i + dy - 3;
+    rok[dy] = y >= 0 && y < p.Hc;
+    shift[dy] = 0;
+    if (!rok[dy]) continue;
+    const uint8_t* src = in + (((long)b * p.Hin + y + oy) * p.Win + ox) * 3;
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3);
+    shift[dy] = (int)(reinterpret_cast<uintptr_t>(src) - a0);
+    const int nw = (shift[dy] + p.Wc * 3 + 3) / 4;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a0);
+    for (int k = threadIdx.x; k < nw; k += blockDim.x) rowbuf[dy][k] = w[k];
+  }
+  __syncthreads();
+  const bool fl = p.flip && p.flip[b];
+  const uint8_t* rb = reinterpret_cast<const uint8_t*>(&rowbuf[0][0]);
+  constexpr int ROWB = ((STEM_ROW_MAXW * 3) / 4 + 2) * 4;
+  for (int j = threadIdx.x; j < p.Ws; j += blockDim.x) {
+    float v[16];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int dy = d >> 1;
+      int x = 2 * j + (d & 1) - 3;
+      const bool in_ = rok[dy] && x >= 0 && x < p.Wc;
+      if (fl) x = p.Wc - 1 - x;
+      const int o = dy * ROWB + shift[dy] + x * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[d * 4 + c] = in_ ? (float)rb[o + c] * p.scale : 0.f;
+      v[d * 4 + 3] = 0.f;
+    }
+    uint4* o = reinterpret_cast<uint4*>(p.out + (((long)b * p.Hs + i) * p.Ws + j) * 16);
+    o[0] = pack8(v);
+    o[1] = pack8(v + 8);
+  }
+}
+int g_stem_variant = 1;   // 1: row form for uint8 modes 0 / 2 (default), 0: per-pixel form everywhere
+
 const char* stem_s2d_launch(const StemParams& p, hipStream_t s) {
   if ((p.Hc + 6) != 2 * p.Hs || (p.Wc + 6) != 2 * p.Ws) return "stem_s2d: Hs must be (Hc + 6) / 2 (even crop)";
   const long npix = (long)p.B * p.Hs * p.Ws;
   if (npix >= (1L << 31) - (1L << 24)) return "stem_s2d: too many pixels for 32-bit indexing";
+  if (g_stem_variant == 1 && p.in_u8 && p.mode != 1 && p.Wc <= STEM_ROW_MAXW) {
+    hipLaunchKernelGGL(stem_s2d_rows_kernel, dim3(p.B * p.Hs), dim3(128), 0, s, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? nullptr : hipGetErrorString(e);
+  }
   const int grid = (int)lmin((npix + 255) / 256, 16384);
   hipLaunchKernelGGL(stem_s2d_kernel, dim3(grid), dim3(256), 0, s, p, (int)npix, fdiv_magic(p.Ws), fdiv_magic(p.Hs));
   hipError_t e = hipGetLastError();

@@ -535,6 +535,28 @@ def test_device_hparams_adam_steps():
     assert torch.allclose(p, pr, atol=1e-6, rtol=1e-5)
 
 
+@pytest.mark.parametrize("S,crop,oy,ox", [(32, 32, 0, 0), (35, 24, 3, 5), (224, 224, 0, 0), (250, 244, 2, 1)])
+def test_stem_s2d_row_form_matches_pixel_form(S, crop, oy, ox):
+    """Row-staged stem (knob stem=1, default for uint8 identity / crop) is bitwise equal to the
+    per-pixel form, with flips, odd source widths and unaligned crop offsets."""
+    torch.manual_seed(10)
+    B = 3
+    img = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev)
+    flip = torch.tensor([0, 1, 1], dtype=torch.uint8, device=dev)
+    hs = (crop + 6) // 2
+    m = 0 if crop == S else 2
+    outs = []
+    try:
+        for v in (0, 1):
+            N().set_variant("stem", v)
+            x2 = torch.full((B, hs, hs, 16), float("nan"), dtype=torch.bfloat16, device=dev)
+            N().stem_s2d(img, flip, m, crop, crop, oy, ox, x2, None)
+            outs.append(x2)
+    finally:
+        N().set_variant("stem", 1)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("mode", ["identity", "resize", "crop"])
 def test_stem_s2d_conv_and_wgrad(mode):
     """Preprocess + space-to-depth + 4x4 window igemm == Keras stem conv (7x7/s2 after
