@@ -445,6 +445,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "pool") pddl::g_pool_variant = v;
     else if (which == "igemm_n64") pddl::g_igemm_n64 = v;
     else if (which == "stem") pddl::g_stem_variant = v;
+    else if (which == "igemm8_ragged") pddl::g_igemm8_ragged = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;

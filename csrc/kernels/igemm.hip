@@ -716,6 +716,8 @@ int g_igemm8_expand = 0;
 int g_igemm8_min_n = 512;  // ... and only for GEMM widths Nn >= this (with single-stage 128x128
                            // tiles the 8-phase kernel wins only the stage-5 layers, kbench)  // A/B: also run the expansion 1x1s (Nn >= 4K) on the 8-phase kernel
 int g_igemm8_min_tiles = 128;   // ... when the problem has at least this many 256x256 tiles
+int g_igemm8_ragged = 0;   // 1: 8-phase tiles also for widths that are not a multiple of 256 (conv3_block1
+                           // c1+shortcut, Nn = 640: 680 us vs 588 us on five 128-wide tiles; not kept)
 int g_igemm_n64 = 1;       // see igemm_config (1: conv2_block1 c1+c0 fwd 831 -> 765 us; 2: no further gain)
 int g_igemm_il = 0;        // 2-stage tiles issue the next tile's LDS-DMA interleaved with the MFMAs:
                            // off (measured -3..-12% on the compute-bound layers, -2.5% end to end;
@@ -763,6 +765,7 @@ static int igemm_config(int M, int Nn, int K) {
   // residual gradient: measured 30-40% slower there than the 2-block 128x128 tile with the
   // epilogue-operand prefetch (per-layer A/B, profiles/r2_igemm8_per_layer_ab.txt)
   if (g_igemm8 && Nn >= g_igemm8_min_n && K >= 256 && (Nn < 4 * K || g_igemm8_expand) &&
+      (g_igemm8_ragged || Nn % 256 == 0) &&
       (long)((M + 255) / 256) * ((Nn + 255) / 256) >= g_igemm8_min_tiles)
     return 4;
   if (g_igemm_big == 4 && Nn > 128) return 3;   // forced (equivalence tests)
