@@ -774,32 +774,77 @@ const char* colsum_launch(const uint16_t* g, int M, int C, int ldg, float* out, 
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
-// Fold partial column-sum rows: grid (row chunks, layers).  A block = RL row-lanes x C
-// columns (C <= 256) reduced through LDS, then one atomic per column per block.  A layer may
-// fold a column range of wider rows (ColRedLayer::pad = row stride): the (sum g | sum g*(z-mu))
-// halves of a fused BN-backward dgrad land in two separate accumulators.
-__global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRedLayer* __restrict__ L,
-                                     float* __restrict__ colsum) {
-  __shared__ float red[256];
+// Fold partial column-sum rows: grid (row chunks, layers).  A layer may fold a column range of
+// wider rows (ColRedLayer::pad = row stride): the (sum g | sum g*(z-mu)) halves of a fused
+// BN-backward dgrad land in two separate accumulators.
+// The fold is bound by same-address atomics, not by bytes: atomics onto one column serialize
+// at ~60-100 ns each, so 512-1024 row chunks per layer cost 30-100 us even for a 6 MB layer
+// (the previous 256-thread, 512-chunk fold: 2.5 ms per train-BN b1024 step,
+// profiles/r2_bntrain_b1024_summary.txt).  So: few chunks (COLRED_CHUNKS = 64, at least
+// COLRED_MIN_ROWS rows each), and enough loads in flight per chunk to stream its rows anyway --
+// 1024-thread blocks of RL row-lanes x NC float4 column lanes (NC <= 1024 float4 = 4096 columns
+// per pass), 8 rows in flight per lane with independent accumulators (128 KiB per block), the
+// row-lanes folded through LDS, one atomic per column per chunk.
+// Vector path when C, the row stride and the offset are multiples of 4 floats (every engine
+// table); scalar fallback otherwise.
+constexpr int COLRED_MIN_ROWS = 32;
+constexpr int COLRED_THREADS = 1024;
+__global__ void __launch_bounds__(COLRED_THREADS) colsum_reduce_kernel(const float* __restrict__ part,
+                                                                       const ColRedLayer* __restrict__ L,
+                                                                       float* __restrict__ colsum) {
+  __shared__ float4 red[COLRED_THREADS];
   const ColRedLayer l = L[blockIdx.y];
-  const int chunks = gridDim.x;
-  const int r0 = (int)((long)l.rows * blockIdx.x / chunks), r1 = (int)((long)l.rows * (blockIdx.x + 1) / chunks);
+  const int eff = max(1, min((int)gridDim.x, l.rows / COLRED_MIN_ROWS));
+  if ((int)blockIdx.x >= eff) return;
+  const int r0 = (int)((long)l.rows * blockIdx.x / eff), r1 = (int)((long)l.rows * (blockIdx.x + 1) / eff);
   if (r0 >= r1) return;
   const int t = threadIdx.x;
   const long ld = l.pad > 0 ? l.pad : l.C;   // row stride (pad > 0: one column range of wider rows)
-  if (l.C <= 256) {
-    const int RL = 256 / l.C;
-    const int c = t % l.C, rl = t / l.C;
-    float s = 0.f;
-    if (rl < RL)
-      for (int r = r0 + rl; r < r1; r += RL) s += part[l.part + (long)r * ld + c];
-    red[t] = s;
-    __syncthreads();
-    if (t < l.C) {
-      for (int i = 1; i < RL; ++i) s += red[t + i * l.C];
-      unsafeAtomicAdd(colsum + l.out + c, s);
+  if ((l.C & 3) == 0 && (ld & 3) == 0 && (l.part & 3) == 0) {
+    const int C4 = l.C >> 2;
+    const long ld4 = ld >> 2;
+    const float4* base = reinterpret_cast<const float4*>(part + l.part);
+    for (int cb = 0; cb < C4; cb += COLRED_THREADS) {
+      const int nc = min(COLRED_THREADS, C4 - cb);
+      const int RL = COLRED_THREADS / nc;
+      const int c4 = cb + t % nc, rl = t / nc;
+      float4 acc[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rl < RL) {
+        const float4* col = base + c4;
+        int r = r0 + rl;
+        for (; r < r1; r += 8 * RL) {   // 8 rows per lane in flight; rows past r1 re-read row r
+          float4 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int rr = r + u * RL;
+            const float4 x = col[(long)(rr < r1 ? rr : r) * ld4];
+            v[u] = rr < r1 ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) { acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w; }
+        }
+      }
+      float4 s0 = acc[0];
+#pragma unroll
+      for (int u = 1; u < 8; ++u) { s0.x += acc[u].x; s0.y += acc[u].y; s0.z += acc[u].z; s0.w += acc[u].w; }
+      red[t] = s0;
+      __syncthreads();
+      if (t < nc) {
+        for (int i = 1; i < RL; ++i) {
+          const float4 o = red[t + i * nc];
+          s0.x += o.x; s0.y += o.y; s0.z += o.z; s0.w += o.w;
+        }
+        float* dst = colsum + l.out + 4 * c4;
+        unsafeAtomicAdd(dst + 0, s0.x);
+        unsafeAtomicAdd(dst + 1, s0.y);
+        unsafeAtomicAdd(dst + 2, s0.z);
+        unsafeAtomicAdd(dst + 3, s0.w);
+      }
+      __syncthreads();
     }
-  } else {
+  } else {   // scalar fallback (unaligned column ranges)
     for (int c = t; c < l.C; c += blockDim.x) {
       float s = 0.f;
       for (int r = r0; r < r1; ++r) s += part[l.part + (long)r * ld + c];
@@ -807,13 +852,12 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, const ColRe
     }
   }
 }
-int g_colred_chunks = 512;   // row chunks per layer (knob colred_chunks): train-BN b256 end to end
-                             // 16/32/64/128/512/1024/2048 chunks = 8.3k/9.3k/9.9k/10.2k/10.25k/10.0k/9.8k img/s
+int g_colred_chunks = 64;   // row-chunk cap per layer (knob colred_chunks)
 const char* colsum_reduce_launch(const float* part, const ColRedLayer* layers_dev, int nlayers, float* colsum,
                                  hipStream_t s) {
-  // 512 row chunks per layer: every CU gets work even for one large layer (chunks past a
-  // small layer's rows exit at once); one atomic per column per chunk
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(g_colred_chunks, nlayers), dim3(256), 0, s, part, layers_dev, colsum);
+  // up to g_colred_chunks row chunks per layer (at least COLRED_MIN_ROWS rows each): every CU
+  // gets work for one large layer; chunks past a short layer's share exit at once
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(g_colred_chunks, nlayers), dim3(COLRED_THREADS), 0, s, part, layers_dev, colsum);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -615,3 +615,22 @@ def test_synth_kernel_matches_cpu_reference():
     ic, lc = ds.fetch(idx, "cpu")
     ig, lg = ds.fetch(idx, "cuda")
     assert torch.equal(ic, ig.cpu()) and torch.equal(lc, lg.cpu())
+
+
+@pytest.mark.parametrize("rows,C,pad,off", [(1, 4, 0, 0), (31, 128, 0, 0), (33, 640, 0, 0), (1000, 4096, 0, 0),
+                                            (50000, 512, 0, 0), (7, 6, 0, 0), (300, 64, 128, 64), (4097, 1028, 0, 4)])
+def test_colsum_reduce_layers(rows, C, pad, off):
+    """colsum_reduce (float4 row-lane fold, scalar fallback for unaligned ranges, strided column
+    ranges, several layers per launch) against an fp32 torch column sum."""
+    import struct
+    torch.manual_seed(5)
+    ld = pad if pad > 0 else C
+    part = torch.randn(off + rows * ld + 3, device=dev)
+    out = torch.zeros(2 * C + 5, device=dev)
+    tab = torch.frombuffer(bytearray(struct.pack("<q4i", off, rows, C, 0, pad) +
+                                     struct.pack("<q4i", off, rows, C, C + 5, pad)), dtype=torch.uint8).to(dev)
+    N().colsum_reduce(part, tab, 2, out)
+    ref = part[off:off + rows * ld].view(rows, ld)[:, :C].double().sum(0).float()
+    assert rel(out[:C], ref) < 1e-5
+    assert rel(out[C + 5:], ref) < 1e-5
+    assert torch.all(out[C:C + 5] == 0)
