@@ -97,6 +97,7 @@ void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, 
              "dgrad out2 is the compact [N*Ho*Wo][Nn] copy of an up2 scatter");
   }
   p.relu2 = (int)relu2; p.n_split = (int)n_split;
+  PCHECK(up2 >= 0 && up2 <= 2, "up2: 0 none, 1 scatter + zero fill, 2 grid positions only");
   p.up2 = (int)up2; p.Hf = (int)Hf; p.Wf = (int)Wf;
   p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;
   if (p.colsum)

@@ -198,7 +198,7 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
           for (int q = 0; q < 4; ++q) {
             long rq = row;
             if (q > 0) {
-              if (!p.up2) break;
+              if (p.up2 != 1) break;   // up2 == 2: the caller's tensor is zero off the grid already
               const int hh = 2 * i + (q >> 1), ww = 2 * j + (q & 1);
               if (hh >= p.Hf || ww >= p.Wf) continue;
               rq = ((long)n * p.Hf + hh) * p.Wf + ww;

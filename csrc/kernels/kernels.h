@@ -27,7 +27,8 @@ struct IgemmParams {
   const uint16_t* add; int ld_add;                  // DGRAD: added before the mask
   void* out; int ldo; int relu;
   void* out2; int ldo2; int relu2; int n_split;     // FWD: columns >= n_split -> out2
-  int up2; int Hf, Wf;                              // DGRAD: scatter to a 2x finer grid
+  int up2; int Hf, Wf;                              // DGRAD: scatter to a 2x finer grid (1: zero-fill the
+                                                    //   off-grid positions; 2: write grid positions only)
   float* colsum;                                    // DGRAD: per-wave partial column sums [rows][Nn]
   // ReLU masks as bitmasks (bit e of byte [row][c/8] = value[row][8*(c/8)+e] > 0):
   uint8_t* bits_out; int ld_bits_out;               // FWD: write the mask of the (segment-0) output

@@ -634,3 +634,31 @@ def test_colsum_reduce_layers(rows, C, pad, off):
     assert rel(out[:C], ref) < 1e-5
     assert rel(out[C + 5:], ref) < 1e-5
     assert torch.all(out[C:C + 5] == 0)
+
+
+@pytest.mark.parametrize("hc,cin,co", [(7, 256, 128), (4, 512, 256), (8, 128, 64)])
+def test_dgrad_up2_grid_only_scatter(hc, cin, co):
+    """Stride-2 scatter dgrad with up2 = 2 writes only the grid positions (and the compact
+    copy): into a pre-zeroed tensor it equals the zero-filling up2 = 1 scatter bitwise, the
+    off-grid positions are never touched, and the fused column sums are the same."""
+    torch.manual_seed(21)
+    n, H = 3, 2 * hc
+    g1 = rnd(n, hc, hc, co)
+    wt = rnd(cin, co, scale=0.05)
+    mask = torch.randint(0, 256, (n, H, H, cin // 8), dtype=torch.uint8, device=dev)
+    rows = N().igemm_partial_rows(n * hc * hc, cin, co)
+    res = []
+    for up2, fill in ((1, 7.0), (2, 7.0)):
+        full = torch.full((n, H, H, cin), fill, dtype=torch.bfloat16, device=dev)
+        comp = torch.empty(n, hc, hc, cin, dtype=torch.bfloat16, device=dev)
+        part = torch.zeros(rows * cin, device=dev)
+        N().igemm(g1, None, hc, hc, 1, 1, 1, 0, hc, hc, wt, 1, None, None, None, mask, None, full, 0, comp, 0, 0,
+                  up2, H, H, part, None)
+        res.append((full, comp, _fold(part, rows, cin)))
+    (f1, c1, s1), (f2, c2, s2) = res
+    assert torch.equal(c1, c2) and torch.equal(s1, s2)
+    assert torch.equal(f1[:, ::2, ::2], f2[:, ::2, ::2]) and torch.equal(f1[:, ::2, ::2], c1)
+    off = torch.ones(H, H, dtype=torch.bool, device=dev)
+    off[::2, ::2] = False
+    assert torch.all(f1[:, off] == 0)          # up2 = 1 zero-fills
+    assert torch.all(f2[:, off] == 7.0)        # up2 = 2 leaves them alone
