@@ -242,6 +242,8 @@ class HipEngine:
             b = L.blocks[bi]
             Hb = self.geo[b.name][1]
             self.s2full[bi] = torch.zeros(B * Hb * Hb * 4 * b.filters, **bf)
+        self.s2g2full = {bi: torch.zeros(B * self.geo[L.blocks[bi].name][1] ** 2 * L.blocks[bi].filters, **bf)
+                         for bi in self._s2_fed()}   # (same for their conv2-output gradient)
         self.g2cbuf = torch.empty(g2c, **bf)
         self.pooled = torch.empty(B, 2048, **bf)
         self.logits = torch.empty(B, self.num_classes, dtype=torch.float32, device=dev)
@@ -448,7 +450,7 @@ class HipEngine:
             y1, y2 = a["y1"][:B], a["y2"][:B]
             gout = (self.s2full[bi] if bi in s2 else self.gbuf[cur])[: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
             c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
-            g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            g2 = (self.s2g2full[bi] if bi in s2 else self.g2buf)[: B * Ho * Ho * f].view(B, Ho, Ho, f)
             if bi in s2:
                 # gout is zero off the stride-2 grid (the next block reads only even rows /
                 # columns); its compact copy `gc` came from that block's dgrad epilogue
@@ -457,7 +459,7 @@ class HipEngine:
                 g2c = self.g2cbuf[: B * Hc * Hc * f].view(B, Hc, Hc, f)
                 N.wgrad(y2, Ho, Ho, 1, 1, 2, 0, Hc, Hc, gc, None, 0, self._gview(c3n, 4 * f, f), f, 0)
                 N.igemm(gc, None, Hc, Hc, 1, 1, 1, 0, Hc, Hc, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
-                        None, g2, 0, g2c, 0, 0, 1, Ho, Ho, part(c2n), None)
+                        None, g2, 0, g2c, 0, 0, 2, Ho, Ho, part(c2n), None)
                 N.wgrad(y1, Ho, Ho, 3, 3, 2, 1, Hc, Hc, g2c, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
             else:
                 # conv3

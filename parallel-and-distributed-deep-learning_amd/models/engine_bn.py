@@ -140,6 +140,7 @@ class HipEngineBNTrain(HipEngine):
     # ------------------------------------------------------------------ buffers
     def _alloc_acts(self, B):
         super()._alloc_acts(B)
+        self.s2full, self.s2g2full = {}, {}   # (frozen-engine stride-2-grid backward buffers: unused here)
         L, dev = self.L, self.device
         bf = dict(dtype=torch.bfloat16, device=dev)
         self.zs = torch.empty(B, self.H1, self.H1, 64, **bf)
