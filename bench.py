@@ -196,7 +196,10 @@ def run(args):
     # synthetic batch, resident on each local device (BASELINE: synthetic data)
     ims, lbs = [], []
     for i, d in enumerate(local_devs):
-        g = torch.Generator(device=d).manual_seed(1234 + 7919 * (rank * len(local_devs) + i))
+        # (PDDL_BENCH_SAME_DATA=1: every replica gets replica 0's batch -- a multi-rank run then
+        # follows the 1-GPU loss trajectory, a check of the gradient reduction)
+        rep = 0 if os.environ.get("PDDL_BENCH_SAME_DATA") == "1" else rank * len(local_devs) + i
+        g = torch.Generator(device=d).manual_seed(1234 + 7919 * rep)
         ims.append(torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=d, generator=g))
         lbs.append(torch.randint(0, 1000, (B,), dtype=torch.int64, device=d, generator=g))
     if len(local_devs) == 1:
