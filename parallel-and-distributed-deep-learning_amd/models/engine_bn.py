@@ -140,7 +140,8 @@ class HipEngineBNTrain(HipEngine):
     # ------------------------------------------------------------------ buffers
     def _alloc_acts(self, B):
         super()._alloc_acts(B)
-        self.s2full, self.s2g2full = {}, {}   # (frozen-engine stride-2-grid backward buffers: unused here)
+        self.s2g2full = {}   # (the frozen engine's compact conv2-gradient path is not used here; s2full is:
+        #                    the downsampling blocks' dgrads write only the stride-2 grid into it)
         L, dev = self.L, self.device
         bf = dict(dtype=torch.bfloat16, device=dev)
         self.zs = torch.empty(B, self.H1, self.H1, 64, **bf)
@@ -317,6 +318,7 @@ class HipEngineBNTrain(HipEngine):
         blocks = L.blocks
         gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
         N.gap_bwd(dpooled, x5, gout, None)
+        s2 = self._s2_fed()
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
             a = self.acts[b.name]
@@ -331,7 +333,7 @@ class HipEngineBNTrain(HipEngine):
                 mask_in = self.bits[blocks[bi - 1].name]["out"][:B] if bi > 0 else self.pool_bits[:B]
                 y1m, y2m = self.bits[b.name]["y1"][:B], self.bits[b.name]["y2"][:B]
             y1, y2 = a["y1"][:B], a["y2"][:B]
-            gout = self.gbuf[cur][: M * 4 * f].view(B, Ho, Ho, 4 * f)
+            gout = (self.s2full[bi] if bi in s2 else self.gbuf[cur])[: M * 4 * f].view(B, Ho, Ho, 4 * f)
             dz3 = self.gbuf3[: M * 4 * f].view(B, Ho, Ho, 4 * f)
             c1c, c2c, c3c = b.convs["1"], b.convs["2"], b.convs["3"]
             if b.proj:   # BN3 and the shortcut BN0 share gout; dz0 overwrites gout in place
@@ -351,8 +353,11 @@ class HipEngineBNTrain(HipEngine):
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
             if b.proj:
                 N.wgrad(x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1c.name, 5 * f, cin), cin, 0)
+                up2 = 1 if b.stride == 2 else 0
+                if bi - 1 in s2:   # grid positions only, into the pre-zeroed full-resolution buffer
+                    gx, up2 = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin), 2
                 N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1c.name, cin, 5 * f), 1, None, None, None,
-                        mask_in, None, gx, 0, None, 0, 0, 1 if b.stride == 2 else 0, H, H, None, None)
+                        mask_in, None, gx, 0, None, 0, 0, up2, H, H, None, None)
                 last = L.entry(b.convs["0"].name, "kernel")
             else:
                 N.wgrad(x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1c.name, f, cin), cin, 0)
