@@ -34,12 +34,28 @@ non-zero if fewer than N GPUs are visible or the launched world does not match N
 PDDL_REHEARSE=1 lifts the device check for rehearsals of the multi-rank code on one GPU (ranks
 share device 0 over gloo; the JSON then says "rehearsal": true and the number is not a
 multi-GPU measurement).
+
+Bounded by construction (a hang must never eat the driver's scaling run):
+  * every rank arms a deadline (--timeout, default derived from steps + warmup): on expiry it
+    dumps every thread's stack (faulthandler) and exits non-zero, which makes torchrun tear
+    the other ranks down;
+  * the stall watchdogs (fusion engine, native RCCL communicator, gloo bucket waits) report a
+    collective that does not complete within PDDL_STALL_TIMEOUT and, under the bench,
+    terminate the rank PDDL_STALL_SHUTDOWN seconds later (exit 124);
+  * the spawning parent (no torchrun) enforces the same deadline over its children, stops all
+    of them as soon as one fails, and names the ranks that never reported, with the last
+    phase / step each one reached.
+The JSON's "comm" block records what the collectives actually spanned: backend, the world
+size c10d / RCCL report, an all-reduce of ones over the gradient path's communicator, and
+every rank's device index + PCI bus id gathered to rank 0.
 """
 import argparse
+import faulthandler
 import json
 import os
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -74,11 +90,17 @@ def parse(argv=None):
                     help="HIP graphs: 1 GPU = whole step; mirrored = per-device segments (default on)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: BASELINE config 1 plumbing (fp32 PyTorch reference engine, gloo ranks)")
+    ap.add_argument("--timeout", type=float, default=None,
+                    help="job deadline in seconds (default: derived from steps + warmup); on expiry every "
+                         "rank dumps its stacks and the job exits non-zero")
     args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = 32 if args.device == "cpu" else (256 if args.precision == "fp32" else 1024)
     if args.crop is None:
         args.crop = args.image_size
+    if args.timeout is None:
+        per_step = 60.0 if args.device == "cpu" else 10.0
+        args.timeout = 300.0 + per_step * (args.steps + args.warmup)
     return args
 
 
@@ -99,39 +121,96 @@ def visible_gpus() -> int:
 
 def launch(args, argv):
     """Parent of an N-GPU job without torchrun: spawn one child per worker process with the
-    torchrun environment.  Nothing here touches the GPU."""
+    torchrun environment.  Nothing here touches the GPU.  The job is bounded: the first child
+    to fail stops the rest, and at the deadline every child is stopped and the ranks that never
+    reported are named with the last phase / step each reached."""
     from pddl.parallel.launch import pick_unused_port
     per = args.local_gpus if args.strategy == "multiworker" else 1
     if args.gpus % per:
         fail(f"--gpus {args.gpus} is not a multiple of --local-gpus {per}")
     nproc = args.gpus // per
     port = pick_unused_port()
+    prog = tempfile.mkdtemp(prefix="pddl_bench_")
     env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(nproc),
-                LOCAL_WORLD_SIZE=str(nproc), PDDL_BENCH_CHILD="1")
+                LOCAL_WORLD_SIZE=str(nproc), PDDL_BENCH_CHILD="1", PDDL_BENCH_PROGRESS=prog)
     if args.device == "cpu" or rehearsing():
         env0.setdefault("PDDL_DIST_BACKEND", "gloo")
-    procs = []
+    procs = {}
     for r in range(nproc):
         env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
+        procs[r] = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                    stdout=None if r == 0 else subprocess.DEVNULL)
+    # children arm their own deadline at args.timeout; the parent's is a little later, so a
+    # child's stack dump lands first
+    deadline = time.monotonic() + args.timeout + 30.0
+    codes = {}
     rc = 0
     try:
-        while procs:
-            for p in list(procs):
+        while len(codes) < nproc:
+            for r, p in procs.items():
+                if r in codes:
+                    continue
                 code = p.poll()
                 if code is None:
                     continue
-                procs.remove(p)
+                codes[r] = code
                 if code != 0 and rc == 0:
                     rc = code
-                    for q in procs:      # a dead rank would leave its peers inside a collective
-                        q.terminate()
+                    sys.stderr.write(f"bench.py: rank {r} exited with status {code}; stopping the other ranks\n")
+                    _report_ranks(procs, codes, prog)
+                    _stop(procs, codes)
+            if len(codes) < nproc and time.monotonic() > deadline:
+                sys.stderr.write(f"bench.py: job deadline ({args.timeout:.0f} s) expired\n")
+                _report_ranks(procs, codes, prog)
+                _stop(procs, codes)
+                rc = rc or 124
             time.sleep(0.2)
     finally:
-        for p in procs:
-            p.kill()
+        for p in procs.values():
+            if p.poll() is None:
+                p.kill()
     return rc
+
+
+def _progress(prog, r):
+    try:
+        with open(os.path.join(prog, f"rank{r}")) as f:
+            return f.read().strip() or "?"
+    except OSError:
+        return "never reported"
+
+
+def _report_ranks(procs, codes, prog):
+    for r, p in sorted(procs.items()):
+        state = f"exited {codes[r]}" if r in codes else ("running" if p.poll() is None else f"exited {p.poll()}")
+        sys.stderr.write(f"bench.py:   rank {r} (pid {p.pid}): {state}; last progress: {_progress(prog, r)}\n")
+    sys.stderr.flush()
+
+
+def _stop(procs, codes):
+    for r, p in procs.items():
+        if p.poll() is None:
+            p.terminate()
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 10 and any(p.poll() is None for p in procs.values()):
+        time.sleep(0.1)
+    for r, p in procs.items():
+        if p.poll() is None:
+            p.kill()
+        codes.setdefault(r, p.wait())
+
+
+class Progress:
+    """This rank's last phase / step, for the launcher's report (PDDL_BENCH_PROGRESS dir)."""
+
+    def __init__(self, rank):
+        d = os.environ.get("PDDL_BENCH_PROGRESS")
+        self.path = os.path.join(d, f"rank{rank}") if d else None
+
+    def __call__(self, phase, step=None):
+        if self.path:
+            with open(self.path, "w") as f:
+                f.write(phase if step is None else f"{phase} step {step}")
 
 
 # ---------------------------------------------------------------------------- measured job
@@ -145,7 +224,16 @@ def build_cfg(args, strategy):
                        graphs=graphs, data="synthetic_fixed", seed=0, precision=args.precision)
 
 
+def arm_deadline(args):
+    """Every rank: dump all stacks and exit non-zero at the deadline (faulthandler's watchdog
+    thread runs without the GIL, so it fires even with the main thread stuck in native code);
+    stalled collectives end the rank PDDL_STALL_SHUTDOWN seconds after their report."""
+    faulthandler.dump_traceback_later(args.timeout, exit=True)
+    os.environ.setdefault("PDDL_STALL_SHUTDOWN", "30")
+
+
 def run(args):
+    arm_deadline(args)
     import torch
     import torch.distributed as dist
     import pddl  # noqa: F401
@@ -154,6 +242,8 @@ def run(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    progress = Progress(rank)
+    progress("init")
     cpu = args.device == "cpu"
     devices = None
     if args.strategy == "mirrored":
@@ -188,6 +278,7 @@ def run(args):
     if devices is not None:
         st._devices = devices
     tr = Trainer(cfg, st)
+    progress("broadcast")
     st.broadcast_state(tr)
     replicas = st.num_replicas_in_sync
     local_devs = [e.params.device for e, _ in st._replicas()]
@@ -219,14 +310,19 @@ def run(args):
         sync_all()
 
     stats = None
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        progress("warmup", i)
         stats = st.train_step(images, labels)
+    progress("barrier (after warmup)")
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        progress("timed", i)
         stats = st.train_step(images, labels)
+    progress("barrier (after timed steps)")
     barrier()
     dt = time.perf_counter() - t0
+    progress("report")
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         if dist.get_backend() == "nccl":
@@ -234,6 +330,7 @@ def run(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(stats[0].item()) / (B * len(local_devs)) if stats is not None else float("nan")
+    comm = comm_report(st, world, rank, local_devs, cpu)
     total = B * args.gpus
     ips = total * args.steps / dt
     desc = {
@@ -268,13 +365,71 @@ def run(args):
         }
         if not cpu:   # HBM footprint of the step (torch caching allocator, device of rank 0)
             out["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(local_devs[0]) / 1e9, 2)
+        out["comm"] = comm
         if rehearsing():
             out["rehearsal"] = True
         print(json.dumps(out), flush=True)
+    progress("done")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    faulthandler.cancel_dump_traceback_later()
     return 0
+
+
+def comm_report(st, world, rank, local_devs, cpu):
+    """What the gradient collectives actually spanned (gathered to rank 0)."""
+    import socket
+    import torch
+    import torch.distributed as dist
+
+    def dev_info(d):
+        if cpu or d.type != "cuda":
+            return {"device": str(d)}
+        p = torch.cuda.get_device_properties(d)
+        bus = getattr(p, "pci_bus_id", None)
+        dom = getattr(p, "pci_domain_id", 0)
+        devid = getattr(p, "pci_device_id", 0)
+        out = {"device": d.index, "name": p.name, "gcn_arch": getattr(p, "gcnArchName", "")}
+        if bus is not None:
+            out["pci_bus_id"] = f"{dom:04x}:{bus:02x}:{devid:02x}.0"
+        return out
+
+    mine = {"rank": rank, "host": socket.gethostname(), "pid": os.getpid(),
+            "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "devices": [dev_info(d) for d in local_devs]}
+    rep = {"world_size_env": world, "local_replicas": len(local_devs)}
+    mirror = getattr(st, "mirror", None)
+    rccl = getattr(mirror, "comm", None) if mirror is not None else None
+    if rccl is not None:            # the native RcclComm: ask RCCL what it built
+        rep["native_rccl"] = {"nranks": rccl.nranks, "communicators": rccl.info(),
+                              "watchdog": {k: v for k, v in rccl.watchdog_state().items() if k != "message"}}
+        ones = [torch.ones(1, device=d) for d in local_devs]
+        rccl.all_reduce(ones, "sum", "comm check")
+        rep["allreduce_ones"] = float(ones[0].item())
+    if world > 1 and dist.is_initialized():
+        rep["backend"] = dist.get_backend()
+        rep["c10d_world_size"] = dist.get_world_size()
+        if rccl is None:            # the gradient path's process group: an all-reduce of ones
+            dev = local_devs[0] if dist.get_backend() == "nccl" else "cpu"
+            t = torch.ones(1, device=dev)
+            dist.all_reduce(t)
+            rep["allreduce_ones"] = float(t.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        rep["ranks"] = gathered
+    else:
+        rep["backend"] = "native RCCL (in-process)" if rccl is not None else "none (1 replica)"
+        rep["ranks"] = [mine]
+    fusion = getattr(st, "fusion", None)
+    if fusion is not None:
+        rep["fusion_engine"] = {"world": fusion.world, "wire": fusion.wire, "buckets": len(st.buckets),
+                                "issued": int(fusion.issued)}
+    if not cpu:
+        try:
+            rep["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception:
+            pass
+    return rep
 
 
 def run_ps(args):
@@ -282,7 +437,9 @@ def run_ps(args):
     and W = gpus - P workers, one GPU each, the native HIP-IPC data plane over xGMI.  One
     untimed warmup epoch, then a timed epoch of `steps` worker steps claimed by the workers
     asynchronously; value = aggregate worker images/sec of the timed epoch (worker 0's clock
-    over every worker's training steps, parameter_server.py)."""
+    over every worker's training steps, parameter_server.py).  The role processes are bounded
+    by run_ps_job's job deadline (PDDL_PS_JOB_TIMEOUT, set from --timeout)."""
+    os.environ.setdefault("PDDL_PS_JOB_TIMEOUT", str(args.timeout))
     import pddl  # noqa: F401
     from pddl.config import make_config
     from pddl.parallel.parameter_server import run_ps_job
@@ -340,7 +497,8 @@ def main(argv=None):
             if have < args.gpus:
                 fail(f"--gpus {args.gpus} but only {have} GPU(s) are visible")
         return launch(args, argv)
-    return run(args)
+    from pddl.parallel.faults import run_fail_fast
+    return run_fail_fast(run, args, multi=args.gpus > 1)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <deque>
 #include <functional>
 #include <memory>
@@ -123,6 +124,14 @@ class FusionCore {
     std::lock_guard<std::mutex> lk(mu_);
     return step_;
   }
+  // Horovod's HOROVOD_STALL_SHUTDOWN_TIME_SECONDS: once a stall has been reported and `s` more
+  // seconds pass without the caller ending the job, terminate the process (exit 124) -- on the
+  // GPU the caller may sit in a device synchronize behind the stuck collective and never see
+  // the verdict.  0 = report only.
+  void set_shutdown(double s) {
+    std::lock_guard<std::mutex> lk(mu_);
+    shutdown_s_ = s;
+  }
   int64_t issued() const { return issued_.load(); }
 
  private:
@@ -135,6 +144,7 @@ class FusionCore {
   void report_stall(const std::string& msg) {   // (mu_ held)
     stall_msg_ = msg;
     stalled_ = true;
+    t_stall_ = fc_now_us();
     std::fprintf(stderr, "[pddl stall inspector] %s\n", stall_msg_.c_str());
   }
 
@@ -193,6 +203,12 @@ class FusionCore {
             report_stall(os.str());
           }
         }
+        if (stalled_ && shutdown_s_ > 0 && (fc_now_us() - t_stall_) * 1e-6 > shutdown_s_) {
+          std::fprintf(stderr, "[pddl stall inspector] rank %d: still stalled %.1f s after the report; terminating"
+                       " the process (exit 124)\n", rank_, (fc_now_us() - t_stall_) * 1e-6);
+          std::fflush(stderr);
+          std::_Exit(124);
+        }
       }
       cv_.notify_all();
     }
@@ -208,6 +224,7 @@ class FusionCore {
   std::vector<Item> inflight_;
   std::deque<Watch> watch_;
   bool stop_ = false, busy_ = false, stalled_ = false;
+  double shutdown_s_ = 0, t_stall_ = 0;
   std::string error_, stall_msg_;
   int next_expected_ = 0, step_ = 0;
   std::atomic<int64_t> issued_{0};

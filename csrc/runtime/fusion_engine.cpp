@@ -192,6 +192,7 @@ class FusionEngine {
   }
 
   void set_timeline(bool on) { timeline_on_ = on; }
+  void set_stall_shutdown(double s) { core_->set_shutdown(s); }
   // Chrome-trace JSON.  GPU: READY (instant) and ALLREDUCE (span) from HIP events; host:
   // QUEUED spans.  CPU backends: QUEUED and ALLREDUCE from the host clock.
   std::string timeline_json() {
@@ -344,6 +345,7 @@ void register_fusion(py::module& m) {
       .def("finish", &FusionEngine::finish, py::call_guard<py::gil_scoped_release>())
       .def("shutdown", &FusionEngine::shutdown, py::call_guard<py::gil_scoped_release>())
       .def("set_timeline", &FusionEngine::set_timeline)
+      .def("set_stall_shutdown", &FusionEngine::set_stall_shutdown)
       .def("timeline_json", &FusionEngine::timeline_json)
       .def_property_readonly("world", &FusionEngine::world)
       .def_property_readonly("issued", &FusionEngine::issued)

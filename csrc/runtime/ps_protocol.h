@@ -9,8 +9,9 @@
 // (plain stores) and publishes `done_seq` with RELEASE; the worker ACQUIREs `done_seq` before
 // reading the receive buffer.  Those two release/acquire pairs are the only ordering the
 // plain mailbox / receive-buffer traffic relies on.  (GPU roles: the mailbox and receive
-// buffers are HIP-IPC device memory written by kernels and peer copies, fenced by a stream
-// synchronize before the release store.)
+// buffers are HIP-IPC device memory written by kernels and peer copies; the worker's pack
+// kernel is fenced by an event synchronize on the worker's poster thread before its release
+// store, the PS's Adam + snapshot copy by an event query before the PS's release store.)
 #pragma once
 #include <atomic>
 #include <chrono>
@@ -54,19 +55,36 @@ inline double now_s() {
 }
 
 // Service loop of one PS: serve every worker's requests in arrival order until each has sent
-// OP_STOP or vanished.  apply(w, lr): the update of worker w's mailbox; snapshot(w): the fresh
-// shard into w's receive buffer; idle(): called when no request was pending (housekeeping);
-// alive(pid): false once a worker process is gone (polled every 0.5 s while idle).
-template <class Apply, class Snapshot, class Idle, class Alive>
-void serve(PSCtrl* ctrl, int W, const std::atomic<bool>& stop, Apply apply, Snapshot snapshot, Idle idle,
-           Alive alive, std::vector<int>* dead) {
-  std::vector<uint64_t> seen(W, 0);
-  std::vector<char> finished(W, 0);
-  int n_done = 0;
+// OP_STOP or vanished.  apply(w, lr): ENQUEUE the update of worker w's mailbox; snapshot(w):
+// ENQUEUE the copy of the fresh shard into w's receive buffer; complete(w): true once both have
+// finished (GPU roles: an event recorded after the copy on the PS stream -- the loop never
+// blocks on the device, so requests of other workers are enqueued behind it while the copy
+// runs; host roles: always true).  `done_seq` is published only on completion.  idle(): called
+// when nothing happened in a sweep (housekeeping); alive(pid): false once a worker process is
+// gone (polled every 0.5 s while idle).
+template <class Apply, class Snapshot, class Complete, class Idle, class Alive>
+void serve(PSCtrl* ctrl, int W, const std::atomic<bool>& stop, Apply apply, Snapshot snapshot, Complete complete,
+           Idle idle, Alive alive, std::vector<int>* dead) {
+  std::vector<uint64_t> seen(W, 0), pending(W, 0);
+  std::vector<char> finished(W, 0), busy(W, 0), pushed(W, 0);
+  int n_done = 0, n_busy = 0;
   double last_check = now_s();
-  while (n_done < W && !stop.load()) {
+  auto retire = [&](int w) {   // the enqueued work of w's request finished: publish it
+    if (pushed[w]) ctrl->updates.fetch_add(1);
+    ctrl->slot[w].done_seq.store(pending[w], std::memory_order_release);
+    busy[w] = 0;
+    --n_busy;
+  };
+  while ((n_done < W || n_busy > 0) && !stop.load()) {
     bool any = false;
     for (int w = 0; w < W; ++w) {
+      if (busy[w]) {
+        if (complete(w)) {
+          retire(w);
+          any = true;
+        }
+        continue;
+      }
       if (finished[w]) continue;
       WorkerSlot& s = ctrl->slot[w];
       const uint64_t r = s.req_seq.load(std::memory_order_acquire);
@@ -77,14 +95,16 @@ void serve(PSCtrl* ctrl, int W, const std::atomic<bool>& stop, Apply apply, Snap
       if (op == OP_STOP) {
         finished[w] = 1;
         ++n_done;
+        s.done_seq.store(r, std::memory_order_release);
       } else {
-        if (op == OP_PUSH) {
-          apply(w, s.lr);
-          ctrl->updates.fetch_add(1);
-        }
+        pushed[w] = op == OP_PUSH;
+        if (pushed[w]) apply(w, s.lr);
         snapshot(w);
+        pending[w] = r;
+        busy[w] = 1;
+        ++n_busy;
+        if (complete(w)) retire(w);
       }
-      s.done_seq.store(r, std::memory_order_release);
     }
     if (!any) {
       idle();

@@ -9,12 +9,18 @@
 //     process-shared atomics with release / acquire ordering; no RPC layer at all.
 //   * Data plane over xGMI with HIP IPC (dmabuf): a worker's pack kernel gathers its gradient
 //     ranges and writes them STRAIGHT into its mailbox slot on the PS GPU (peer writes), then
-//     bumps its request sequence number.  The PS service thread sees the request, runs the
-//     fused Adam kernel (optim.hip, TF epsilon-hat form) on the mailbox, and copies the fresh
-//     shard into the worker's receive buffer on the worker GPU (peer copy) before publishing
-//     `done`.  Updates are applied one at a time in arrival order on the PS stream, so every
+//     bumps its request sequence number.  The PS service thread sees the request, ENQUEUES the
+//     fused Adam kernel (optim.hip, TF epsilon-hat form) on the mailbox and the copy of the
+//     fresh shard into the worker's receive buffer on the worker GPU (peer copy) on the PS
+//     stream, records the worker's completion event and moves on to the next request; `done`
+//     is published when that event has completed (the service thread never blocks on the
+//     device, so the Adam / copy work of several workers' requests queues back to back on the
+//     PS GPU).  Updates are applied one at a time in arrival order on the PS stream, so every
 //     pull is a consistent snapshot of the shard; workers never wait for each other
 //     (unbounded staleness, as the reference's asynchronous coordinator).
+//   * Worker side, `begin()` returns right after enqueueing the pack kernel: a poster thread
+//     waits for the pack's event and only then publishes the request, so the training thread
+//     goes on launching the next step instead of synchronizing with the end of backward.
 //   * CPU roles (tests, `--device cpu`): the same protocol with the mailboxes and receive
 //     buffers in shared memory and a host Adam loop.
 //   * The request / completion protocol and the service loop are in runtime/ps_protocol.h
@@ -37,7 +43,9 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -134,6 +142,8 @@ class PSServer {
       std::memcpy(ctrl_->mailbox_handle, &mh, sizeof(mh));
       hck(hipDeviceSynchronize(), "init sync");
       rx_ptr_.assign(W_, nullptr);
+      done_ev_.assign(W_, nullptr);
+      for (auto& e : done_ev_) hck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     } else {
       host_.assign(3 * n_, 0.f);
       std::memcpy(host_.data(), host.data_ptr<float>(), n_real_ * sizeof(float));
@@ -150,6 +160,7 @@ class PSServer {
     if (dev_ >= 0) {
       hipSetDevice(dev_);
       for (float* r : rx_ptr_) if (r) hipIpcCloseMemHandle(r);
+      for (auto e : done_ev_) if (e) hipEventDestroy(e);
       if (mailbox_) hipFree(mailbox_);
       if (params_) hipFree(params_);
       if (stream_) hipStreamDestroy(stream_);
@@ -206,7 +217,7 @@ class PSServer {
         rx_ptr_[w] = static_cast<float*>(ptr);
       }
       hck(hipMemcpyAsync(rx_ptr_[w], params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
-      hck(hipStreamSynchronize(stream_), "sync");
+      hck(hipEventRecord(done_ev_[w], stream_), "record done");
     } else {
       std::memcpy(static_cast<float*>(rx_shm_.ptr) + (size_t)w * n_, params_, n_ * sizeof(float));
     }
@@ -216,6 +227,13 @@ class PSServer {
       if (dev_ >= 0) hck(hipSetDevice(dev_), "set device");
       pddl::ps::serve(
           ctrl_, W_, stop_, [this](int w, float lr) { apply_adam(w, lr); }, [this](int w) { send_snapshot(w); },
+          [this](int w) {
+            if (dev_ < 0) return true;
+            const hipError_t q = hipEventQuery(done_ev_[w]);
+            if (q == hipErrorNotReady) return false;
+            hck(q, "completion event");
+            return true;
+          },
           [this] {
             if (!unlinked_) {   // every worker attached: drop the names (no /dev/shm leak on a crash)
               bool all = true;
@@ -244,6 +262,7 @@ class PSServer {
   float* mailbox_ = nullptr;
   std::vector<float> host_;
   std::vector<float*> rx_ptr_;
+  std::vector<hipEvent_t> done_ev_;   // per worker: its request's Adam + snapshot copy finished
   hipStream_t stream_ = nullptr;
   std::thread thr_;
   std::atomic<bool> stop_{false};
@@ -325,10 +344,21 @@ class PSClient {
       }
       s.pid.store((int32_t)getpid());
     }
+    if (dev_ >= 0) {
+      hck(hipEventCreateWithFlags(&pack_ev_, hipEventDisableTiming), "pack event");
+      poster_ = std::thread([this] { post_loop(); });
+    }
   }
   ~PSClient() {
+    {
+      std::lock_guard<std::mutex> lk(post_mu_);
+      post_stop_ = true;
+    }
+    post_cv_.notify_all();
+    if (poster_.joinable()) poster_.join();
     if (dev_ >= 0) {
       hipSetDevice(dev_);
+      if (pack_ev_) hipEventDestroy(pack_ev_);
       for (Remote& r : rem_) {
         if (r.mb_base) hipIpcCloseMemHandle(r.mb_base);
         if (r.rx) hipFree(r.rx);
@@ -370,9 +400,19 @@ class PSClient {
         }
       }
     }
-    if (dev_ >= 0 && push) hck(hipStreamSynchronize(st), "sync push");   // peer writes complete + visible
-    for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], ++r.seq, push ? OP_PUSH : OP_PULL, (float)lr);
+    const int op = push ? OP_PUSH : OP_PULL;
+    for (Remote& r : rem_) ++r.seq;
     in_flight_ = true;
+    if (dev_ >= 0 && push) {
+      // The peer writes must be complete and visible before the release store of the request:
+      // hand the event wait + post to the poster thread instead of blocking this thread.
+      hck(hipEventRecord(pack_ev_, st), "record pack");
+      std::lock_guard<std::mutex> lk(post_mu_);
+      post_job_ = {true, op, (float)lr};
+      post_cv_.notify_all();
+      return;
+    }
+    for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], r.seq, op, (float)lr);
   }
 
   void end(Tensor params) {
@@ -405,11 +445,49 @@ class PSClient {
   }
 
  private:
-  void wait_done(Remote& r, int p) { pddl::ps::wait_done(r.ctrl->slot[w_], r.seq, timeout_, p); }
+  void wait_done(Remote& r, int p) {
+    pddl::ps::wait_done(r.ctrl->slot[w_], r.seq, timeout_, p);
+    std::lock_guard<std::mutex> lk(post_mu_);
+    TORCH_CHECK(post_err_.empty(), "pddl ps client: ", post_err_);
+  }
 
+  // Poster thread (GPU workers): wait for the pack kernel's event, then publish the requests.
+  void post_loop() {
+    hipSetDevice(dev_);
+    while (true) {
+      PostJob job;
+      {
+        std::unique_lock<std::mutex> lk(post_mu_);
+        post_cv_.wait(lk, [this] { return post_stop_ || post_job_.valid; });
+        if (post_stop_ && !post_job_.valid) return;
+        job = post_job_;
+        post_job_.valid = false;
+      }
+      const hipError_t e = hipEventSynchronize(pack_ev_);
+      if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(post_mu_);
+        post_err_ = std::string("pack event: ") + hipGetErrorString(e);
+        continue;   // (end() reports it; the requests are never posted)
+      }
+      for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], r.seq, job.op, job.lr);
+    }
+  }
+
+  struct PostJob {
+    bool valid = false;
+    int op = OP_PUSH;
+    float lr = 0.f;
+  };
   int w_, dev_;
   double timeout_;
   bool in_flight_ = false;
+  hipEvent_t pack_ev_ = nullptr;
+  std::thread poster_;
+  std::mutex post_mu_;
+  std::condition_variable post_cv_;
+  PostJob post_job_;
+  bool post_stop_ = false;
+  std::string post_err_;
   int64_t flat_end_ = 0;
   std::vector<Remote> rem_;
 };

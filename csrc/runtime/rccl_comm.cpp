@@ -10,12 +10,24 @@
 //                                               one ncclGroupStart/End (P processes x R GPUs)
 // Every collective is issued for all local ranks inside one group, each on the CURRENT HIP
 // stream of its tensor's device, so it is ordered after the kernels that produced the data.
+//
+// Failure detection: `set_watchdog(timeout_s, shutdown_s, rank)` arms a
+// runtime/comm_watch.h watchdog.  Every collective then records a HIP event on each local
+// stream; a collective not complete after `timeout_s` aborts every local communicator
+// (ncclCommAbort: the blocked RCCL kernels exit, so a device synchronize returns), the next
+// call raises with the collective's tag (e.g. "bucket 3 all_reduce"), and with
+// `shutdown_s` > 0 the process exits 124 if it is still stuck after that grace.
+// `info()` reports what RCCL itself built: rank count, user rank and device of every local
+// communicator, plus the device's PCI bus id.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <rccl/rccl.h>
 
+#include "runtime/comm_watch.h"
+
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -78,6 +90,7 @@ class RcclComm {
     nck(ncclCommInitAll(comms_.data(), nranks_, devs_.data()), "comm init all");
   }
   ~RcclComm() {
+    watch_.reset();
     for (auto c : comms_)
       if (c) ncclCommDestroy(c);
   }
@@ -88,62 +101,104 @@ class RcclComm {
     return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
   }
 
-  void all_reduce(std::vector<Tensor> ts, const std::string& op) {
-    check_local(ts);
-    nck(ncclGroupStart(), "group start");
-    for (size_t i = 0; i < ts.size(); ++i) {
-      c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
-      nck(ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), comms_[i],
-                        stream_of(ts[i])),
-          "all_reduce");
-    }
-    nck(ncclGroupEnd(), "group end (all_reduce)");
+  void all_reduce(std::vector<Tensor> ts, const std::string& op, const std::string& tag) {
+    std::vector<hipStream_t> ss;
+    for (auto& t : ts) ss.push_back(stream_of(t));
+    issue(ts, ss, tag.empty() ? "all_reduce" : tag, [&](size_t i) {
+      return ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), comms_[i],
+                           ss[i]);
+    });
   }
 
   // Same, on explicit streams (one per local rank, e.g. the comm streams of a replica driver
   // that overlaps bucket all-reduces with the next graph segment's compute).
-  void all_reduce_on(std::vector<Tensor> ts, const std::string& op, std::vector<int64_t> streams) {
-    check_local(ts);
+  void all_reduce_on(std::vector<Tensor> ts, const std::string& op, std::vector<int64_t> streams,
+                     const std::string& tag) {
     TORCH_CHECK(streams.size() == ts.size(), "pddl rccl: one stream per local rank");
-    nck(ncclGroupStart(), "group start");
-    for (size_t i = 0; i < ts.size(); ++i) {
-      c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
-      nck(ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), comms_[i],
-                        reinterpret_cast<hipStream_t>(streams[i])),
-          "all_reduce");
-    }
-    nck(ncclGroupEnd(), "group end (all_reduce)");
+    std::vector<hipStream_t> ss;
+    for (auto s : streams) ss.push_back(reinterpret_cast<hipStream_t>(s));
+    issue(ts, ss, tag.empty() ? "all_reduce" : tag, [&](size_t i) {
+      return ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), comms_[i],
+                           ss[i]);
+    });
   }
 
   void broadcast(std::vector<Tensor> ts, int root) {
-    check_local(ts);
-    nck(ncclGroupStart(), "group start");
-    for (size_t i = 0; i < ts.size(); ++i) {
-      c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
-      nck(ncclBroadcast(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), root, comms_[i],
-                        stream_of(ts[i])),
-          "broadcast");
-    }
-    nck(ncclGroupEnd(), "group end (broadcast)");
+    std::vector<hipStream_t> ss;
+    for (auto& t : ts) ss.push_back(stream_of(t));
+    issue(ts, ss, "broadcast", [&](size_t i) {
+      return ncclBroadcast(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), root, comms_[i], ss[i]);
+    });
   }
 
   // Point-to-point from local rank `li` (PS push/pull over xGMI).
   void send(Tensor t, int peer, int li) {
+    check();
     c10::hip::HIPGuardMasqueradingAsCUDA g(devs_.at(li));
     nck(ncclSend(t.data_ptr(), t.numel(), dtype_of(t), peer, comms_.at(li), stream_of(t)), "send");
   }
   void recv(Tensor t, int peer, int li) {
+    check();
     c10::hip::HIPGuardMasqueradingAsCUDA g(devs_.at(li));
     nck(ncclRecv(t.data_ptr(), t.numel(), dtype_of(t), peer, comms_.at(li), stream_of(t)), "recv");
   }
 
   // Failure path (stall watchdog / PS failure): abort every local communicator.
   void abort() {
+    std::lock_guard<std::mutex> lk(issue_mu_);
     for (auto& c : comms_)
       if (c) {
         ncclCommAbort(c);
         c = nullptr;
       }
+  }
+
+  void set_watchdog(double timeout_s, double shutdown_s, int rank) {
+    watch_.reset();
+    if (timeout_s <= 0) return;
+    watch_ = std::make_unique<pddl::CommWatch>(timeout_s, shutdown_s, rank, [this](const std::string&) {
+      const std::string e = async_error();
+      if (!e.empty()) std::fprintf(stderr, "[pddl comm watchdog] RCCL async error: %s\n", e.c_str());
+      std::fprintf(stderr, "[pddl comm watchdog] aborting %zu local RCCL communicator(s)\n", comms_.size());
+      abort();
+    });
+  }
+  void check() const {
+    if (watch_) watch_->check();
+  }
+  py::dict watchdog_state() const {
+    py::dict d;
+    d["armed"] = (bool)watch_;
+    if (watch_) {
+      d["stalled"] = watch_->stalled();
+      d["message"] = watch_->message();
+      d["issued"] = watch_->issued();
+      d["retired"] = watch_->retired();
+      d["outstanding"] = (int64_t)watch_->outstanding();
+    }
+    return d;
+  }
+
+  // What RCCL built, per local communicator.
+  py::list info() const {
+    py::list out;
+    for (size_t i = 0; i < comms_.size(); ++i) {
+      py::dict d;
+      int count = -1, urank = -1, dev = -1;
+      if (comms_[i]) {
+        nck(ncclCommCount(comms_[i], &count), "comm count");
+        nck(ncclCommUserRank(comms_[i], &urank), "comm user rank");
+        nck(ncclCommCuDevice(comms_[i], &dev), "comm device");
+      }
+      char bus[64] = {0};
+      if (hipDeviceGetPCIBusId(bus, sizeof(bus), devs_[i]) != hipSuccess) bus[0] = 0;
+      d["nranks"] = count;
+      d["rank"] = urank;
+      d["device"] = dev;
+      d["pci_bus_id"] = std::string(bus);
+      out.append(d);
+    }
+    return out;
   }
   std::string async_error() {
     for (auto c : comms_) {
@@ -159,6 +214,39 @@ class RcclComm {
   std::vector<int> devices() const { return devs_; }
 
  private:
+  // One grouped collective over every local rank; registered with the watchdog when armed.
+  template <class F>
+  void issue(const std::vector<Tensor>& ts, const std::vector<hipStream_t>& ss, const std::string& tag, F&& op) {
+    check();
+    std::lock_guard<std::mutex> lk(issue_mu_);
+    check_local(ts);
+    nck(ncclGroupStart(), "group start");
+    for (size_t i = 0; i < ts.size(); ++i) {
+      c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
+      nck(op(i), tag.c_str());
+    }
+    nck(ncclGroupEnd(), "group end");
+    if (!watch_) return;
+    auto evs = std::make_shared<std::vector<hipEvent_t>>();
+    for (size_t i = 0; i < ts.size(); ++i) {
+      c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
+      hipEvent_t e;
+      TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "pddl rccl: hipEventCreate");
+      TORCH_CHECK(hipEventRecord(e, ss[i]) == hipSuccess, "pddl rccl: hipEventRecord");
+      evs->push_back(e);
+    }
+    watch_->add(
+        tag,
+        [evs] {
+          for (auto e : *evs)
+            if (hipEventQuery(e) == hipErrorNotReady) return false;
+          return true;
+        },
+        [evs] {
+          for (auto e : *evs) (void)hipEventDestroy(e);
+        });
+  }
+
   void check_local(const std::vector<Tensor>& ts) {
     TORCH_CHECK(ts.size() == comms_.size(), "pddl rccl: need one tensor per local rank");
     for (size_t i = 0; i < ts.size(); ++i) {
@@ -172,6 +260,8 @@ class RcclComm {
   int nranks_;
   std::vector<int> ranks_, devs_;
   std::vector<ncclComm_t> comms_;
+  std::mutex issue_mu_;   // collective issue vs. the watchdog's abort
+  std::unique_ptr<pddl::CommWatch> watch_;
 };
 
 }  // namespace
@@ -182,15 +272,20 @@ void register_rccl(py::module& m) {
            py::arg("uid"), py::arg("ranks"), py::arg("devices"))
       .def_static("init_all", [](std::vector<int> devs) { return std::make_shared<RcclComm>(devs); })
       .def_static("unique_id", &RcclComm::unique_id)
-      .def("all_reduce", &RcclComm::all_reduce, py::arg("tensors"), py::arg("op") = "sum",
+      .def("all_reduce", &RcclComm::all_reduce, py::arg("tensors"), py::arg("op") = "sum", py::arg("tag") = "",
            py::call_guard<py::gil_scoped_release>())
       .def("all_reduce_on", &RcclComm::all_reduce_on, py::arg("tensors"), py::arg("op"), py::arg("streams"),
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("tag") = "", py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &RcclComm::broadcast, py::arg("tensors"), py::arg("root") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("send", &RcclComm::send, py::call_guard<py::gil_scoped_release>())
       .def("recv", &RcclComm::recv, py::call_guard<py::gil_scoped_release>())
-      .def("abort", &RcclComm::abort)
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def("set_watchdog", &RcclComm::set_watchdog, py::arg("timeout_s"), py::arg("shutdown_s") = 0.0,
+           py::arg("rank") = 0)
+      .def("check", &RcclComm::check)
+      .def("watchdog_state", &RcclComm::watchdog_state)
+      .def("info", &RcclComm::info)
       .def("async_error", &RcclComm::async_error)
       .def_property_readonly("nranks", &RcclComm::nranks)
       .def_property_readonly("ranks", &RcclComm::ranks)

@@ -5,7 +5,10 @@
 //   g++ -std=c++17 -O1 -g -fsanitize=thread -I csrc csrc/tests/ps_protocol_test.cpp -lpthread
 #include <cassert>
 #include <cstdio>
+#include <deque>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -26,13 +29,47 @@ int main() {
   std::atomic<bool> stop{false};
   std::vector<int> dead;
   int idles = 0;
+  // A fake in-order "PS stream": apply / snapshot only enqueue jobs, a device thread runs them
+  // later and bumps the worker's completion count (the GPU path's event), so done_seq must be
+  // published on completion, not on enqueue, for the workers' reads below to be race-free.
+  std::mutex qmu;
+  std::deque<std::function<void()>> q;
+  std::vector<std::atomic<int>> enq(W), fin(W);
+  for (int w = 0; w < W; ++w) enq[w] = fin[w] = 0;
+  std::atomic<bool> dev_stop{false};
+  std::thread device([&] {
+    while (!dev_stop.load()) {
+      std::function<void()> job;
+      {
+        std::lock_guard<std::mutex> lk(qmu);
+        if (!q.empty()) {
+          job = std::move(q.front());
+          q.pop_front();
+        }
+      }
+      if (job) job();
+      else std::this_thread::sleep_for(std::chrono::microseconds(30));
+    }
+  });
   std::thread server([&] {
     serve(
         ctrl, W, stop,
         [&](int w, float lr) {   // "SGD" with lr = 1: params += grad (deterministic sum of all pushes)
-          for (int i = 0; i < N; ++i) params[i] += lr * mailbox[w][i];
+          std::lock_guard<std::mutex> lk(qmu);
+          q.push_back([&, w, lr] {
+            for (int i = 0; i < N; ++i) params[i] += lr * mailbox[w][i];
+          });
         },
-        [&](int w) { rx[w] = params; }, [&] { ++idles; }, [](int) { return true; }, &dead);
+        [&](int w) {
+          enq[w]++;
+          std::lock_guard<std::mutex> lk(qmu);
+          q.push_back([&, w] {
+            rx[w] = params;
+            fin[w].fetch_add(1, std::memory_order_release);
+          });
+        },
+        [&](int w) { return fin[w].load(std::memory_order_acquire) == enq[w].load(); }, [&] { ++idles; },
+        [](int) { return true; }, &dead);
   });
   ctrl->ready.store(1, std::memory_order_release);
   std::vector<std::thread> workers;
@@ -60,6 +97,8 @@ int main() {
   }
   for (auto& t : workers) t.join();
   server.join();
+  dev_stop.store(true);
+  device.join();
   const float expect = (float)(W * (ITERS - ITERS / 4));
   for (int i = 0; i < N; ++i) assert(params[i] == expect);
   assert(ctrl->updates.load() == (uint64_t)(W * (ITERS - ITERS / 4)) && dead.empty());

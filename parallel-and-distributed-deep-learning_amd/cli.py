@@ -39,6 +39,12 @@ def run(preset: str, argv: Optional[List[str]] = None, extra=None) -> int:
     from .train.trainer import Trainer, default_callbacks
     cfg = config_from_args(preset, argv, extra)
     if cfg.strategy == "ps":
+        if cfg.resume:
+            # (the PS job's variables and Adam slots live on the PS roles; the reference has no
+            # resume path at all, imagenet-resnet50-ps.py:142-148)
+            sys.stderr.write("--resume is not supported for --strategy ps: the parameter-server job restarts from "
+                             "--weights (the final PS checkpoint holds the trained variables, no optimizer state)\n")
+            return 2
         from .parallel.parameter_server import run_ps_job
         return run_ps_job(cfg)
     if cfg.roctx:

@@ -188,22 +188,50 @@ class _LockedStore:
 
 class _Heartbeat:
     """A worker's liveness beacon (the coordinator's worker-failure watch): a daemon thread
-    stamps `hb/<rank>` every period, so a worker that is waiting (an epoch barrier, worker 0's
-    validation, a drained ticket queue) is not mistaken for a dead one; a dead process stops
-    beating with its last thread."""
+    stamps `hb/<rank>` every period while the worker is alive AND making progress.  The main
+    loop marks each step with `step()` (compute + exchange) and each wait with `wait()` (epoch
+    barrier, worker 0's validation, a drained ticket queue); a step that runs longer than
+    `stall_s` (a GPU hang, a stuck exchange) stops the stamps, so a live but stalled worker is
+    declared dead and its ticket re-queued exactly like a crashed one."""
 
-    def __init__(self, store, rank: int, period: float):
-        self.store, self.rank, self.period = store, rank, period
+    def __init__(self, store, rank: int, period: float, stall_s: float):
+        self.store, self.rank, self.period, self.stall_s = store, rank, period, stall_s
         self._stop = threading.Event()
+        self._lock = threading.Lock()
+        self._state, self._since = "wait", time.time()
         self.beat()
         self._th = threading.Thread(target=self._run, daemon=True)
         self._th.start()
+
+    def step(self):
+        with self._lock:
+            self._state, self._since = "step", time.time()
+
+    def wait(self):
+        with self._lock:
+            self._state, self._since = "wait", time.time()
+
+    def healthy(self) -> bool:
+        with self._lock:
+            return self._state == "wait" or time.time() - self._since < self.stall_s
 
     def beat(self):
         self.store.set(_hb_key(self.rank), str(time.time()))
 
     def _run(self):
         while not self._stop.wait(self.period):
+            if not self.healthy():
+                # stalled inside a step: let the coordinator's watch expire; past twice the
+                # timeout the ticket has been re-queued, and a worker that may still wake up and
+                # push a stale gradient is worse than a dead one -- end the process (fail fast)
+                with self._lock:
+                    stuck = time.time() - self._since
+                if stuck > 2 * self.stall_s:
+                    sys.stderr.write(f"[ps worker rank {self.rank}] stuck in a step for {stuck:.0f} s "
+                                     f"(heartbeat timeout {self.stall_s:g} s): exiting\n")
+                    sys.stderr.flush()
+                    os._exit(18)
+                continue
             try:
                 self.beat()
             except Exception:
@@ -212,6 +240,48 @@ class _Heartbeat:
     def stop(self):
         self._stop.set()
         self._th.join(timeout=5)
+
+
+def _claimed(store, epoch: int) -> int:
+    key = f"claim/{epoch}"
+    if not store.check([key]):
+        return 0
+    return int(store.get(key).decode().split("/")[0])
+
+
+def _missing_tickets(store, epoch: int, lo: int, hi: int) -> List[int]:
+    """Tickets in [lo, hi) of `epoch` without a completion marker (bisection over store.check,
+    which is true only when every listed key exists: O(k log n) round trips for k misses)."""
+    if hi <= lo:
+        return []
+    if store.check([f"tdone/{epoch}/{t}" for t in range(lo, hi)]):
+        return []
+    if hi - lo == 1:
+        return [lo]
+    mid = (lo + hi) // 2
+    return _missing_tickets(store, epoch, lo, mid) + _missing_tickets(store, epoch, mid, hi)
+
+
+def requeue_orphans(store, epoch: int, live_workers: List[int]) -> List[int]:
+    """Re-queue every claimed ticket of `epoch` that is neither done nor held by a live worker.
+    Relies on nothing the dead worker may or may not have written between its claim and its
+    death: a ticket is orphaned iff its `tdone` marker is missing and no live worker's `cur`
+    names it.  Each orphan is counted once (atomic add on `rq/<epoch>/<ticket>`); a live
+    worker caught between its claim and its `cur` write makes at most one extra step run."""
+    held = set()
+    for r in live_workers:
+        if store.check([f"cur/{r}"]):
+            ep, t = (int(x) for x in store.get(f"cur/{r}").decode().split(":"))
+            if ep == epoch and t >= 0:
+                held.add(t)
+    out = []
+    for t in _missing_tickets(store, epoch, 0, _claimed(store, epoch)):
+        if t in held:
+            continue
+        if store.add(f"rq/{epoch}/{t}", 1) == 1:     # (atomic: exactly one scan counts it)
+            store.add(f"requeue/{epoch}", 1)
+            out.append(t)
+    return out
 
 
 class PSServer:
@@ -280,12 +350,12 @@ class PSServer:
         """Coordinator duty on PS 0: heartbeat watch + closure re-queue of dead workers."""
         cl = self.cl
         timeout = float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30"))
-        requeued = set()
+        dead = set()
         while any(t.is_alive() for t in threads):
             time.sleep(0.2)
             now = time.time()
             for w in range(cl.num_ps, cl.world):
-                if w in requeued:
+                if w in dead:
                     continue
                 try:
                     last = float(cl.store.get(_hb_key(w)).decode())
@@ -293,15 +363,16 @@ class PSServer:
                     continue
                 finished = cl.store.check([f"fin/{w}"])
                 if not finished and now - last > timeout:
-                    cur, ep = -1, -1
-                    if cl.store.check([f"cur/{w}"]):
-                        ep, cur = (int(x) for x in cl.store.get(f"cur/{w}").decode().split(":"))
-                    if cur >= 0:
-                        cl.store.add(f"requeue/{ep}", 1)    # only the dead worker's epoch re-runs it
-                    requeued.add(w)
+                    dead.add(w)
+                    cl.store.set(f"dead/{w}", "1")
                     cl.store.add("dead_workers", 1)
-                    print(f"[coordinator] worker {w} missed heartbeats for {now - last:.1f}s: re-queued its "
-                          f"step {cur}", flush=True)
+                    ep = 0
+                    if cl.store.check([f"cur/{w}"]):
+                        ep = int(cl.store.get(f"cur/{w}").decode().split(":")[0])
+                    live = [r for r in range(cl.num_ps, cl.world) if r not in dead]
+                    req = requeue_orphans(cl.store, ep, live)
+                    print(f"[coordinator] worker {w} missed heartbeats for {now - last:.1f}s: declared dead, "
+                          f"re-queued step(s) {req} of epoch {ep}", flush=True)
 
 
 class NativePSServer(PSServer):
@@ -439,13 +510,9 @@ def _claim(store, spe: int, epoch: int, rank: int) -> int:
         raw = got
 
 
-def _fault_step(rank_in_workers: int) -> Optional[int]:
-    spec = os.environ.get("PDDL_FAULT", "")
-    if spec.startswith("kill_worker:"):
-        who, at = spec.split(":", 1)[1].split("@")
-        if int(who) == rank_in_workers:
-            return int(at)
-    return None
+def _fault_step(rank_in_workers: int):
+    from .faults import ps_fault
+    return ps_fault(rank_in_workers)
 
 
 def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
@@ -510,7 +577,9 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     if cfg.max_steps:
         spe = min(spe, cfg.max_steps)
     fault_at = _fault_step(widx)
-    hb = _Heartbeat(store, rank, max(0.05, float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30")) / 6))
+    hb_timeout = float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30"))
+    hb = _Heartbeat(store, rank, max(0.05, hb_timeout / 6), hb_timeout)
+    epoch_timeout = float(os.environ.get("PDDL_PS_EPOCH_TIMEOUT", str(max(600.0, 10 * hb_timeout))))
     it = pipe.iterate(device)
     from .strategies import Augment
     aug = Augment(cfg, device, cfg.seed + 7919 * widx)
@@ -536,19 +605,33 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             lr = float(store.get("lr").decode())
         acc = torch.zeros(3, dtype=torch.float64)
         t_epoch = time.perf_counter()
+        t_drained = None
         while True:
             t = _claim(store, spe, epoch, rank)
             if t < 0:
                 # out of tickets: the epoch ends when every ticket is DONE; until then a ticket
                 # of a worker that died holding it may be re-queued by the coordinator
+                hb.wait()
                 if store.add(f"done/{epoch}", 0) >= spe:
                     break
+                t_drained = t_drained or time.time()
+                if time.time() - t_drained > epoch_timeout:
+                    raise TimeoutError(
+                        f"PS worker {widx}: epoch {epoch} drained its tickets {time.time() - t_drained:.0f} s ago but "
+                        f"only {store.add(f'done/{epoch}', 0)}/{spe} steps are done (claimed "
+                        f"{_claimed(store, epoch)}, re-queued {store.add(f'requeue/{epoch}', 0)}, dead workers "
+                        f"{store.add('dead_workers', 0)}) - a worker holding a ticket is stuck and was not declared dead")
                 time.sleep(0.02)
                 continue
+            t_drained = None
+            hb.step()
             store.set(f"cur/{rank}", f"{epoch}:{t}")
-            if fault_at is not None and steps_done == fault_at:
-                print(f"[worker {widx}] injected failure at step {steps_done}", flush=True)
-                os._exit(17)
+            if fault_at is not None and steps_done == fault_at[1]:
+                print(f"[worker {widx}] injected {fault_at[0]} at step {steps_done}", flush=True)
+                if fault_at[0] == "kill_worker":
+                    os._exit(17)
+                while True:                       # hang_worker: stuck inside the step
+                    time.sleep(3600)
             images, labels = next(it)
             B = images.shape[0]
             flip, off = aug(B)
@@ -560,10 +643,13 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
                 worker.exchange_begin(lr)        # this push flies while the next step computes
             else:
                 worker._exchange(OP_PUSH, lr)
+            store.set(f"tdone/{epoch}/{t}", "1")
             store.set(f"cur/{rank}", f"{epoch}:-1")
             store.add(f"done/{epoch}", 1)
             steps_done += 1
+        hb.step()
         worker.exchange_end()                    # drain the last overlapped push of the epoch
+        hb.wait()
         # epoch end: worker 0 (coordinator-side logic) validates and runs the callbacks
         store.add(f"acc/{epoch}/loss", int(acc[0].item() * 1e6))
         store.add(f"acc/{epoch}/correct", int(acc[1].item()))
@@ -598,7 +684,9 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     if widx == 0 and cfg.save:
         # the reference saves the PS-held variables (imagenet-resnet50-ps.py:145-148): wait until
         # every live worker pushed its last step and stopped, then pull the final state
-        _wait_count(store, "fin_count", lambda: cl.num_workers - 1 - store.add("dead_workers", 0))
+        others = [r for r in range(cl.num_ps, cl.world) if r != rank]
+        _wait_until(lambda: all(store.check([f"fin/{r}"]) or store.check([f"dead/{r}"]) for r in others),
+                    "every live worker's final push")
         worker._exchange(OP_PULL, lr)
     worker.stop()
     hb.stop()
@@ -619,6 +707,14 @@ def _wait_count(store, key, n, timeout=600):
     while store.add(key, 0) < (n() if callable(n) else n):
         if time.time() - t0 > timeout:
             raise TimeoutError(key)
+        time.sleep(0.05)
+
+
+def _wait_until(pred, what, timeout=600):
+    t0 = time.time()
+    while not pred():
+        if time.time() - t0 > timeout:
+            raise TimeoutError(what)
         time.sleep(0.05)
 
 

@@ -29,7 +29,33 @@ from ..models.resnet50 import ParamLayout
 from ..train.optim import make_optimizer
 from ..utils import profiling as prof
 from .collectives import BucketAllReducer
+from .faults import StepFaults
 from .launch import ClusterInfo, export_torch_env, resolve_cluster
+
+
+def rehearsing() -> bool:
+    """PDDL_REHEARSE=1: several ranks / replicas may share one GPU (1-GPU rehearsals of the
+    multi-GPU code).  Outside a rehearsal a rank never wraps onto another rank's device."""
+    return os.environ.get("PDDL_REHEARSE", "0") == "1"
+
+
+def stall_timeout() -> float:
+    """Seconds a gradient collective may stay incomplete before the stall watchdogs (fusion
+    engine, native RCCL communicator) report it (Horovod's HOROVOD_STALL_CHECK_TIME_SECONDS)."""
+    return float(os.environ.get("PDDL_STALL_TIMEOUT", "60"))
+
+
+def stall_shutdown() -> float:
+    """Grace after a stall report before the process exits 124 (HOROVOD_STALL_SHUTDOWN_TIME_SECONDS);
+    0 = report only (the next collective call raises)."""
+    return float(os.environ.get("PDDL_STALL_SHUTDOWN", "0"))
+
+
+def collective_timeout():
+    """c10d process-group timeout: ProcessGroupNCCL's own watchdog tears the process down when a
+    collective exceeds it, so a dead peer cannot hang a rank inside a device synchronize."""
+    import datetime
+    return datetime.timedelta(seconds=float(os.environ.get("PDDL_COLLECTIVE_TIMEOUT", "600")))
 
 
 def gpu_available() -> bool:
@@ -110,7 +136,13 @@ class Strategy:
         want = self.cfg.device
         if want == "cpu" or (want == "auto" and not gpu_available()):
             return torch.device("cpu")
-        local_index %= torch.cuda.device_count()   # (rehearsals may put several ranks on one GPU)
+        have = torch.cuda.device_count()
+        if local_index >= have:
+            if not rehearsing():
+                raise RuntimeError(f"local rank {local_index} needs GPU {local_index} but only {have} GPU(s) are "
+                                   "visible: launch at most one rank per visible GPU (PDDL_REHEARSE=1 lets "
+                                   "rehearsal ranks share devices)")
+            local_index %= have
         torch.cuda.set_device(local_index)
         return torch.device("cuda", local_index)
 
@@ -166,6 +198,11 @@ class Strategy:
         return self._pipe("val", vb, self.world, self.rank)
 
     # ------------------------------------------------------------------ steps
+    def _fault_tick(self):
+        if not hasattr(self, "_faults"):
+            self._faults = StepFaults(self.rank)
+        self._faults.tick()
+
     def set_lr(self, lr: float):
         for _, opt in self._replicas():
             opt.lr = lr
@@ -207,6 +244,7 @@ class SingleStrategy(Strategy):
                                             1.0 / B)
 
     def train_step(self, images, labels):
+        self._fault_tick()
         B = images.shape[0]
         flip, off = self.aug(B)
         if self.graphed is not None and B == self.graphed.B and tuple(images.shape[1:3]) == self.graphed.images.shape[1:3]:
@@ -227,7 +265,7 @@ class _ProcessGroupMixin:
             backend = "nccl" if self.device.type == "cuda" else "gloo"
             # PDDL_DIST_BACKEND=gloo: rehearse GPU ranks sharing one device (RCCL refuses that)
             backend = os.environ.get("PDDL_DIST_BACKEND", backend)
-            kw = {}
+            kw = {"timeout": collective_timeout()}
             if backend == "nccl":
                 kw["device_id"] = self.device
             dist.init_process_group(backend, init_method="env://", rank=info.rank, world_size=info.world_size, **kw)
@@ -287,11 +325,13 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
                 if native_available():
                     self.fusion = require_native().FusionEngine(
                         dist.group.WORLD, self.engine.grads, [(s, e - s) for s, e in self.buckets],
-                        float(os.environ.get("PDDL_STALL_TIMEOUT", "60")), False, self.rank, self.cfg.grad_dtype)
+                        stall_timeout(), False, self.rank, self.cfg.grad_dtype)
+                    self.fusion.set_stall_shutdown(stall_shutdown())
                     if self.cfg.timeline:
                         self.fusion.set_timeline(True)
             if self.fusion is None:
-                self.reducer = BucketAllReducer(self.engine.grads, self.buckets, comm_dtype=self.cfg.grad_dtype)
+                self.reducer = BucketAllReducer(self.engine.grads, self.buckets, comm_dtype=self.cfg.grad_dtype,
+                                                stall_timeout=stall_timeout())
 
     _TUNE_STEPS = int(os.environ.get("PDDL_AUTOTUNE_STEPS", "4"))   # per candidate: 1 discarded + rest timed
 
@@ -322,11 +362,24 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
         return s
 
     def train_step(self, images, labels):
+        self._fault_tick()
         if self._tune is not None:
             return self._autotune_step(images, labels)
         return self._step(images, labels)
 
     def _step(self, images, labels):
+        s = self.compute_gradients(images, labels)
+        prof.push("step/optimizer")
+        self.opt.step()
+        self.engine.after_update()
+        prof.pop()
+        return s
+
+    def compute_gradients(self, images, labels):
+        """Forward + backward + the bucketed all-reduce, without applying the update
+        (Optimizer.compute_gradients of the reference's DistributedOptimizer,
+        imagenet-resnet50-hvd.py:101): afterwards `engine.grads` holds the global-batch mean
+        gradient on every rank.  Returns the step's (loss sum, correct) stats."""
         B = images.shape[0]
         flip, off = self.aug(B)
         gscale = 1.0 / (B * self.world)
@@ -344,10 +397,6 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
             self.fusion.finish()
         elif self.reducer is not None:
             self.reducer.finish()
-        prof.pop()
-        prof.push("step/optimizer")
-        self.opt.step()
-        self.engine.after_update()
         prof.pop()
         return s
 
@@ -398,7 +447,8 @@ class MultiWorkerStrategy(HorovodStrategy):
         export_torch_env(info)
         self.rank, self.world = info.rank, info.world_size
         if not dist.is_initialized() and self.world > 1:
-            dist.init_process_group("gloo", init_method="env://", rank=info.rank, world_size=info.world_size)
+            dist.init_process_group("gloo", init_method="env://", rank=info.rank, world_size=info.world_size,
+                                    timeout=collective_timeout())
         self.mirror = _LocalReplicas(self.cfg, devs, global_rank_base=self.rank * R, world_ranks=self.world * R)
         self.engine, self.opt = self.mirror.replicas[0]
         self.device = self.mirror.devices[0]
@@ -416,6 +466,7 @@ class MultiWorkerStrategy(HorovodStrategy):
     def train_step(self, images, labels):
         if not hasattr(self, "mirror"):
             return super().train_step(images, labels)
+        self._fault_tick()
         return self.mirror.step(images, labels, self.global_batch)
 
     def broadcast_state(self, trainer, root=0):
@@ -466,14 +517,20 @@ class _LocalReplicas:
         if self.gpu and distinct:
             from ..ops.native import require_native
             N = require_native()
-            if world_ranks == self.R:
+            # (PDDL_RCCL_INIT=rank forces the multi-process constructor for a single-process job:
+            # the 1-GPU test of MWMS's P x R path)
+            if world_ranks == self.R and os.environ.get("PDDL_RCCL_INIT", "all") != "rank":
                 self.comm = N.RcclComm.init_all([d.index for d in self.devices])
             else:
                 uid = N.RcclComm.unique_id() if global_rank_base == 0 else b""
                 obj = [uid]
-                dist.broadcast_object_list(obj, src=0)
+                if dist.is_initialized() and dist.get_world_size() > 1:
+                    dist.broadcast_object_list(obj, src=0)
                 self.comm = N.RcclComm(world_ranks, obj[0], [global_rank_base + i for i in range(self.R)],
                                        [d.index for d in self.devices])
+            # stall watchdog: a bucket collective not complete within the timeout aborts the
+            # communicators (blocked kernels exit) and the next step raises with the bucket id
+            self.comm.set_watchdog(stall_timeout(), stall_shutdown(), global_rank_base)
         self.graph_mode = (self.comm is not None and hasattr(self.replicas[0][0], "wbf")
                            and (cfg.graphs if cfg.graphs is not None else True))
         self.graphs = None
@@ -552,7 +609,7 @@ class _LocalReplicas:
                     self.graphs[r].replay_segment(k)
                     self.evs[k][r].record(cur[r])
                     self.comm_streams[r].wait_event(self.evs[k][r])
-            self.comm.all_reduce_on([gr[s:e] for gr in grads], "sum", streams)
+            self.comm.all_reduce_on([gr[s:e] for gr in grads], "sum", streams, f"bucket {k} all_reduce")
         for r, d in enumerate(self.devices):
             with torch.cuda.device(d):
                 cur[r].wait_stream(self.comm_streams[r])
@@ -594,14 +651,14 @@ class _LocalReplicas:
             s, e = self.buckets[i]
             for r in range(self.R):
                 self.comm_streams[r].wait_event(self._events[i][r])
-            self.comm.all_reduce_on([g[s:e] for g in grads], "sum", streams)
+            self.comm.all_reduce_on([g[s:e] for g in grads], "sum", streams, f"bucket {i} all_reduce")
         self._done = []
         for r in range(self.R):
             ev = torch.cuda.Event()
             ev.record(self.comm_streams[r])
             self._done.append(ev)
 
-    def _eager_step(self, parts, global_batch: int):
+    def _eager_step(self, parts, global_batch: int, apply: bool = True):
         R = self.R
         stats = [None] * R
         overlap = self.comm is not None and os.environ.get("PDDL_MIRROR_OVERLAP", "1") != "0"
@@ -652,12 +709,20 @@ class _LocalReplicas:
             for g in grads:
                 if g is not tot:
                     g.copy_(tot)
-        for e, o in self.replicas:
-            o.step()
-            e.after_update()
+        if apply:
+            for e, o in self.replicas:
+                o.step()
+                e.after_update()
         return self._sum_stats(stats)
 
+    def compute_gradients(self, images, labels, global_batch: int):
+        """Eager forward + backward + cross-replica sum without the update: afterwards every
+        replica's `grads` holds the global-batch mean gradient."""
+        return self._eager_step(self._split(images, labels), global_batch, apply=False)
+
     def step(self, images, labels, global_batch: int):
+        if self.comm is not None:
+            self.comm.check()      # a stall verdict of the previous step's collectives raises here
         parts = self._split(images, labels)
         if self.graph_mode:
             return self._graphed_step(parts, global_batch)
@@ -689,7 +754,11 @@ class MirroredStrategy(Strategy):
         return self.mirror.replicas
 
     def train_step(self, images, labels):
+        self._fault_tick()
         return self.mirror.step(images, labels, self.global_batch)
+
+    def compute_gradients(self, images, labels):
+        return self.mirror.compute_gradients(images, labels, self.global_batch)
 
     def broadcast_state(self, trainer, root=0):
         self.mirror.broadcast()

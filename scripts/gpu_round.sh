@@ -20,7 +20,8 @@ for s in "$@"; do
     kernels) step kernels 600 python -m pytest tests/test_gpu_kernels.py -x -q ;;
     engine)  step engine 600 python -m pytest tests/test_gpu_engine.py -x -q ;;
     gputests) step gputests 900 python -m pytest tests -m gpu -x -q ;;
-    runtime) step runtime 600 python -m pytest tests/test_gpu_runtime.py -x -q ;;
+    runtime) step runtime 600 python -u -m pytest tests/test_gpu_runtime.py -x -v --timeout 300 --timeout-method thread ;;
+    multirank) step multirank 600 python -u -m pytest tests/test_gpu_multirank.py -x -v -s --timeout 400 --timeout-method thread ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench256) step bench256 600 python bench.py --steps 20 --warmup 5 --batch 256 ;;

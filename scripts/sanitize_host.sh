@@ -39,7 +39,7 @@ g++ -std=c++17 -O1 -g -fsanitize=thread -I csrc -I /opt/conda/include \
     csrc/tests/io_core_test.cpp "$OUT/lib/libjpeg.so.9" -Wl,-rpath,"$PWD/$OUT/lib" -lpthread -o "$OUT/io_core_tsan"
 TSAN_OPTIONS=halt_on_error=1 "$OUT/io_core_tsan"
 CLANG=${CLANG:-/opt/rocm/llvm/bin/clang++}
-for t in fusion_core ps_protocol; do
+for t in fusion_core comm_watch ps_protocol; do
   echo "== TSan: $t"
   "$CLANG" -std=c++17 -O1 -g -fsanitize=thread -I csrc "csrc/tests/${t}_test.cpp" -lpthread -o "$OUT/${t}_tsan"
   TSAN_OPTIONS=halt_on_error=1 "$OUT/${t}_tsan"

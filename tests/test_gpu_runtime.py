@@ -180,3 +180,66 @@ def test_bench_mirrored_one_gpu_graphed():
     """The in-process Mirrored bench on 1 GPU runs RCCL + segmented HIP graphs."""
     out = _bench_json(["--gpus", "1", "--strategy", "mirrored", "--batch", "64", "--steps", "3", "--warmup", "2"], {})
     assert out["n_gpus"] == 1 and out["config"]["hip_graph"] is True and "rehearsal" not in out
+
+
+def test_rccl_comm_init_rank_constructor_and_watchdog():
+    """The multi-process constructor (ncclCommInitRank for every local rank inside one group --
+    MWMS's P x R layout, imagenet-resnet50-multiworkers.py:20-26) with nranks=1: collectives on
+    explicit streams, what RCCL reports it built, and the stall watchdog retiring every
+    collective without a false alarm."""
+    import time
+    from pddl.ops.native import require_native
+    N = require_native()
+    comm = N.RcclComm(1, N.RcclComm.unique_id(), [0], [0])
+    info = comm.info()
+    assert len(info) == 1 and info[0]["nranks"] == 1 and info[0]["rank"] == 0 and info[0]["device"] == 0
+    assert info[0]["pci_bus_id"]
+    comm.set_watchdog(20.0, 0.0, 0)
+    side = torch.cuda.Stream()
+    t = torch.arange(4096, dtype=torch.float32, device="cuda")
+    ref = t.clone()
+    side.wait_stream(torch.cuda.current_stream())
+    for k in range(8):
+        comm.all_reduce_on([t], "sum", [side.cuda_stream], f"bucket {k} all_reduce")
+    torch.cuda.current_stream().wait_stream(side)
+    comm.broadcast([t], 0)
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+    t0 = time.time()
+    while comm.watchdog_state()["retired"] < 9 and time.time() - t0 < 10:
+        time.sleep(0.05)
+    st = comm.watchdog_state()
+    assert st["armed"] and st["issued"] == 9 and st["retired"] == 9 and not st["stalled"], st
+    comm.check()
+    comm.abort()
+    with pytest.raises(RuntimeError, match="aborted"):
+        comm.all_reduce([t], "sum")
+
+
+def test_mirrored_on_init_rank_communicator(monkeypatch):
+    """The whole graphed Mirrored / MWMS replica driver on the ncclCommInitRank communicator
+    (PDDL_RCCL_INIT=rank), with its bucket collectives under the watchdog."""
+    from pddl.parallel.strategies import make_strategy
+    from pddl.train.trainer import Trainer
+    monkeypatch.setenv("PDDL_RCCL_INIT", "rank")
+    cfg = _cfg("mirrored", max_steps=4, batch_size=8)
+    st = make_strategy(cfg)
+    tr = Trainer(cfg, st)
+    h = tr.fit(1, [], validation=False)
+    comm = st.mirror.comm
+    assert comm is not None and comm.info()[0]["nranks"] == 1
+    assert h.history["loss"][0] == h.history["loss"][0]
+    torch.cuda.synchronize()
+    ws = comm.watchdog_state()
+    assert ws["armed"] and ws["issued"] >= 4 * len(st.mirror.buckets) and not ws["stalled"], ws
+
+
+def test_bench_parameter_server_rehearsal_on_one_gpu():
+    """BASELINE config 5's code path on the GPU: bench.py --strategy ps with 1 PS + 2 workers as
+    three processes sharing the card (PDDL_REHEARSE=1) over the native HIP-IPC data plane --
+    event-chained PS service (Adam + snapshot copy per request, `done` published on event
+    completion) and the workers' poster threads (no host sync on push)."""
+    out = _bench_json(["--gpus", "3", "--strategy", "ps", "--ps", "1", "--batch", "32", "--steps", "8"],
+                      {"PDDL_REHEARSE": "1", "PDDL_PS_IMPL": "native"})
+    assert out["n_gpus"] == 3 and out["config"]["parallelism"] == "ps1+w2" and out["rehearsal"] is True
+    assert out["steps_timed_epoch"] == 8 and out["value"] > 0

@@ -197,3 +197,41 @@ def test_resume_continues_epochs_lr_and_callbacks(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Resuming after epoch 2 at lr 0.0005" in r.stdout
     assert "Epoch 3/3" in r.stdout and "Epoch 1/3" not in r.stdout and "lr: 0.0005" in r.stdout
+
+
+def test_ps_stalled_worker_declared_dead_and_requeued(monkeypatch):
+    """A LIVE worker stuck inside a step (hang_worker) stops heartbeating (the beacon stamps
+    only while the main loop makes progress), is declared dead, its ticket is re-queued and
+    the epoch completes; the stuck process ends itself after twice the timeout."""
+    from pddl.parallel.parameter_server import run_ps_job
+    monkeypatch.setenv("PDDL_FAULT", "hang_worker:1@1")
+    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
+    cfg = _cfg("ps", steps_per_epoch=6, batch_size=2, epochs=1)
+    res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
+    wk = [r for r in res if r[0] == "worker"]
+    ps = [r for r in res if r[0] == "ps"]
+    assert len(wk) == 1 and wk[0][2] >= 5                    # worker 0 ran the re-queued ticket too
+    assert ps[0][2] >= 6
+
+
+def test_requeue_orphans_counts_each_lost_ticket_once():
+    """Orphaned tickets are found from completion markers, not from what the dead worker wrote:
+    a worker that died between its claim and its `cur` write still gets its ticket re-queued."""
+    import torch.distributed as dist
+    from pddl.parallel.parameter_server import requeue_orphans
+    st = dist.HashStore()
+    st.set("claim/0", "6/3")                 # tickets 0..5 claimed
+    for t in (0, 1, 3, 5):
+        st.set(f"tdone/0/{t}", "1")
+    st.set("cur/4", "0:4")                   # live worker 4 holds ticket 4; ticket 2 is orphaned
+    assert requeue_orphans(st, 0, [4]) == [2]
+    assert st.add("requeue/0", 0) == 1
+    assert requeue_orphans(st, 0, [4]) == []  # a second scan does not count it again
+    assert st.add("requeue/0", 0) == 1
+
+
+def test_ps_resume_rejected(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "imagenet-resnet50-ps.py"), "--ps", "1", "--worker", "1",
+                        "--resume", str(tmp_path / "x.h5"), "--device", "cpu"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 2 and "--resume is not supported for --strategy ps" in r.stderr, r.stderr[-2000:]
