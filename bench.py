@@ -459,6 +459,7 @@ def run_ps(args):
     res = run_ps_job(cfg, num_ps=n_ps, num_workers=n_w, return_results=True)
     wall = time.perf_counter() - t0
     hist = [r[3] for r in res if r[0] == "worker" and r[3]]
+    svc = [r[5] for r in res if r[0] == "ps" and len(r) > 5 and r[5]]
     if not hist or len(hist[0]) < 2:
         fail("parameter-server job returned no timed epoch")
     ep = hist[0][1]
@@ -477,6 +478,7 @@ def run_ps(args):
                    "note": "ms_per_step = one synchronous-equivalent step of all workers; warmup = one untimed epoch"},
         "per_gpu_images_per_sec": round(ips / n_w, 2), "steps_timed_epoch": ep.get("steps"),
         "job_wall_s": round(wall, 1), **({"rehearsal": True} if rehearsing() else {}),
+        **({"ps_service": svc} if svc else {}),
     }), flush=True)
     return 0
 

@@ -5,6 +5,7 @@
 // a GPU tensor.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/util/Optional.h>
 
 #include "kernels/kernels.h"
@@ -38,6 +39,23 @@ int ld(const Tensor& t) {
   return t.dim() >= 2 ? (int)t.stride(-2) : (int)t.size(-1);
 }
 int old(const OptT& t) { return t.has_value() ? ld(*t) : 0; }
+
+// Split-K workspace (fp32 partial tiles of the small-M layers, igemm.hip), owned by the
+// calling engine and made current for the calling THREAD (`splitk_use`): two engines whose
+// launches interleave on one device (Mirrored replicas driven from threads, rehearsals) must
+// never share one -- replica B's slices would overwrite replica A's partials between A's
+// slices and A's combine.  Nothing is allocated inside a launch, so graph capture bakes the
+// engine's own buffer into its kernels.
+thread_local Tensor tls_splitk;
+void splitk_use(OptT ws) {
+  if (ws.has_value()) PCHECK(ws->is_cuda() && ws->scalar_type() == torch::kFloat32 && ws->is_contiguous(),
+                             "split-K workspace: contiguous fp32 GPU tensor");
+  tls_splitk = ws.has_value() ? *ws : Tensor();
+}
+int64_t splitk_default_floats(int64_t device) {   // the heuristic's bound: < 2 x (2 x #CUs) tiles of 16384 floats
+  c10::hip::HIPGuardMasqueradingAsCUDA g((int)device);
+  return 4L * pddl::num_cus() * 16384;
+}
 
 // Generic implicit-GEMM (conv forward / dgrad / fp32 dense).
 void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
@@ -121,6 +139,10 @@ void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, 
   PCHECK(out.numel() / std::max<int64_t>(1, out.size(-1)) >= (out2.has_value() ? p.M : rows_out) ||
              out.dim() >= 2,
          "output too small");
+  if (tls_splitk.defined() && tls_splitk.device() == a1.device()) {
+    p.slab = tls_splitk.data_ptr<float>();
+    p.slab_floats = tls_splitk.numel();
+  }
   ok(pddl::igemm_launch(p, cur_stream()), "igemm");
 }
 
@@ -445,6 +467,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
     else if (which == "pool") pddl::g_pool_variant = v;
     else if (which == "igemm_n64") pddl::g_igemm_n64 = v;
+    else if (which == "igemm_splitk") pddl::g_igemm_splitk = v;
+    else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
     else if (which == "igemm8_ragged") pddl::g_igemm8_ragged = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
@@ -455,10 +479,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("igemm_partial_rows", [](int M, int Nn, int K, bool bnz) { return pddl::igemm_partial_rows(M, Nn, K, bnz); },
         py::arg("M"), py::arg("Nn"), py::arg("K"), py::arg("bnz") = false);
+  m.def("igemm_splitk_floats", [](int M, int Nn, int K) { return (int64_t)pddl::igemm_splitk_floats(M, Nn, K); });
+  m.def("splitk_use", &splitk_use, py::arg("workspace"));
+  m.def("splitk_default_floats", &splitk_default_floats, py::arg("device"));
   m.def("igemm_plan", [](int M, int Nn, int K) {
-    int cfg = 0, split = 0;
-    pddl::igemm_plan_query(M, Nn, K, &cfg, &split);
-    return std::make_pair(cfg, split);
+    int cfg = 0, split = 0, ks = 1;
+    pddl::igemm_plan_query(M, Nn, K, &cfg, &split, &ks);
+    return std::make_tuple(cfg, split, ks);
   });
   m.def("maxpool_bwd_partial_rows", &pddl::maxpool_bwd_partial_rows);
   m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);

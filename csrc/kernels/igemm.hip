@@ -302,7 +302,9 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 // accumulators are staged through LDS, so its HBM latency overlaps the staging instead of
 // stalling every store iteration (short-K 1x1 layers are epilogue-bound).
 // WTM_: wave-tile rows (64, or 128 for the 256x256 tile: 8 waves as 2 x 4, 128x64 each).
-template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64, bool BNZ = false>
+// SK: split-K slice instantiation (separate, so the unsplit kernels keep their register budget:
+// the slice bookkeeping compiled into every instantiation cost 33 VGPRs, occupancy 3 -> 2).
+template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64, bool BNZ = false, bool SK = false>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParams p) {
   constexpr int WTM = WTM_, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -323,10 +325,18 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably uniform: M0 from SGPRs
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int mt = (p.M - p.m_begin + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, mt * nt);
+  // split-K: the K loop of every tile is cut into `ks` slices run by adjacent workgroups (same
+  // XCD after the remap); each slice leaves its fp32 partial tile in the workspace and
+  // igemm_splitk_reduce_kernel sums them and runs the fused epilogue
+  const int ks = SK ? p.ksplit : 1;
+  const int wgs = xcd_remap(blockIdx.x, mt * nt * ks);
+  const int slice = wgs % ks, wg = wgs / ks;
   const int tn = wg % nt, tm = wg / nt;
   const int m0 = p.m_begin + tm * BM, n0 = tn * BN;
   const int HoWo = p.Ho * p.Wo;
+  const int KT_all = p.K / 64;
+  const int kt0 = (int)((long)slice * KT_all / ks);
+  const int KT = (int)((long)(slice + 1) * KT_all / ks) - kt0;
 
   // Buffer descriptors (wave-uniform kernel arguments only, so no waterfall loops).
   const int pix_total = p.N * p.H * p.W;
@@ -374,6 +384,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   // of source `src2`; a "window" tile (C * S == 64) spans all S taps of one r.
   int ld_r = 0, ld_s = 0, ld_c0 = 0, ld_src2 = 0, ld_k = 0;
   const bool window = p.C1 * p.S == 64 && p.C1 < 64;
+  if (SK && kt0 > 0) {   // (split-K slices: single source, C1 % 64 == 0 -- igemm_launch guarantees)
+    ld_k = kt0 * 64;
+    ld_c0 = ld_k % p.C1;
+    const int tq = ld_k / p.C1;
+    ld_s = tq % p.S;
+    ld_r = tq / p.S;
+  }
   // piece j (< AI: A rows, else B rows) of the current walk position into LDS buffer buf
   auto tile_delta = [&]() { return ((ld_r * p.W + ld_s) * (ld_src2 ? p.C2 : p.C1) + ld_c0) * 2; };   // bytes
   auto load_piece = [&](int buf, int j, int delta) {
@@ -424,7 +441,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  const int KT = p.K / 64;
   const int a_off = (wm * WTM + (lane & 15)) * 128;
   const int b_off = (wn * WTN + (lane & 15)) * 128;
   load_tile(0);
@@ -486,12 +502,73 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   }
   if (NSTAGE == 3) __syncthreads();   // all fragment reads done before the epilogue reuses LDS
 
+  if constexpr (SK) {   // split-K slice: the fp32 partial tile in fragment order (16-byte coalesced stores)
+    float4* dst = reinterpret_cast<float4*>(p.slab) + ((long)(wg * ks + slice) * NW + wave) * (TM * TN) * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        dst[(i * TN + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    return;
+  }
+
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (WTN + 4));
   igemm_epilogue<TM, TN, PF, BNZ>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, stage,
                                   lane);
 }
 
+
+// Split-K combine: one single-wave workgroup per 64x64 wave sub-tile (4 per output tile, so a
+// small-M layer's few tiles still spread over the chip: the combine is bound by how fast ONE
+// CU pulls its slabs) sums the `ksplit` fp32 partial tiles its slices left in the workspace
+// (same fragment order, so each lane reads 16-byte vectors of its own accumulator registers,
+// two slices' loads in flight at a time) and runs the unchanged fused epilogue on the sum.
+// A separate launch instead of an in-launch last-arriver reduction: one boundary per layer
+// (cdna_hip_programming §5, "In-launch split-K reduction": only worth it when it beats the
+// boundary it replaces).
+template <int BM, int BN>
+__global__ void __launch_bounds__(64) igemm_splitk_reduce_kernel(IgemmParams p) {
+  constexpr int NW = 4, WTM = 64, WTN = 64, TM = 4, TN = 4, WAVES_N = BN / WTN, F = TM * TN;
+  __shared__ __attribute__((aligned(16))) char smem[32 * (WTN + 4) * 4];
+  const int lane = threadIdx.x;
+  const int wave = blockIdx.x % NW;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int nt = (p.Nn + BN - 1) / BN;
+  const int tile = blockIdx.x / NW, tn = tile % nt, tm = tile / nt;
+  v4f acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const float4* src = reinterpret_cast<const float4*>(p.slab) + ((long)tile * p.ksplit * NW + wave) * F * 64 + lane;
+  const long sstride = (long)NW * F * 64;
+  auto add = [&](const float4 (&v)[F]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float4 q = v[i * TN + j];
+        acc[i][j][0] += q.x; acc[i][j][1] += q.y; acc[i][j][2] += q.z; acc[i][j][3] += q.w;
+      }
+  };
+  int sl = 0;
+  for (; sl + 1 < p.ksplit; sl += 2) {
+    float4 v0[F], v1[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) { v0[f] = src[sl * sstride + f * 64]; v1[f] = src[(sl + 1) * sstride + f * 64]; }
+    add(v0);
+    add(v1);
+  }
+  if (sl < p.ksplit) {
+    float4 v0[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) v0[f] = src[sl * sstride + f * 64];
+    add(v0);
+  }
+  igemm_epilogue<TM, TN, false>(p, acc, p.m_begin + tm * BM + wm * WTM, tn * BN + wn * WTN,
+                                p.prow_begin + tm * (BM / WTM) + wm, reinterpret_cast<float*>(smem), lane);
+}
 
 // ---------------------------------------------------------------------------------------
 // 8-phase 256x256 implicit GEMM (cdna_hip_programming.md §5 "The 256² 8-phase template",
@@ -799,12 +876,53 @@ int num_cus() {
 // that fills at most half of the chip is handed to the 4x finer 128x128 tile (2 blocks per
 // CU) instead of leaving CUs idle for a whole 256x256 tile time (b1024 stage 4: 784 tiles on
 // 256 CUs = 3 full rounds + 16 tiles).
-struct IgemmPlan { int cfg, split; };
+struct IgemmPlan { int cfg, split, ks; };
+
+int g_igemm_splitk = 1;
+
+// Split-K for layers with too few output tiles to fill the chip (small batches, small spatial
+// stages: stage 5 at batch 32-256, crop 160): the 4-wave tiles stay resident 2-3 per CU, so a
+// problem with at most #CUs / 2 tiles leaves most CUs idle for its whole K loop.  Slices keep
+// >= 4 k-tiles each (the LDS pipeline's prologue / epilogue amortised) and at most 8, aiming at
+// ~2 x #CUs slice workgroups.
+static int igemm_splitk_slices(int M, int Nn, int K, int cfg) {
+  if (!g_igemm_splitk || (cfg != 0 && cfg != 1)) return 1;
+  const int KT = K / 64;
+  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : 128;
+  const long T = (long)((M + BM - 1) / BM) * ((Nn + BN - 1) / BN);
+  if (g_igemm_splitk >= 2) return KT >= 2 ? (g_igemm_splitk < KT ? g_igemm_splitk : KT) : 1;
+  // Split only problems that fill at most half the CUs: measured per layer at b32 / b256-crop160
+  // (profiles/r3_splitk_b32_per_layer.txt), 52-98 tiles gain 20-60 us per layer while 196-490
+  // tiles LOSE 4-16 us (the slab round trip + the combine launch outweigh the fill gained)
+  // Long-K layers (K >= 2048: the stage-4/5 3x3s) also split up to 2 x #CUs tiles: their K loop
+  // is long enough that the slab round trip is a few % of the layer (b256 crop 160: the stage-5
+  // 3x3 runs 200 tiles = 200 lone 4-wave blocks on 256 CUs at 340 TF/s unsplit).
+  const long C = num_cus();
+  const long target = 2L * C;
+  if (KT < 8) return 1;
+  if (2 * T > C && !(T < target && KT >= 32)) return 1;
+  long ks = (target + T - 1) / T;
+  if (ks > KT / 4) ks = KT / 4;
+  if (ks > 8) ks = 8;
+  return ks >= 2 ? (int)ks : 1;
+}
+
 static IgemmPlan igemm_plan(int M, int Nn, int K, bool bnz = false) {
-  IgemmPlan pl{igemm_config(M, Nn, K), M};
+  IgemmPlan pl{igemm_config(M, Nn, K), M, 1};
   if (bnz) {   // fused BN-backward sums: only the 4-wave single-stage tiles carry that epilogue
     if (pl.cfg != 0) pl.cfg = 1;
     return pl;
+  }
+  // (the split decision depends on the shape only -- never on the workspace -- so the partial
+  // column-sum row count igemm_partial_rows reports always matches the launch)
+  {
+    const int c = pl.cfg == 4 ? 1 : pl.cfg;
+    const int ks = igemm_splitk_slices(M, Nn, K, c);
+    if (ks > 1) {
+      pl.cfg = c;
+      pl.ks = ks;
+      return pl;
+    }
   }
   if (pl.cfg != 4) return pl;
   const int nt = (Nn + 255) / 256, mt = (M + 255) / 256;
@@ -819,10 +937,18 @@ static IgemmPlan igemm_plan(int M, int Nn, int K, bool bnz = false) {
   return pl;
 }
 
-void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split) {
+void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split, int* ksplit) {
   const IgemmPlan pl = igemm_plan(M, Nn, K);
   *cfg = pl.cfg;
   *split = pl.split;
+  if (ksplit) *ksplit = pl.ks;
+}
+
+long igemm_splitk_floats(int M, int Nn, int K) {
+  const IgemmPlan pl = igemm_plan(M, Nn, K);
+  if (pl.ks <= 1) return 0;
+  const int BM = igemm_bm(pl.cfg), BN = pl.cfg == 0 ? 64 : 128;
+  return (long)((M + BM - 1) / BM) * ((Nn + BN - 1) / BN) * pl.ks * BM * BN;
 }
 
 int igemm_partial_rows(int M, int Nn, int K, bool bnz) {
@@ -840,8 +966,20 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   p.mg_wo = fdiv_magic(p.Wo);
   p.m_begin = 0;
   p.prow_begin = 0;
+  p.ksplit = 1;
   const IgemmPlan pl = igemm_plan(p.M, p.Nn, p.K, p.bn_z != nullptr);
-  if (pl.split < p.M) {
+  const bool window = (p.C1 * p.S == 64) && p.C1 < 64;
+  if (pl.ks > 1 && !p.a2 && !window && p.C1 % 64 == 0 && p.slab &&
+      p.slab_floats >= igemm_splitk_floats(p.M, p.Nn, p.K)) {
+    // slices -> workspace, then the combine + fused epilogue (without a workspace the same
+    // tile config runs unsplit, so the partial-row layout does not change)
+    p.ksplit = pl.ks;
+    igemm_launch_cfg(p, pl.cfg, stream);
+    const int BM = igemm_bm(pl.cfg), BN = pl.cfg == 0 ? 64 : 128;
+    const int tiles = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
+    if (pl.cfg == 0) hipLaunchKernelGGL((igemm_splitk_reduce_kernel<256, 64>), dim3(tiles * 4), dim3(64), 0, stream, p);
+    else hipLaunchKernelGGL((igemm_splitk_reduce_kernel<128, 128>), dim3(tiles * 4), dim3(64), 0, stream, p);
+  } else if (pl.split < p.M) {
     IgemmParams head = p, tail = p;
     head.M = pl.split;
     tail.m_begin = pl.split;
@@ -874,12 +1012,25 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
     else IG_GO(BM_, BN_, NW_, NS_, AM_DUAL);                         \
   }
   const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : (cfg >= 3 ? 256 : 128);
-  const int nwg = ((p.M - p.m_begin + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
+  const int nwg = ((p.M - p.m_begin + BM - 1) / BM) * ((p.Nn + BN - 1) / BN) * (p.ksplit > 1 ? p.ksplit : 1);
   // PF where the prefetched operand exists for every element (forward residual; dgrad
   // residual-gradient without the stride-2 scatter).  Measured (bench/epilogue.py, b1024,
   // profiles/r1_epilogue_prefetch_ab.json): forward +3-20% on every stage; dgrad +10-14% for
   // K >= 256 but -8-10% for the single-stage K <= 128 tiles, whose occupancy the 24 extra
   // VGPRs cut from 3 to 2 waves per SIMD -- so dgrad uses it only on 2-stage tiles.
+  if (p.ksplit > 1) {   // split-K slices (cfg 0 / 1, single source; igemm_launch)
+#define IG_SK(BM_, BN_, NS_, AM_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_, false, 64, false, true>), dim3(nwg), dim3(256), 0, stream, p)
+    if (cfg == 1) {
+      if (ns == 1) { if (am == AM_DIRECT) IG_SK(128, 128, 1, AM_DIRECT); else IG_SK(128, 128, 1, AM_HALO); }
+      else { if (am == AM_DIRECT) IG_SK(128, 128, 2, AM_DIRECT); else IG_SK(128, 128, 2, AM_HALO); }
+    } else {
+      if (ns == 1) { if (am == AM_DIRECT) IG_SK(256, 64, 1, AM_DIRECT); else IG_SK(256, 64, 1, AM_HALO); }
+      else { if (am == AM_DIRECT) IG_SK(256, 64, 2, AM_DIRECT); else IG_SK(256, 64, 2, AM_HALO); }
+    }
+#undef IG_SK
+    return;
+  }
   const bool pf = g_igemm_pf && am == AM_DIRECT && cfg <= 1 &&
                   ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && (ns == 2 || g_igemm_pf == 2)));
   if (p.bn_z) {   // (igemm_check: DGRAD, no dual source; plan: cfg 0 / 1)

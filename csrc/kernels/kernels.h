@@ -41,13 +41,18 @@ struct IgemmParams {
   uint64_t mg_howo, mg_wo;                          // set by igemm_launch: magic divisors (fdiv)
   int m_begin, prow_begin;                          // set by igemm_launch: this launch covers GEMM rows
                                                     // [m_begin, M); its partial rows start at prow_begin
+  float* slab; long slab_floats;                    // split-K workspace (fp32 partial tiles), optional
+  int ksplit;                                       // set by igemm_launch: K slices per tile (1 = none)
 };
 const char* igemm_launch(const IgemmParams& p, hipStream_t stream);
 int igemm_partial_rows(int M, int Nn, int K, bool bnz = false);   // rows of the partial column-sum buffer
                                                     // (bnz: a launch with the fused BN-backward sums)
-void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split);   // tile config; rows >= split: 128x128 tail
+void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split, int* ksplit = nullptr);   // tile config;
+                                                    // rows >= split: 128x128 tail; ksplit: K slices (split-K)
+long igemm_splitk_floats(int M, int Nn, int K);     // split-K workspace a problem wants (0: no split)
 extern int g_igemm8, g_igemm8_min_tiles, g_igemm8_expand, g_igemm8_min_n, g_igemm_ns1_kt, g_wgrad8, g_wgrad1;
 int num_cus();   // compute units of the current device (cached)
+extern int g_igemm_splitk, g_wgrad8_min_rows;   // split-K: 0 off, 1 heuristic (default), >= 2 forced slices (where legal)
 extern int g_igemm8_ragged, g_stem_variant, g_igemm_n64, g_igemm_variant, g_igemm_deep, g_igemm_big, g_igemm_pf, g_igemm_il, g_wgrad_variant, g_pool_variant, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
 
 struct WgradParams {

@@ -143,7 +143,9 @@ class PSServer {
       hck(hipDeviceSynchronize(), "init sync");
       rx_ptr_.assign(W_, nullptr);
       done_ev_.assign(W_, nullptr);
-      for (auto& e : done_ev_) hck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+      start_ev_.assign(W_, nullptr);
+      for (auto& e : done_ev_) hck(hipEventCreate(&e), "event");   // (timed: per-request service time)
+      for (auto& e : start_ev_) hck(hipEventCreate(&e), "event");
     } else {
       host_.assign(3 * n_, 0.f);
       std::memcpy(host_.data(), host.data_ptr<float>(), n_real_ * sizeof(float));
@@ -161,6 +163,7 @@ class PSServer {
       hipSetDevice(dev_);
       for (float* r : rx_ptr_) if (r) hipIpcCloseMemHandle(r);
       for (auto e : done_ev_) if (e) hipEventDestroy(e);
+      for (auto e : start_ev_) if (e) hipEventDestroy(e);
       if (mailbox_) hipFree(mailbox_);
       if (params_) hipFree(params_);
       if (stream_) hipStreamDestroy(stream_);
@@ -174,6 +177,16 @@ class PSServer {
     return (int64_t)ctrl_->updates.load();
   }
   int64_t updates() const { return (int64_t)ctrl_->updates.load(); }
+  // Per-request GPU service time (start of Adam -> end of the snapshot copy), after join().
+  py::dict service_stats() const {
+    py::dict d;
+    d["requests"] = svc_n_;
+    d["mean_ms"] = svc_n_ ? svc_sum_ms_ / svc_n_ : 0.0;
+    d["max_ms"] = svc_max_ms_;
+    d["total_ms"] = svc_sum_ms_;
+    d["shard_elems"] = n_real_;
+    return d;
+  }
   std::vector<int> dead() const { return dead_; }
   Tensor params() const {
     Tensor out = torch::empty({n_real_}, torch::kFloat32);
@@ -193,6 +206,8 @@ class PSServer {
     const double lr_t = lr * std::sqrt(1.0 - std::pow(b2_, t_)) / (1.0 - std::pow(b1_, t_));
     const float* g = mailbox_ + (size_t)w * n_;
     if (dev_ >= 0) {
+      hck(hipEventRecord(start_ev_[w], stream_), "record start");
+      started_[w] = true;
       kck(pddl::adam_launch(params_, g, m_, v_, n_, (float)lr_t, (float)b1_, (float)b2_, (float)eps_, 1.f, nullptr,
                             stream_),
           "adam");
@@ -216,6 +231,8 @@ class PSServer {
         hck(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "open rx handle");
         rx_ptr_[w] = static_cast<float*>(ptr);
       }
+      if (!started_[w]) hck(hipEventRecord(start_ev_[w], stream_), "record start");   // (pull: copy only)
+      started_[w] = false;
       hck(hipMemcpyAsync(rx_ptr_[w], params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
       hck(hipEventRecord(done_ev_[w], stream_), "record done");
     } else {
@@ -232,6 +249,12 @@ class PSServer {
             const hipError_t q = hipEventQuery(done_ev_[w]);
             if (q == hipErrorNotReady) return false;
             hck(q, "completion event");
+            float ms = 0.f;   // GPU time of this request's Adam + snapshot copy (both events are in-stream)
+            if (hipEventElapsedTime(&ms, start_ev_[w], done_ev_[w]) == hipSuccess) {
+              svc_n_++;
+              svc_sum_ms_ += ms;
+              svc_max_ms_ = std::max(svc_max_ms_, (double)ms);
+            }
             return true;
           },
           [this] {
@@ -263,6 +286,10 @@ class PSServer {
   std::vector<float> host_;
   std::vector<float*> rx_ptr_;
   std::vector<hipEvent_t> done_ev_;   // per worker: its request's Adam + snapshot copy finished
+  std::vector<hipEvent_t> start_ev_;  // per worker: its request's work started (timing)
+  std::vector<char> started_ = std::vector<char>(pddl::ps::kMaxWorkers, 0);
+  int64_t svc_n_ = 0;
+  double svc_sum_ms_ = 0, svc_max_ms_ = 0;
   hipStream_t stream_ = nullptr;
   std::thread thr_;
   std::atomic<bool> stop_{false};
@@ -503,6 +530,7 @@ void register_ps(py::module& m) {
       .def("join", &PSServer::join, py::call_guard<py::gil_scoped_release>())
       .def("params", &PSServer::params)
       .def_property_readonly("updates", &PSServer::updates)
+      .def("service_stats", &PSServer::service_stats)
       .def_property_readonly("dead", &PSServer::dead);
   py::class_<PSClient, std::shared_ptr<PSClient>>(m, "PSClient")
       .def(py::init<const std::string&, std::vector<std::vector<std::pair<int64_t, int64_t>>>, int, int, double>(),

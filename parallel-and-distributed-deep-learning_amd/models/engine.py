@@ -92,6 +92,10 @@ class HipEngine:
         self.shift = torch.zeros(self.nch, dtype=torch.float32, device=dev)
         self._build_weight_tables()
         self._alloc_acts(batch)
+        # split-K workspace of the small-M layers (igemm.hip: stage 5 at small batches, the Dense
+        # head), this engine's own (N.splitk_use makes it current for the launching thread)
+        self.splitk_ws = torch.empty(self.N.splitk_default_floats(self.device.index or 0), dtype=torch.float32,
+                                     device=dev)
 
     # ------------------------------------------------------------------ tables
     def _build_weight_tables(self):
@@ -327,6 +331,7 @@ class HipEngine:
         return 2, crop_offset[0], crop_offset[1]
 
     def _forward(self, images, B, training, flip, crop_offset):
+        self.N.splitk_use(self.splitk_ws)   # this engine's split-K workspace, for this thread's launches
         N, L = self.N, self.L
         mode, oy, ox = self._stem_mode(training, crop_offset)
         x2 = self.stem_x2[:B]

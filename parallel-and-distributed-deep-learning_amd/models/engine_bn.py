@@ -177,6 +177,7 @@ class HipEngineBNTrain(HipEngine):
                        self.bn_shift, BN_EPS, BN_MOMENTUM)
 
     def _forward(self, images, B, training, flip, crop_offset):
+        self.N.splitk_use(self.splitk_ws)   # this engine's split-K workspace, for this thread's launches
         N, L = self.N, self.L
         tabs = self._launch_tables(B) if training else None
         if not training:   # inference: every BN layer from its moving statistics, one launch

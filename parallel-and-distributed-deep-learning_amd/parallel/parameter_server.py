@@ -554,7 +554,8 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         dist.barrier()
         srv.run()
         if result_q is not None:
-            result_q.put(("ps", rank, srv.updates, sorted(srv.dead), impl))
+            stats = srv.srv.service_stats() if impl == "native" and use_gpu else {}
+            result_q.put(("ps", rank, srv.updates, sorted(srv.dead), impl, dict(stats)))
         dist.destroy_process_group()
         return
     # ---------------------------------------------------------------- worker

@@ -60,7 +60,8 @@ def schedule(B, crop):
         else:
             ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * n1, (M * n1 + B * H * H * cin) * 2))
         ev.append(("wgrad_finalize", b.name, 0, 0))
-        ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2, (M, cin, n1)))
+        ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2, (M, cin, n1),
+                   "dual" if b.proj else ""))
     ev.append(("maxpool_bwd", "pool", 0, 0))
     ev.append(("wgrad", "conv1 wgrad", 2 * B * H1 * H1 * 256 * 64, 0))
     ev.append(("stem_wgrad_fold", "fold", 0, 0))
@@ -91,7 +92,15 @@ def main():
         plan = require_native().igemm_plan
     except Exception:   # no native module: unsplit schedule
         plan = None
-    nd = [2 if (e[0] == "igemm" and plan is not None and plan(*e[4])[1] < e[4][0]) else 1 for e in ev]
+    # ... and a split-K launch is the slices + the combine (igemm_splitk_reduce_kernel); the
+    # projection blocks' dual-source c1 dgrad is never split
+    def ndisp(e):
+        if e[0] != "igemm" or plan is None:
+            return 1
+        cfg, split, ks = plan(*e[4])
+        dual = len(e) > 5 and e[5] == "dual"
+        return 2 if split < e[4][0] or (ks > 1 and not dual) else 1
+    nd = [ndisp(e) for e in ev]
     need = sum(nd)
     starts = [i for i, r in enumerate(rows) if "stem_s2d" in r["Kernel_Name"]]
     st = None

@@ -22,6 +22,9 @@ for s in "$@"; do
     gputests) step gputests 900 python -m pytest tests -m gpu -x -q ;;
     runtime) step runtime 600 python -u -m pytest tests/test_gpu_runtime.py -x -v --timeout 300 --timeout-method thread ;;
     multirank) step multirank 600 python -u -m pytest tests/test_gpu_multirank.py -x -v -s --timeout 400 --timeout-method thread ;;
+    psrt)    step psrt 600 python -u -m pytest tests/test_gpu_runtime.py -x -v -k parameter_server --timeout 400 --timeout-method thread ;;
+    psbench) step psbench32 300 env PDDL_REHEARSE=1 python bench.py --gpus 3 --strategy ps --ps 1 --batch 32 --steps 60 &&
+             step psbench256 300 env PDDL_REHEARSE=1 python bench.py --gpus 3 --strategy ps --ps 1 --batch 256 --steps 24 ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench256) step bench256 600 python bench.py --steps 20 --warmup 5 --batch 256 ;;

@@ -18,6 +18,19 @@ def N():
     return require_native()
 
 
+@pytest.fixture(autouse=True)
+def _unsplit_by_default(request):
+    """Kernel-equivalence tests compare tilings that must share one k order: split-K (on by
+    default for small-M problems when the calling thread has a workspace current, e.g. after an
+    engine ran) is switched off here and exercised explicitly by the split-K tests."""
+    if "splitk" in request.node.name:
+        yield
+        return
+    N().set_variant("igemm_splitk", 0)
+    yield
+    N().set_variant("igemm_splitk", 1)
+
+
 def rel(a, b):
     a, b = a.float(), b.float()
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
@@ -662,3 +675,101 @@ def test_dgrad_up2_grid_only_scatter(hc, cin, co):
     off[::2, ::2] = False
     assert torch.all(f1[:, off] == 0)          # up2 = 1 zero-fills
     assert torch.all(f2[:, off] == 7.0)        # up2 = 2 leaves them alone
+
+
+SPLITK_CASES = [
+    # kind, N, H, Cin, Cout, R, pad   (stage-5 3x3 at a small batch, a long-K 1x1, odd widths)
+    ("fwd", 2, 7, 512, 512, 3, 1),
+    ("fwd", 3, 5, 1024, 256, 1, 0),
+    ("fwd", 1, 7, 256, 136, 3, 1),
+    ("dgrad", 2, 7, 512, 512, 3, 1),
+    ("dgrad", 2, 7, 256, 2048, 1, 0),
+]
+
+
+@pytest.mark.parametrize("ks", [0, 3, 8])
+@pytest.mark.parametrize("case", SPLITK_CASES)
+def test_igemm_splitk_matches_unsplit_and_fp32(case, ks):
+    """Split-K (K slices -> fp32 partial tiles in the workspace -> combine kernel running the
+    unchanged fused epilogue) against the unsplit kernel and the fp32 reference: forward with
+    BN affine + residual + ReLU + bitmask, dgrad with residual-gradient add + ReLU mask + fused
+    column sums.  ks 0 = the heuristic (these problems have 1-16 tiles: it splits them)."""
+    torch.manual_seed(31)
+    kind, n, h, cin, co, r, pad = case
+    M = n * h * h
+    nat = N()
+    results = []
+    for knob in (0, ks if ks else 1):
+        nat.set_variant("igemm_splitk", knob)
+        try:
+            if kind == "fwd":
+                K = r * r * cin
+                if knob:
+                    ws = torch.empty(nat.igemm_splitk_floats(M, co, K), device=dev)
+                    nat.splitk_use(ws)
+                    assert nat.igemm_plan(M, co, K)[2] > 1
+                if not results:
+                    x = rnd(n, h, h, cin)
+                    w = rnd(co, r, r, cin, scale=0.03)
+                    sc, sh = torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev)
+                    res = rnd(n, h, h, co)
+                out = torch.empty(n, h, h, co, dtype=torch.bfloat16, device=dev)
+                bits = torch.zeros(n, h, h, (co + 7) // 8, dtype=torch.uint8, device=dev)
+                nat.igemm(x, None, h, h, r, r, 1, pad, h, h, w.view(co, -1), 0, sc, sh, res, None, None, out, 1,
+                          None, 0, 0, 0, 0, 0, None, bits)
+                results.append((out.float(), bits.clone(), None))
+                ref = (conv_ref(x, w, 1, pad) * sc + sh + res.float()).relu()
+            else:
+                K = r * r * co
+                if knob:
+                    ws = torch.empty(nat.igemm_splitk_floats(M, cin, K), device=dev)
+                    nat.splitk_use(ws)
+                    assert nat.igemm_plan(M, cin, K)[2] > 1
+                if not results:
+                    g = rnd(n, h, h, co)
+                    w = rnd(co, r, r, cin, scale=0.03)
+                    a = torch.rand(co, device=dev) + 0.5
+                    add, mask = rnd(n, h, h, cin), rnd(n, h, h, cin)
+                    wt = dgrad_weights(w, a)
+                out = torch.empty(n, h, h, cin, dtype=torch.bfloat16, device=dev)
+                rows = nat.igemm_partial_rows(M, cin, K)
+                part = torch.full((rows * cin,), float("nan"), device=dev)
+                nat.igemm(g, None, h, h, r, r, 1, r - 1 - pad, h, h, wt.view(cin, -1), 1, None, None, None, mask, add,
+                          out, 0, None, 0, 0, 0, 0, 0, part, None)
+                results.append((out.float(), None, _fold(part, rows, cin)))
+                gs = (g.float() * a).permute(0, 3, 1, 2)
+                ref = torch.nn.grad.conv2d_input((n, cin, h, h), w.float().permute(0, 3, 1, 2), gs, stride=1,
+                                                 padding=pad)
+                ref = (ref.permute(0, 2, 3, 1) + add.float()) * (mask.float() > 0)
+        finally:
+            nat.set_variant("igemm_splitk", 1)
+            nat.splitk_use(None)
+    (o0, b0, c0), (o1, b1, c1) = results
+    assert rel(o1, ref) < 1e-2 and rel(o0, ref) < 1e-2
+    assert rel(o1, o0) < 5e-3                       # same math, fp32 partial sums in another order
+    if b0 is not None:
+        assert (b0 != b1).float().mean().item() < 1e-3   # ReLU bits agree except at exact-zero ties
+    if c0 is not None:
+        assert rel(c1, c0) < 1e-3
+
+
+def test_igemm_splitk_dense_head_f32():
+    """The fp32 Dense head at a small batch (M = batch rows, 8 tiles of 1000 columns, K = 2048)
+    is split by the heuristic; the combine runs the fp32 epilogue."""
+    torch.manual_seed(5)
+    nat = N()
+    a = rnd(32, 2048)
+    wd = rnd(1000, 2048, scale=0.02)
+    bias = torch.randn(1000, device=dev)
+    ones = torch.ones(1000, device=dev)
+    assert nat.igemm_plan(32, 1000, 2048)[2] > 1
+    ws = torch.empty(nat.igemm_splitk_floats(32, 1000, 2048), device=dev)
+    nat.splitk_use(ws)
+    out = torch.empty(32, 1000, device=dev)
+    try:
+        nat.igemm(a.view(32, 1, 1, 2048), None, 1, 1, 1, 1, 1, 0, 1, 1, wd, 2, ones, bias, None, None, None, out, 0,
+                  None, 0, 0, 0, 0, 0, None, None)
+    finally:
+        nat.splitk_use(None)
+    ref = a.float() @ wd.float().t() + bias
+    assert rel(out, ref) < 1e-3
