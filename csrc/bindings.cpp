@@ -257,6 +257,109 @@ void conv_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tenso
   ok(pddl::conv_f32_launch(p, cur_stream()), "conv_f32");
 }
 
+// conv_f32 with a fused epilogue (the fp32 engine): epi 1 = FWD (scale/shift [+res] [relu]),
+// epi 2 = DGRAD ([+add] * (mask > 0), up2 grid scatter into y of [N, Hf, Wf, Cout], partial
+// column sums [ceil(M/64)][Cout]).  x / y NHWC fp32; w [Cout][K] rows with row stride K.
+void conv_f32_epi(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Ho, int64_t Wo, Tensor w,
+                  int64_t epi, OptT scale, OptT shift, OptT res, int64_t relu, OptT add, OptT mask, int64_t up2,
+                  Tensor y, OptT colsum) {
+  pddl::ConvF32Params p{};
+  PCHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 4,
+         "conv_f32_epi: contiguous fp32 NHWC x");
+  PCHECK(w.is_contiguous() && w.dim() == 2 && y.is_contiguous() && y.dim() == 4, "conv_f32_epi: w [Cout][K], NHWC y");
+  p.x = f32p(x); p.N = (int)x.size(0); p.H = (int)x.size(1); p.W = (int)x.size(2); p.C = (int)x.size(3);
+  p.R = (int)R; p.S = (int)S; p.stride = (int)stride; p.pad = (int)pad;
+  p.Ho = (int)Ho; p.Wo = (int)Wo; p.M = p.N * p.Ho * p.Wo;
+  PCHECK(p.Ho == (p.H + 2 * p.pad - p.R) / p.stride + 1 && p.Wo == (p.W + 2 * p.pad - p.S) / p.stride + 1,
+         "conv_f32_epi: output size");
+  p.w = f32p(w); p.Cout = (int)w.size(0); p.K = (int)w.size(1);
+  PCHECK(p.K == p.R * p.S * p.C, "conv_f32_epi: K must be R*S*C");
+  PCHECK(y.size(0) == p.N && y.size(3) == p.Cout, "conv_f32_epi: output batch / channels");
+  if (up2) {
+    PCHECK(epi == pddl::F32_EPI_DGRAD, "conv_f32_epi: up2 is a dgrad scatter");
+    p.Hf = (int)y.size(1); p.Wf = (int)y.size(2);
+  } else {
+    PCHECK(y.size(1) == p.Ho && y.size(2) == p.Wo, "conv_f32_epi: output shape");
+  }
+  const int64_t out_el = y.numel();
+  auto same = [&](const OptT& t, const char* what) {
+    PCHECK(!t.has_value() || (t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous() &&
+                              t->numel() == out_el), what);
+  };
+  same(res, "conv_f32_epi: res must match y");
+  if (up2) {
+    PCHECK(!add.has_value() || (add->is_contiguous() && add->scalar_type() == torch::kFloat32 &&
+                                add->numel() == (int64_t)p.M * p.Cout),
+           "conv_f32_epi: with up2, add is the compact [N, Ho, Wo, Cout] tensor");
+  } else {
+    same(add, "conv_f32_epi: add must match y");
+  }
+  same(mask, "conv_f32_epi: mask must match y");
+  p.epi = (int)epi;
+  if (epi == pddl::F32_EPI_FWD) {
+    PCHECK(scale.has_value() && shift.has_value() && scale->numel() >= p.Cout && shift->numel() >= p.Cout,
+           "conv_f32_epi: forward scale / shift");
+  }
+  p.scale = of32p(scale); p.shift = of32p(shift);
+  p.res = of32p(res); p.relu = (int)relu;
+  p.add = of32p(add); p.mask = of32p(mask); p.up2 = (int)up2;
+  if (colsum.has_value()) {
+    PCHECK(epi == pddl::F32_EPI_DGRAD && colsum->numel() >= (int64_t)((p.M + 63) / 64) * p.Cout,
+           "conv_f32_epi: colsum partial rows [ceil(M/64)][Cout] of a dgrad");
+    p.colsum = f32p(*colsum);
+  }
+  p.y = f32p(y);
+  ok(pddl::conv_f32_launch(p, cur_stream()), "conv_f32_epi");
+}
+
+void maxpool_fwd_f32(Tensor x, Tensor y, Tensor idx) {
+  PCHECK(x.dim() == 4 && y.dim() == 4 && x.is_contiguous() && y.is_contiguous() && idx.numel() == y.numel() &&
+             idx.scalar_type() == torch::kUInt8, "maxpool_fwd_f32 shapes");
+  ok(pddl::maxpool_fwd_f32_launch(f32p(x), f32p(y), idx.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1),
+                                  (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), cur_stream()),
+     "maxpool_fwd_f32");
+}
+void maxpool_bwd_f32(Tensor gy, Tensor idx, Tensor xmask, Tensor gx) {
+  PCHECK(gx.dim() == 4 && gy.dim() == 4 && gx.is_contiguous() && gy.is_contiguous() && xmask.numel() == gx.numel() &&
+             idx.numel() == gy.numel(), "maxpool_bwd_f32 shapes");
+  ok(pddl::maxpool_bwd_f32_launch(f32p(gy), idx.data_ptr<uint8_t>(), f32p(xmask), f32p(gx), (int)gx.size(0),
+                                  (int)gx.size(1), (int)gx.size(2), (int)gx.size(3), (int)gy.size(1), (int)gy.size(2),
+                                  cur_stream()),
+     "maxpool_bwd_f32");
+}
+void gap_fwd_f32(Tensor x, Tensor y) {
+  PCHECK(x.dim() == 4 && x.is_contiguous() && y.numel() == x.size(0) * x.size(3), "gap_fwd_f32 shapes");
+  ok(pddl::gap_fwd_f32_launch(f32p(x), f32p(y), (int)x.size(0), (int)(x.size(1) * x.size(2)), (int)x.size(3),
+                              cur_stream()), "gap_fwd_f32");
+}
+void gap_bwd_f32(Tensor gp, Tensor ymask, Tensor g, OptT colsum_rows) {
+  PCHECK(g.dim() == 4 && g.is_contiguous() && ymask.numel() == g.numel() && gp.numel() == g.size(0) * g.size(3),
+         "gap_bwd_f32 shapes");
+  if (colsum_rows.has_value()) PCHECK(colsum_rows->numel() >= gp.numel(), "gap_bwd_f32 colsum rows [B][C]");
+  ok(pddl::gap_bwd_f32_launch(f32p(gp), f32p(ymask), f32p(g), (int)g.size(0), (int)(g.size(1) * g.size(2)),
+                              (int)g.size(3), colsum_rows.has_value() ? f32p(*colsum_rows) : nullptr, cur_stream()),
+     "gap_bwd_f32");
+}
+void colsum_f32(Tensor g, int64_t C, Tensor out) {
+  PCHECK(g.is_contiguous() && out.numel() >= C, "colsum_f32 shapes");
+  ok(pddl::colsum_f32_launch(f32p(g), g.numel() / ld(g), (int)C, ld(g), f32p(out), cur_stream()), "colsum_f32");
+}
+void softmax_xent_f32(Tensor logits, Tensor labels, int64_t ncls, double gscale, Tensor dlogits, Tensor loss_sum,
+                      Tensor correct) {
+  PCHECK(labels.scalar_type() == torch::kInt64 && labels.is_cuda(), "labels int64 GPU");
+  ok(pddl::softmax_xent_f32_launch(f32p(logits), ld(logits), labels.data_ptr<int64_t>(), (int)logits.size(0),
+                                   (int)ncls, (float)gscale, f32p(dlogits), ld(dlogits), f32p(loss_sum),
+                                   f32p(correct), cur_stream()),
+     "softmax_xent_f32");
+}
+void prep_f32(Tensor params, Tensor table, int64_t nlayers, Tensor wf32, Tensor scale, Tensor shift, double eps) {
+  PCHECK(table.is_cuda() && table.scalar_type() == torch::kUInt8, "prep table");
+  PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::PrepLayer), "prep table size");
+  ok(pddl::prep_f32_launch(f32p(params), reinterpret_cast<const pddl::PrepLayer*>(table.data_ptr()), (int)nlayers,
+                           f32p(wf32), f32p(scale), f32p(shift), (float)eps, cur_stream()),
+     "prep_f32");
+}
+
 // dw[Cout, R*S*C] += sum_m dy[m, Cout] * im2col(x)[m, :]
 void wgrad_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tensor dy, Tensor dw) {
   pddl::ConvF32Params p{};
@@ -295,6 +398,10 @@ void stem_s2d(Tensor in, OptT flip, int64_t mode, int64_t Hc, int64_t Wc, int64_
   p.scale = 1.f / 255.f;
   p.Hs = (int)((Hc + 6) / 2); p.Ws = (int)((Wc + 6) / 2);
   PCHECK(out.is_contiguous() && out.numel() >= (int64_t)p.B * p.Hs * p.Ws * 16, "stem s2d output too small");
+  if (out.scalar_type() == torch::kFloat32) {   // the fp32 engine's stem image
+    ok(pddl::stem_s2d_f32_launch(p, f32p(out), cur_stream()), "stem_s2d_f32");
+    return;
+  }
   p.out = bfpm(out);
   ok(pddl::stem_s2d_launch(p, cur_stream()), "stem_s2d");
 }
@@ -441,6 +548,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("BNSTAT_LAYER_BYTES") = (int)sizeof(pddl::BnStatLayer);
   m.def("wgrad", &wgrad, REL);
   m.def("conv_f32", &conv_f32, REL);
+  m.def("conv_f32_epi", &conv_f32_epi, REL);
+  m.def("maxpool_fwd_f32", &maxpool_fwd_f32, REL);
+  m.def("maxpool_bwd_f32", &maxpool_bwd_f32, REL);
+  m.def("gap_fwd_f32", &gap_fwd_f32, REL);
+  m.def("gap_bwd_f32", &gap_bwd_f32, REL);
+  m.def("colsum_f32", &colsum_f32, REL);
+  m.def("softmax_xent_f32", &softmax_xent_f32, REL);
+  m.def("prep_f32", &prep_f32, REL);
   m.def("wgrad_f32", &wgrad_f32, REL);
   m.def("stem_s2d", &stem_s2d, REL);
   m.def("stem_wgrad_fold", &stem_wgrad_fold, REL);

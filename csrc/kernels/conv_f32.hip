@@ -2,8 +2,10 @@
 // precision (imagenet-resnet50.py:56-62 builds and trains the Keras model in float32 with no
 // mixed-precision policy).  NHWC activations, OHWI weights, fp32 accumulate AND fp32 operands.
 //
-//   conv_f32_kernel:   y[m][n] = sum_k im2col(x)[m][k] * w[n][k] (+ bias[n])   (forward, and the
-//                      data gradient as a forward conv of dy with flipped/transposed weights)
+//   conv_f32_kernel:   y[m][n] = epi(sum_k im2col(x)[m][k] * w[n][k])   (forward, and the data
+//                      gradient as a forward conv of dy with flipped/transposed weights), with
+//                      the fused epilogues of ConvF32Params (frozen BN + bias + residual + ReLU;
+//                      residual-gradient add + ReLU mask + stride-2 scatter + column sums)
 //   wgrad_f32_kernel:  dw[n][k] += sum_m dy[m][n] * im2col(x)[m][k]           (weight gradient,
 //                      m split over workgroups, fp32 atomics into dw)
 //
@@ -135,19 +137,107 @@ __global__ void __launch_bounds__(256) conv_f32_kernel(ConvF32Params p) {
     }
     __syncthreads();
   }
-  // D fragment: lane holds rows 4g .. 4g+3 of column lane % 16
+  // Epilogue: D fragments (lane: rows 4g .. 4g+3 of column lane % 16) -> LDS tile -> each
+  // thread owns one 4-column group and 4 rows: 16-byte loads of the epilogue operands and
+  // 16-byte stores; per-m-tile partial column sums folded through the same LDS tile.
+  __shared__ __attribute__((aligned(16))) float Cs[F_BM * (F_BN + 4)];
+  constexpr int CLD = F_BN + 4;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 32 + j * 16 + fr;
-    if (col >= p.Cout) continue;
-    const float b = p.bias ? p.bias[col] : 0.f;
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Cs[(wm * 32 + i * 16 + 4 * g + e) * CLD + wn * 32 + j * 16 + fr] = acc[i][j][e];
+  __syncthreads();
+  const int c4 = (tid & 15) * 4, col = n0 + c4;
+  const bool vec = col + 3 < p.Cout;                 // (a ragged last column group: scalar path)
+  float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (col + e < p.Cout) {
+      if (p.epi == F32_EPI_FWD) { sc[e] = p.scale[col + e]; sh[e] = p.shift[col + e]; }
+      else if (p.epi == F32_EPI_PLAIN && p.bias) sh[e] = p.bias[col + e];
+    }
+  }
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int rl = (tid >> 4) + 16 * it, row = m0 + rl;
+    if (row >= p.M || col >= p.Cout) continue;
+    const float4 q = *reinterpret_cast<const float4*>(&Cs[rl * CLD + c4]);
+    float v[4] = {q.x, q.y, q.z, q.w};
+    long orow = row;
+    if (p.epi == F32_EPI_DGRAD && p.up2) {
+      const int nn = fdiv(row, p.mg_howo), rem = row - nn * p.Ho * p.Wo, ii = fdiv(rem, p.mg_wo), jj = rem - ii * p.Wo;
+      orow = ((long)nn * p.Hf + 2 * ii) * p.Wf + 2 * jj;
+    }
+    const long o = orow * p.Cout + col;
+    const long oa = p.up2 ? (long)row * p.Cout + col : o;   // (up2: `add` is indexed by the GEMM row)
+    if (vec) {
+      if (p.epi == F32_EPI_FWD) {
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.res) r = *reinterpret_cast<const float4*>(p.res + o);
+        const float rv[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = v[e] * sc[e] + sh[e] + rv[e];
+          if (p.relu) v[e] = fmaxf(v[e], 0.f);
+        }
+      } else if (p.epi == F32_EPI_DGRAD) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), mk = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (p.add) a = *reinterpret_cast<const float4*>(p.add + oa);
+        if (p.mask) mk = *reinterpret_cast<const float4*>(p.mask + o);
+        const float av[4] = {a.x, a.y, a.z, a.w}, mv[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = mv[e] > 0.f ? v[e] + av[e] : 0.f;
+          cs[e] += v[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += sh[e];
+      }
+      *reinterpret_cast<float4*>(p.y + o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wm * 32 + i * 16 + 4 * g + e;
-        if (row < p.M) p.y[(long)row * p.Cout + col] = acc[i][j][e] + b;
+        if (col + e >= p.Cout) break;
+        float x = v[e];
+        if (p.epi == F32_EPI_FWD) {
+          x = x * sc[e] + sh[e] + (p.res ? p.res[o + e] : 0.f);
+          if (p.relu) x = fmaxf(x, 0.f);
+        } else if (p.epi == F32_EPI_DGRAD) {
+          x = (!p.mask || p.mask[o + e] > 0.f) ? x + (p.add ? p.add[oa + e] : 0.f) : 0.f;
+          cs[e] += x;
+        } else {
+          x += sh[e];
+        }
+        p.y[o + e] = x;
       }
+    }
+  }
+  if (p.epi == F32_EPI_DGRAD && p.colsum) {
+    // fold the 16 row groups of each 4-column group: lanes l, l+16, l+32, l+48 of a wave, then
+    // the 4 waves through LDS; one plain-store partial row per m-tile (colsum_reduce folds them)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      cs[e] += __shfl_xor(cs[e], 16, 64);
+      cs[e] += __shfl_xor(cs[e], 32, 64);
+    }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Cs[wave * CLD + c4 + e] = cs[e];
+    }
+    __syncthreads();
+    if (tid < 16) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = Cs[c4 + e] + Cs[CLD + c4 + e] + Cs[2 * CLD + c4 + e] + Cs[3 * CLD + c4 + e];
+        if (col + e < p.Cout) p.colsum[(long)tm * p.Cout + col + e] = t;
+      }
+    }
   }
 }
 
@@ -172,7 +262,12 @@ __global__ void __launch_bounds__(256) wgrad_f32_kernel(ConvF32Params p, int m_p
     const int mm = mb + lm;
     const bool ok = mm < mend;
     gv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok && gcol < p.Cout) gv = *reinterpret_cast<const float4*>(p.y + (long)mm * p.Cout + gcol);
+    if (ok && gcol + 3 < p.Cout) {
+      gv = *reinterpret_cast<const float4*>(p.y + (long)mm * p.Cout + gcol);
+    } else if (ok && gcol < p.Cout) {   // ragged last column group (Dense head, classes % 4 != 0)
+      const float* r = p.y + (long)mm * p.Cout + gcol;
+      gv = make_float4(r[0], gcol + 1 < p.Cout ? r[1] : 0.f, gcol + 2 < p.Cout ? r[2] : 0.f, 0.f);
+    }
     int n = 0, hi0 = 0, wi0 = 0;
     if (ok) {
       n = fdiv(mm, p.mg_howo);
@@ -237,6 +332,10 @@ __global__ void __launch_bounds__(256) wgrad_f32_kernel(ConvF32Params p, int m_p
 
 static const char* check_f32(const ConvF32Params& p) {
   if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "conv_f32: empty problem";
+  if (p.epi == F32_EPI_FWD && (!p.scale || !p.shift)) return "conv_f32: forward epilogue needs scale and shift";
+  if (p.epi == F32_EPI_DGRAD && p.up2 && (p.Hf < 2 * p.Ho - 1 || p.Wf < 2 * p.Wo - 1))
+    return "conv_f32: up2 grid smaller than the scattered rows";
+  if (p.epi != F32_EPI_PLAIN && p.epi != F32_EPI_FWD && p.epi != F32_EPI_DGRAD) return "conv_f32: unknown epilogue";
   if (p.K != p.R * p.S * p.C) return "conv_f32: K must be R*S*C";
   if ((long)p.N * p.H * p.W * p.C >= (1L << 31) || (long)p.M * p.Cout >= (1L << 31))
     return "conv_f32: tensor too large for 32-bit row indexing";
@@ -256,7 +355,6 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
 
 const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (const char* e = check_f32(p)) return e;
-  if (p.Cout % 4) return "wgrad_f32: Cout must be a multiple of 4";
   p.mg_howo = fdiv_magic(p.Ho * p.Wo);
   p.mg_wo = fdiv_magic(p.Wo);
   const int ntiles = ((p.Cout + F_BM - 1) / F_BM) * ((p.K + F_BN - 1) / F_BN);

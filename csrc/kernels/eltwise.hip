@@ -64,6 +64,35 @@ __global__ void stem_s2d_kernel(StemParams p, int npix, uint64_t mg_ws, uint64_t
   }
 }
 
+// fp32 form (the reference-precision engine): same values, 16 fp32 channels per s2d pixel.
+__global__ void stem_s2d_f32_kernel(StemParams p, float* __restrict__ out, int npix, uint64_t mg_ws, uint64_t mg_hs) {
+  if (p.crop_dev) { p.oy = p.crop_dev[0]; p.ox = p.crop_dev[1]; }
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < npix; q += gridDim.x * blockDim.x) {
+    const int t = fdiv(q, mg_ws);
+    const int j = q - t * p.Ws;
+    const int b = fdiv(t, mg_hs);
+    const int i = t - b * p.Hs;
+    float4* o = reinterpret_cast<float4*>(out + (long)q * 16);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int y = 2 * i + (d >> 1) - 3, x = 2 * j + (d & 1) - 3;
+      const bool in = y >= 0 && y < p.Hc && x >= 0 && x < p.Wc;
+      o[d] = make_float4(in ? stem_pix(p, b, y, x, 0) : 0.f, in ? stem_pix(p, b, y, x, 1) : 0.f,
+                         in ? stem_pix(p, b, y, x, 2) : 0.f, 0.f);
+    }
+  }
+}
+const char* stem_s2d_f32_launch(const StemParams& p, float* out, hipStream_t s) {
+  if ((p.Hc + 6) != 2 * p.Hs || (p.Wc + 6) != 2 * p.Ws) return "stem_s2d_f32: Hs must be (Hc + 6) / 2 (even crop)";
+  const long npix = (long)p.B * p.Hs * p.Ws;
+  if (npix >= (1L << 31) - (1L << 24)) return "stem_s2d_f32: too many pixels for 32-bit indexing";
+  const int grid = (int)lmin((npix + 255) / 256, 16384);
+  hipLaunchKernelGGL(stem_s2d_f32_kernel, dim3(grid), dim3(256), 0, s, p, out, (int)npix, fdiv_magic(p.Ws),
+                     fdiv_magic(p.Hs));
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
 // Row form for uint8 identity / crop input (modes 0 and 2, the training path): one block per
 // s2d row (b, i) stages the two preprocessed source rows 2i-3, 2i-2 through LDS with
 // coalesced 4-byte loads (the per-pixel form issues 12 scattered byte loads per thread and
@@ -914,7 +943,15 @@ const char* softmax_xent_launch(const float* logits, int ldl, const int64_t* lab
 // After each optimizer step: fp32 master -> bf16 forward weights [cout][kpad] (zero padded),
 // bf16 dgrad weights W'[c][R-1-r][S-1-s][co] = a[co] * W[co][r][s][c], and the folded
 // frozen-BN affine a = gamma / sqrt(var + eps), b = (bias - mean) * a + beta.
-__global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __restrict__ L, uint16_t* __restrict__ wbf,
+// (T = uint16_t: bf16 weights of the bf16 engine; T = float: the fp32 engine, whose forward
+// convs read the fp32 master directly -- only the stem's space-to-depth copy and the dgrad
+// weights are prepared)
+template <typename T> __device__ __forceinline__ T wcvt(float v);
+template <> __device__ __forceinline__ uint16_t wcvt<uint16_t>(float v) { return f2bf(v); }
+template <> __device__ __forceinline__ float wcvt<float>(float v) { return v; }
+
+template <typename T>
+__global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __restrict__ L, T* __restrict__ wbf,
                             float* __restrict__ scale, float* __restrict__ shift, float eps) {
   const PrepLayer l = L[blockIdx.y];
   const int RSC = l.R * l.S * l.cin;
@@ -933,7 +970,7 @@ __global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __re
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nf; e += gridDim.x * blockDim.x) {
       const int co = e / RSC, k = e - co * RSC;
       const int r = k / (l.S * l.cin), rm = k - r * l.S * l.cin, s = rm / l.cin, c = rm - s * l.cin;
-      wbf[l.wf_off + (long)co * l.kpad + s2d_col(r, s, c)] = f2bf(prm[l.w_off + e]);
+      wbf[l.wf_off + (long)co * l.kpad + s2d_col(r, s, c)] = wcvt<T>(prm[l.w_off + e]);
       if (k == 0) {
         float a, b;
         fold(co, &a, &b);
@@ -944,15 +981,17 @@ __global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __re
     return;
   }
   // every non-stem layer has kpad == R*S*cin: the forward copy is a flat fp32 -> bf16 cast
-  const long nf = (long)l.cout * RSC;
-  const long n4 = nf / 4;
-  const float4* src = reinterpret_cast<const float4*>(prm + l.w_off);
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
-    const float4 w = src[e];
-    uint2 o;
-    o.x = pack2(w.x, w.y);
-    o.y = pack2(w.z, w.w);
-    *reinterpret_cast<uint2*>(wbf + l.wf_off + e * 4) = o;
+  if constexpr (sizeof(T) == 2) {
+    const long nf = (long)l.cout * RSC;
+    const long n4 = nf / 4;
+    const float4* src = reinterpret_cast<const float4*>(prm + l.w_off);
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n4; e += (long)gridDim.x * blockDim.x) {
+      const float4 w = src[e];
+      uint2 o;
+      o.x = pack2(w.x, w.y);
+      o.y = pack2(w.z, w.w);
+      *reinterpret_cast<uint2*>(wbf + l.wf_off + e * 4) = o;
+    }
   }
   for (int co = blockIdx.x * blockDim.x + threadIdx.x; co < l.cout; co += gridDim.x * blockDim.x) {
     float a, b;
@@ -964,8 +1003,9 @@ __global__ void prep_kernel(const float* __restrict__ prm, const PrepLayer* __re
 
 // dgrad weights W'[c][R-1-r][S-1-s][co] = a[co] * W[co][r][s][c]: per (layer, tap) a batch of
 // [cout][cin] -> [cin][cout] transposes through a 64x64 LDS tile (coalesced both ways).
+template <typename T>
 __global__ void prep_dgrad_kernel(const float* __restrict__ prm, const PrepLayer* __restrict__ L,
-                                  uint16_t* __restrict__ wbf, float eps) {
+                                  T* __restrict__ wbf, float eps) {
   __shared__ float tile[64][65];
   const PrepLayer l = L[blockIdx.y];
   if (l.wd_off < 0 || l.mode != 0) return;
@@ -996,7 +1036,7 @@ __global__ void prep_dgrad_kernel(const float* __restrict__ prm, const PrepLayer
       const int c = c0 + i;
       if (c < l.cin && co < l.cout) {
         const long d = (((long)c * l.R + (l.R - 1 - r)) * l.S + (l.S - 1 - s)) * l.cout_pad + co;
-        wbf[l.wd_off + d] = f2bf(a * tile[j][i]);
+        wbf[l.wd_off + d] = wcvt<T>(a * tile[j][i]);
       }
     }
     __syncthreads();
@@ -1007,8 +1047,16 @@ const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nl
                         float* scale, float* shift, float eps, hipStream_t s) {
   int gx = (max_elems / 4 + 255) / 256;
   if (gx > 512) gx = 512;
-  hipLaunchKernelGGL(prep_kernel, dim3(gx, nlayers), dim3(256), 0, s, params, layers_dev, wbf, scale, shift, eps);
-  hipLaunchKernelGGL(prep_dgrad_kernel, dim3(576, nlayers), dim3(256), 0, s, params, layers_dev, wbf, eps);
+  hipLaunchKernelGGL(prep_kernel<uint16_t>, dim3(gx, nlayers), dim3(256), 0, s, params, layers_dev, wbf, scale, shift,
+                     eps);
+  hipLaunchKernelGGL(prep_dgrad_kernel<uint16_t>, dim3(576, nlayers), dim3(256), 0, s, params, layers_dev, wbf, eps);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+const char* prep_f32_launch(const float* params, const PrepLayer* layers_dev, int nlayers, float* wf32, float* scale,
+                            float* shift, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(prep_kernel<float>, dim3(64, nlayers), dim3(256), 0, s, params, layers_dev, wf32, scale, shift, eps);
+  hipLaunchKernelGGL(prep_dgrad_kernel<float>, dim3(576, nlayers), dim3(256), 0, s, params, layers_dev, wf32, eps);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -76,9 +76,33 @@ struct ConvF32Params {
   float* y;                            // forward: output [M][Cout]; wgrad: the output gradient (read)
   float* dw;                           // wgrad: [Cout][K], accumulated with atomics
   uint64_t mg_howo, mg_wo;             // (set by the launchers)
+  // fused epilogue of conv_f32 (the fp32 engine, models/engine_f32.py), staged through LDS into
+  // 16-byte row stores:
+  //   F32_EPI_PLAIN: y = acc (+ bias)
+  //   F32_EPI_FWD:   y = act(acc * scale[n] + shift[n] (+ res))          (frozen BN + bias folded)
+  //   F32_EPI_DGRAD: y = (acc (+ add)) * (mask > 0), optional stride-2 grid scatter (up2: GEMM
+  //                  row (n, i, j) -> output row (n, 2i, 2j) of an Hf x Wf grid; the caller's
+  //                  buffer holds zeros off the grid; `add` is then indexed by the GEMM row,
+  //                  `mask` by the output row), and per-m-tile partial column sums
+  int epi;
+  const float* scale; const float* shift; const float* res; int relu;
+  const float* add; const float* mask; int up2, Hf, Wf;
+  float* colsum;                       // [ceil(M / 64)][Cout] partial column sums (DGRAD, optional)
 };
+enum { F32_EPI_PLAIN = 0, F32_EPI_FWD = 1, F32_EPI_DGRAD = 2 };
 const char* conv_f32_launch(ConvF32Params p, hipStream_t stream);
 const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream);
+// fp32 elementwise kernels of the fp32 engine (f32.hip)
+const char* maxpool_fwd_f32_launch(const float* x, float* y, uint8_t* idx, int B, int H, int W, int C, int Ho, int Wo,
+                                   hipStream_t s);
+const char* maxpool_bwd_f32_launch(const float* gy, const uint8_t* idx, const float* xmask, float* gx, int B, int H,
+                                   int W, int C, int Ho, int Wo, hipStream_t s);
+const char* gap_fwd_f32_launch(const float* x, float* y, int B, int HW, int C, hipStream_t s);
+const char* gap_bwd_f32_launch(const float* gp, const float* ymask, float* g, int B, int HW, int C, float* colsum_rows,
+                               hipStream_t s);
+const char* colsum_f32_launch(const float* g, long M, int C, int ldg, float* out, hipStream_t s);
+const char* softmax_xent_f32_launch(const float* logits, int ldl, const int64_t* labels, int B, int ncls, float gscale,
+                                    float* dlogits, int ldd, float* loss_sum, float* correct, hipStream_t s);
 
 // ---- elementwise / reduction kernels (eltwise.hip) ----
 struct StemParams {
@@ -96,6 +120,7 @@ struct StemParams {
 // is the padded preprocessed pixel (2i+dy-3, 2j+dx-3, c) (c = 3 is zero).  The 7x7/s2 stem
 // conv then becomes a 4x4/s1 "window" implicit GEMM with K = 4*4*16 = 256.
 const char* stem_s2d_launch(const StemParams& p, hipStream_t s);
+const char* stem_s2d_f32_launch(const StemParams& p, float* out, hipStream_t s);   // fp32 image (out ignored)
 // Fold the s2d-domain stem weight gradient [64][256] back to [64][7][7][3] (added into dw).
 const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStream_t s);
 
@@ -129,6 +154,8 @@ struct PrepLayer {
   int ch_off;         // offset of this layer's folded scale/shift (per output channel)
   int mode;           // 0: dense [cout][kpad] rows; 1: stem in the 4x4x16 space-to-depth layout
 };
+const char* prep_f32_launch(const float* params, const PrepLayer* layers_dev, int nlayers, float* wf32, float* scale,
+                            float* shift, float eps, hipStream_t s);   // fp32 stem s2d + dgrad weights
 const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems,
                         uint16_t* wbf, float* scale, float* shift, float eps, hipStream_t s);
 

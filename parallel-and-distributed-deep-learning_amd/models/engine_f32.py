@@ -1,22 +1,34 @@
-"""Reference-precision (fp32) GPU engine: every convolution and the Dense layer run on the
-hand-written fp32-MFMA kernels (ops/conv_f32.py -> csrc/kernels/conv_f32.hip); the elementwise
-rest of the graph (frozen / batch-statistics BN, ReLU, residual add, max-pool, GAP, softmax
-cross-entropy) runs as PyTorch's native GPU kernels with MIOpen switched off, so no library
-convolution is involved anywhere in the step.
+"""Reference-precision (fp32) GPU engines (`--precision fp32`; the reference trains in float32
+with no mixed-precision policy, imagenet-resnet50.py:56-62).
 
-The graph is models/reference.py's (the Keras model of imagenet-resnet50.py:51-61) with its
-convolutions swapped for `conv2d_f32`; activations live channels_last (NHWC in memory), the
-layout the kernels read.  Selected by `--precision fp32` on a GPU (parallel/strategies.py);
-the bf16 engine (models/engine.py) is the throughput path.
+HipF32Engine (frozen BN, the reference's `training=False`, Q3): the bf16 engine's explicit
+schedule (models/engine.py) in fp32 end to end -- no autograd, no PyTorch kernel in the step:
+  forward  : stem_s2d (fp32 space-to-depth image) -> conv_f32 (4x4 window stem) -> maxpool_f32
+             -> 16 bottleneck blocks of conv_f32 launches whose epilogues fold frozen BN + bias
+             + residual + ReLU -> gap_f32 -> conv_f32 (Dense, bias epilogue)
+  backward : softmax_xent_f32 -> per layer wgrad_f32 (raw dW, fp32 atomics) + a conv_f32 dgrad
+             whose epilogue adds the residual gradient, applies the ReLU mask of the layer
+             below, scatters the stride-2 grid and writes per-m-tile column sums; the
+             projection block's two dgrad sources are two launches (the second adds the
+             first); then the bf16 engine's wgrad_finalize / colsum_reduce / bn_grad kernels
+             (dW *= BN scale, dgamma / dbeta / dbias).
+HipF32AutogradEngine: the PyTorch-autograd form over the fp32 conv op (ops/conv_f32.py), for
+--bn-mode train in fp32.
 """
 from __future__ import annotations
+
+import struct
+from typing import Callable, Dict, Optional
 
 import torch
 import torch.nn.functional as F
 
 from ..ops.conv_f32 import conv2d_f32
+from ..ops.native import require_native
+from ..utils import profiling as prof
+from .engine import _BNG_FMT, _CRED_FMT, _FIN_FMT, _PREP_FMT, STEM_K
 from .reference import ReferenceResNet50, TorchEngine, preprocess
-from .resnet50 import ParamLayout
+from .resnet50 import BN_EPS, ParamLayout
 
 
 class HipF32ResNet50(ReferenceResNet50):
@@ -55,9 +67,10 @@ class HipF32ResNet50(ReferenceResNet50):
         return out.reshape(f.shape[0], -1)
 
 
-class HipF32Engine(TorchEngine):
+class HipF32AutogradEngine(TorchEngine):
     """TorchEngine interface (flat fp32 params / grads, forward_backward, evaluate) over
-    HipF32ResNet50 on the GPU."""
+    HipF32ResNet50 on the GPU: the autograd form, kept for --bn-mode train in fp32 (batch
+    statistics); the frozen-BN reference configuration runs HipF32Engine below."""
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, device="cuda", bn_mode="frozen",
                  num_classes: int = 1000):
@@ -77,3 +90,368 @@ class HipF32Engine(TorchEngine):
             lab = labels.to(self.device)
             loss_sum = F.cross_entropy(logits, lab, reduction="sum")
             return torch.stack([loss_sum, (logits.argmax(1) == lab).sum().float()])
+
+
+EPI_PLAIN, EPI_FWD, EPI_DGRAD = 0, 1, 2
+
+
+def _rows64(m: int) -> int:
+    return (m + 63) // 64
+
+
+class HipF32Engine:
+    """Explicit-schedule fp32 engine (frozen BN).  Interface of HipEngine / TorchEngine: flat
+    fp32 `params` / `grads`, `init`, `after_update`, `forward_backward`, `evaluate`."""
+    BN_MODES = ("frozen",)
+
+    def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: Optional[int] = None,
+                 device="cuda", bn_mode: str = "frozen", num_classes: int = 1000):
+        if bn_mode not in self.BN_MODES:
+            raise ValueError("HipF32Engine runs frozen BN (the reference's training=False); "
+                             "use HipF32AutogradEngine for bn_mode='train'")
+        self.N = require_native()
+        self.L = L = layout
+        self.device = dev = torch.device(device)
+        self.batch, self.crop = batch, crop
+        self.image_size = image_size if image_size is not None else crop
+        self.num_classes = num_classes
+        self.bn_mode = bn_mode
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.params = torch.zeros(L.total, **f32)
+        # per-channel bookkeeping, identical to the bf16 engine's (shared finalize / bn_grad kernels)
+        self.ch: Dict[str, int] = {}
+        off = 0
+        for c in L.convs:
+            self.ch[c.name] = off
+            off += c.cout
+        self.ch["dense"] = off
+        off += (num_classes + 7) // 8 * 8
+        self.nch = (off + 63) // 64 * 64
+        n_tr = L.n_trainable
+        nst = 64 * STEM_K
+        self.ws = torch.zeros(n_tr + 2 * self.nch + 64 + nst, **f32)   # zeroed every step
+        self.grads = self.ws[:n_tr]
+        self.colsum = self.ws[n_tr:n_tr + self.nch]
+        self.dgr = self.ws[n_tr + self.nch:n_tr + 2 * self.nch]
+        self.stats = self.ws[n_tr + 2 * self.nch:n_tr + 2 * self.nch + 2]
+        o = n_tr + 2 * self.nch + 64
+        self.stem_dw2 = self.ws[o:o + nst].view(64, STEM_K)
+        self.scale = torch.ones(self.nch, **f32)
+        self.shift = torch.zeros(self.nch, **f32)
+        self._tables()
+        self._alloc(batch)
+
+    # ------------------------------------------------------------------ tables
+    def _dev_table(self, rows):
+        return torch.frombuffer(bytearray(b"".join(rows)), dtype=torch.uint8).clone().to(self.device)
+
+    def _tables(self):
+        L = self.L
+        # fp32 prepared weights: the stem in the 4x4x16 space-to-depth layout, then every layer's
+        # dgrad weights [cin][R][S][cout] (flipped, transposed, scaled by the folded BN)
+        self.wd: Dict[str, int] = {}
+        off = 64 * STEM_K
+        for c in L.convs[1:]:
+            self.wd[c.name] = off
+            off += c.cin * c.k * c.k * c.cout
+        self.wd["dense"] = off
+        off += 2048 * self.num_classes
+        self.wf32 = torch.zeros(off, dtype=torch.float32, device=self.device)
+        rows = []
+        for c in L.convs:
+            stem = c is L.stem
+            g, b, m, v = L.off(c.bn, "gamma"), L.off(c.bn, "beta"), L.off(c.bn, "moving_mean"), \
+                L.off(c.bn, "moving_variance")
+            rows.append(struct.pack(_PREP_FMT, L.off(c.name, "kernel"), c.cout, c.k, c.k, c.cin,
+                                    STEM_K if stem else c.k * c.k * c.cin, 0, -1 if stem else self.wd[c.name],
+                                    c.cout, L.off(c.name, "bias"), g, b, m, v, self.ch[c.name], 1 if stem else 0))
+        rows.append(struct.pack(_PREP_FMT, L.off("dense", "kernel"), self.num_classes, 1, 1, 2048, 2048, 0,
+                                self.wd["dense"], self.num_classes, L.off("dense", "bias"), -1, -1, -1, -1,
+                                self.ch["dense"], 0))
+        self._prep_tab, self._prep_n = self._dev_table(rows), len(rows)
+        fin = {c.name: struct.pack(_FIN_FMT, L.off(c.name, "kernel"), c.cout, c.k * c.k * c.cin, self.ch[c.name],
+                                   self.ch[c.name]) for c in L.convs}
+        self._fin = {b.name: self._dev_table([fin[b.convs[k].name] for k in (["3", "2", "1", "0"] if b.proj
+                                                                              else ["3", "2", "1"])])
+                     for b in L.blocks}
+        self._fin["stem"] = self._dev_table([fin[L.stem.name]])
+        bg = []
+        for c in L.convs:
+            cs = self.ch[c.name]
+            for b in L.blocks:   # a projection block's conv0 BN sees conv3's output gradient
+                if b.proj and b.convs["0"].name == c.name:
+                    cs = self.ch[b.convs["3"].name]
+            bg.append(struct.pack(_BNG_FMT, c.cout, self.ch[c.name], L.off(c.name, "bias"), L.off(c.bn, "gamma"),
+                                  L.off(c.bn, "beta"), L.off(c.bn, "moving_mean"), L.off(c.bn, "moving_variance"),
+                                  cs, self.ch[c.name]))
+        bg.append(struct.pack(_BNG_FMT, self.num_classes, self.ch["dense"], L.off("dense", "bias"), -1, -1, -1, -1,
+                              self.ch["dense"], -1))
+        self._bng_tab, self._bng_n = self._dev_table(bg), len(bg)
+
+    def _w(self, name, rows, k):           # forward weights: the fp32 master itself ([cout][R*S*cin])
+        o = self.L.off(name, "kernel")
+        return self.params[o:o + rows * k].view(rows, k)
+
+    def _wd(self, name, cin, k):           # dgrad weights [cin][R*S*cout]
+        o = self.wd[name]
+        return self.wf32[o:o + cin * k].view(cin, k)
+
+    def _gv(self, name, rows, k):
+        o = self.L.off(name, "kernel")
+        return self.grads[o:o + rows * k].view(rows, k)
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self, B):
+        L, dev = self.L, self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        crop = self.crop
+        assert crop % 2 == 0, "crop must be even (space-to-depth stem)"
+        self.H1 = H1 = (crop + 6 - 7) // 2 + 1
+        self.H2 = H2 = (H1 + 2 - 3) // 2 + 1
+        self.Hs = (crop + 6) // 2
+        self.x2 = torch.empty(B, self.Hs, self.Hs, 16, **f32)
+        self.c1 = torch.empty(B, H1, H1, 64, **f32)
+        self.pool = torch.empty(B, H2, H2, 64, **f32)
+        self.pidx = torch.empty(B, H2, H2, 64, dtype=torch.uint8, device=dev)
+        self.acts, self.geo = {}, {}
+        H, inner, outer, tmp = H2, 0, B * H1 * H1 * 64, 1
+        for b in L.blocks:
+            f = b.filters
+            Ho = (H - 1) // b.stride + 1
+            a = {"y1": torch.empty(B, Ho, Ho, f, **f32), "y2": torch.empty(B, Ho, Ho, f, **f32),
+                 "out": torch.empty(B, Ho, Ho, 4 * f, **f32)}
+            if b.proj:
+                a["sc"] = torch.empty(B, Ho, Ho, 4 * f, **f32)
+                tmp = max(tmp, B * Ho * Ho * b.cin)
+            self.acts[b.name] = a
+            self.geo[b.name] = (H, Ho)
+            inner = max(inner, B * Ho * Ho * f)
+            outer = max(outer, B * H * H * b.cin, B * Ho * Ho * 4 * f)
+            H = Ho
+        self.H5 = H
+        self.gbuf = [torch.empty(outer, **f32), torch.empty(outer, **f32)]
+        self.g1buf, self.g2buf = torch.empty(inner, **f32), torch.empty(inner, **f32)
+        self.tmp = torch.empty(tmp, **f32)
+        # blocks feeding a stride-2 projection block: their output gradient is written on the
+        # stride-2 grid only (dgrad up2 scatter) into a buffer zeroed once here
+        bl = L.blocks
+        self.s2 = {bi for bi in range(len(bl) - 1) if bl[bi + 1].proj and bl[bi + 1].stride == 2}
+        self.s2full = {bi: torch.zeros(B * self.geo[bl[bi].name][1] ** 2 * 4 * bl[bi].filters, **f32)
+                       for bi in self.s2}
+        self.pooled = torch.empty(B, 2048, **f32)
+        self.logits = torch.empty(B, self.num_classes, **f32)
+        self.dlogits = torch.empty(B, self.num_classes, **f32)
+        self.dpooled = torch.empty(B, 2048, **f32)
+        self.labels_dev = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.cap = B
+        self._cred = {}
+        self.colpart = torch.empty(self._colred(B)[2], **f32)
+
+    def _colred(self, B):
+        """Partial column-sum regions of the fused producers: (offsets by layer, table, floats, n)."""
+        if B in self._cred:
+            return self._cred[B]
+        offs, rows, off = {}, [], 0
+
+        def add(layer, nrows, C):
+            nonlocal off
+            offs[layer] = off
+            rows.append(struct.pack(_CRED_FMT, off, nrows, C, self.ch[layer], 0))
+            off += nrows * C
+        bl = self.L.blocks
+        add(bl[-1].convs["3"].name, B, 2048)                        # gap_bwd: one row per image
+        for bi in range(len(bl) - 1, -1, -1):
+            b = bl[bi]
+            H, Ho = self.geo[b.name]
+            M = B * Ho * Ho
+            add(b.convs["2"].name, _rows64(M), b.filters)            # c3 dgrad -> g2
+            add(b.convs["1"].name, _rows64(M), b.filters)            # c2 dgrad -> g1
+            if bi > 0:                                               # c1 dgrad -> previous output
+                add(bl[bi - 1].convs["3"].name, _rows64(M if b.stride == 2 else B * H * H), b.cin)
+        res = (offs, self._dev_table(rows), off, len(rows))
+        self._cred[B] = res
+        return res
+
+    # ------------------------------------------------------------------ params
+    def init(self, seed=0):
+        self.L.init_params(self.params, seed)
+        self.after_update()
+
+    def after_update(self):
+        """Folded BN affine + fp32 stem / dgrad weights from the master (one launch pair)."""
+        self.N.prep_f32(self.params, self._prep_tab, self._prep_n, self.wf32, self.scale, self.shift, BN_EPS)
+
+    # ------------------------------------------------------------------ forward
+    def _stem_mode(self, training, crop_offset):
+        if self.crop == self.image_size:
+            return 0, 0, 0
+        if self.crop > self.image_size or not training:
+            return 1, 0, 0
+        return 2, crop_offset[0], crop_offset[1]
+
+    def _conv(self, x, R, stride, pad, Ho, w, out, scale=None, shift=None, res=None, relu=0, epi=EPI_FWD,
+              add=None, mask=None, up2=0, colsum=None):
+        self.N.conv_f32_epi(x, R, R, stride, pad, Ho, Ho, w, epi, scale, shift, res, relu, add, mask, up2, out,
+                            colsum)
+
+    def _fwd_conv(self, c, x, out, res=None, relu=1):
+        ch = self.ch[c.name]
+        self._conv(x, c.k, c.stride, c.pad, out.shape[1], self._w(c.name, c.cout, c.k * c.k * c.cin), out,
+                   self.scale[ch:], self.shift[ch:], res, relu)
+
+    def _forward(self, images, B, training, flip, crop_offset):
+        N, L = self.N, self.L
+        mode, oy, ox = self._stem_mode(training, crop_offset)
+        x2 = self.x2[:B]
+        N.stem_s2d(images, flip if training else None, mode, self.crop, self.crop, oy, ox, x2, None)
+        s = L.stem
+        c1 = self.c1[:B]
+        ch = self.ch[s.name]
+        self._conv(x2, 4, 1, 0, self.H1, self.wf32[:64 * STEM_K].view(64, STEM_K), c1, self.scale[ch:],
+                   self.shift[ch:], None, 1)
+        pool = self.pool[:B]
+        N.maxpool_fwd_f32(c1, pool, self.pidx[:B])
+        x = pool
+        for b in L.blocks:
+            a = {k: v[:B] for k, v in self.acts[b.name].items()}
+            if b.proj:
+                self._fwd_conv(b.convs["1"], x, a["y1"])
+                self._fwd_conv(b.convs["0"], x, a["sc"], relu=0)
+                res = a["sc"]
+            else:
+                self._fwd_conv(b.convs["1"], x, a["y1"])
+                res = x
+            self._fwd_conv(b.convs["2"], a["y1"], a["y2"])
+            self._fwd_conv(b.convs["3"], a["y2"], a["out"], res=res)
+            x = a["out"]
+        pooled = self.pooled[:B]
+        N.gap_fwd_f32(x, pooled)
+        chd = self.ch["dense"]
+        self._conv(pooled.view(B, 1, 1, 2048), 1, 1, 0, 1, self._w("dense", self.num_classes, 2048),
+                   self.logits[:B].view(B, 1, 1, self.num_classes), self.scale[chd:], self.shift[chd:], None, 0)
+        return x
+
+    def _labels(self, labels, B):
+        lab = self.labels_dev[:B]
+        lab.copy_(labels, non_blocking=True)
+        return lab
+
+    # ------------------------------------------------------------------ train step
+    def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0),
+                         bucket_cb: Optional[Callable[[int], None]] = None, buckets=None):
+        N, L = self.N, self.L
+        B = images.shape[0]
+        assert B <= self.cap, "batch larger than the engine's buffers"
+        self.ws.zero_()
+        lab = self._labels(labels, B)
+        prof.push("step/forward")
+        x5 = self._forward(images, B, True, flip, crop_offset)
+        prof.pop()
+        prof.push("step/backward")
+        ncls = self.num_classes
+        dl = self.dlogits[:B]
+        N.softmax_xent_f32(self.logits[:B], lab, ncls, float(gscale), dl, self.stats[0:1], self.stats[1:2])
+        bks = buckets if buckets is not None else []
+        nb = [0]
+
+        def done_upto(off):
+            while bucket_cb is not None and nb[0] < len(bks) - 1 and bks[nb[0]][1] <= off:
+                bucket_cb(nb[0])
+                nb[0] += 1
+
+        # ---- head
+        pooled = self.pooled[:B]
+        chd = self.ch["dense"]
+        N.wgrad_f32(pooled.view(B, 1, 1, 2048), 1, 1, 1, 0, dl.view(B, 1, 1, ncls), self._gv("dense", ncls, 2048))
+        N.colsum_f32(dl, ncls, self.colsum[chd:])
+        dpooled = self.dpooled[:B]
+        self._conv(dl.view(B, 1, 1, ncls), 1, 1, 0, 1, self._wd("dense", 2048, ncls), dpooled.view(B, 1, 1, 2048),
+                   epi=EPI_PLAIN)
+        e = L.entry("dense", "kernel")
+        done_upto(e.offset + e.size)
+        cur = 0
+        H5, bl = self.H5, L.blocks
+        coffs, ctab, _, cn = self._colred(B)
+        cp = self.colpart
+
+        def part(layer):
+            return cp[coffs[layer]:]
+        gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
+        N.gap_bwd_f32(dpooled, x5, gout, part(bl[-1].convs["3"].name))
+        for bi in range(len(bl) - 1, -1, -1):
+            b = bl[bi]
+            a = {k: v[:B] for k, v in self.acts[b.name].items()}
+            H, Ho = self.geo[b.name]
+            f, cin = b.filters, b.cin
+            x_in = self.acts[bl[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
+            c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
+            gsrc = self.s2full[bi] if bi in self.s2 else self.gbuf[cur]
+            gout = gsrc[: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
+            g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            # conv3 (1x1) and conv2 (3x3): raw dW, then dgrad with the ReLU mask of their input
+            N.wgrad_f32(a["y2"], 1, 1, 1, 0, gout, self._gv(c3n, 4 * f, f))
+            self._conv(gout, 1, 1, 0, Ho, self._wd(c3n, f, 4 * f), g2, epi=EPI_DGRAD, mask=a["y2"],
+                       colsum=part(c2n))
+            N.wgrad_f32(a["y1"], 3, 3, 1, 1, g2, self._gv(c2n, f, 9 * f))
+            self._conv(g2, 3, 1, 1, Ho, self._wd(c2n, f, 9 * f), g1, epi=EPI_DGRAD, mask=a["y1"],
+                       colsum=part(c1n))
+            # conv1 (+ conv0): input gradient of the block
+            nxt = 1 - cur
+            cs_in = part(bl[bi - 1].convs["3"].name) if bi > 0 else None
+            if b.proj:
+                c0n = b.convs["0"].name
+                N.wgrad_f32(x_in, 1, 1, b.stride, 0, g1, self._gv(c1n, f, cin))
+                N.wgrad_f32(x_in, 1, 1, b.stride, 0, gout, self._gv(c0n, 4 * f, cin))
+                N.wgrad_finalize(self.params, self.grads, self._fin[b.name], 4, self.scale, self.dgr)
+                # dx = (W1'.g1 + W0'.gout) * mask: the first source into `tmp`, added by the second
+                tmp = self.tmp[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
+                self._conv(g1, 1, 1, 0, Ho, self._wd(c1n, cin, f), tmp, epi=EPI_PLAIN)
+                if b.stride == 2:
+                    gx = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin)   # grid positions only
+                    self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
+                               mask=x_in, up2=1, colsum=cs_in)
+                else:
+                    gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                    self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
+                               mask=x_in, colsum=cs_in)
+                last = L.entry(c0n, "kernel")
+            else:
+                N.wgrad_f32(x_in, 1, 1, 1, 0, g1, self._gv(c1n, f, cin))
+                N.wgrad_finalize(self.params, self.grads, self._fin[b.name], 3, self.scale, self.dgr)
+                gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                self._conv(g1, 1, 1, 0, H, self._wd(c1n, cin, f), gx, epi=EPI_DGRAD, add=gout, mask=x_in,
+                           colsum=cs_in)
+                last = L.entry(c1n, "kernel")
+            done_upto(last.offset + last.size)
+            cur = nxt
+        # ---- stem: max-pool backward (with conv1's ReLU mask), s2d-domain wgrad folded to 7x7x3
+        H1, H2 = self.H1, self.H2
+        gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
+        gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
+        s = L.stem
+        N.maxpool_bwd_f32(gpool, self.pidx[:B], self.c1[:B], gc1)
+        N.colsum_f32(gc1.view(-1, 64), 64, self.colsum[self.ch[s.name]:])
+        N.wgrad_f32(self.x2[:B], 4, 4, 1, 0, gc1, self.stem_dw2)
+        N.stem_wgrad_fold(self.stem_dw2, self._gv(s.name, 64, 147), 64)
+        N.wgrad_finalize(self.params, self.grads, self._fin["stem"], 1, self.scale, self.dgr)
+        done_upto(L.kernels_end)
+        N.colsum_reduce(cp, ctab, cn, self.colsum)
+        N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
+        prof.pop()
+        if bucket_cb is not None:
+            while nb[0] < len(bks):
+                bucket_cb(nb[0])
+                nb[0] += 1
+        return self.stats
+
+    @torch.no_grad()
+    def evaluate(self, images, labels):
+        B = images.shape[0]
+        assert B <= self.cap
+        self.stats.zero_()
+        lab = self._labels(labels, B)
+        self._forward(images, B, False, None, (0, 0))
+        self.N.softmax_xent_f32(self.logits[:B], lab, self.num_classes, 0.0, self.dlogits[:B], self.stats[0:1],
+                                self.stats[1:2])
+        return self.stats

@@ -103,8 +103,8 @@ def _ref_grads(L, params, img, lab, B, crop, dtype, masks=None):
     return st, ref.grads
 
 
-def test_f32_engine_matches_reference():
-    """One training step of the fp32 HIP engine vs the PyTorch reference model in float64 on
+def test_f32_autograd_engine_matches_reference():
+    """One training step of the autograd fp32 HIP engine (--bn-mode train's fp32 path) vs the PyTorch reference model in float64 on
     the CPU, every gradient tensor within 1e-4 relative.  The reference replays the engine's
     ReLU masks: a pre-activation within fp32 rounding of zero (1-2 of ~10^6 per step) can take
     the other side of the ReLU in any fp32 run, which re-routes that element's gradient and
@@ -115,7 +115,7 @@ def test_f32_engine_matches_reference():
     torch.manual_seed(2)
     L = ParamLayout()
     B, crop = 4, 96
-    eng = E.HipF32Engine(L, B, crop=crop, device=dev)
+    eng = E.HipF32AutogradEngine(L, B, crop=crop, device=dev)
     eng.init(seed=3)
     img = torch.randint(0, 256, (B, crop, crop, 3), dtype=torch.uint8)
     lab = torch.randint(0, 1000, (B,))
@@ -146,3 +146,176 @@ def test_f32_engine_matches_reference():
     rows.sort(reverse=True)
     print("worst (engine vs f64 with the engine's ReLU masks):", rows[:3])
     assert rows[0][0] < 1e-4, rows[:3]
+
+
+def _engine_masks(eng, B):
+    """The ReLU decisions the fused engine took, in the reference's call order (stem, then per
+    block y1, y2, out), as NCHW bool tensors."""
+    nchw = lambda t: (t[:B] > 0).permute(0, 3, 1, 2).cpu()   # noqa: E731
+    out = [nchw(eng.c1)]
+    for b in eng.L.blocks:
+        a = eng.acts[b.name]
+        out += [nchw(a["y1"]), nchw(a["y2"]), nchw(a["out"])]
+    return out
+
+
+@pytest.mark.parametrize("crop,image", [(96, 96), (64, 80)])
+def test_f32_fused_engine_matches_reference(crop, image):
+    """One training step of the explicit fp32 engine (fused conv epilogues, fp32 pool / GAP /
+    softmax kernels, no PyTorch op in the step) vs the reference model in float64 on the CPU,
+    with the engine's ReLU decisions replayed: every gradient tensor within 1e-4 relative and
+    the loss within 1e-5 (crop < image: the RandomCrop offset path)."""
+    from pddl.models.engine_f32 import HipF32Engine
+    from pddl.models.resnet50 import ParamLayout
+    torch.manual_seed(2)
+    L = ParamLayout()
+    B = 4
+    eng = HipF32Engine(L, B, crop=crop, image_size=image, device=dev)
+    eng.init(seed=3)
+    # non-trivial frozen-BN statistics / affine so the folding is exercised
+    g = torch.Generator().manual_seed(11)
+    host = eng.params.cpu()
+    for e in L.entries.values():
+        sl = host[e.offset:e.offset + e.size]
+        if e.kind == "gamma":
+            sl.copy_(0.5 + torch.rand(e.size, generator=g))
+        elif e.kind in ("beta", "bias", "moving_mean"):
+            sl.copy_(0.1 * torch.randn(e.size, generator=g))
+        elif e.kind == "moving_variance":
+            sl.copy_(0.5 + torch.rand(e.size, generator=g))
+    eng.params.copy_(host.to(dev))
+    eng.after_update()
+    img = torch.randint(0, 256, (B, image, image, 3), dtype=torch.uint8)
+    lab = torch.randint(0, 1000, (B,))
+    off = (5, 9) if crop < image else (0, 0)
+    st = eng.forward_backward(img.to(dev), lab.to(dev), 1.0 / B, crop_offset=off).clone()
+    torch.cuda.synchronize()
+    masks = _engine_masks(eng, B)
+    src = img[:, off[0]:off[0] + crop, off[1]:off[1] + crop] if crop < image else img
+    s64, g64 = _ref_grads(L, eng.params, src.contiguous(), lab, B, crop, torch.float64, masks)
+    assert abs(st[0].item() - s64[0].item()) / abs(s64[0].item()) < 1e-5
+    gr = eng.grads.cpu().double()
+    rows = []
+    for e in L.entries.values():
+        if e.offset + e.size > L.n_trainable:
+            continue
+        sl = slice(e.offset, e.offset + e.size)
+        if g64[sl].norm() < 1e-12:
+            continue
+        rows.append((rel(gr[sl], g64[sl]), e.name))
+    rows.sort(reverse=True)
+    print("worst (fused fp32 engine vs f64 with the engine's ReLU masks):", rows[:3])
+    assert rows[0][0] < 1e-4, rows[:3]
+
+
+def test_f32_fused_engine_trains_and_evaluates():
+    """Adam steps of the fused fp32 engine follow the autograd fp32 engine (same model, same
+    precision, PyTorch autograd over the fp32 conv op) step for step; odd class count
+    (Cout % 4 != 0 through the Dense head's wgrad / dgrad / column sums)."""
+    from pddl.models.engine_f32 import HipF32AutogradEngine, HipF32Engine
+    from pddl.models.resnet50 import ParamLayout
+    from pddl.train.optim import make_optimizer
+    torch.manual_seed(0)
+    B, ncls = 8, 10
+    L = ParamLayout(ncls)
+    img = torch.randint(0, 256, (B, 64, 64, 3), dtype=torch.uint8, device=dev)
+    lab = torch.randint(0, ncls, (B,), device=dev)
+    traj = []
+    for cls in (HipF32Engine, HipF32AutogradEngine):
+        eng = cls(L, B, crop=64, device=dev, num_classes=ncls)
+        eng.init(seed=1)
+        opt = make_optimizer("adam", eng, lr=1e-3)
+        losses = []
+        for _ in range(8):
+            losses.append(eng.forward_backward(img, lab, 1.0 / B)[0].item() / B)
+            opt.step()
+            eng.after_update()
+        traj.append(losses)
+        if cls is HipF32Engine:
+            ev = eng.evaluate(img, lab)
+            assert torch.isfinite(ev).all()
+    fused, ref = traj
+    print("fused / autograd fp32 losses:", [(round(a, 5), round(b, 5)) for a, b in zip(fused, ref)])
+    # measured: identical to 1e-5 for 3 steps, then fp32 summation-order differences grow in
+    # this lr-1e-3 / 8-image problem (loss 2.30 -> 1.42 -> 1.63: the trajectory turns chaotic)
+    dev_ = [abs(a - b) / abs(b) for a, b in zip(fused, ref)]
+    assert fused[-1] < fused[0]
+    assert max(dev_[:5]) < 1e-3 and max(dev_) < 2e-2, (fused, ref)
+
+
+@pytest.mark.parametrize("up2", [0, 1])
+def test_conv_f32_fused_epilogues(up2):
+    """conv_f32_epi against float64: forward (folded BN affine + residual + ReLU) and dgrad
+    (residual-gradient add + ReLU mask + stride-2 grid scatter + per-m-tile column sums)."""
+    torch.manual_seed(4)
+    n, h, c, co = 3, 9, 64, 100            # 100 output channels: a ragged last column group
+    x = torch.randn(n, h, h, c, device=dev)
+    w = torch.randn(co, c, device=dev) * 0.1
+    sc, sh = torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev)
+    res = torch.randn(n, h, h, co, device=dev)
+    y = torch.empty(n, h, h, co, device=dev)
+    N().conv_f32_epi(x, 1, 1, 1, 0, h, h, w, 1, sc, sh, res, 1, None, None, 0, y, None)
+    ref = (x.double() @ w.double().t() * sc.double() + sh.double() + res.double()).relu()
+    assert rel(y, ref) < 1e-6
+    # dgrad: GEMM rows over an h x h grid, optionally scattered to a (2h - 1) x (2h - 1) grid
+    H = 2 * h - 1 if up2 else h
+    add = torch.randn(n, h, h, co, device=dev) if up2 else torch.randn(n, H, H, co, device=dev)
+    mask = torch.randn(n, H, H, co, device=dev)
+    out = torch.zeros(n, H, H, co, device=dev)
+    rows = (n * h * h + 63) // 64
+    part = torch.full((rows * co,), float("nan"), device=dev)
+    N().conv_f32_epi(x, 1, 1, 1, 0, h, h, w, 2, None, None, None, 0, add, mask, up2, out, part)
+    acc = x.double() @ w.double().t()
+    full = torch.zeros(n, H, H, co, dtype=torch.float64, device=dev)
+    if up2:
+        full[:, ::2, ::2] = acc + add.double()
+    else:
+        full = acc + add.double()
+    want = full * (mask.double() > 0)
+    assert rel(out, want) < 1e-6
+    if up2:
+        assert out[:, 1::2].abs().sum().item() == 0 and out[:, :, 1::2].abs().sum().item() == 0
+    assert rel(part.view(rows, co).sum(0), want.sum((0, 1, 2))) < 1e-6
+
+
+def test_f32_pool_gap_softmax_kernels():
+    torch.manual_seed(6)
+    B, H, C = 3, 13, 64
+    x = torch.randn(B, H, H, C, device=dev).relu()
+    Ho = (H + 2 - 3) // 2 + 1
+    y = torch.empty(B, Ho, Ho, C, device=dev)
+    idx = torch.empty(B, Ho, Ho, C, dtype=torch.uint8, device=dev)
+    N().maxpool_fwd_f32(x, y, idx)
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(F.pad(xr, (1, 1, 1, 1)), 3, 2)
+    assert rel(y, yr.permute(0, 2, 3, 1)) == 0
+    gy = torch.randn(B, Ho, Ho, C, device=dev)
+    gx = torch.empty_like(x)
+    N().maxpool_bwd_f32(gy, idx, x, gx)
+    yr.backward(gy.double().permute(0, 3, 1, 2))
+    want = xr.grad.permute(0, 2, 3, 1) * (x.double() > 0)
+    assert rel(gx, want) < 1e-12
+    # GAP
+    p = torch.empty(B, C, device=dev)
+    N().gap_fwd_f32(x, p)
+    assert rel(p, x.double().mean((1, 2))) < 1e-6
+    gp = torch.randn(B, C, device=dev)
+    g = torch.empty_like(x)
+    rows = torch.empty(B * C, device=dev)
+    N().gap_bwd_f32(gp, x, g, rows)
+    wg = (gp.double()[:, None, None, :] / (H * H)) * (x.double() > 0)
+    assert rel(g, wg) < 1e-6 and rel(rows.view(B, C).sum(0), wg.sum((0, 1, 2))) < 1e-6
+    cs = torch.zeros(C, device=dev)
+    N().colsum_f32(g.view(-1, C), C, cs)
+    assert rel(cs, wg.sum((0, 1, 2))) < 1e-6
+    # softmax-xent with fp32 dlogits
+    logits = torch.randn(5, 10, device=dev)
+    lab = torch.randint(0, 10, (5,), device=dev)
+    dl = torch.empty(5, 10, device=dev)
+    ls, cr = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+    N().softmax_xent_f32(logits, lab, 10, 0.5, dl, ls, cr)
+    lr = logits.double().requires_grad_(True)
+    loss = F.cross_entropy(lr, lab, reduction="sum")
+    (loss * 0.5).backward()
+    assert abs(ls.item() - loss.item()) < 1e-4 and rel(dl, lr.grad) < 1e-6
+    assert cr.item() == (logits.argmax(1) == lab).sum().item()
