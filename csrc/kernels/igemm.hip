@@ -63,9 +63,52 @@ __device__ __forceinline__ int sw_read(int lane, int kh) { return (((kh * 4) + (
 // and batch statistics (train-mode BN forward) go to partial row `prow`.
 // PF: the per-element epilogue operand of the whole sub-tile is loaded into registers before
 // the accumulators are staged, so its HBM latency overlaps the staging.
-template <int TM, int TN, bool PF, bool BNZ = false>
+// The per-element epilogue operand rows of a wave sub-tile (forward residual / dgrad `add`, plus
+// the dgrad ReLU bits), 32-row passes [pass0, pass0 + npass) into dst / bits.  Branch-free loads
+// (row and column clamped into the tensor, the value zeroed afterwards): under an exec branch
+// the compiler completes each load (and everything issued before it) inside the branch, which
+// serialises the prefetch into one HBM round trip per row.  Both loads are issued whenever
+// either operand is in use (an unused one reads the output tensor's first element) so that
+// neither sits under a uniform branch either.
+template <int TM, int TN>
+__device__ __forceinline__ void igemm_epi_load(const IgemmParams& p, int mb, int nb, int lane, int pass0, int npass,
+                                               uint4* dst, uint32_t* bits) {
+  constexpr int WTN = 16 * TN, LPR = WTN / 8, RPI = 64 / LPR, NIT = 32 / RPI;
+  const int c8 = lane % LPR, rr = lane / LPR;
+  const int gn = nb + c8 * 8;
+  const bool col_ok = gn < p.Nn;
+  const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
+  const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
+  const bf16_t* pre_src = p.mode == EPI_FWD ? p.res : p.add;
+  const int pre_ld = p.mode == EPI_FWD ? p.ld_res : p.ld_add;
+  const int gn_c = col_ok ? gn : 0;
+  const bf16_t* psrc = pre_on ? pre_src : reinterpret_cast<const bf16_t*>(p.out);
+  const long pld = pre_on ? pre_ld : 0;
+  const int pcol = pre_on ? gn_c : 0;
+  const uint8_t* bsrc = pf_bits ? p.bits_mask : reinterpret_cast<const uint8_t*>(p.out);
+  const long bld = pf_bits ? p.ld_bits_mask : 0;
+  const int bcol = pf_bits ? (gn_c >> 3) : 0;
+#pragma unroll
+  for (int q = 0; q < npass; ++q)
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int gm = mb + (pass0 + q) * 32 + it * RPI + rr;
+      const bool ok = gm < p.M && col_ok;
+      const long gr = gm < p.M ? gm : p.M - 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + pcol);
+      const uint32_t b = bsrc[gr * bld + bcol];
+      dst[q * NIT + it] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
+      bits[q * NIT + it] = (ok && pf_bits) ? b : 0u;
+    }
+}
+
+// EARLY: the caller loaded the whole sub-tile's operand (igemm_epi_load) before its K loop and
+// passes it in `epre` / `ebits` (the short-K layers: their HBM latency then overlaps the
+// operand loads instead of following the MFMAs).
+template <int TM, int TN, bool PF, bool BNZ = false, bool EARLY = false>
 __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
-                                               float* stage, int lane) {
+                                               float* stage, int lane, const uint4* epre = nullptr,
+                                               const uint32_t* ebits = nullptr) {
   constexpr int WTN = 16 * TN;
   constexpr int EPI_LD = WTN + 4;
   const int HoWo = p.Ho * p.Wo;
@@ -101,45 +144,17 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
   // 32-row pass at a time at the top of the pass.  (Loaded inside the store loop, each load
   // would wait behind the previous iteration's store -- `out` may alias `add` as far as the
   // compiler knows -- and the pass would pay NIT serialised HBM round trips.)
-  uint4 pre[PF ? (TM / 2) * NIT : NIT];
-  uint32_t pre_bits[PF ? (TM / 2) * NIT : NIT];
+  constexpr bool WHOLE = PF && !EARLY;
+  uint4 pre[WHOLE ? (TM / 2) * NIT : (EARLY ? 1 : NIT)];
+  uint32_t pre_bits[WHOLE ? (TM / 2) * NIT : (EARLY ? 1 : NIT)];
   const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
   const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
-  const bf16_t* pre_src = p.mode == EPI_FWD ? p.res : p.add;
-  const int pre_ld = p.mode == EPI_FWD ? p.ld_res : p.ld_add;
-  // Branch-free loads (row and column clamped into the tensor, the value zeroed afterwards):
-  // under an exec branch the compiler completes each load (and everything issued before it)
-  // inside the branch, which serialises the prefetch into one HBM round trip per row.
-  // Both loads are issued whenever either operand is in use (an unused one reads the output
-  // tensor's first element) so that neither sits under a uniform branch either.
-  const int gn_c = col_ok ? gn : 0;
-  const bf16_t* psrc = pre_on ? pre_src : reinterpret_cast<const bf16_t*>(p.out);
-  const long pld = pre_on ? pre_ld : 0;
-  const int pcol = pre_on ? gn_c : 0;
-  const uint8_t* bsrc = pf_bits ? p.bits_mask : reinterpret_cast<const uint8_t*>(p.out);
-  const long bld = pf_bits ? p.ld_bits_mask : 0;
-  const int bcol = pf_bits ? (gn_c >> 3) : 0;
-  auto prefetch = [&](int pass, uint4* dst, uint32_t* bits) {
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int gm = mb + pass * 32 + it * RPI + rr;
-      const bool ok = gm < p.M && col_ok;
-      const long gr = gm < p.M ? gm : p.M - 1;
-      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + pcol);
-      const uint32_t b = bsrc[gr * bld + bcol];
-      dst[it] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
-      bits[it] = (ok && pf_bits) ? b : 0u;
-    }
-  };
-  if (PF && (pre_on || pf_bits)) {
-#pragma unroll
-    for (int pass = 0; pass < TM / 2; ++pass) prefetch(pass, pre + pass * NIT, pre_bits + pass * NIT);
-  }
+  if (WHOLE && (pre_on || pf_bits)) igemm_epi_load<TM, TN>(p, mb, nb, lane, 0, TM / 2, pre, pre_bits);
 #pragma unroll
   for (int pass = 0; pass < TM / 2; ++pass) {
-    if (!PF && (pre_on || pf_bits)) prefetch(pass, pre, pre_bits);
-    const uint4* ppre = PF ? pre + pass * NIT : pre;
-    const uint32_t* pbits = PF ? pre_bits + pass * NIT : pre_bits;
+    if (!PF && !EARLY && (pre_on || pf_bits)) igemm_epi_load<TM, TN>(p, mb, nb, lane, pass, 1, pre, pre_bits);
+    const uint4* ppre = EARLY ? epre + pass * NIT : (PF ? pre + pass * NIT : pre);
+    const uint32_t* pbits = EARLY ? ebits + pass * NIT : (PF ? pre_bits + pass * NIT : pre_bits);
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -304,7 +319,10 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 // WTM_: wave-tile rows (64, or 128 for the 256x256 tile: 8 waves as 2 x 4, 128x64 each).
 // SK: split-K slice instantiation (separate, so the unsplit kernels keep their register budget:
 // the slice bookkeeping compiled into every instantiation cost 33 VGPRs, occupancy 3 -> 2).
-template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64, bool BNZ = false, bool SK = false>
+// EPF: early epilogue-operand prefetch (igemm_epi_load issued right after the first k-tile's
+// LDS-DMA, so the residual / residual-gradient round trip overlaps the operand round trip).
+template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64, bool BNZ = false, bool SK = false,
+          bool EPF = false>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParams p) {
   constexpr int WTM = WTM_, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -444,6 +462,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   const int a_off = (wm * WTM + (lane & 15)) * 128;
   const int b_off = (wn * WTN + (lane & 15)) * 128;
   load_tile(0);
+  constexpr int ENIT = 32 / (64 / (WTN / 8));
+  uint4 epre[EPF ? (TM / 2) * ENIT : 1];
+  uint32_t ebits[EPF ? (TM / 2) * ENIT : 1];
+  if constexpr (EPF) igemm_epi_load<TM, TN>(p, m0 + wm * WTM, n0 + wn * WTN, lane, 0, TM / 2, epre, ebits);
   if (NSTAGE == 3) {
     if (KT > 1) load_tile(1);
   } else {
@@ -514,8 +536,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (WTN + 4));
-  igemm_epilogue<TM, TN, PF, BNZ>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, stage,
-                                  lane);
+  igemm_epilogue<TM, TN, PF || EPF, BNZ, EPF>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm,
+                                              stage, lane, epre, ebits);
 }
 
 
@@ -879,6 +901,7 @@ int num_cus() {
 struct IgemmPlan { int cfg, split, ks; };
 
 int g_igemm_splitk = 1;
+int g_igemm_epf = 0;       // early epilogue-operand prefetch for the short-K single-stage tiles (A/B knob)
 
 // Split-K for layers with too few output tiles to fill the chip (small batches, small spatial
 // stages: stage 5 at batch 32-256, crop 160): the 4-wave tiles stay resident 2-3 per CU, so a
@@ -1029,6 +1052,18 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
       else { if (am == AM_DIRECT) IG_SK(256, 64, 2, AM_DIRECT); else IG_SK(256, 64, 2, AM_HALO); }
     }
 #undef IG_SK
+    return;
+  }
+  // early prefetch (knob igemm_epf: 1 = single-stage tiles with a residual / residual-gradient
+  // operand, K <= 256; 2 = also the ReLU-bits-only dgrads)
+  const bool epf_op = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
+  const bool epf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
+  if (g_igemm_epf && am == AM_DIRECT && cfg <= 1 && ns == 1 && KT <= 4 && (epf_op || (g_igemm_epf == 2 && epf_bits))) {
+#define IG_EPF(BM_, BN_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, 1, AM_DIRECT, false, 64, false, false, true>), dim3(nwg), dim3(256), 0, \
+                     stream, p)
+    if (cfg == 1) IG_EPF(128, 128); else IG_EPF(256, 64);
+#undef IG_EPF
     return;
   }
   const bool pf = g_igemm_pf && am == AM_DIRECT && cfg <= 1 &&

@@ -294,7 +294,7 @@ def test_f32_pool_gap_softmax_kernels():
     N().maxpool_bwd_f32(gy, idx, x, gx)
     yr.backward(gy.double().permute(0, 3, 1, 2))
     want = xr.grad.permute(0, 2, 3, 1) * (x.double() > 0)
-    assert rel(gx, want) < 1e-12
+    assert rel(gx, want) < 1e-6          # (fp32 sums of up to 4 routed gradients)
     # GAP
     p = torch.empty(B, C, device=dev)
     N().gap_fwd_f32(x, p)

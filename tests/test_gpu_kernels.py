@@ -146,8 +146,8 @@ def test_igemm_dgrad(case):
 
 
 @pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1), ("igemm8", 1),
-                                      ("igemm8", 2), ("igemm", 2)])
-@pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual"])
+                                      ("igemm8", 2), ("igemm", 2), ("igemm_epf", 1), ("igemm_epf", 2)])
+@pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual", "fwd1x1resid", "dgrad1x1add"])
 def test_igemm_big_tile_matches(kind, knob, big):
     """The 8-wave 256x128 3-stage (igemm_big 2) and 256x256 2-stage (igemm_big 4)
     configurations, the interleaved-issue 2-stage pipeline (igemm_il 1) and the 8-phase
@@ -164,6 +164,16 @@ def test_igemm_big_tile_matches(kind, knob, big):
         x = rnd(n, h, h, 256)
         w = rnd(320, 256, scale=0.05)
         sc, sh = torch.rand(320, device=dev) + 0.5, torch.randn(320, device=dev)
+    elif kind == "fwd1x1resid":      # short-K 1x1 with a residual (the early-prefetch path)
+        x = rnd(n, h, h, 128)
+        w = rnd(512, 128, scale=0.05)
+        sc, sh = torch.rand(512, device=dev) + 0.5, torch.randn(512, device=dev)
+        res = rnd(n, h, h, 512)
+    elif kind == "dgrad1x1add":      # short-K 1x1 dgrad: residual-gradient add + ReLU bits + column sums
+        g = rnd(n, h, h, 64)
+        wt = rnd(256, 64, scale=0.05)
+        addv = rnd(n, h, h, 256)
+        bits = pack_bits(rnd(n, h, h, 256))
     else:
         g1, g0 = rnd(n, ho, ho, 128), rnd(n, ho, ho, 512)
         wt = rnd(256, 640, scale=0.05)
@@ -180,6 +190,19 @@ def test_igemm_big_tile_matches(kind, knob, big):
                 N().igemm(x, None, h, h, 3, 3, 1, 1, h, h, w, 0, sc, sh, None, None, None, y, 1, None, 0, 0, 0, 0, 0,
                           None, None)
                 outs.append(y.float())
+            elif kind == "fwd1x1resid":
+                y = torch.empty(n, h, h, 512, dtype=torch.bfloat16, device=dev)
+                bo = torch.zeros(n, h, h, 64, dtype=torch.uint8, device=dev)
+                N().igemm(x, None, h, h, 1, 1, 1, 0, h, h, w, 0, sc, sh, res, None, None, y, 1, None, 0, 0, 0, 0, 0,
+                          None, bo)
+                outs.append(torch.cat([y.float().flatten(), bo.float().flatten()]))
+            elif kind == "dgrad1x1add":
+                out = torch.empty(n, h, h, 256, dtype=torch.bfloat16, device=dev)
+                rows = N().igemm_partial_rows(n * h * h, 256, 64)
+                part = torch.full((rows * 256,), float("nan"), device=dev)
+                N().igemm(g, None, h, h, 1, 1, 1, 0, h, h, wt, 1, None, None, None, bits, addv, out, 0, None, 0, 0,
+                          0, 0, 0, part, None)
+                outs.append(torch.cat([out.float().flatten(), _fold(part, rows, 256)]))
             elif kind == "fwd1x1res":
                 y1 = torch.empty(n, h, h, 64, dtype=torch.bfloat16, device=dev)
                 y2 = torch.empty(n, h, h, 256, dtype=torch.bfloat16, device=dev)
