@@ -52,8 +52,9 @@ __device__ __forceinline__ uint32_t pos_bits8(const uint4& u) {
   return byte;
 }
 
-// Buffer offset past every descriptor's range (operands are checked to stay below 2 GiB):
-// the buffer unit returns zeros for it.
+// Buffer offset past every descriptor's range (record counts are clamped below 2 GiB; large
+// activations are reached through per-tile rebased descriptors, make_rsrc_at): the buffer
+// unit returns zeros for it.
 constexpr uint32_t OOB_OFF = 0x80000000u;
 
 // 16-byte-per-lane buffer LDS-DMA (buffer_load_dwordx4 ... lds): LDS destination = M0 base
@@ -73,6 +74,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
 static __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
 __host__ __device__ __forceinline__ long lmin(long a, long b) { return a < b ? a : b; }
+
+// Descriptor over elements [e0, e_end) of a bf16 tensor, rebased at e0 with 64-bit pointer
+// arithmetic: a workgroup's lane offsets (relative to the first image / row its tile reads)
+// stay 32-bit at any batch, and the record count is clamped below OOB_OFF so that marker
+// still reads zeros.  This is what lets one GPU train at b2048 (stage-1 activations > 2 GiB).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_at(const uint16_t* base, long e0, long e_end) {
+  return make_rsrc(base + e0, (int)lmin((e_end - e0) * 2, 0x7fffffffL));
+}
 
 // Division by a runtime divisor d as one 64-bit multiply + shift: exact for
 // 0 <= x < 2^40 / d (every row index of the ResNet-50 GEMMs: x < 2^26, d < 2^14).

@@ -356,11 +356,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   const int kt0 = (int)((long)slice * KT_all / ks);
   const int KT = (int)((long)(slice + 1) * KT_all / ks) - kt0;
 
-  // Buffer descriptors (wave-uniform kernel arguments only, so no waterfall loops).
-  const int pix_total = p.N * p.H * p.W;
-  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(p.a1, pix_total * p.C1 * 2);
-  const __amdgpu_buffer_rsrc_t ra2 =
-      make_rsrc(AM == AM_DUAL ? p.a2 : p.a1, pix_total * (AM == AM_DUAL ? p.C2 : p.C1) * 2);
+  // Buffer descriptors (wave-uniform values only, so no waterfall loops).  The A descriptors
+  // start at the first image this tile's rows read (n_first), so lane offsets span only the
+  // tile's few images, whatever the batch.
+  const int n_first = fdiv(m0, p.mg_howo);
+  const long HW = (long)p.H * p.W, pix0 = n_first * HW, pix_end = p.N * HW;
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc_at(p.a1, pix0 * p.C1, pix_end * p.C1);
+  const int C2r = AM == AM_DUAL ? p.C2 : p.C1;
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc_at(AM == AM_DUAL ? p.a2 : p.a1, pix0 * C2r, pix_end * C2r);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
 
   // Per-lane constant source chunk: LDS position (lane & 7) of row (lane >> 3) holds the
@@ -379,7 +382,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
       const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
       const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
       const int hi = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
-      const int pix = (n * p.H + hi) * p.W + wi;
+      const int pix = ((n - n_first) * p.H + hi) * p.W + wi;
       a_o1[i] = (uint32_t)((pix * p.C1 + sw_chunk(lane, i) * 8) * 2);
       if (AM == AM_DUAL) a_o2[i] = (uint32_t)((pix * p.C2 + sw_chunk(lane, i) * 8) * 2);
       if (AM == AM_HALO) {
@@ -625,10 +628,11 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
   const int tn = wg % nt, tm = wg / nt;
   const int m0 = p.m_begin + tm * BM, n0 = tn * BN;
   const int HoWo = p.Ho * p.Wo;
-  const int pix_total = p.N * p.H * p.W;
-  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(p.a1, pix_total * p.C1 * 2);
-  const __amdgpu_buffer_rsrc_t ra2 =
-      make_rsrc(AM == AM_DUAL ? p.a2 : p.a1, pix_total * (AM == AM_DUAL ? p.C2 : p.C1) * 2);
+  const int n_first = fdiv(m0, p.mg_howo);   // A descriptors rebased at the tile's first image
+  const long HW = (long)p.H * p.W, pix0 = n_first * HW, pix_end = p.N * HW;
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc_at(p.a1, pix0 * p.C1, pix_end * p.C1);
+  const int C2r = AM == AM_DUAL ? p.C2 : p.C1;
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc_at(AM == AM_DUAL ? p.a2 : p.a1, pix0 * C2r, pix_end * C2r);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
   // LDS-DMA piece i of a wave holds rows 8*(piece) + lane/8 (piece parity = i & 1); its lane-linear
   // 16-byte chunk (lane & 7) carries logical chunk (lane & 7) ^ ((row >> 1) & 7) (sw_chunk).
@@ -644,7 +648,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
       const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
       const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
       const int hi_ = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
-      const int pix = (n * p.H + hi_) * p.W + wi;
+      const int pix = ((n - n_first) * p.H + hi_) * p.W + wi;
       a_o1[hi] = (uint32_t)((pix * p.C1 + sw_chunk(lane, hi) * 8) * 2);
       if (AM == AM_DUAL) a_o2[hi] = (uint32_t)((pix * p.C2 + sw_chunk(lane, hi) * 8) * 2);
       if (AM == AM_HALO) {
@@ -842,9 +846,15 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
     *why = "bn_z: fused BN-backward sums need a single-source dgrad without scatter, with stats rows"; return false;
   }
   if ((long)p.M * p.Ho * p.Wo >= (1L << 40)) { *why = "too many output rows for the magic-number row decode"; return false; }
-  // buffer offsets are 32-bit byte offsets with 0x80000000 reserved as "out of range"
-  if ((long)p.N * p.H * p.W * (p.C1 > p.C2 ? p.C1 : p.C2) * 2 >= (1L << 31) || (long)p.Nn * p.ldb * 2 >= (1L << 31)) {
+  // buffer offsets are 32-bit byte offsets with 0x80000000 reserved as "out of range"; the A
+  // descriptors are rebased per tile, so only the images one 256-row tile spans must fit
+  // (and every element index below is an int: < 2^31 elements per tensor)
+  const long span = 256 / (p.Ho * p.Wo) + 2, cmax = p.C1 > p.C2 ? p.C1 : p.C2;
+  if (span * p.H * p.W * cmax * 2 >= (1L << 31) || (long)p.Nn * p.ldb * 2 >= (1L << 31)) {
     *why = "operand too large for 31-bit buffer offsets"; return false;
+  }
+  if ((long)p.N * p.H * p.W * cmax >= (1L << 31) || (long)p.M * (p.ldo > p.Nn ? p.ldo : p.Nn) >= (1L << 31)) {
+    *why = "tensor has more than 2^31 elements"; return false;
   }
   return true;
 }

@@ -74,9 +74,13 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
   const int mend = min(p.M, mbeg + m_per_split);
 
   // buffer descriptors: 32-bit lane offsets, the m-step in the scalar soffset, and
-  // out-of-range offsets (padding taps, tile overhang) load zeros
-  const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.g, p.M * p.ldg * 2);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, FAST ? p.M * p.ldx * 2 : p.N * p.H * p.W * p.C * 2);
+  // out-of-range offsets (padding taps, tile overhang) load zeros.  They are rebased at the
+  // split's first row (gradient, 1x1 input) or first image (gathered input), so the offsets
+  // span one split whatever the batch (the launcher bounds the split span).
+  const int pix0 = FAST ? 0 : (mbeg / (p.Ho * p.Wo)) * p.H * p.W;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc_at(p.g, (long)mbeg * p.ldg, (long)p.M * p.ldg);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, FAST ? (long)mbeg * p.ldx : (long)pix0 * p.C,
+                                                 FAST ? (long)p.M * p.ldx : (long)p.N * p.H * p.W * p.C);
 
   // (r, s, c0) of the two 64-column halves of this k tile (generic path only).
   int hr[2], hs[2], hc[2]; bool hv[2];
@@ -132,17 +136,17 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradParams p, int m_per_
 #pragma unroll
     for (int i = 0; i < GI; ++i) {  // gradient operand
       const uint32_t off = (full || mb + g_row[i] < mend) ? g_off[i] : OOB_OFF;
-      buf_lds16(rg, LDS_PTR(gb + (wave * GI + i) * 1024), off, mb * p.ldg * 2);
+      buf_lds16(rg, LDS_PTR(gb + (wave * GI + i) * 1024), off, (mb - mbeg) * p.ldg * 2);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // input operand
       const int row = (wave * 4 + i) * 4 + lrow;
       const bool mok = full || mb + row < mend;
       if (FAST) {
-        buf_lds16(rx, LDS_PTR(xb + (wave * 4 + i) * 1024), mok ? x_off[i] : OOB_OFF, mb * p.ldx * 2);
+        buf_lds16(rx, LDS_PTR(xb + (wave * 4 + i) * 1024), mok ? x_off[i] : OOB_OFF, (mb - mbeg) * p.ldx * 2);
       } else {
         const bool ok = mok && x_tap[i] < 32 && ((ri[i].y >> x_tap[i]) & 1);
-        const uint32_t off = ok ? (uint32_t)((ri[i].x * p.C + x_delta[i]) * 2) : OOB_OFF;
+        const uint32_t off = ok ? (uint32_t)(((ri[i].x - pix0) * p.C + x_delta[i]) * 2) : OOB_OFF;
         buf_lds16(rx, LDS_PTR(xb + (wave * 4 + i) * 1024), off, 0);
       }
     }
@@ -277,8 +281,12 @@ __global__ void __launch_bounds__(512, 1) wgrad8_kernel(WgradParams p, int m_per
   const int mend = min(p.M, mbeg + m_per_split);
   const int nit = (mend - mbeg + 63) / 64;
   if (nit <= 0) return;   // (block-uniform, before any barrier)
-  const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.g, p.M * p.ldg * 2);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, FAST ? p.M * p.ldx * 2 : p.N * p.H * p.W * p.C * 2);
+  // descriptors rebased at the split's first row / first image (as in wgrad_kernel)
+  const int n_first = FAST ? 0 : fdiv(mbeg, geo.mg_howo);
+  const long pix0 = (long)n_first * p.H * p.W;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc_at(p.g, (long)mbeg * p.ldg, (long)p.M * p.ldg);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, FAST ? (long)mbeg * p.ldx : pix0 * p.C,
+                                                 FAST ? (long)p.M * p.ldx : (long)p.N * p.H * p.W * p.C);
 
   // staging lanes: piece i of a half covers m-rows (2*wave + i)*4 .. +3, 16 chunks per row
   const int lrow = lane >> 4, lpos = lane & 15;
@@ -318,7 +326,7 @@ __global__ void __launch_bounds__(512, 1) wgrad8_kernel(WgradParams p, int m_per
       const int n = fdiv(m, geo.mg_howo), rem = m - n * p.Ho * p.Wo;
       gho[i] = fdiv(rem, geo.mg_wo);
       gwo[i] = rem - gho[i] * p.Wo;
-      gpix[i] = (n * p.H + gho[i] * p.stride - p.pad) * p.W + gwo[i] * p.stride - p.pad;
+      gpix[i] = ((n - n_first) * p.H + gho[i] * p.stride - p.pad) * p.W + gwo[i] * p.stride - p.pad;
     }
   }
   auto row_geometry = [&](int mb) {
@@ -352,7 +360,7 @@ __global__ void __launch_bounds__(512, 1) wgrad8_kernel(WgradParams p, int m_per
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const uint32_t off = (full || mb + prow[i] < mend) ? g_off[h][i] : OOB_OFF;
-        buf_lds16(rg, LDS_PTR(hb + (2 * wave + i) * 1024), off, mb * p.ldg * 2);
+        buf_lds16(rg, LDS_PTR(hb + (2 * wave + i) * 1024), off, (mb - mbeg) * p.ldg * 2);
       }
     } else {
       const int h = part == 1 ? 0 : 1;
@@ -362,7 +370,7 @@ __global__ void __launch_bounds__(512, 1) wgrad8_kernel(WgradParams p, int m_per
       for (int i = 0; i < 2; ++i) {
         if (FAST) {
           const bool mok = full || mb + prow[i] < mend;
-          buf_lds16(rx, LDS_PTR(hb + (2 * wave + i) * 1024), mok ? x_off[h][i] : OOB_OFF, mb * p.ldx * 2);
+          buf_lds16(rx, LDS_PTR(hb + (2 * wave + i) * 1024), mok ? x_off[h][i] : OOB_OFF, (mb - mbeg) * p.ldx * 2);
         } else {
           const uint32_t off = (rmask[i] & x_bit[h][i]) ? (uint32_t)(rpix2[i] + x_delta2[h][i]) : OOB_OFF;
           buf_lds16(rx, LDS_PTR(hb + (2 * wave + i) * 1024), off, 0);
@@ -576,21 +584,31 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
   if (p.Cout % 8 || p.ldg % 8 || (fast && p.ldx % 8)) return "wgrad: Cout / ldg / ldx must be multiples of 8";
   if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "wgrad: empty problem";
   if (!fast && p.R * p.S > 32) return "wgrad: at most 32 taps";
-  // 31-bit buffer byte offsets (0x80000000 marks out-of-range lanes)
-  if ((fast ? (long)p.M * p.ldx : (long)p.N * p.H * p.W * p.C) * 2 >= (1L << 31) ||
-      (long)p.M * p.ldg * 2 >= (1L << 31))
-    return "wgrad: operand too large for 31-bit buffer offsets";
-  if (g_wgrad8 && p.Cout >= 256 && p.K >= 256 && !window && p.splits <= 0 &&
-      (fast || ((long)p.N * p.H * p.W < (1L << 22) && 2L * p.C < (1L << 23)))) {
-    // one 256x256 block per CU: split the m reduction so tiles x splits ~ one round of CUs,
-    // each split at least 16 m-tiles (1024 rows)
-    const int cus = num_cus();
-    const int nt8 = ((p.Cout + 255) / 256) * ((p.K + 255) / 256);
-    int sp = (cus + nt8 / 2) / nt8;
-    const int cap = (p.M + g_wgrad8_min_rows - 1) / g_wgrad8_min_rows;
-    if (sp > cap) sp = cap;
-    if (sp < 1) sp = 1;
-    int mps = ((p.M + sp - 1) / sp + 63) / 64 * 64;
+  // element indices are ints; buffer byte offsets are 31-bit (0x80000000 marks out-of-range
+  // lanes) relative to each split's first row / image (the kernels rebase their descriptors
+  // there), so only one split's span has to fit
+  if ((long)p.N * p.H * p.W * p.C >= (1L << 31) || (long)p.M * p.ldg >= (1L << 31) ||
+      (fast && (long)p.M * p.ldx >= (1L << 31)))
+    return "wgrad: tensor has more than 2^31 elements";
+  const long HoWo = (long)p.Ho * p.Wo;
+  auto span_pix = [&](int mps) { return ((mps + 64) / HoWo + 2) * p.H * p.W; };
+  auto span_ok = [&](int mps) {
+    const long rows = mps + 64;
+    const long xs = fast ? rows * p.ldx : span_pix(mps) * p.C;
+    return xs * 2 < (1L << 31) - (1L << 24) && rows * p.ldg * 2 < (1L << 31) - (1L << 24);
+  };
+  // one 256x256 block per CU: split the m reduction so tiles x splits ~ one round of CUs,
+  // each split at least g_wgrad8_min_rows rows
+  const int nt8 = ((p.Cout + 255) / 256) * ((p.K + 255) / 256);
+  int sp = (num_cus() + nt8 / 2) / nt8;
+  const int cap = (p.M + g_wgrad8_min_rows - 1) / g_wgrad8_min_rows;
+  if (sp > cap) sp = cap;
+  if (sp < 1) sp = 1;
+  int mps8 = ((p.M + sp - 1) / sp + 63) / 64 * 64;
+  // (the generic gather steps pixel indices through 24-bit multiplies: < 2^22 pixels per split)
+  if (g_wgrad8 && p.Cout >= 256 && p.K >= 256 && !window && p.splits <= 0 && span_ok(mps8) &&
+      (fast || (span_pix(mps8) < (1L << 22) && 2L * p.C < (1L << 23)))) {
+    const int mps = mps8;
     sp = (p.M + mps - 1) / mps;
     Wg8Geom geo{};
     geo.mg_howo = fdiv_magic(p.Ho * p.Wo);
@@ -632,6 +650,8 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
   }
   int mps = (p.M + splits - 1) / splits;
   mps = (mps + 63) / 64 * 64;
+  while (!span_ok(mps) && mps > 64) mps = (mps / 2 + 63) / 64 * 64;   // (batches beyond ~1.5k)
+  if (!span_ok(mps)) return "wgrad: one 64-row tile spans more than 2 GiB";
   splits = (p.M + mps - 1) / mps;
   const int nwg = ntiles * splits;
   // 2 LDS stages + 2 blocks/CU (a 3-stage ring at 1 block/CU measured slower and was removed)

@@ -456,6 +456,46 @@ def test_wgrad8_vs_fp32(case, stagger):
     assert rel(outs[2], outs[1]) < 1e-5
 
 
+BIG_CASES = [
+    # N, H, C, Cout, R, stride, pad: each input is larger than the 31-bit buffer range
+    (5400, 56, 64, 64, 3, 1, 1),      # 3x3 halo gather: igemm AM_HALO, wgrad rowinfo gather
+    (1400, 56, 256, 256, 1, 1, 0),    # 1x1 rows: igemm direct, wgrad8 direct
+    (21500, 14, 256, 256, 3, 1, 1),   # 3x3 on wgrad8's stepped gather
+]
+
+
+@pytest.mark.parametrize("case", BIG_CASES)
+def test_operands_beyond_2gib(case):
+    """Activations larger than 2 GiB (b2048 training: the stage-1 tensors are 3.3 GB) go through
+    the per-tile / per-split rebased buffer descriptors.  Only the first and last 3 images are
+    non-zero, so an offset that wraps or starts from the wrong image shows up as wrong values
+    there or as non-zeros in between (forward), or as a wrong weight gradient."""
+    torch.manual_seed(7)
+    n, h, c, co, r, st, pad = case
+    ho = (h + 2 * pad - r) // st + 1
+    assert n * h * h * c * 2 > 2 ** 31
+    x = torch.zeros(n, h, h, c, dtype=torch.bfloat16, device=dev)
+    g = torch.zeros(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
+    ends = [slice(0, 3), slice(n - 3, n)]
+    for s in ends:
+        x[s] = rnd(3, h, h, c)
+        g[s] = rnd(3, ho, ho, co)
+    w = rnd(co, r, r, c, scale=0.05)
+    ones, zero = torch.ones(co, device=dev), torch.zeros(co, device=dev)
+    out = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
+    N().igemm(x, None, h, h, r, r, st, pad, ho, ho, w.view(co, -1), 0, ones, zero, None, None, None, out, 0,
+              None, 0, 0, 0, 0, 0, None, None)
+    for s in ends:
+        assert rel(out[s], conv_ref(x[s], w, st, pad)) < 1e-2
+    assert out[3:n - 3].count_nonzero().item() == 0
+    del out
+    dw = torch.zeros(co, r * r * c, device=dev)
+    N().wgrad(x, h, h, r, r, st, pad, ho, ho, g, None, 0, dw, r * r * c, 0)
+    ref = sum(torch.nn.grad.conv2d_weight(x[s].float().permute(0, 3, 1, 2), (co, c, r, r),
+                                          g[s].float().permute(0, 3, 1, 2), stride=st, padding=pad) for s in ends)
+    assert rel(dw, ref.permute(0, 2, 3, 1).reshape(co, -1)) < 5e-3
+
+
 @pytest.mark.parametrize("variant,h,c", [(0, 12, 64), (0, 13, 64), (1, 12, 64), (1, 13, 64), (2, 13, 64),
                                          (3, 12, 64), (3, 18, 64), (4, 12, 64), (4, 13, 64), (4, 35, 64),
                                          (4, 13, 128), (4, 18, 256)])
