@@ -304,6 +304,189 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
   }
 }
 
+// Register-direct (RD) epilogue.  The K loop ran with the MFMA operands swapped (weights as the
+// MFMA's A operand, activations as its B), so lane l of every 16x16 accumulator block [i][j]
+// holds FOUR CONSECUTIVE COLUMNS of one row: D[n = 16j + 4(l>>4) + jj][m = 16i + (l&15)].
+// One v_permlane16_swap per register pair of the column blocks (2q, 2q+1) (odd 16-lane rows of
+// the first operand <-> even rows of the second) turns those 4-column runs into 8-column
+// (16-byte) runs: lane group g = l>>4 then holds columns 32q + 16(g&1) + 8(g>>1) + 0..7 of row
+// 16i + (l&15) -- acc[i][2q][0..3] then acc[i][2q+1][0..3].  Each such chunk goes through the
+// same fused operations as the LDS-staged epilogue and is stored straight from registers: no
+// LDS staging (64 ds_write_b32 + 16 ds_read_b128 per lane), no barriers, and no epilogue LDS
+// (the block needs only its operand stages, so more blocks fit per CU).  A store instruction
+// writes 16 rows x 64 contiguous bytes (4 lanes per row).  Not for the train-mode BN sums
+// (stats / bn_z: those keep the staged epilogue).
+template <int TM, int TN>
+__device__ __forceinline__ void igemm_epilogue_rd(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
+                                                  int lane) {
+  static_assert(TN % 2 == 0, "the RD epilogue pairs column blocks");
+  constexpr int NP = TN / 2;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int cb = 16 * (g & 1) + 8 * (g >> 1);
+  const int HoWo = p.Ho * p.Wo;
+  const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
+  const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
+  const bf16_t* psrc = pre_on ? (p.mode == EPI_FWD ? p.res : p.add) : reinterpret_cast<const bf16_t*>(p.out);
+  const long pld = pre_on ? (p.mode == EPI_FWD ? p.ld_res : p.ld_add) : 0;
+  const uint8_t* bsrc = pf_bits ? p.bits_mask : reinterpret_cast<const uint8_t*>(p.out);
+  const long bld = pf_bits ? p.ld_bits_mask : 0;
+  // per-element operand (forward residual / dgrad residual-gradient) and ReLU bits of the TM
+  // chunks of column run q, loaded branch-free (row / column clamped, value zeroed) ahead of
+  // their use
+  uint4 pre[TM];
+  uint32_t pbits[TM];
+  auto load_pre = [&](int q) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int gm = mb + 16 * i + r16, gn = nb + 32 * q + cb;
+      const bool ok = gm < p.M && gn < p.Nn;
+      const long gr = gm < p.M ? gm : p.M - 1;
+      const int gc = gn < p.Nn ? gn : 0;
+      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + (pre_on ? gc : 0));
+      const uint32_t b = bsrc[gr * bld + (pf_bits ? (gc >> 3) : 0)];
+      pre[i] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
+      pbits[i] = (ok && pf_bits) ? b : 0u;
+    }
+  };
+  if (pre_on || pf_bits) load_pre(0);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * q][jj]),
+                                                        __float_as_uint(acc[i][2 * q + 1][jj]), false, false);
+        acc[i][2 * q][jj] = __uint_as_float(r[0]);
+        acc[i][2 * q + 1][jj] = __uint_as_float(r[1]);
+      }
+  float csum[NP][8];
+#pragma unroll
+  for (int q = 0; q < NP; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[q][e] = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    if (q > 0 && (pre_on || pf_bits)) load_pre(q);
+    const int gn = nb + 32 * q + cb;
+    const bool col_ok = gn < p.Nn;
+    float sc[8], sh[8];
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+    int ldo = p.ldo, col = gn;
+    bool relu = p.relu != 0, seg0 = true;
+    if (p.mode != EPI_DGRAD && col_ok) {
+      const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
+      const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
+      const float4 a = s4[0], b = s4[1], c = h4[0], d = h4[1];
+      sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+      sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
+      if (p.out2 && gn >= p.n_split) {
+        out = reinterpret_cast<bf16_t*>(p.out2); ldo = p.ldo2; relu = p.relu2 != 0; col = gn - p.n_split;
+        seg0 = false;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int gm = mb + 16 * i + r16;
+      if (gm >= p.M || !col_ok) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = acc[i][2 * q][e]; v[4 + e] = acc[i][2 * q + 1][e]; }
+      if (p.mode == EPI_FWD) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
+        if (p.res) {
+          float rv[8];
+          unpack8(pre[i], rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += rv[e];
+        }
+        if (relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        const uint4 pk = pack8(v);
+        *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pk;
+        if (p.bits_out && seg0) p.bits_out[(long)gm * p.ld_bits_out + (col >> 3)] = (uint8_t)pos_bits8(pk);
+      } else if (p.mode == EPI_F32) {
+        float* o = reinterpret_cast<float*>(p.out) + (long)gm * p.ldo + gn;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
+        reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+      } else {  // EPI_DGRAD (same operations as igemm_epilogue)
+        long row = gm;
+        int n = 0, ii = 0, jw = 0;
+        if (p.up2) {
+          n = fdiv(gm, p.mg_howo); const int rem = gm - n * HoWo; ii = fdiv(rem, p.mg_wo); jw = rem - ii * p.Wo;
+          row = ((long)n * p.Hf + 2 * ii) * p.Wf + 2 * jw;
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          long rq = row;
+          if (qq > 0) {
+            if (p.up2 != 1) break;
+            const int hh = 2 * ii + (qq >> 1), ww = 2 * jw + (qq & 1);
+            if (hh >= p.Hf || ww >= p.Wf) continue;
+            rq = ((long)n * p.Hf + hh) * p.Wf + ww;
+          }
+          float w[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] = (qq == 0) ? v[e] : 0.f;
+          if (p.add) {
+            float av[8];
+            uint4 a4;
+            if (!p.up2) a4 = pre[i];
+            else a4 = *reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn);
+            unpack8(a4, av);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] += av[e];
+          }
+          if (p.mask) {
+            float mv[8];
+            unpack8(*reinterpret_cast<const uint4*>(p.mask + rq * p.ld_mask + gn), mv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
+          } else if (p.bits_mask) {
+            uint32_t byte;
+            if (pf_bits) byte = pbits[i];
+            else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
+          }
+          const uint4 pk = pack8(w);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[q][e] += w[e];
+          *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pk;
+          if (qq == 0 && p.up2 && p.out2)
+            *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out2) + (long)gm * p.ldo2 + gn) = pk;
+        }
+      }
+    }
+  }
+  // partial column sums: fold the 16 lanes (rows) of each lane group, then lane r16 == 0 of
+  // every group stores its 8-column runs into the wave's partial row
+  if (p.colsum) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[q][e] += __shfl_xor(csum[q][e], o, 64);
+    if (r16 == 0) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int gn = nb + 32 * q + cb;
+        if (gn < p.Nn) {
+          float4* dst = reinterpret_cast<float4*>(p.colsum + (long)prow * p.Nn + gn);
+          dst[0] = make_float4(csum[q][0], csum[q][1], csum[q][2], csum[q][3]);
+          dst[1] = make_float4(csum[q][4], csum[q][5], csum[q][6], csum[q][7]);
+        }
+      }
+    }
+  }
+}
+
 // Block tile BM x BN of NW waves, each wave a 64x64 tile of 16x16x32 MFMAs.
 //   NW = 4, NSTAGE 1/2: 2 blocks per CU, the next k-tile's LDS-DMA overlaps this tile's MFMAs.
 //   NW = 8 (256x128), NSTAGE 3: one 144 KiB block per CU, 2 waves per SIMD; a 3-deep LDS ring
@@ -321,8 +504,9 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 // the slice bookkeeping compiled into every instantiation cost 33 VGPRs, occupancy 3 -> 2).
 // EPF: early epilogue-operand prefetch (igemm_epi_load issued right after the first k-tile's
 // LDS-DMA, so the residual / residual-gradient round trip overlaps the operand round trip).
+// RD: register-direct epilogue (igemm_epilogue_rd; MFMA operands swapped in the K loop).
 template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64, bool BNZ = false, bool SK = false,
-          bool EPF = false>
+          bool EPF = false, bool RD = false>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParams p) {
   constexpr int WTM = WTM_, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -335,7 +519,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // 1 KiB LDS-DMA pieces per wave per tile
   static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows must split evenly over the waves");
   constexpr int EPI_LD = WTN + 4;
-  constexpr int EPI_BYTES = NW * 32 * EPI_LD * 4;
+  constexpr int EPI_BYTES = RD ? 0 : NW * 32 * EPI_LD * 4;
   constexpr int SMEM = (NS * STAGE > EPI_BYTES) ? NS * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -503,8 +687,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (RD) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
         if (IL) {
 #pragma unroll
           for (int q = 0; q < PPG; ++q) {
@@ -537,6 +723,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
     return;
   }
 
+  if constexpr (RD) {
+    igemm_epilogue_rd<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, lane);
+    return;
+  }
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (WTN + 4));
   igemm_epilogue<TM, TN, PF || EPF, BNZ, EPF>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm,
@@ -912,6 +1102,8 @@ struct IgemmPlan { int cfg, split, ks; };
 
 int g_igemm_splitk = 1;
 int g_igemm_epf = 0;       // early epilogue-operand prefetch for the short-K single-stage tiles (A/B knob)
+int g_igemm_rd = 1;        // register-direct epilogue on the 4-wave tiles (igemm_epilogue_rd): 0 off,
+                           // 1 on (every unsplit cfg 0 / 1 launch without train-BN sums)
 
 // Split-K for layers with too few output tiles to fill the chip (small batches, small spatial
 // stages: stage 5 at batch 32-256, crop 160): the 4-wave tiles stay resident 2-3 per CU, so a
@@ -1062,6 +1254,25 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
       else { if (am == AM_DIRECT) IG_SK(256, 64, 2, AM_DIRECT); else IG_SK(256, 64, 2, AM_HALO); }
     }
 #undef IG_SK
+    return;
+  }
+  if (g_igemm_rd && cfg <= 1 && !p.stats && !p.bn_z && !il && !g_igemm_epf) {
+#define IG_RD(BM_, BN_, NS_, AM_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_, false, 64, false, false, false, true>), dim3(nwg), dim3(256), 0, \
+                     stream, p)
+#define IG_RD_MODES(BM_, BN_, NS_)                              \
+  {                                                             \
+    if (am == AM_DIRECT) IG_RD(BM_, BN_, NS_, AM_DIRECT);       \
+    else if (am == AM_HALO) IG_RD(BM_, BN_, NS_, AM_HALO);      \
+    else IG_RD(BM_, BN_, NS_, AM_DUAL);                         \
+  }
+    if (cfg == 1) {
+      if (ns == 1) IG_RD_MODES(128, 128, 1) else IG_RD_MODES(128, 128, 2)
+    } else {
+      if (ns == 1) IG_RD_MODES(256, 64, 1) else IG_RD_MODES(256, 64, 2)
+    }
+#undef IG_RD_MODES
+#undef IG_RD
     return;
   }
   // early prefetch (knob igemm_epf: 1 = single-stage tiles with a residual / residual-gradient

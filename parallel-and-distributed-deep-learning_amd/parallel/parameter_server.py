@@ -468,14 +468,20 @@ class PSWorker:
         if cl.impl == "native":
             if hasattr(self, "cli"):
                 self.cli.stop()
-            cl.store.set(f"fin/{cl.rank}", "1")
-            cl.store.add("fin_count", 1)
+            self._finish()
             return
         ctrl = torch.tensor([OP_STOP, 0.0], dtype=torch.float64, device=cl.device)
         for p in range(cl.num_ps):
             dist.send(ctrl, dst=p, group=cl.pair[(cl.rank, p)])
-        cl.store.set(f"fin/{cl.rank}", "1")
-        cl.store.add("fin_count", 1)
+        self._finish()
+
+    def _finish(self):
+        """Count this worker as finished BEFORE publishing its fin key: a worker that dies between
+        the two is then either counted (its fin_count add landed) or, with no fin key, declared
+        dead by the coordinator -- never neither, which would leave worker 0's final-save wait
+        short of its target until the timeout."""
+        self.cl.store.add("fin_count", 1)
+        self.cl.store.set(f"fin/{self.cl.rank}", "1")
 
 
 class _PSControl:

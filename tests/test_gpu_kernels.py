@@ -145,8 +145,12 @@ def test_igemm_dgrad(case):
     assert rel(cs, ref.sum((0, 1, 2))) < 1e-2
 
 
+KNOB_DEFAULTS = {"igemm_rd": 1}
+
+
 @pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1), ("igemm8", 1),
-                                      ("igemm8", 2), ("igemm", 2), ("igemm_epf", 1), ("igemm_epf", 2)])
+                                      ("igemm8", 2), ("igemm", 2), ("igemm_epf", 1), ("igemm_epf", 2),
+                                      ("igemm_rd", 1)])
 @pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual", "fwd1x1resid", "dgrad1x1add"])
 def test_igemm_big_tile_matches(kind, knob, big):
     """The 8-wave 256x128 3-stage (igemm_big 2) and 256x256 2-stage (igemm_big 4)
@@ -182,6 +186,7 @@ def test_igemm_big_tile_matches(kind, knob, big):
     N().set_variant("igemm8_min_tiles", 1)
     N().set_variant("igemm8_min_n", 256)       # (tiny problems: let the 8-phase kernel take them)
     N().set_variant("igemm8", 0)                 # baseline: the 128x128 tile
+    default = KNOB_DEFAULTS.get(knob, 0)
     for kv in (0, big):
         N().set_variant(knob, kv)
         try:
@@ -218,7 +223,7 @@ def test_igemm_big_tile_matches(kind, knob, big):
                           1, h, h, part, None)
                 outs.append(torch.cat([out.float().flatten(), _fold(part, rows, 256)]))
         finally:
-            N().set_variant(knob, 0)
+            N().set_variant(knob, default)
     N().set_variant("igemm8_min_tiles", 128)
     N().set_variant("igemm8_min_n", 512)
     N().set_variant("igemm8", 2)
