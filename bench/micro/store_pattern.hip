@@ -6,6 +6,7 @@
 //   rows   : 64-row x 256-col block tiles; one instruction = 2 rows x 512 B (full rows)
 //   tile_rd: the tile pattern plus a same-shaped read of a second tensor (residual add)
 //   rows_rd: the rows pattern plus the same read
+//   read   : pure streaming read (1 KiB per wave instruction), copy: streaming read + write
 // hipcc --offload-arch=gfx950 -O3 bench/micro/store_pattern.hip -o /tmp/store_pattern
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -53,6 +54,22 @@ __global__ void __launch_bounds__(256) k_rows(uint4* out, const uint4* in, int M
   }
 }
 
+// pure read: every wave instruction loads 1 KiB contiguous; the per-thread sum is stored once
+__global__ void __launch_bounds__(256) k_read(const uint4* in, uint4* out, long n16) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const uint4 v = in[i];
+    acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+  }
+  out[(long)blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+// streaming copy (read 1 KiB + write 1 KiB per wave instruction pair)
+__global__ void __launch_bounds__(256) k_copy(const uint4* in, uint4* out, long n16) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) out[i] = in[i];
+}
+
 int main() {
   const int M = 1024 * 56 * 56;
   const long n16 = (long)M * 32;
@@ -63,7 +80,7 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const double bytes = (double)n16 * 16;
-  for (int pat = 0; pat < 5; ++pat) {
+  for (int pat = 0; pat < 7; ++pat) {
     float best = 1e30f;
     for (int rep = 0; rep < 6; ++rep) {
       CK(hipEventRecord(e0));
@@ -72,13 +89,15 @@ int main() {
       if (pat == 2) hipLaunchKernelGGL(k_rows<false>, dim3(M / 64), dim3(256), 0, 0, out, in, M);
       if (pat == 3) hipLaunchKernelGGL(k_tile<true>, dim3((M / 128) * 2), dim3(256), 0, 0, out, in, M);
       if (pat == 4) hipLaunchKernelGGL(k_rows<true>, dim3(M / 64), dim3(256), 0, 0, out, in, M);
+      if (pat == 5) hipLaunchKernelGGL(k_read, dim3(256 * 32), dim3(256), 0, 0, in, out, n16);
+      if (pat == 6) hipLaunchKernelGGL(k_copy, dim3(256 * 32), dim3(256), 0, 0, in, out, n16);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       if (rep > 0 && ms < best) best = ms;
     }
-    const char* nm[] = {"linear", "tile", "rows", "tile_rd", "rows_rd"};
-    const double b = bytes * (pat >= 3 ? 2 : 1);
+    const char* nm[] = {"linear", "tile", "rows", "tile_rd", "rows_rd", "read", "copy"};
+    const double b = bytes * ((pat == 3 || pat == 4 || pat == 6) ? 2 : 1);
     printf("{\"pattern\": \"%s\", \"us\": %.1f, \"TBps\": %.2f}\n", nm[pat], best * 1e3, b / (best * 1e-3) / 1e12);
   }
   return 0;

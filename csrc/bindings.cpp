@@ -585,6 +585,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm_splitk") pddl::g_igemm_splitk = v;
     else if (which == "igemm_epf") pddl::g_igemm_epf = v;
     else if (which == "igemm_rd") pddl::g_igemm_rd = v;
+    else if (which == "igemm_pk_all") pddl::g_igemm_pk_all = v;
+    else if (which == "igemm_pk") { TORCH_CHECK(v == 0 || (v >= 2 && v <= 4), "igemm_pk: 0 or ring depth 2-4"); pddl::g_igemm_pk = v; }
     else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
     else if (which == "igemm8_ragged") pddl::g_igemm8_ragged = v;

@@ -79,8 +79,10 @@ __host__ __device__ __forceinline__ long lmin(long a, long b) { return a < b ? a
 // arithmetic: a workgroup's lane offsets (relative to the first image / row its tile reads)
 // stay 32-bit at any batch, and the record count is clamped below OOB_OFF so that marker
 // still reads zeros.  This is what lets one GPU train at b2048 (stage-1 activations > 2 GiB).
+// (An empty range -- e_end <= e0 -- gives a zero-size descriptor: every access reads zeros / is dropped.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_at(const uint16_t* base, long e0, long e_end) {
-  return make_rsrc(base + e0, (int)lmin((e_end - e0) * 2, 0x7fffffffL));
+  const long bytes = (e_end - e0) * 2;
+  return make_rsrc(base + e0, (int)(bytes <= 0 ? 0 : lmin(bytes, 0x7fffffffL)));
 }
 
 // Division by a runtime divisor d as one 64-bit multiply + shift: exact for

@@ -305,99 +305,125 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 }
 
 // Register-direct (RD) epilogue.  The K loop ran with the MFMA operands swapped (weights as the
-// MFMA's A operand, activations as its B), so lane l of every 16x16 accumulator block [i][j]
-// holds FOUR CONSECUTIVE COLUMNS of one row: D[n = 16j + 4(l>>4) + jj][m = 16i + (l&15)].
-// One v_permlane16_swap per register pair of the column blocks (2q, 2q+1) (odd 16-lane rows of
-// the first operand <-> even rows of the second) turns those 4-column runs into 8-column
-// (16-byte) runs: lane group g = l>>4 then holds columns 32q + 16(g&1) + 8(g>>1) + 0..7 of row
-// 16i + (l&15) -- acc[i][2q][0..3] then acc[i][2q+1][0..3].  Each such chunk goes through the
-// same fused operations as the LDS-staged epilogue and is stored straight from registers: no
-// LDS staging (64 ds_write_b32 + 16 ds_read_b128 per lane), no barriers, and no epilogue LDS
-// (the block needs only its operand stages, so more blocks fit per CU).  A store instruction
-// writes 16 rows x 64 contiguous bytes (4 lanes per row).  Not for the train-mode BN sums
-// (stats / bn_z: those keep the staged epilogue).
-template <int TM, int TN>
-__device__ __forceinline__ void igemm_epilogue_rd(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
-                                                  int lane) {
-  static_assert(TN % 2 == 0, "the RD epilogue pairs column blocks");
-  constexpr int NP = TN / 2;
-  const int g = lane >> 4, r16 = lane & 15;
-  const int cb = 16 * (g & 1) + 8 * (g >> 1);
-  const int HoWo = p.Ho * p.Wo;
+// MFMA's A operand, activations as its B), so lane l = 16g + r of every 16x16 accumulator block
+// [i][j] holds FOUR CONSECUTIVE COLUMNS of one row: D[n = 16j + 4g + jj][m = 16i + r].
+//  1. One v_permlane16_swap per register pair of the column blocks (2q, 2q+1) (odd 16-lane rows
+//     of the first operand <-> even rows of the second) turns the 4-column runs into 8-column
+//     (16-byte) runs: lane (g, r) then holds columns 32q + cb(g) + 0..7 of row 16i + r,
+//     cb(g) = 16(g&1) + 8(g>>1), in acc[i][2q][0..3], acc[i][2q+1][0..3].
+//  2. One DPP row_ror:8 move per value exchanges run q = 1 of lane r < 8 with run q = 0 of lane
+//     r + 8: afterwards lane (g, r) holds run q = r >> 3 of rows 16i + (r & 7) and 16i + 8 + (r & 7)
+//     (acc[i][0..1] and acc[i][2..3]), so every store instruction writes 8 rows x 128 contiguous
+//     bytes (8 lanes per row: 4 groups x 2 runs) -- the store shape of the LDS-staged epilogue.
+//     (Without it, 16 rows x 64 B per instruction: measured 25-35 % slower on the short-K layers.)
+// Each lane then has ONE column set (8 scale / shift values, 8 column sums), and every chunk goes
+// through the same fused operations as the LDS-staged epilogue, stored straight from registers:
+// no LDS staging (64 ds_write_b32 + 16 ds_read_b128 per lane), no barriers, no epilogue LDS.
+// 4-wave tiles with 64-column wave tiles only (TN = 4); not for the train-mode BN sums.
+// Epilogue operands of the RD chunk layout: per-element operand (forward residual / dgrad
+// residual-gradient) and ReLU bits of chunk (i, h) = row 16i + 8h + r8 at this lane's 8 columns.
+// Branch-free and unconditional: exactly 2 * TM 16-byte + 2 * TM 1-byte loads per lane (row /
+// column clamped into the tensor, value zeroed; an unused operand reads the output's first
+// element), so a caller that counts its vector-memory operations (igemm_pk_kernel) can rely
+// on the number.
+template <int TM>
+__device__ __forceinline__ void igemm_rd_prefetch(const IgemmParams& p, int mb, int nb, int lane, uint4 (&pre)[TM][2],
+                                                  uint32_t (&pbits)[TM][2]) {
+  const int g = lane >> 4, r = lane & 15, r8 = r & 7;
+  const int gn = nb + 32 * (r >> 3) + 16 * (g & 1) + 8 * (g >> 1);
+  const bool col_ok = gn < p.Nn;
   const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
   const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
   const bf16_t* psrc = pre_on ? (p.mode == EPI_FWD ? p.res : p.add) : reinterpret_cast<const bf16_t*>(p.out);
   const long pld = pre_on ? (p.mode == EPI_FWD ? p.ld_res : p.ld_add) : 0;
   const uint8_t* bsrc = pf_bits ? p.bits_mask : reinterpret_cast<const uint8_t*>(p.out);
   const long bld = pf_bits ? p.ld_bits_mask : 0;
-  // per-element operand (forward residual / dgrad residual-gradient) and ReLU bits of the TM
-  // chunks of column run q, loaded branch-free (row / column clamped, value zeroed) ahead of
-  // their use
-  uint4 pre[TM];
-  uint32_t pbits[TM];
-  auto load_pre = [&](int q) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int gm = mb + 16 * i + r16, gn = nb + 32 * q + cb;
-      const bool ok = gm < p.M && gn < p.Nn;
-      const long gr = gm < p.M ? gm : p.M - 1;
-      const int gc = gn < p.Nn ? gn : 0;
-      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + (pre_on ? gc : 0));
-      const uint32_t b = bsrc[gr * bld + (pf_bits ? (gc >> 3) : 0)];
-      pre[i] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
-      pbits[i] = (ok && pf_bits) ? b : 0u;
-    }
-  };
-  if (pre_on || pf_bits) load_pre(0);
+  const int gc = col_ok ? gn : 0;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int q = 0; q < NP; ++q)
+    for (int h = 0; h < 2; ++h) {
+      const int gm = mb + 16 * i + 8 * h + r8;
+      const bool ok = gm < p.M && col_ok;
+      const long gr = gm < p.M ? gm : p.M - 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + (pre_on ? gc : 0));
+      const uint32_t b = bsrc[gr * bld + (pf_bits ? (gc >> 3) : 0)];
+      pre[i][h] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
+      pbits[i][h] = (ok && pf_bits) ? b : 0u;
+    }
+}
+
+// EXT: the caller already prefetched the epilogue operands (igemm_rd_prefetch) into pre / pbits;
+// otherwise they are loaded here, after the shuffles.
+template <int TM, int TN, bool EXT = false>
+__device__ __forceinline__ void igemm_epilogue_rd(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
+                                                  int lane, uint4 (&pre)[TM][2], uint32_t (&pbits)[TM][2]) {
+  static_assert(TN == 4, "the RD epilogue exchanges the two 32-column runs of a 64-column wave tile");
+  const int g = lane >> 4, r = lane & 15, r8 = r & 7;
+  const int gn = nb + 32 * (r >> 3) + 16 * (g & 1) + 8 * (g >> 1);   // this lane's 8 columns
+  const bool col_ok = gn < p.Nn;
+  const int HoWo = p.Ho * p.Wo;
+  // rows of chunk (i, h): 16i + 8h + r8
+  const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
+  const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * q][jj]),
-                                                        __float_as_uint(acc[i][2 * q + 1][jj]), false, false);
-        acc[i][2 * q][jj] = __uint_as_float(r[0]);
-        acc[i][2 * q + 1][jj] = __uint_as_float(r[1]);
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * q][jj]),
+                                                         __float_as_uint(acc[i][2 * q + 1][jj]), false, false);
+        acc[i][2 * q][jj] = __uint_as_float(sw[0]);
+        acc[i][2 * q + 1][jj] = __uint_as_float(sw[1]);
       }
-  float csum[NP][8];
+    // run q0 = acc[i][0..1], run q1 = acc[i][2..3]: lanes r >= 8 take run q1 of lane r - 8 into
+    // their first chunk, lanes r < 8 take run q0 of lane r + 8 into their second (DPP row_ror:8
+    // with the bank mask selecting the written half of each 16-lane row; the other half keeps
+    // its own value -- no selects, no extra live registers)
 #pragma unroll
-  for (int q = 0; q < NP; ++q)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) csum[q][e] = 0.f;
-#pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    if (q > 0 && (pre_on || pf_bits)) load_pre(q);
-    const int gn = nb + 32 * q + cb;
-    const bool col_ok = gn < p.Nn;
-    float sc[8], sh[8];
-    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-    int ldo = p.ldo, col = gn;
-    bool relu = p.relu != 0, seg0 = true;
-    if (p.mode != EPI_DGRAD && col_ok) {
-      const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
-      const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
-      const float4 a = s4[0], b = s4[1], c = h4[0], d = h4[1];
-      sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
-      sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
-      if (p.out2 && gn >= p.n_split) {
-        out = reinterpret_cast<bf16_t*>(p.out2); ldo = p.ldo2; relu = p.relu2 != 0; col = gn - p.n_split;
-        seg0 = false;
+      for (int jj = 0; jj < 4; ++jj) {
+        const int c0 = __float_as_int(acc[i][j][jj]), c1 = __float_as_int(acc[i][2 + j][jj]);
+        acc[i][j][jj] = __int_as_float(__builtin_amdgcn_update_dpp(c0, c1, 0x128, 0xf, 0xc, false));      // row 16i + r8
+        acc[i][2 + j][jj] = __int_as_float(__builtin_amdgcn_update_dpp(c1, c0, 0x128, 0xf, 0x3, false));  // row 16i + 8 + r8
       }
+  }
+  if constexpr (!EXT) {
+    if (pre_on || pf_bits) igemm_rd_prefetch<TM>(p, mb, nb, lane, pre, pbits);
+  }
+  float sc[8], sh[8];
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  int ldo = p.ldo, col = gn;
+  bool relu = p.relu != 0, seg0 = true;
+  if (p.mode != EPI_DGRAD && col_ok) {
+    const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
+    const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
+    const float4 a = s4[0], b = s4[1], c = h4[0], d = h4[1];
+    sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+    sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
+    if (p.out2 && gn >= p.n_split) {
+      out = reinterpret_cast<bf16_t*>(p.out2); ldo = p.ldo2; relu = p.relu2 != 0; col = gn - p.n_split;
+      seg0 = false;
     }
+  }
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int gm = mb + 16 * i + r16;
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int gm = mb + 16 * i + 8 * h + r8;
       if (gm >= p.M || !col_ok) continue;
       float v[8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] = acc[i][2 * q][e]; v[4 + e] = acc[i][2 * q + 1][e]; }
+      for (int e = 0; e < 4; ++e) { v[e] = acc[i][2 * h][e]; v[4 + e] = acc[i][2 * h + 1][e]; }
       if (p.mode == EPI_FWD) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
         if (p.res) {
           float rv[8];
-          unpack8(pre[i], rv);
+          unpack8(pre[i][h], rv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += rv[e];
         }
@@ -436,7 +462,7 @@ __device__ __forceinline__ void igemm_epilogue_rd(const IgemmParams& p, v4f (&ac
           if (p.add) {
             float av[8];
             uint4 a4;
-            if (!p.up2) a4 = pre[i];
+            if (!p.up2) a4 = pre[i][h];
             else a4 = *reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn);
             unpack8(a4, av);
 #pragma unroll
@@ -449,40 +475,31 @@ __device__ __forceinline__ void igemm_epilogue_rd(const IgemmParams& p, v4f (&ac
             for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
           } else if (p.bits_mask) {
             uint32_t byte;
-            if (pf_bits) byte = pbits[i];
+            if (pf_bits) byte = pbits[i][h];
             else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
 #pragma unroll
             for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
           }
           const uint4 pk = pack8(w);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) csum[q][e] += w[e];
+          for (int e = 0; e < 8; ++e) csum[e] += w[e];
           *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pk;
           if (qq == 0 && p.up2 && p.out2)
             *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out2) + (long)gm * p.ldo2 + gn) = pk;
         }
       }
     }
-  }
-  // partial column sums: fold the 16 lanes (rows) of each lane group, then lane r16 == 0 of
-  // every group stores its 8-column runs into the wave's partial row
+  // partial column sums: fold the 8 lanes (r8) sharing this lane's columns, then lane r8 == 0 of
+  // each (group, run) stores its 8 columns into the wave's partial row
   if (p.colsum) {
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1)
+    for (int o = 1; o < 8; o <<= 1)
 #pragma unroll
-      for (int q = 0; q < NP; ++q)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) csum[q][e] += __shfl_xor(csum[q][e], o, 64);
-    if (r16 == 0) {
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        const int gn = nb + 32 * q + cb;
-        if (gn < p.Nn) {
-          float4* dst = reinterpret_cast<float4*>(p.colsum + (long)prow * p.Nn + gn);
-          dst[0] = make_float4(csum[q][0], csum[q][1], csum[q][2], csum[q][3]);
-          dst[1] = make_float4(csum[q][4], csum[q][5], csum[q][6], csum[q][7]);
-        }
-      }
+      for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
+    if (r8 == 0 && col_ok) {
+      float4* dst = reinterpret_cast<float4*>(p.colsum + (long)prow * p.Nn + gn);
+      dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
     }
   }
 }
@@ -724,7 +741,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   }
 
   if constexpr (RD) {
-    igemm_epilogue_rd<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, lane);
+    uint4 pre[TM][2];
+    uint32_t pbits[TM][2];
+    igemm_epilogue_rd<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, lane, pre,
+                              pbits);
     return;
   }
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
@@ -733,6 +753,378 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
                                               stage, lane, epre, ebits);
 }
 
+
+// Persistent ring implicit GEMM for the short-K 1x1 layers (K = 64 * KT, KT <= 8): the
+// expansion 1x1s of every block in forward, whose epilogue streams the residual, and the 1x1
+// dgrads with their residual-gradient add and ReLU bits (cdna_hip_programming §5.6, loader
+// ring).  The single-stage tiles run those layers at 3.4-4.8 TB/s: each block is a serial chain
+// load -> MFMA -> load ... -> residual load -> store, overlapped only across 3 resident blocks.
+//
+// One launch of #CUs x (LDS / ring) workgroups; each owns a contiguous range of 128x128 output
+// tiles (column tiles fastest: consecutive tiles re-read the same A rows from L2; the XCD remap
+// keeps neighbouring ranges on one XCD).  A tile is SPT = KT (+1) RING STEPS of 32 KiB: its KT
+// k-steps (A | B operand tiles) and, when the epilogue has a per-element operand, one OPERAND
+// step (the residual / residual-gradient tile, plus its ReLU-bit rows or, forward, the tile's
+// scale / shift columns: the epilogue issues no global load at all).  Every step is
+// LDS-DMA; step s + NB - 1 is issued right after step s landed, so NB - 1 steps are always in
+// flight ACROSS tile boundaries: while a tile's epilogue runs, the next tile's operands and
+// residual are already on their way.  The epilogue is register direct (the igemm_epilogue_rd
+// shuffles) and reads its operand from the ring slot; its stores are branch-free buffer stores
+// (out-of-range rows / columns get the out-of-range offset, which the hardware drops).
+//
+// vmcnt bookkeeping (loads, stores and LDS-DMA share one in-order counter): a k-step is exactly
+// PPS = 8 LDS-DMA pieces per wave, an operand step op_n (8 residual pieces + 2 four-byte ReLU-bit
+// pieces, or 1 scale / shift piece), a tile epilogue e_n stores; steps past the block's range are issued anyway (zeros
+// from out-of-range offsets into a slot nobody reads), so every count is a launch constant and
+// the wait for step s counts exactly the younger operations (rounded down: a lower bound only
+// makes the wait stricter).  AM_DIRECT only (1x1, any stride); no stride-2 scatter, no split
+// outputs, no train-BN sums (those layers keep igemm_kernel).
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int cdiv_signed(int a, int b) { return a >= 0 ? (a + b - 1) / b : -((-a) / b); }
+// LDS chunk swizzle of the operand tile ([128 rows][16 chunks of 16 B], row-major): the RD
+// epilogue's ds_read_b128 serves 8 rows x 2 chunks per 16 lanes; XOR-ing the chunk with
+// (row & 3) | (row & 4) << 1 keeps those 16 positions distinct (conflict-free).
+__device__ __forceinline__ int pk_sw(int row) { return (row & 3) | ((row & 4) << 1); }
+
+template <int KT, int NB, bool OPS>
+__global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmParams p) {
+  constexpr int BM = 128, BN = 128, NW = 4, TM = 4, TN = 4, WAVES_N = 2;
+  constexpr int A_BYTES = BM * 128, STAGE = A_BYTES + BN * 128;   // 32 KiB: A | B, or the operand tile
+  constexpr int BITS_BYTES = BM * 16;                             // ReLU-bit rows of one tile
+  constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW), PPS = AI + BI;
+  constexpr int SPT = KT + (OPS ? 1 : 0);
+  static_assert(NB >= 2 && NB * (STAGE + (OPS ? BITS_BYTES : 0)) <= 160 * 1024, "ring must fit the LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NB * STAGE + (OPS ? NB * BITS_BYTES : 1)];
+  char* bits_lds = smem + NB * STAGE;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int mt = (p.M - p.m_begin + BM - 1) / BM, nt = (p.Nn + BN - 1) / BN;
+  const int T = mt * nt, G = gridDim.x;
+  // tiles bq, bq + G, bq + 2G, ...: at any moment the co-resident workgroups of one XCD (consecutive
+  // bq after the remap) work on consecutive tiles, i.e. on all column tiles of a few row tiles,
+  // so each A row block is fetched once and shared through that XCD's L2 (a contiguous range
+  // per workgroup re-fetched A for every column tile: measured 2.4x the fabric reads)
+  const int bq = xcd_remap(blockIdx.x, G);
+  if (bq >= T) return;   // (whole workgroup)
+  const int t_begin = bq, t_end = T;
+  const long HW = (long)p.H * p.W, pix_end = p.N * HW;
+  const int HoWo = p.Ho * p.Wo;
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
+
+  // launch-uniform epilogue configuration and the vector-memory op counts it implies
+  const bool is_fwd = p.mode == EPI_FWD;
+  const uint16_t* opnd = is_fwd ? p.res : p.add;
+  const int ld_op = is_fwd ? p.ld_res : p.ld_add;
+  const bool res_on = OPS && opnd != nullptr;
+  const bool bits_in = OPS && !is_fwd && p.bits_mask != nullptr;
+  const bool bits_out = is_fwd && p.bits_out != nullptr;
+  const bool csum_on = !is_fwd && p.colsum != nullptr;
+  const int op_n = (res_on ? 8 : 0) + (bits_in ? 2 : 0) + (is_fwd ? 1 : 0);
+  const int e_n = 2 * TM * (bits_out ? 2 : 1) + (csum_on ? 2 : 0);
+
+  // ---- loader: LDS-DMA of ring step (ld_t, ld_j) ----
+  int ld_t = t_begin, ld_j = 0;
+  uint32_t a_o[AI], b_o[BI];
+  __amdgpu_buffer_rsrc_t ra;
+  auto set_tile = [&](int t) {
+    const int m0 = p.m_begin + (t / nt) * BM, n0 = (t % nt) * BN;
+    const int n_first = fdiv(m0, p.mg_howo);
+    ra = make_rsrc_at(p.a1, n_first * HW * p.C1, pix_end * p.C1);
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int m = m0 + (wave * AI + i) * 8 + (lane >> 3);
+      a_o[i] = OOB_OFF;
+      if (m < p.M) {
+        const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
+        const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
+        const int pix = ((n - n_first) * p.H + ho * p.stride) * p.W + wo * p.stride;
+        a_o[i] = (uint32_t)((pix * p.C1 + sw_chunk(lane, i) * 8) * 2);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int n = n0 + (wave * BI + i) * 8 + (lane >> 3);
+      b_o[i] = (n < p.Nn) ? (uint32_t)((n * p.ldb + sw_chunk(lane, i) * 8) * 2) : OOB_OFF;
+    }
+  };
+  set_tile(t_begin);
+  auto issue = [&](int buf) {
+    const bool live = ld_t < t_end;    // (uniform) past the range: zeros into a slot nobody reads
+    char* base = smem + buf * STAGE;
+    if (!OPS || ld_j < KT) {           // k-step: channels [64 ld_j, 64 ld_j + 64) of the rows
+      const int kofs = ld_j * 128;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) buf_lds16(ra, LDS_PTR(base + (wave * AI + i) * 1024), live ? a_o[i] : OOB_OFF, kofs);
+#pragma unroll
+      for (int i = 0; i < BI; ++i)
+        buf_lds16(rb, LDS_PTR(base + A_BYTES + (wave * BI + i) * 1024), live ? b_o[i] : OOB_OFF, kofs);
+    } else {                           // operand step: rows 32 wave + 4 i + lane / 16, chunk (lane & 15)
+      const int lt = live ? ld_t : t_begin;   // (past the range: a valid tile's descriptors, zero reads)
+      const int m0 = p.m_begin + (lt / nt) * BM, n0 = (lt % nt) * BN;
+      if (res_on) {
+        const __amdgpu_buffer_rsrc_t ro = make_rsrc_at(opnd, (long)m0 * ld_op, (long)p.M * ld_op);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int row = wave * 32 + i * 4 + (lane >> 4);
+          const int ch = (lane & 15) ^ pk_sw(row);
+          const int col = n0 + ch * 8;
+          const bool ok = live && m0 + row < p.M && col < p.Nn;
+          buf_lds16(ro, LDS_PTR(base + (wave * 32 + i * 4) * 256), ok ? (uint32_t)((row * ld_op + col) * 2) : OOB_OFF, 0);
+        }
+      }
+      if (is_fwd) {                    // the tile's 128 scale | 128 shift values: one 256 B piece per wave
+        const float* src = wave < 2 ? p.scale : p.shift;
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, p.Nn * 4);
+        const int col = n0 + (wave & 1) * 64 + lane;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(bits_lds + buf * BITS_BYTES + wave * 256), 4,
+                                                 live && col < p.Nn ? (uint32_t)(col * 4) : OOB_OFF, 0, 0, 0);
+      }
+      if (bits_in) {                   // 16 bytes (128 columns) per row, 4 bytes per lane
+        const int ldb8 = p.ld_bits_mask;
+        const __amdgpu_buffer_rsrc_t rbm =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.bits_mask) + (long)m0 * ldb8, (short)0,
+                                              (int)lmin(((long)p.M - m0) * ldb8, 0x7fffffffL), 0x00020000);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int row = wave * 32 + q * 16 + (lane >> 2);
+          const int byte = (n0 >> 3) + (lane & 3) * 4;
+          const bool ok = live && m0 + row < p.M && byte * 8 < p.Nn;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rbm, LDS_PTR(bits_lds + buf * BITS_BYTES + (wave * 32 + q * 16) * 16), 4,
+                                                   ok ? (uint32_t)(row * ldb8 + byte) : OOB_OFF, 0, 0, 0);
+        }
+      }
+    }
+    if (++ld_j == SPT) {
+      ld_j = 0;
+      ld_t += G;
+      if (ld_t < t_end) set_tile(ld_t);
+    }
+  };
+  // wait until step s landed in every wave's view: `younger` = vector-memory ops this wave issued
+  // after it (a lower bound is safe); vmcnt takes an immediate, so buckets of 4
+  auto wait_barrier = [&](int younger) {
+    switch ((younger > 63 ? 63 : younger) >> 2) {
+#define PK_W(n, c) case n: asm volatile("s_waitcnt vmcnt(" #c ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+      PK_W(1, 4) PK_W(2, 8) PK_W(3, 12) PK_W(4, 16) PK_W(5, 20) PK_W(6, 24) PK_W(7, 28) PK_W(8, 32) PK_W(9, 36)
+      PK_W(10, 40) PK_W(11, 44) PK_W(12, 48) PK_W(13, 52) PK_W(14, 56) PK_W(15, 60)
+#undef PK_W
+      default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    }
+  };
+
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j) issue(j);   // prologue: ring steps 0 .. NB-2
+  int cur = 0;                                   // ring slot of the current step
+  const int a_off = (wm * 64 + (lane & 15)) * 128;
+  const int b_off = (wn * 64 + (lane & 15)) * 128;
+  const int g = lane >> 4, r = lane & 15, r8 = r & 7;
+  const int lc = wn * 64 + 32 * (r >> 3) + 16 * (g & 1) + 8 * (g >> 1);   // this lane's 8 columns in the tile
+  for (int t = t_begin, u = 0; t < t_end; t += G, ++u) {
+    const int m0 = p.m_begin + (t / nt) * BM, n0 = (t % nt) * BN;
+    v4f acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    int op_slot = 0;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      // younger than step s = u * SPT + j: steps s+1 .. s+NB-2, and the epilogues of tiles
+      // v in [u - 1 + cdiv(j - NB + 2, SPT), u - 1] (issued after step s was)
+      int y = 0;
+#pragma unroll
+      for (int x = 1; x <= NB - 2; ++x) y += (OPS && (j + x) % SPT == KT) ? op_n : PPS;
+      int ce = 1 - cdiv_signed(j - NB + 2, SPT);
+      ce = ce < 0 ? 0 : (ce > u ? u : ce);
+      wait_barrier(y + ce * e_n);
+      issue(cur == 0 ? NB - 1 : cur - 1);        // step s + NB - 1 into the slot step s - 1 used
+      if (!OPS || j < KT) {
+        const char* As = smem + cur * STAGE;
+        const char* Bs = As + A_BYTES;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          const int pos = sw_read(lane, kh);
+          v8bf af[TM], bfr[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const v8bf*>(As + a_off + i * 16 * 128 + pos);
+#pragma unroll
+          for (int jn = 0; jn < TN; ++jn) bfr[jn] = *reinterpret_cast<const v8bf*>(Bs + b_off + jn * 16 * 128 + pos);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jn = 0; jn < TN; ++jn)
+              acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
+        }
+      } else {
+        op_slot = cur;
+      }
+      cur = cur + 1 == NB ? 0 : cur + 1;
+    }
+
+    // ---------------- epilogue (register direct; operand from the ring slot) ----------------
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * q][jj]),
+                                                           __float_as_uint(acc[i][2 * q + 1][jj]), false, false);
+          acc[i][2 * q][jj] = __uint_as_float(sw[0]);
+          acc[i][2 * q + 1][jj] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int c0 = __float_as_int(acc[i][j][jj]), c1 = __float_as_int(acc[i][2 + j][jj]);
+          acc[i][j][jj] = __int_as_float(__builtin_amdgcn_update_dpp(c0, c1, 0x128, 0xf, 0xc, false));
+          acc[i][2 + j][jj] = __int_as_float(__builtin_amdgcn_update_dpp(c1, c0, 0x128, 0xf, 0x3, false));
+        }
+    }
+    const int gn = n0 + lc;
+    const bool col_ok = gn < p.Nn;
+    const char* bits_base = bits_lds + op_slot * BITS_BYTES;
+    float sc[8], sh[8];
+    if (is_fwd) {
+      // from the operand step (no global load whose wait would drain the ring), read as inline
+      // asm: the compiler drains the LDS-DMA queue (vmcnt(0)) before a ds_read it cannot tell
+      // apart from the four-byte DMA targets
+      float4 a, b, c, d;
+      const uint32_t sa = (uint32_t)(uintptr_t)LDS_PTR(bits_base + lc * 4);
+      asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+                   "ds_read_b128 %2, %4 offset:512\n\tds_read_b128 %3, %4 offset:528\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d) : "v"(sa) : "memory");   // (early clobber: the
+                                                                                  // address must survive)
+      sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+      sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
+    }
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_at(reinterpret_cast<const uint16_t*>(p.out), (long)m0 * p.ldo,
+                                                     (long)p.M * p.ldo);
+    const __amdgpu_buffer_rsrc_t rbo =
+        __builtin_amdgcn_make_buffer_rsrc(bits_out ? p.bits_out + (long)m0 * p.ld_bits_out : reinterpret_cast<uint8_t*>(p.out),
+                                          (short)0, bits_out ? (int)lmin(((long)p.M - m0) * p.ld_bits_out, 0x7fffffffL) : 0,
+                                          0x00020000);
+    char* op_w = smem + op_slot * STAGE;
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // Every LDS access of the epilogue is inline asm: the compiler cannot tell these addresses
+    // from the LDS-DMA targets still in flight and would otherwise drain the ring (vmcnt(0))
+    // before the first one.  Chunk k = 2i + h: row wm*64 + 16i + 8h + r8, this lane's 8 columns.
+    uint32_t la[2 * TM];
+#pragma unroll
+    for (int k = 0; k < 2 * TM; ++k) {
+      const int row = wm * 64 + 8 * k + r8;
+      la[k] = (uint32_t)(uintptr_t)LDS_PTR(op_w + row * 256 + (((lc >> 3) ^ pk_sw(row)) << 4));
+    }
+    v4u_t ov4[2 * TM];
+    uint32_t bytes[2 * TM];
+    if (res_on) {
+      asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\t"
+                   "ds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\tds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\t"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=&v"(ov4[0]), "=&v"(ov4[1]), "=&v"(ov4[2]), "=&v"(ov4[3]), "=&v"(ov4[4]), "=&v"(ov4[5]),
+                     "=&v"(ov4[6]), "=&v"(ov4[7])
+                   : "v"(la[0]), "v"(la[1]), "v"(la[2]), "v"(la[3]), "v"(la[4]), "v"(la[5]), "v"(la[6]), "v"(la[7])
+                   : "memory");
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2 * TM; ++k) ov4[k] = v4u_t{0u, 0u, 0u, 0u};
+    }
+    if (bits_in) {
+      uint32_t ba[2 * TM];
+#pragma unroll
+      for (int k = 0; k < 2 * TM; ++k)
+        ba[k] = (uint32_t)(uintptr_t)LDS_PTR(bits_base + (wm * 64 + 8 * k + r8) * 16 + (lc >> 3));
+      asm volatile("ds_read_u8 %0, %8\n\tds_read_u8 %1, %9\n\tds_read_u8 %2, %10\n\tds_read_u8 %3, %11\n\t"
+                   "ds_read_u8 %4, %12\n\tds_read_u8 %5, %13\n\tds_read_u8 %6, %14\n\tds_read_u8 %7, %15\n\t"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=&v"(bytes[0]), "=&v"(bytes[1]), "=&v"(bytes[2]), "=&v"(bytes[3]), "=&v"(bytes[4]), "=&v"(bytes[5]),
+                     "=&v"(bytes[6]), "=&v"(bytes[7])
+                   : "v"(ba[0]), "v"(ba[1]), "v"(ba[2]), "v"(ba[3]), "v"(ba[4]), "v"(ba[5]), "v"(ba[6]), "v"(ba[7])
+                   : "memory");
+    }
+    // 1. fused element-wise work in the register layout; each lane writes its result chunk over
+    //    the operand chunk it read (same LDS address: no other lane's data is touched)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = 2 * i + h;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[e] = acc[i][2 * h][e]; v[4 + e] = acc[i][2 * h + 1][e]; }
+        float ov[8];
+        unpack8(make_uint4(ov4[k].x, ov4[k].y, ov4[k].z, ov4[k].w), ov);
+        uint4 pk;
+        if (is_fwd) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e] + ov[e];
+          if (p.relu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          pk = pack8(v);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += ov[e];
+          if (bits_in) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = ((bytes[k] >> e) & 1u) ? v[e] : 0.f;
+          }
+          pk = pack8(v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += v[e];   // (rows / columns outside the problem are zero)
+        }
+        const v4u_t pkv = {pk.x, pk.y, pk.z, pk.w};
+        asm volatile("ds_write_b128 %0, %1" ::"v"(la[k]), "v"(pkv) : "memory");
+      }
+    // 2. row-contiguous stores of the wave's 64 x 64 region from the slot: 8 consecutive lanes
+    //    cover one row's 128 B, so each store instruction writes whole 128 B lines (the register
+    //    layout puts consecutive lanes on different rows: 16 B partial-line writes, which the
+    //    counters show as a second read + write of the whole output through the fabric)
+    uint32_t ra2[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = wm * 64 + it * 8 + (lane >> 3), c = wn * 8 + (lane & 7);
+      ra2[it] = (uint32_t)(uintptr_t)LDS_PTR(op_w + row * 256 + ((c ^ pk_sw(row)) << 4));
+    }
+    v4u_t so[8];
+    asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\tds_read_b128 %3, %11\n\t"
+                 "ds_read_b128 %4, %12\n\tds_read_b128 %5, %13\n\tds_read_b128 %6, %14\n\tds_read_b128 %7, %15\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(so[0]), "=&v"(so[1]), "=&v"(so[2]), "=&v"(so[3]), "=&v"(so[4]), "=&v"(so[5]), "=&v"(so[6]),
+                   "=&v"(so[7])
+                 : "v"(ra2[0]), "v"(ra2[1]), "v"(ra2[2]), "v"(ra2[3]), "v"(ra2[4]), "v"(ra2[5]), "v"(ra2[6]), "v"(ra2[7])
+                 : "memory");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = wm * 64 + it * 8 + (lane >> 3), c = wn * 8 + (lane & 7);
+      const int gc = n0 + c * 8;
+      const bool ok = m0 + row < p.M && gc < p.Nn;
+      __builtin_amdgcn_raw_buffer_store_b128(so[it], rout, ok ? (uint32_t)((row * p.ldo + gc) * 2) : OOB_OFF, 0, 0);
+      if (bits_out)
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)pos_bits8(make_uint4(so[it].x, so[it].y, so[it].z, so[it].w)), rbo,
+                                             ok ? (uint32_t)(row * p.ld_bits_out + (gc >> 3)) : OOB_OFF, 0, 0);
+    }
+    if (csum_on) {   // fold the 8 lanes (r8) sharing this lane's columns; lane r8 == 0 stores
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
+      const int prow = p.prow_begin + ((m0 - p.m_begin) / BM) * (BM / 64) + wm;
+      const __amdgpu_buffer_rsrc_t rcs = __builtin_amdgcn_make_buffer_rsrc(p.colsum + (long)prow * p.Nn, (short)0,
+                                                                           p.Nn * 4, 0x00020000);
+      const bool w_ok = r8 == 0 && col_ok;
+      typedef float v4fl __attribute__((ext_vector_type(4)));
+      const v4fl c0 = {csum[0], csum[1], csum[2], csum[3]}, c1 = {csum[4], csum[5], csum[6], csum[7]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, c0), rcs, w_ok ? (uint32_t)(gn * 4) : OOB_OFF, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, c1), rcs, w_ok ? (uint32_t)(gn * 4 + 16) : OOB_OFF,
+                                             0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring's trailing (zero) steps land before exit
+}
 
 // Split-K combine: one single-wave workgroup per 64x64 wave sub-tile (4 per output tile, so a
 // small-M layer's few tiles still spread over the chip: the combine is bound by how fast ONE
@@ -1102,8 +1494,17 @@ struct IgemmPlan { int cfg, split, ks; };
 
 int g_igemm_splitk = 1;
 int g_igemm_epf = 0;       // early epilogue-operand prefetch for the short-K single-stage tiles (A/B knob)
-int g_igemm_rd = 1;        // register-direct epilogue on the 4-wave tiles (igemm_epilogue_rd): 0 off,
-                           // 1 on (every unsplit cfg 0 / 1 launch without train-BN sums)
+int g_igemm_pk = 2;        // persistent ring kernel (igemm_pk_kernel) for the short-K 1x1 layers:
+                           // 0 off, else the ring depth NB (2: two 68 KiB blocks per CU; 3, 4: one
+                           // 128 KiB+ block per CU, measured 5-7 % slower end to end)
+int g_igemm_pk_all = 0;    // 0: only where it measured faster (dgrads with a residual-gradient add:
+                           // -10..-18 % per layer; forwards with a residual and K >= 128: -4..-10 %);
+                           // 1: every eligible layer (K = 64 forwards +5 %, no-residual ones +5..8 %)
+int g_igemm_rd = 0;        // register-direct epilogue on the 4-wave tiles (igemm_epilogue_rd): 0 off,
+                           // 1 on (every unsplit cfg 0 / 1 launch without train-BN sums).  Off: its
+                           // stores put consecutive lanes on different rows, and the resulting 16 B
+                           // partial-line writes cost a second read + write of the output through
+                           // the fabric (WRITE_SIZE / FETCH_SIZE, profiles/r3_hbm_bytes_per_layer.txt)
 
 // Split-K for layers with too few output tiles to fill the chip (small batches, small spatial
 // stages: stage 5 at batch 32-256, crop 160): the 4-wave tiles stay resident 2-3 per CU, so a
@@ -1183,6 +1584,34 @@ int igemm_partial_rows(int M, int Nn, int K, bool bnz) {
 
 static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream);
 
+// The persistent ring kernel for a short-K 1x1 problem (false: not eligible, nothing launched).
+static bool igemm_pk_launch(const IgemmParams& p, hipStream_t stream) {
+  const int KT = p.K / 64;
+  if (p.a2 || p.R != 1 || p.S != 1 || p.pad != 0 || p.C1 != p.K || !igemm_no_halo(p)) return false;
+  if (KT != 1 && KT != 2 && KT != 4 && KT != 8) return false;
+  if (p.mode != EPI_FWD && p.mode != EPI_DGRAD) return false;
+  if (p.up2 || p.out2 || p.stats || p.bn_z || p.mask || p.Nn % 32) return false;
+  if (p.mode == EPI_FWD && (!p.scale || !p.shift)) return false;
+  const bool ops = p.mode == EPI_FWD || p.add || p.bits_mask;
+  if (!ops) return false;   // (the epilogue stages its stores through the operand step's slot)
+  if (!g_igemm_pk_all && !((p.mode == EPI_DGRAD && p.add) || (p.mode == EPI_FWD && p.res && KT >= 2))) return false;
+  const long T = (long)((p.M - p.m_begin + 127) / 128) * ((p.Nn + 127) / 128);
+  const int nb = g_igemm_pk;
+  long G = (long)num_cus() * (nb == 2 ? 2 : 1);
+  if (G > T) G = T;
+#define PK_GO(KT_, NB_) hipLaunchKernelGGL((igemm_pk_kernel<KT_, NB_, true>), dim3((unsigned)G), dim3(256), 0, stream, p);
+#define PK_NB(KT_)                          \
+  {                                         \
+    if (nb == 2) PK_GO(KT_, 2)              \
+    else if (nb == 3) PK_GO(KT_, 3)         \
+    else PK_GO(KT_, 4)                      \
+  }
+  if (KT == 1) PK_NB(1) else if (KT == 2) PK_NB(2) else if (KT == 4) PK_NB(4) else PK_NB(8)
+#undef PK_NB
+#undef PK_GO
+  return true;
+}
+
 const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   const char* why = nullptr;
   if (!igemm_check(p_in, &why)) return why;
@@ -1193,6 +1622,10 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   p.prow_begin = 0;
   p.ksplit = 1;
   const IgemmPlan pl = igemm_plan(p.M, p.Nn, p.K, p.bn_z != nullptr);
+  if (g_igemm_pk && pl.ks == 1 && pl.split >= p.M && pl.cfg == 1 && igemm_pk_launch(p, stream)) {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? nullptr : hipGetErrorString(e);
+  }
   const bool window = (p.C1 * p.S == 64) && p.C1 < 64;
   if (pl.ks > 1 && !p.a2 && !window && p.C1 % 64 == 0 && p.slab &&
       p.slab_floats >= igemm_splitk_floats(p.M, p.Nn, p.K)) {

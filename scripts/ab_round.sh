@@ -1,16 +1,16 @@
 # ad-hoc GPU session (edited per experiment); every step bounded, chained with &&
-# current: register-direct epilogue (igemm_rd) -> kernel numerics, then b1024 / b2048 A/B and a
-# kernel-trace profile of the RD build
+# current: persistent ring kernel on by default (selective) -> whole GPU suite + smoke, then
+# b1024 / b2048 A/B against igemm_pk=0 on the same box
 set -o pipefail
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
 b() { local n=$1; shift; timeout -k 10 300 python bench.py "$@" > gpurun_out/ab/$n.log 2>&1; }
 true && \
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py > gpurun_out/ab/tests.log 2>&1 && \
-b rd1_b1024 --batch 1024 && PDDL_KNOBS=igemm_rd=0 b rd0_b1024 --batch 1024 && \
-b rd1_b2048 && PDDL_KNOBS=igemm_rd=0 b rd0_b2048 && b rd1_b1024b --batch 1024 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab/prof -o run --output-format csv -- python bench.py --batch 1024 --steps 6 --warmup 3 > gpurun_out/ab/prof.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/ab/gputests.log 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/ab/smoke.log 2>&1 && \
+b pk2 --batch 1024 && PDDL_KNOBS=igemm_pk=0 b pk0 --batch 1024 && b pk2b --batch 1024 && PDDL_KNOBS=igemm_pk=0 b pk0b --batch 1024 && \
+b pk2_b2048 && PDDL_KNOBS=igemm_pk=0 b pk0_b2048
 rc=$?
-tail -n 3 gpurun_out/ab/tests.log
-for f in gpurun_out/ab/*.log; do echo "$f $(grep -h '"value"' $f | cut -c100-160)"; done
+tail -n 3 gpurun_out/ab/gputests.log; tail -2 gpurun_out/ab/smoke.log
+for f in gpurun_out/ab/*.log; do echo "$f $(grep -ho '"value": [0-9.]*' $f)"; done
 exit $rc

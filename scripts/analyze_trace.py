@@ -124,8 +124,15 @@ def main():
         agg[k2] = agg.get(k2, 0) + t
         tf = flops / t / 1e12 if flops else 0
         gb = byts / t / 1e9 if byts else 0
-        grid = "+".join(r["Grid_Size_X"] for r in rs)
-        print(f"{t*1e6:9.1f} us  {tf:7.1f} TF/s  {gb:7.0f} GB/s  grid={grid:>16}  {kn[:40]:40s} {name}")
+        grid = "+".join(r.get("Grid_Size_X") or r.get("Grid_Size", "?") for r in rs)
+        meas = ""
+        if "Counter_Value" in rs[0]:
+            # rocprofv3 counter collection: WRITE_SIZE / FETCH_SIZE in KiB (FETCH_SIZE reads half the
+            # bytes on gfx950: calibrated against a streaming read of known size, profiles/r3_hbm_bytes)
+            cn = rs[0]["Counter_Name"]
+            mb = sum(float(r["Counter_Value"]) for r in rs) * 1024 * (2 if cn == "FETCH_SIZE" else 1) / 1e6
+            meas = f"  {cn[:5]} {mb:8.1f} MB ({mb * 1e6 / t / 1e9:6.0f} GB/s)"
+        print(f"{t*1e6:9.1f} us  {tf:7.1f} TF/s  {gb:7.0f} GB/s  grid={grid:>16}  {kn[:40]:40s} {name}{meas}")
     print(f"step total {tot*1e3:.2f} ms")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1]):
         print(f"  {k:24s} {v*1e3:8.3f} ms")

@@ -145,7 +145,7 @@ def test_igemm_dgrad(case):
     assert rel(cs, ref.sum((0, 1, 2))) < 1e-2
 
 
-KNOB_DEFAULTS = {"igemm_rd": 1}
+KNOB_DEFAULTS = {"igemm_pk": 2}
 
 
 @pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1), ("igemm8", 1),
@@ -841,3 +841,52 @@ def test_igemm_splitk_dense_head_f32():
         nat.splitk_use(None)
     ref = a.float() @ wd.float().t() + bias
     assert rel(out, ref) < 1e-3
+
+
+@pytest.mark.parametrize("nb", [2, 3, 4])
+@pytest.mark.parametrize("case", ["fwd_res_k64", "fwd_res_k256_s2", "fwd_nores_k128", "fwd_res_k512",
+                                  "dgrad_add_k64", "dgrad_bits_k256", "dgrad_add_k128_nn320"])
+def test_igemm_pk_matches(case, nb):
+    """The persistent ring kernel (igemm_pk) computes exactly what the per-tile kernel does on
+    the short-K 1x1 layers: forward with residual + ReLU-bit output, dgrad with residual-gradient
+    add + ReLU bits + fused column sums; several tiles per workgroup (the ring crosses tile
+    boundaries), an M tail (rows % 128 != 0), a half-empty column tile (Nn = 320) and stride 2."""
+    torch.manual_seed(31)
+    n, h = 32, 55                                  # M = 96800 rows: 757 row tiles, ~3-9 tiles per workgroup
+    K = int(case.split("_k")[1].split("_")[0])
+    Nn = 320 if "nn320" in case else 256
+    st = 2 if case.endswith("_s2") else 1
+    hi = h * st
+    if case.startswith("fwd"):
+        x = rnd(n, hi, hi, K)
+        w = rnd(Nn, K, scale=0.05)
+        sc, sh = torch.rand(Nn, device=dev) + 0.5, torch.randn(Nn, device=dev)
+        res = rnd(n, h, h, Nn) if "nores" not in case else None
+    else:
+        g = rnd(n, h, h, K)
+        wt = rnd(Nn, K, scale=0.05)
+        addv = rnd(n, h, h, Nn) if "add" in case else None
+        bits = pack_bits(rnd(n, h, h, Nn))
+    outs = []
+    N().set_variant("igemm_pk_all", 1)
+    for kv in (0, nb):
+        N().set_variant("igemm_pk", kv)
+        try:
+            if case.startswith("fwd"):
+                y = torch.empty(n, h, h, Nn, dtype=torch.bfloat16, device=dev)
+                bo = torch.zeros(n, h, h, Nn // 8, dtype=torch.uint8, device=dev)
+                N().igemm(x, None, hi, hi, 1, 1, st, 0, h, h, w, 0, sc, sh, res, None, None, y, 1, None, 0, 0, 0, 0, 0,
+                          None, bo)
+                outs.append(torch.cat([y.float().flatten(), bo.float().flatten()]))
+            else:
+                out = torch.empty(n, h, h, Nn, dtype=torch.bfloat16, device=dev)
+                rows = N().igemm_partial_rows(n * h * h, Nn, K)
+                part = torch.full((rows * Nn,), float("nan"), device=dev)
+                N().igemm(g, None, h, h, 1, 1, 1, 0, h, h, wt, 1, None, None, None, bits, addv, out, 0, None, 0, 0,
+                          0, 0, 0, part, None)
+                outs.append(torch.cat([out.float().flatten(), _fold(part, rows, Nn)]))
+            torch.cuda.synchronize()
+        finally:
+            N().set_variant("igemm_pk", 2)
+    N().set_variant("igemm_pk_all", 0)
+    assert rel(outs[1], outs[0]) < 1e-5
