@@ -20,4 +20,5 @@ run() {  # tag op shape
 run fwd_s3 fwd 1024,28,128,128,3,1,1 && run fwd_s4 fwd 1024,14,256,256,3,1,1 && \
 run fwd_s5 fwd 1024,7,512,512,3,1,1 && run fwd_s2 fwd 1024,56,64,64,3,1,1 && \
 run wg_s3 wgrad 1024,28,128,128,3,1,1 && run wg_s4 wgrad 1024,14,256,256,3,1,1 && \
-run dg_s4c1 dgrad_add 1024,14,1024,256,1,1,0
+run dg_s4c1 dgrad_add 1024,14,1024,256,1,1,0 && \
+run fwdres_s3c3 fwdres 1024,28,128,512,1,1,0 && run fwdres_s4c3 fwdres 1024,14,256,1024,1,1,0
