@@ -23,6 +23,13 @@ from typing import Optional, Tuple
 import torch
 
 
+
+# Capture in thread-local mode: under the default global mode any potentially unsafe HIP call
+# from ANOTHER thread (the input pipeline's producer thread staging its next batch, a fusion
+# engine worker) invalidates the capture -- seen as an intermittent
+# hipErrorStreamCaptureUnsupported on the Mirrored entry script's first (captured) step.
+CAPTURE_MODE = "thread_local"
+
 class GraphedTrainStep:
     """with_optimizer=False records forward + backward only (Mirrored: the cross-device
     all-reduce runs between the replay and an eager optimizer step)."""
@@ -75,7 +82,7 @@ class GraphedTrainStep:
         torch.cuda.synchronize()
         it = self.opt._iterations
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             self.stats = self._body()
         self.opt._iterations = it    # the capture pass did not step (no setter: hs is current)
         self.graph = g
@@ -129,7 +136,7 @@ class SegmentedStepGraphs(GraphedTrainStep):
 
         def begin():
             g = torch.cuda.CUDAGraph()
-            g.capture_begin(pool=segs[0].pool() if segs else None)
+            g.capture_begin(pool=segs[0].pool() if segs else None, capture_error_mode=CAPTURE_MODE)
             mark.zero_()     # never an empty graph (two buckets can complete at the same layer)
             segs.append(g)
 
@@ -146,7 +153,7 @@ class SegmentedStepGraphs(GraphedTrainStep):
                 self.stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip,
                                                   crop_offset=self.crop, bucket_cb=cut, buckets=self.buckets)
                 og = torch.cuda.CUDAGraph()
-                og.capture_begin(pool=segs[0].pool())
+                og.capture_begin(pool=segs[0].pool(), capture_error_mode=CAPTURE_MODE)
                 opt.step()
                 eng.after_update()
                 og.capture_end()
