@@ -57,6 +57,23 @@ enum { AM_DIRECT = 0, AM_HALO = 1, AM_DUAL = 2 };
 __device__ __forceinline__ int sw_chunk(int lane, int i) { return (lane & 7) ^ ((4 * (i & 1) + (lane >> 4)) & 7); }
 __device__ __forceinline__ int sw_read(int lane, int kh) { return (((kh * 4) + (lane >> 4)) ^ ((lane >> 1) & 7)) * 16; }
 
+// Bitmask of the in-bounds taps (bit r * S + s) of an output row whose window starts at input
+// (hi, wi).  The 3x3 case (every padded conv of ResNet-50) is unrolled: the generic runtime-R/S
+// loops cost ~45 instructions and three branches per staged row in every tile's prologue.
+__device__ __forceinline__ uint32_t halo_taps(const IgemmParams& p, int hi, int wi) {
+  if (p.R == 3 && p.S == 3) {
+    const uint32_t cols = ((unsigned)wi < (unsigned)p.W ? 1u : 0u) | ((unsigned)(wi + 1) < (unsigned)p.W ? 2u : 0u) |
+                          ((unsigned)(wi + 2) < (unsigned)p.W ? 4u : 0u);
+    return ((unsigned)hi < (unsigned)p.H ? cols : 0u) | ((unsigned)(hi + 1) < (unsigned)p.H ? cols << 3 : 0u) |
+           ((unsigned)(hi + 2) < (unsigned)p.H ? cols << 6 : 0u);
+  }
+  uint32_t rows = 0, cols = 0, mk = 0;
+  for (int r = 0; r < p.R; ++r) rows |= (uint32_t)((unsigned)(hi + r) < (unsigned)p.H) << r;
+  for (int s = 0; s < p.S; ++s) cols |= (uint32_t)((unsigned)(wi + s) < (unsigned)p.W) << s;
+  for (int r = 0; r < p.R; ++r) mk |= ((rows >> r) & 1u) ? cols << (r * p.S) : 0u;
+  return mk;
+}
+
 // Epilogue of one wave sub-tile of TM x TN 16x16 fragments at global rows [mb, mb + 16*TM)
 // and columns [nb, nb + 16*TN): fragments -> LDS (fp32, per-wave `stage` of 32 x (16*TN + 4))
 // -> 16-byte row stores with the fused FWD / F32 / DGRAD operations; the column sums (dgrad)
@@ -586,13 +603,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
       const int pix = ((n - n_first) * p.H + hi) * p.W + wi;
       a_o1[i] = (uint32_t)((pix * p.C1 + sw_chunk(lane, i) * 8) * 2);
       if (AM == AM_DUAL) a_o2[i] = (uint32_t)((pix * p.C2 + sw_chunk(lane, i) * 8) * 2);
-      if (AM == AM_HALO) {
-        uint32_t rows = 0, cols = 0, mk = 0;
-        for (int r = 0; r < p.R; ++r) rows |= (uint32_t)((unsigned)(hi + r) < (unsigned)p.H) << r;
-        for (int s = 0; s < p.S; ++s) cols |= (uint32_t)((unsigned)(wi + s) < (unsigned)p.W) << s;
-        for (int r = 0; r < p.R; ++r) mk |= ((rows >> r) & 1u) ? cols << (r * p.S) : 0u;
-        a_taps[i] = mk;
-      }
+      if (AM == AM_HALO) a_taps[i] = halo_taps(p, hi, wi);
     }
   }
   uint32_t b_o[BI];
@@ -1233,13 +1244,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
       const int pix = ((n - n_first) * p.H + hi_) * p.W + wi;
       a_o1[hi] = (uint32_t)((pix * p.C1 + sw_chunk(lane, hi) * 8) * 2);
       if (AM == AM_DUAL) a_o2[hi] = (uint32_t)((pix * p.C2 + sw_chunk(lane, hi) * 8) * 2);
-      if (AM == AM_HALO) {
-        uint32_t rows = 0, cols = 0, mk = 0;
-        for (int rr = 0; rr < p.R; ++rr) rows |= (uint32_t)((unsigned)(hi_ + rr) < (unsigned)p.H) << rr;
-        for (int ss = 0; ss < p.S; ++ss) cols |= (uint32_t)((unsigned)(wi + ss) < (unsigned)p.W) << ss;
-        for (int rr = 0; rr < p.R; ++rr) mk |= ((rows >> rr) & 1u) ? cols << (rr * p.S) : 0u;
-        a_taps[hi] = mk;
-      }
+      if (AM == AM_HALO) a_taps[hi] = halo_taps(p, hi_, wi);
     }
     const int n = n0 + r;
     b_o[hi] = (n < p.Nn) ? (uint32_t)((n * p.ldb + sw_chunk(lane, hi) * 8) * 2) : OOB_OFF;
