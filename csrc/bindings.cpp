@@ -74,11 +74,22 @@ void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, 
   p.Ho = (int)Ho; p.Wo = (int)Wo; p.M = p.N * (int)Ho * (int)Wo;
   p.K1 = (int)(R * S * p.C1);
   p.K = p.K1;
+  p.H2 = p.H; p.W2 = p.W; p.stride2 = p.stride;
   if (a2.has_value()) {
     PCHECK(a2->is_contiguous() && a2->size(0) == a1.size(0), "second A source shape");
     p.a2 = bfp(*a2);
     p.C2 = (int)a2->size(-1);
-    PCHECK(a2->numel() == (int64_t)p.N * H * W * p.C2, "second A source numel");
+    if (a2->dim() == 4 && (a2->size(1) != H || a2->size(2) != W)) {
+      // a second source with its own geometry (fused projection shortcut: the block input at
+      // stride 1 or 2 next to conv3's operand): 1x1 / pad 0, stride from the spatial ratio
+      PCHECK(R == 1 && S == 1 && pad == 0, "a second source of other dims needs a 1x1 / pad 0 gather");
+      p.H2 = (int)a2->size(1); p.W2 = (int)a2->size(2);
+      p.stride2 = (int)((p.H2 + Ho - 1) / Ho);
+      PCHECK(p.stride2 >= 1 && (Ho - 1) * p.stride2 < p.H2 && (Wo - 1) * p.stride2 < p.W2 &&
+                 (p.H2 - 1) / p.stride2 + 1 == Ho && (p.W2 - 1) / p.stride2 + 1 == Wo,
+             "second A source dims do not map onto the output grid");
+    }
+    PCHECK(a2->numel() == (int64_t)p.N * p.H2 * p.W2 * p.C2, "second A source numel");
     p.K += (int)(R * S * p.C2);
   }
   PCHECK(b.dim() == 2 && b.size(1) >= p.K, "B must be [Nn][>=K]");
@@ -463,6 +474,14 @@ void prep(Tensor params, Tensor table, int64_t nlayers, int64_t max_elems, Tenso
                        (int)max_elems, bfpm(wbf), f32p(scale), f32p(shift), (float)eps, cur_stream()),
      "prep");
 }
+void prep_fuse(Tensor params, Tensor table, int64_t nlayers, int64_t max_elems, Tensor wbf, Tensor scale, Tensor shift,
+               double eps) {
+  PCHECK(table.is_cuda() && table.scalar_type() == torch::kUInt8, "prep_fuse table");
+  PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::FuseLayer), "prep_fuse table size");
+  ok(pddl::prep_fuse_launch(f32p(params), reinterpret_cast<const pddl::FuseLayer*>(table.data_ptr()), (int)nlayers,
+                            (int)max_elems, bfpm(wbf), f32p(scale), f32p(shift), (float)eps, cur_stream()),
+     "prep_fuse");
+}
 void wgrad_finalize(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor scale, Tensor dgamma_raw) {
   PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::FinLayer), "finalize table size");
   ok(pddl::wgrad_finalize_launch(f32p(params), f32p(grads), reinterpret_cast<const pddl::FinLayer*>(table.data_ptr()),
@@ -609,6 +628,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd_partial_rows", &pddl::maxpool_bwd_partial_rows);
   m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);
   m.def("prep", &prep, REL);
+  m.def("prep_fuse", &prep_fuse, REL);
   m.def("wgrad_finalize", &wgrad_finalize, REL);
   m.def("bn_grad", &bn_grad, REL);
   m.def("synth", &synth, REL);
@@ -619,6 +639,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_bf16", &cast_bf16, REL);
   m.def("cast_f32", &cast_f32, REL);
   m.attr("PREP_LAYER_BYTES") = (int)sizeof(pddl::PrepLayer);
+  m.attr("FUSE_LAYER_BYTES") = (int)sizeof(pddl::FuseLayer);
   m.attr("FIN_LAYER_BYTES") = (int)sizeof(pddl::FinLayer);
   m.attr("BNGRAD_LAYER_BYTES") = (int)sizeof(pddl::BnGradLayer);
   m.attr("EPI_FWD") = (int)pddl::EPI_FWD;

@@ -1043,6 +1043,56 @@ __global__ void prep_dgrad_kernel(const float* __restrict__ prm, const PrepLayer
   }
 }
 
+// Fused projection-block forward weights (FuseLayer): element (co, k) of [cout][k3 + k0] is
+// a3[co] * W3[co][k] (k < k3) or a0[co] * W0[co][k - k3], rounded once to bf16; the fused affine
+// is scale = 1, shift = b3 + b0 (both branches' frozen-BN shifts, summed before the ReLU).
+__device__ __forceinline__ void bn_fold(const float* prm, int bias, int gamma, int beta, int mean, int var, int co,
+                                        float eps, float* a, float* b) {
+  const float g = gamma >= 0 ? prm[gamma + co] : 1.f;
+  const float v = var >= 0 ? prm[var + co] : 1.f - eps;
+  const float mu = mean >= 0 ? prm[mean + co] : 0.f;
+  const float be = beta >= 0 ? prm[beta + co] : 0.f;
+  const float bi = bias >= 0 ? prm[bias + co] : 0.f;
+  *a = (gamma >= 0 || var >= 0) ? g * rsqrtf(v + eps) : 1.f;
+  *b = (bi - mu) * *a + be;
+}
+__global__ void prep_fuse_kernel(const float* __restrict__ prm, const FuseLayer* __restrict__ L,
+                                 uint16_t* __restrict__ wbf, float* __restrict__ scale, float* __restrict__ shift,
+                                 float eps) {
+  const FuseLayer l = L[blockIdx.y];
+  const int K = l.k3 + l.k0;
+  const long n = (long)l.cout * K;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(e / K), k = (int)(e - (long)co * K);
+    float a, b;
+    float w;
+    if (k < l.k3) {
+      bn_fold(prm, l.bias3, l.gamma3, l.beta3, l.mean3, l.var3, co, eps, &a, &b);
+      w = prm[l.w3_off + (long)co * l.k3 + k];
+    } else {
+      bn_fold(prm, l.bias0, l.gamma0, l.beta0, l.mean0, l.var0, co, eps, &a, &b);
+      w = prm[l.w0_off + (long)co * l.k0 + (k - l.k3)];
+    }
+    wbf[l.wf_off + e] = f2bf(a * w);
+    if (k == 0) {
+      float a3, b3, a0, b0;
+      bn_fold(prm, l.bias3, l.gamma3, l.beta3, l.mean3, l.var3, co, eps, &a3, &b3);
+      bn_fold(prm, l.bias0, l.gamma0, l.beta0, l.mean0, l.var0, co, eps, &a0, &b0);
+      scale[l.ch_off + co] = 1.f;
+      shift[l.ch_off + co] = b3 + b0;
+    }
+  }
+}
+const char* prep_fuse_launch(const float* params, const FuseLayer* layers_dev, int nlayers, int max_elems,
+                             uint16_t* wbf, float* scale, float* shift, float eps, hipStream_t s) {
+  int gx = (max_elems + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(prep_fuse_kernel, dim3(gx, nlayers), dim3(256), 0, s, params, layers_dev, wbf, scale, shift, eps);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
 const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems, uint16_t* wbf,
                         float* scale, float* shift, float eps, hipStream_t s) {
   int gx = (max_elems / 4 + 255) / 256;

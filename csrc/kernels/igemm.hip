@@ -581,7 +581,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   const long HW = (long)p.H * p.W, pix0 = n_first * HW, pix_end = p.N * HW;
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc_at(p.a1, pix0 * p.C1, pix_end * p.C1);
   const int C2r = AM == AM_DUAL ? p.C2 : p.C1;
-  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc_at(AM == AM_DUAL ? p.a2 : p.a1, pix0 * C2r, pix_end * C2r);
+  // (the second source may have its own geometry: the fused projection shortcut reads the block
+  // input at H2 x W2 with stride2 next to conv3's stride-1 operand)
+  const long HW2 = AM == AM_DUAL ? (long)p.H2 * p.W2 : HW;
+  const __amdgpu_buffer_rsrc_t ra2 =
+      make_rsrc_at(AM == AM_DUAL ? p.a2 : p.a1, n_first * HW2 * C2r, p.N * HW2 * C2r);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
 
   // Per-lane constant source chunk: LDS position (lane & 7) of row (lane >> 3) holds the
@@ -602,7 +606,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
       const int hi = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
       const int pix = ((n - n_first) * p.H + hi) * p.W + wi;
       a_o1[i] = (uint32_t)((pix * p.C1 + sw_chunk(lane, i) * 8) * 2);
-      if (AM == AM_DUAL) a_o2[i] = (uint32_t)((pix * p.C2 + sw_chunk(lane, i) * 8) * 2);
+      if (AM == AM_DUAL) {
+        const int pix2 = ((n - n_first) * p.H2 + ho * p.stride2) * p.W2 + wo * p.stride2;
+        a_o2[i] = (uint32_t)((pix2 * p.C2 + sw_chunk(lane, i) * 8) * 2);
+      }
       if (AM == AM_HALO) a_taps[i] = halo_taps(p, hi, wi);
     }
   }
@@ -1225,7 +1232,11 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
   const long HW = (long)p.H * p.W, pix0 = n_first * HW, pix_end = p.N * HW;
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc_at(p.a1, pix0 * p.C1, pix_end * p.C1);
   const int C2r = AM == AM_DUAL ? p.C2 : p.C1;
-  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc_at(AM == AM_DUAL ? p.a2 : p.a1, pix0 * C2r, pix_end * C2r);
+  // (the second source may have its own geometry: the fused projection shortcut reads the block
+  // input at H2 x W2 with stride2 next to conv3's stride-1 operand)
+  const long HW2 = AM == AM_DUAL ? (long)p.H2 * p.W2 : HW;
+  const __amdgpu_buffer_rsrc_t ra2 =
+      make_rsrc_at(AM == AM_DUAL ? p.a2 : p.a1, n_first * HW2 * C2r, p.N * HW2 * C2r);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
   // LDS-DMA piece i of a wave holds rows 8*(piece) + lane/8 (piece parity = i & 1); its lane-linear
   // 16-byte chunk (lane & 7) carries logical chunk (lane & 7) ^ ((row >> 1) & 7) (sw_chunk).
@@ -1243,7 +1254,10 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
       const int hi_ = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
       const int pix = ((n - n_first) * p.H + hi_) * p.W + wi;
       a_o1[hi] = (uint32_t)((pix * p.C1 + sw_chunk(lane, hi) * 8) * 2);
-      if (AM == AM_DUAL) a_o2[hi] = (uint32_t)((pix * p.C2 + sw_chunk(lane, hi) * 8) * 2);
+      if (AM == AM_DUAL) {
+        const int pix2 = ((n - n_first) * p.H2 + ho * p.stride2) * p.W2 + wo * p.stride2;
+        a_o2[hi] = (uint32_t)((pix2 * p.C2 + sw_chunk(lane, hi) * 8) * 2);
+      }
       if (AM == AM_HALO) a_taps[hi] = halo_taps(p, hi_, wi);
     }
     const int n = n0 + r;
@@ -1437,10 +1451,14 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
   // descriptors are rebased per tile, so only the images one 256-row tile spans must fit
   // (and every element index below is an int: < 2^31 elements per tensor)
   const long span = 256 / (p.Ho * p.Wo) + 2, cmax = p.C1 > p.C2 ? p.C1 : p.C2;
-  if (span * p.H * p.W * cmax * 2 >= (1L << 31) || (long)p.Nn * p.ldb * 2 >= (1L << 31)) {
+  const long hwmax = (long)p.H * p.W > (long)p.H2 * p.W2 ? (long)p.H * p.W : (long)p.H2 * p.W2;
+  if (p.a2 && ((p.Ho - 1) * p.stride2 >= p.H2 || (p.Wo - 1) * p.stride2 >= p.W2 || p.stride2 < 1)) {
+    *why = "second source geometry does not cover the output rows"; return false;
+  }
+  if (span * hwmax * cmax * 2 >= (1L << 31) || (long)p.Nn * p.ldb * 2 >= (1L << 31)) {
     *why = "operand too large for 31-bit buffer offsets"; return false;
   }
-  if ((long)p.N * p.H * p.W * cmax >= (1L << 31) || (long)p.M * (p.ldo > p.Nn ? p.ldo : p.Nn) >= (1L << 31)) {
+  if ((long)p.N * hwmax * cmax >= (1L << 31) || (long)p.M * (p.ldo > p.Nn ? p.ldo : p.Nn) >= (1L << 31)) {
     *why = "tensor has more than 2^31 elements"; return false;
   }
   return true;

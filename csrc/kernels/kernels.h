@@ -12,8 +12,9 @@ enum EpiMode { EPI_FWD = 0, EPI_DGRAD = 1, EPI_F32 = 2 };
 struct IgemmParams {
   // A operand: NHWC bf16 tensor(s), gathered as im2col rows.
   const uint16_t* a1; int C1;      // first source, channels (multiple of 64)
-  const uint16_t* a2; int C2;      // optional second source (concatenated along K)
-  int N, H, W;                     // input dims shared by both sources
+  const uint16_t* a2; int C2;      // optional second source (concatenated along K), 1x1 pad 0:
+  int H2, W2, stride2;             //   its own spatial dims and stride (= H, W, stride when shared)
+  int N, H, W;                     // input dims of the first source (the second's batch N too)
   int R, S, stride, pad;
   int Ho, Wo, M;                   // GEMM rows = N * Ho * Wo
   int K1, K;                       // K1 = R*S*C1, K = K1 + R*S*C2
@@ -154,6 +155,19 @@ struct PrepLayer {
   int ch_off;         // offset of this layer's folded scale/shift (per output channel)
   int mode;           // 0: dense [cout][kpad] rows; 1: stem in the 4x4x16 space-to-depth layout
 };
+// Fused projection-block forward (conv3 + projection shortcut as one dual-source GEMM): the
+// bf16 weights [cout][k3 + k0] = [a3 * W3 | a0 * W0] with both frozen-BN scales folded in, and
+// the epilogue affine scale = 1, shift = b3 + b0 (prep_fuse_kernel).
+struct FuseLayer {
+  int cout, k3, k0;
+  int w3_off, w0_off;                                   // fp32 kernels [cout][k3], [cout][k0]
+  int bias3, gamma3, beta3, mean3, var3;                // BN of conv3 (-1: absent)
+  int bias0, gamma0, beta0, mean0, var0;                // BN of the shortcut conv
+  int ch_off;                                           // fused scale / shift slots
+  long wf_off;                                          // bf16 destination
+};
+const char* prep_fuse_launch(const float* params, const FuseLayer* layers_dev, int nlayers, int max_elems,
+                             uint16_t* wbf, float* scale, float* shift, float eps, hipStream_t s);
 const char* prep_f32_launch(const float* params, const PrepLayer* layers_dev, int nlayers, float* wf32, float* scale,
                             float* shift, float eps, hipStream_t s);   // fp32 stem s2d + dgrad weights
 const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems,

@@ -36,6 +36,7 @@ STEM_K = 256   # 4x4 taps x 16 channels of the space-to-depth stem
 _FIN_FMT = "<5i"
 _CRED_FMT = "<q4i"
 _BNG_FMT = "<9i"
+_FUSE_FMT = "<16iq"   # FuseLayer (csrc/kernels/kernels.h)
 
 
 def _ceil(a, b):
@@ -44,6 +45,7 @@ def _ceil(a, b):
 
 class HipEngine:
     BN_MODES = ("frozen",)   # HipEngineBNTrain (models/engine_bn.py) runs bn_mode="train"
+    FUSE_PROJ_OK = True      # projection blocks: conv3 + shortcut conv as one dual-source GEMM
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
@@ -65,6 +67,7 @@ class HipEngine:
         assert struct.calcsize(_PREP_FMT) == self.N.PREP_LAYER_BYTES
         assert struct.calcsize(_FIN_FMT) == self.N.FIN_LAYER_BYTES
         assert struct.calcsize(_BNG_FMT) == self.N.BNGRAD_LAYER_BYTES
+        assert struct.calcsize(_FUSE_FMT) == self.N.FUSE_LAYER_BYTES
         assert struct.calcsize(_CRED_FMT) == self.N.COLRED_LAYER_BYTES
         dev = self.device
         L = layout
@@ -77,6 +80,13 @@ class HipEngine:
             off += c.cout
         self.ch["dense"] = off
         off += _ceil(num_classes, 8)
+        # fused projection blocks (conv3 + shortcut conv as one dual-source GEMM, no shortcut
+        # activation in HBM): their own folded affine slots (scale 1, shift b3 + b0)
+        self.fuse_proj = self.FUSE_PROJ_OK and os.environ.get("PDDL_FUSE_PROJ", "1") != "0"
+        for b in L.blocks:
+            if b.proj:
+                self.ch["fuse:" + b.name] = off
+                off += 4 * b.filters
         self.nch = _ceil(off, 64)
         # ---- one zeroed-per-step workspace: grads | colsum | dgamma_raw | stats
         n_tr = L.n_trainable
@@ -108,6 +118,19 @@ class HipEngine:
             off += c.cout * kpad
         wf["dense"] = off
         off += self.num_classes * 2048
+        fuse_rows, fuse_max = [], 0
+        for b in L.blocks:   # fused projection forward weights [4f][f + cin]
+            if b.proj:
+                c3, c0 = b.convs["3"], b.convs["0"]
+                wf["fuse:" + b.name] = off
+                off += c3.cout * (c3.cin + c0.cin)
+                g3, be3, m3, v3 = self._fold_offsets(c3)
+                g0, be0, m0, v0 = self._fold_offsets(c0)
+                fuse_rows.append(struct.pack(_FUSE_FMT, c3.cout, c3.cin, c0.cin, L.off(c3.name, "kernel"),
+                                             L.off(c0.name, "kernel"), L.off(c3.name, "bias"), g3, be3, m3, v3,
+                                             L.off(c0.name, "bias"), g0, be0, m0, v0, self.ch["fuse:" + b.name],
+                                             wf["fuse:" + b.name]))
+                fuse_max = max(fuse_max, c3.cout * (c3.cin + c0.cin))
         # dgrad weights: [cin][R][S][ld]; a projection block's conv1 and conv0 share rows
         wd: Dict[str, int] = {}
         wd_ld: Dict[str, int] = {}
@@ -152,6 +175,8 @@ class HipEngine:
         self._prep_tab = self._dev_table(rows)
         self._prep_n = len(rows)
         self._prep_max = max_el
+        self._fuse_tab = self._dev_table(fuse_rows)
+        self._fuse_n, self._fuse_max = len(fuse_rows), fuse_max
         # finalize table rows per layer, bn-grad table
         self._fin_rows: Dict[str, bytes] = {}
         for c in L.convs:
@@ -215,7 +240,7 @@ class HipEngine:
             Ho = (H - 1) // b.stride + 1
             a = {"y1": torch.empty(B, Ho, Ho, f, **bf), "y2": torch.empty(B, Ho, Ho, f, **bf),
                  "out": torch.empty(B, Ho, Ho, 4 * f, **bf)}
-            if b.proj:
+            if b.proj and not self.fuse_proj:
                 a["sc"] = torch.empty(B, Ho, Ho, 4 * f, **bf)
             self.acts[b.name] = a
             if self.bitmask:
@@ -309,6 +334,9 @@ class HipEngine:
         """Refresh bf16 forward / dgrad weights and folded BN affine from the fp32 master."""
         self.N.prep(self.params, self._prep_tab, self._prep_n, self._prep_max, self.wbf, self.scale, self.shift,
                     BN_EPS)
+        if self.fuse_proj and self._fuse_n:
+            self.N.prep_fuse(self.params, self._fuse_tab, self._fuse_n, self._fuse_max, self.wbf, self.scale,
+                             self.shift, BN_EPS)
 
     def _wf(self, name, rows, k):
         o = self.wf[name]
@@ -357,7 +385,15 @@ class HipEngine:
             y1, y2, out = a["y1"][:B], a["y2"][:B], a["out"][:B]
             c1n = b.convs["1"].name
             ch1 = self.ch[c1n]
-            if b.proj:
+            if b.proj and self.fuse_proj:
+                # conv1 alone; the shortcut conv runs inside conv3's GEMM (second A source = the block
+                # input at the block's stride, K = f + cin, both BN scales folded into the weights), so
+                # the shortcut activation is never written and re-read as a residual
+                N.igemm(x, None, H, H, 1, 1, b.stride, 0, Ho, Ho, self._wf(c1n, f, cin), 0,
+                        self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, None, 0, 0, 0, 0, 0, None,
+                        bt.get("y1"))
+                res = None
+            elif b.proj:
                 N.igemm(x, None, H, H, 1, 1, b.stride, 0, Ho, Ho, self._wf(c1n, 5 * f, cin), 0,
                         self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, a["sc"][:B], 0, f, 0, 0, 0,
                         None, bt.get("y1"))
@@ -372,9 +408,15 @@ class HipEngine:
                     self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0, 0, 0,
                     None, bt.get("y2"))
             c3 = b.convs["3"].name
-            N.igemm(y2, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(c3, 4 * f, f), 0,
-                    self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 0, 0, 0,
-                    None, bt.get("out"))
+            if b.proj and self.fuse_proj:
+                fz = "fuse:" + b.name
+                N.igemm(y2, x, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(fz, 4 * f, f + cin), 0,
+                        self.scale[self.ch[fz]:], self.shift[self.ch[fz]:], None, None, None, out, 1, None, 0, 0, 0,
+                        0, 0, None, bt.get("out"))
+            else:
+                N.igemm(y2, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(c3, 4 * f, f), 0,
+                        self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 0,
+                        0, 0, None, bt.get("out"))
             x = out
         pooled = self.pooled[:B]
         N.gap_fwd(x, pooled)

@@ -13,7 +13,7 @@ import pddl  # noqa
 from pddl.models.resnet50 import ParamLayout
 
 
-def schedule(B, crop):
+def schedule(B, crop, fuse=True):
     L = ParamLayout()
     H1 = (crop + 6 - 7) // 2 + 1
     H2 = (H1 + 2 - 3) // 2 + 1
@@ -27,11 +27,15 @@ def schedule(B, crop):
         f, cin = b.filters, b.cin
         Ho = (H - 1) // b.stride + 1
         M = B * Ho * Ho
-        n1 = 5 * f if b.proj else f
-        ev.append(("igemm", f"{b.name} c1{'+c0' if b.proj else ''} fwd", 2 * M * cin * n1, (B * H * H * cin + M * n1) * 2,
+        n1 = 5 * f if b.proj and not fuse else f
+        ev.append(("igemm", f"{b.name} c1{'+c0' if n1 > f else ''} fwd", 2 * M * cin * n1, (B * H * H * cin + M * n1) * 2,
                    (M, n1, cin)))
         ev.append(("igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2, (M, f, 9 * f)))
-        ev.append(("igemm", f"{b.name} c3 fwd", 2 * M * f * 4 * f, (M * f + 2 * M * 4 * f) * 2, (M, 4 * f, f)))
+        if b.proj and fuse:   # conv3 + the shortcut conv as one dual-source GEMM (K = f + cin)
+            ev.append(("igemm", f"{b.name} c3+c0 fwd", 2 * M * (f + cin) * 4 * f, (M * f + M * cin + M * 4 * f) * 2,
+                       (M, 4 * f, f + cin), "dual"))
+        else:
+            ev.append(("igemm", f"{b.name} c3 fwd", 2 * M * f * 4 * f, (M * f + 2 * M * 4 * f) * 2, (M, 4 * f, f)))
         geo.append((b, H, Ho))
         H = Ho
     ev.append(("gap_fwd", "gap", 0, B * H * H * 2048 * 2))
@@ -82,7 +86,8 @@ def main():
     rows = [r for r in csv.DictReader(open(path))]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
-    ev = schedule(B, crop)
+    import os
+    ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0")
     # a split launch (8-phase kernel for full rounds + 128x128 tail) is two dispatches of one layer
     try:
         from pddl.ops.native import require_native

