@@ -251,6 +251,25 @@ void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
   ok(pddl::wgrad_launch(p, cur_stream()), "wgrad");
 }
 
+// Fused stride-1 1x1 conv backward (bwd1x1.hip): g [.., 256], x [.., 64], wd [64][>=256] bf16,
+// bits [.., 8] uint8, out [.., 64] bf16, colsum fp32 >= partial rows x 64, dw fp32 [256][>=64].
+void bwd1x1(Tensor g, Tensor x, Tensor wd, Tensor bits, Tensor out, Tensor colsum, Tensor dw) {
+  pddl::Bwd1x1Params p{};
+  PCHECK(g.is_contiguous() && x.is_contiguous() && out.is_contiguous() && bits.is_contiguous(), "bwd1x1: contiguous operands");
+  PCHECK(g.size(-1) == 256 && x.size(-1) == 64 && out.size(-1) == 64 && bits.size(-1) == 8, "bwd1x1: channel counts");
+  const int64_t M = rows_of(g);
+  PCHECK(rows_of(x) == M && rows_of(out) == M && rows_of(bits) == M, "bwd1x1: row counts differ");
+  PCHECK(bits.is_cuda() && bits.scalar_type() == torch::kUInt8, "bwd1x1: bits must be a uint8 GPU tensor");
+  PCHECK(wd.dim() == 2 && wd.size(0) == 64 && wd.size(1) >= 256, "bwd1x1: wd must be [64][>=256]");
+  PCHECK(dw.dim() == 2 && dw.size(0) == 256 && dw.size(1) >= 64, "bwd1x1: dw must be [256][>=64]");
+  PCHECK(colsum.is_contiguous() && colsum.numel() >= (int64_t)pddl::bwd1x1_partial_rows((int)M) * 64,
+         "bwd1x1: colsum too small");
+  p.g = bfp(g); p.x = bfp(x); p.wd = bfp(wd); p.ld_wd = ld(wd); p.bits = bits.data_ptr<uint8_t>();
+  p.out = bfpm(out); p.colsum = f32p(colsum); p.dw = f32p(dw); p.ld_dw = ld(dw); p.M = (int)M;
+  ok(pddl::bwd1x1_launch(p, cur_stream()), "bwd1x1");
+}
+int64_t bwd1x1_partial_rows(int64_t M) { return pddl::bwd1x1_partial_rows((int)M); }
+
 // fp32 convolution (reference precision): y[N,Ho,Wo,Cout] = conv(x[N,H,W,C], w[Cout, R*S*C]) (+ bias)
 void conv_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tensor w, OptT bias, Tensor y) {
   pddl::ConvF32Params p{};
@@ -566,6 +585,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply, REL);
   m.attr("BNSTAT_LAYER_BYTES") = (int)sizeof(pddl::BnStatLayer);
   m.def("wgrad", &wgrad, REL);
+  m.def("bwd1x1", &bwd1x1, REL);
+  m.def("bwd1x1_partial_rows", &bwd1x1_partial_rows);
   m.def("conv_f32", &conv_f32, REL);
   m.def("conv_f32_epi", &conv_f32_epi, REL);
   m.def("maxpool_fwd_f32", &maxpool_fwd_f32, REL);

@@ -68,6 +68,21 @@ struct WgradParams {
 };
 const char* wgrad_launch(const WgradParams& p, hipStream_t stream);
 
+// Fused backward of a stride-1 1x1 conv with 256 output / 64 input channels (bwd1x1.hip):
+// out = bits * (g . Wd) with partial column sums, dw += g^T . x, from one read of g.
+struct Bwd1x1Params {
+  const uint16_t* g;                   // output gradient [M][256]
+  const uint16_t* x;                   // conv input [M][64]
+  const uint16_t* wd; int ld_wd;       // data-gradient weights [64][ld_wd >= 256]
+  const uint8_t* bits;                 // ReLU bits of x [M][8]
+  uint16_t* out;                       // input gradient [M][64]
+  float* colsum;                       // partial column sums [bwd1x1_partial_rows(M)][64]
+  float* dw; int ld_dw;                // fp32 [256][ld_dw >= 64], accumulated with atomics
+  int M;
+};
+const char* bwd1x1_launch(const Bwd1x1Params& p, hipStream_t stream);
+int bwd1x1_partial_rows(int M);
+
 // ---- fp32 convolution on the fp32 matrix cores (conv_f32.hip): the reference-precision path ----
 struct ConvF32Params {
   const float* x; int N, H, W, C;      // NHWC input (im2col source)

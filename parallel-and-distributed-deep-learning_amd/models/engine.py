@@ -45,7 +45,8 @@ def _ceil(a, b):
 
 class HipEngine:
     BN_MODES = ("frozen",)   # HipEngineBNTrain (models/engine_bn.py) runs bn_mode="train"
-    FUSE_PROJ_OK = True      # projection blocks: conv3 + shortcut conv as one dual-source GEMM
+    FUSE_PROJ_OK = True     # projection blocks: conv3 + shortcut conv as one dual-source GEMM
+    FUSE_BWD_OK = True      # stage-2 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
@@ -83,6 +84,9 @@ class HipEngine:
         # fused projection blocks (conv3 + shortcut conv as one dual-source GEMM, no shortcut
         # activation in HBM): their own folded affine slots (scale 1, shift b3 + b0)
         self.fuse_proj = self.FUSE_PROJ_OK and os.environ.get("PDDL_FUSE_PROJ", "1") != "0"
+        # stage-2 conv3 backward as one launch (bwd1x1.hip: data + weight gradient from one read
+        # of the 256-channel gradient; needs the ReLU bitmasks)
+        self.fuse_bwd = self.FUSE_BWD_OK and self.bitmask and os.environ.get("PDDL_FUSE_BWD", "1") != "0"
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -316,7 +320,10 @@ class HipEngine:
             if bi in s2:       # c3 dgrad runs on the compact stride-2 grid
                 Hc = Ho // 2 + Ho % 2
                 Mc = B * Hc * Hc
-            add(b.convs["2"].name, N.igemm_partial_rows(Mc, f, 4 * f), f)         # c3 dgrad -> g2
+            if self._bwd_fused(bi, b, s2):                                       # fused c3 backward -> g2
+                add(b.convs["2"].name, N.bwd1x1_partial_rows(M), f)
+            else:
+                add(b.convs["2"].name, N.igemm_partial_rows(Mc, f, 4 * f), f)     # c3 dgrad -> g2
             add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)          # c2 dgrad -> g1
             if bi > 0:                                                           # c1 dgrad -> g_out(prev)
                 add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin, 5 * f if b.proj else f), b.cin)
@@ -341,6 +348,9 @@ class HipEngine:
     def _wf(self, name, rows, k):
         o = self.wf[name]
         return self.wbf[o:o + rows * k].view(rows, k)
+
+    def _bwd_fused(self, bi, b, s2):
+        return self.fuse_bwd and b.filters == 64 and 4 * b.filters == 256 and bi not in s2
 
     def _wdv(self, name, cin, k):
         o = self.wd[name]
@@ -508,6 +518,10 @@ class HipEngine:
                 N.igemm(gc, None, Hc, Hc, 1, 1, 1, 0, Hc, Hc, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
                         None, g2, 0, g2c, 0, 0, 2, Ho, Ho, part(c2n), None)
                 N.wgrad(y1, Ho, Ho, 3, 3, 2, 1, Hc, Hc, g2c, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
+            elif self._bwd_fused(bi, b, s2):
+                # conv3: data and weight gradient from one read of gout
+                N.bwd1x1(gout, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f))
+                N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
             else:
                 # conv3
                 N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)

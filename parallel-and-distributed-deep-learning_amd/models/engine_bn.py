@@ -35,6 +35,7 @@ _STAT_FMT = "<8if i"   # BnStatLayer: C, sum_off, sq_off, ch, gamma, beta, mm, m
 
 class HipEngineBNTrain(HipEngine):
     BN_MODES = ("train",)
+    FUSE_BWD_OK = False    # (its conv3 dgrad carries the fused BN-backward sums)
     FUSE_PROJ_OK = False   # (batch statistics: the shortcut's BN cannot be folded into weights)
 
     def __init__(self, layout: ParamLayout, batch: int, **kw):

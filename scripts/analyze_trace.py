@@ -13,7 +13,7 @@ import pddl  # noqa
 from pddl.models.resnet50 import ParamLayout
 
 
-def schedule(B, crop, fuse=True):
+def schedule(B, crop, fuse=True, fuse_bwd=True):
     L = ParamLayout()
     H1 = (crop + 6 - 7) // 2 + 1
     H2 = (H1 + 2 - 3) // 2 + 1
@@ -53,8 +53,12 @@ def schedule(B, crop, fuse=True):
         M = B * Ho * Ho
         # blocks feeding a stride-2 block: conv3 wgrad/dgrad and conv2 wgrad on the compact quarter
         Mc = B * (Ho // 2 + Ho % 2) ** 2 if bi in s2 else M
-        ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * Mc * f * 4 * f, (Mc * f + Mc * 4 * f) * 2))
-        ev.append(("igemm", f"{b.name} c3 dgrad", 2 * Mc * f * 4 * f, (Mc * 4 * f + Mc * f + M * f) * 2, (Mc, f, 4 * f)))
+        if fuse_bwd and f == 64 and bi not in s2:   # bwd1x1: c3 dgrad + wgrad from one read of g
+            ev.append(("bwd1x1", f"{b.name} c3 dgrad+wgrad", 4 * M * f * 4 * f, (M * 4 * f + 2 * M * f) * 2))
+        else:
+            ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * Mc * f * 4 * f, (Mc * f + Mc * 4 * f) * 2))
+            ev.append(("igemm", f"{b.name} c3 dgrad", 2 * Mc * f * 4 * f, (Mc * 4 * f + Mc * f + M * f) * 2,
+                       (Mc, f, 4 * f)))
         ev.append(("wgrad", f"{b.name} c2 wgrad", 2 * Mc * 9 * f * f, (Mc + M) * f * 2))
         ev.append(("igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2, (M, f, 9 * f)))
         n1 = 5 * f if b.proj else f
@@ -87,7 +91,7 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
     import os
-    ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0")
+    ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0", os.environ.get("PDDL_FUSE_BWD", "1") != "0")
     # a split launch (8-phase kernel for full rounds + 128x128 tail) is two dispatches of one layer
     try:
         from pddl.ops.native import require_native
@@ -121,7 +125,7 @@ def main():
         kind, name, flops, byts = e[:4]
         rs = seg[k:k + n]
         k += n
-        kn = " + ".join(r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pddl::", "")[:22] for r in rs)
+        kn = " + ".join(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("pddl::", "")[:22] for r in rs)
         assert kind.split("_")[0] in kn, (kind, kn)
         t = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rs)
         tot += t
