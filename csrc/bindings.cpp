@@ -251,24 +251,30 @@ void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
   ok(pddl::wgrad_launch(p, cur_stream()), "wgrad");
 }
 
-// Fused stride-1 1x1 conv backward (bwd1x1.hip): g [.., 256], x [.., 64], wd [64][>=256] bf16,
-// bits [.., 8] uint8, out [.., 64] bf16, colsum fp32 >= partial rows x 64, dw fp32 [256][>=64].
+// Fused stride-1 1x1 conv backward (bwd1x1.hip): g [.., CO], x [.., CI], wd [CI][>=CO] bf16,
+// bits [.., CI/8] uint8, out [.., CI] bf16, colsum fp32 >= partial rows x CI, dw fp32 [CO][>=CI];
+// (CO, CI) = (256, 64) or (512, 128).
 void bwd1x1(Tensor g, Tensor x, Tensor wd, Tensor bits, Tensor out, Tensor colsum, Tensor dw) {
   pddl::Bwd1x1Params p{};
   PCHECK(g.is_contiguous() && x.is_contiguous() && out.is_contiguous() && bits.is_contiguous(), "bwd1x1: contiguous operands");
-  PCHECK(g.size(-1) == 256 && x.size(-1) == 64 && out.size(-1) == 64 && bits.size(-1) == 8, "bwd1x1: channel counts");
+  const int64_t CO = g.size(-1), CI = x.size(-1);
+  PCHECK((CO == 256 && CI == 64) || (CO == 512 && CI == 128), "bwd1x1: (CO, CI) must be (256, 64) or (512, 128)");
+  PCHECK(out.size(-1) == CI && bits.size(-1) == CI / 8, "bwd1x1: out / bits channel counts");
   const int64_t M = rows_of(g);
   PCHECK(rows_of(x) == M && rows_of(out) == M && rows_of(bits) == M, "bwd1x1: row counts differ");
   PCHECK(bits.is_cuda() && bits.scalar_type() == torch::kUInt8, "bwd1x1: bits must be a uint8 GPU tensor");
-  PCHECK(wd.dim() == 2 && wd.size(0) == 64 && wd.size(1) >= 256, "bwd1x1: wd must be [64][>=256]");
-  PCHECK(dw.dim() == 2 && dw.size(0) == 256 && dw.size(1) >= 64, "bwd1x1: dw must be [256][>=64]");
-  PCHECK(colsum.is_contiguous() && colsum.numel() >= (int64_t)pddl::bwd1x1_partial_rows((int)M) * 64,
+  PCHECK(wd.dim() == 2 && wd.size(0) == CI && wd.size(1) >= CO, "bwd1x1: wd must be [CI][>=CO]");
+  PCHECK(dw.dim() == 2 && dw.size(0) == CO && dw.size(1) >= CI, "bwd1x1: dw must be [CO][>=CI]");
+  PCHECK(colsum.is_contiguous() && colsum.numel() >= (int64_t)pddl::bwd1x1_partial_rows((int)M, (int)CO, (int)CI) * CI,
          "bwd1x1: colsum too small");
   p.g = bfp(g); p.x = bfp(x); p.wd = bfp(wd); p.ld_wd = ld(wd); p.bits = bits.data_ptr<uint8_t>();
-  p.out = bfpm(out); p.colsum = f32p(colsum); p.dw = f32p(dw); p.ld_dw = ld(dw); p.M = (int)M;
+  p.out = bfpm(out); p.colsum = f32p(colsum); p.dw = f32p(dw); p.ld_dw = ld(dw);
+  p.M = (int)M; p.CO = (int)CO; p.CI = (int)CI;
   ok(pddl::bwd1x1_launch(p, cur_stream()), "bwd1x1");
 }
-int64_t bwd1x1_partial_rows(int64_t M) { return pddl::bwd1x1_partial_rows((int)M); }
+int64_t bwd1x1_partial_rows(int64_t M, int64_t CO, int64_t CI) {
+  return pddl::bwd1x1_partial_rows((int)M, (int)CO, (int)CI);
+}
 
 // fp32 convolution (reference precision): y[N,Ho,Wo,Cout] = conv(x[N,H,W,C], w[Cout, R*S*C]) (+ bias)
 void conv_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tensor w, OptT bias, Tensor y) {

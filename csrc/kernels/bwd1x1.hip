@@ -29,7 +29,7 @@ namespace pddl {
 
 namespace {
 
-constexpr int B1_CO = 256, B1_CI = 64, B1_MT = 64;
+constexpr int B1_MT = 64;
 
 // the wgrad_kernel swizzles (wgrad.hip): [m][128 bf16] rows and [m][64 bf16] rows
 __device__ __forceinline__ int b1_swz256(int row) { return ((row & 3) | ((row >> 1) & 4)) << 1; }
@@ -47,35 +47,52 @@ __device__ __forceinline__ b1_v4u b1_read16(const char* p) {
   return r;
 }
 
-__global__ void __launch_bounds__(256, 2) bwd1x1_kernel(Bwd1x1Params p) {
-  constexpr int CO = B1_CO, CI = B1_CI, MT = B1_MT;
-  constexpr int GH_BYTES = MT * 128 * 2;                 // one 128-co half image: 16 KiB
-  constexpr int G_BYTES = 2 * GH_BYTES, X_BYTES = MT * CI * 2;
-  constexpr int STAGE = G_BYTES + X_BYTES;               // 40 KiB: two stages, two workgroups per CU
-  constexpr int LDF = CI + 4;                            // fp32 staging row of the dgrad tile
+// CO: gradient channels (256 stage 2, 512 stage 3); NW: waves (4: two 80 KiB workgroups per CU;
+// 8: one 144 KiB workgroup).  A workgroup owns input-channel columns [64 half, 64 half + 64) of
+// CI = 64 NH: with NH = 2 (stage 3: CI = 128 would need 272 registers per lane for the dW tile and
+// the weight fragments) the two halves of a tile run as a PAIR of workgroups b, b + 8 -- the same
+// XCD under the round-robin dispatch -- in lockstep, so the second read of each g tile hits L2.
+template <int CO, int NW>
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1Params p) {
+  constexpr int CB = 64, MT = B1_MT;
+  constexpr int NIMG = CO / 128;                         // 128-co half images
+  constexpr int GH_BYTES = MT * 256;                     // one image: 16 KiB
+  constexpr int G_BYTES = NIMG * GH_BYTES, X_BYTES = MT * CB * 2;
+  constexpr int STAGE = G_BYTES + X_BYTES;               // 40 KiB (256) / 72 KiB (512); two stages
+  constexpr int GP = NIMG * 16 / NW, XP = 8 / NW;        // LDS-DMA pieces per wave per tile
+  constexpr int KSPLIT = NW / 4;                         // waves per 16-column dgrad block (co split)
+  constexpr int KS = CO / 32 / KSPLIT;                   // dgrad k-steps per wave
+  constexpr int RPT = 512 / (NW * 64);                   // epilogue rows per thread (8 columns each)
+  constexpr int LDF = CB + 4;                            // fp32 staging row of the dgrad tile
+  constexpr int PART = MT * LDF * 4;                     // one staged partial dgrad tile
+  static_assert(CO == 64 * NW && KS == 8 && GP * NW == NIMG * 16 && XP * NW == 8, "bwd1x1 shape");
+  static_assert(KSPLIT * PART <= G_BYTES, "dgrad staging must fit over the g images");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int CI = p.CI, nh = CI / CB;
+  int pid = blockIdx.x, half = 0, np = gridDim.x;
+  if (nh == 2) {   // workgroups b and b + 8 of every 16 share an XCD: one is each half of a pair
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    half = k & 1; pid = (k >> 1) * 8 + x; np = gridDim.x / 2;
+  }
   const int T = (p.M + MT - 1) / MT;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int nit = b < T ? (T - b + G - 1) / G : 0;
+  const int nit = pid < T ? (T - pid + np - 1) / np : 0;
 
-  // LDS-DMA lane offsets relative to the tile's first row: g half h, piece i covers rows
-  // (wave*4 + i)*4 + lane/16 (16 chunks of 16 B); x piece i covers rows (wave*2 + i)*8 + lane/8
+  // LDS-DMA lane offsets relative to the tile's first row: g piece pi = wave * GP + i fills image
+  // pi / 16, rows (pi % 16) * 4 + lane / 16 (16 chunks of 16 B); x piece xi rows xi * 8 + lane / 8
   const int lrow = lane >> 4, lpos = lane & 15;
-  uint32_t g_off[8], x_off[2];
+  uint32_t g_off[GP], x_off[XP];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int i = 0; i < GP; ++i) {
+    const int pi = wave * GP + i, row = (pi & 15) * 4 + lrow;
+    g_off[i] = (uint32_t)((row * CO + (pi >> 4) * 128 + (lpos ^ b1_swz256(row)) * 8) * 2);
+  }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (wave * 4 + i) * 4 + lrow;
-      g_off[h * 4 + i] = (uint32_t)((row * CO + h * 128 + (lpos ^ b1_swz256(row)) * 8) * 2);
-    }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wave * 2 + i) * 8 + (lane >> 3);
-    x_off[i] = (uint32_t)((row * CI + ((lane & 7) ^ b1_swz128(row)) * 8) * 2);
+  for (int i = 0; i < XP; ++i) {
+    const int row = (wave * XP + i) * 8 + (lane >> 3);
+    x_off[i] = (uint32_t)((row * CI + half * CB + ((lane & 7) ^ b1_swz128(row)) * 8) * 2);
   }
   auto load_tile = [&](int tile, int buf) {
     const long m0 = (long)tile * MT;
@@ -83,19 +100,22 @@ __global__ void __launch_bounds__(256, 2) bwd1x1_kernel(Bwd1x1Params p) {
     const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, m0 * CI, (long)p.M * CI);
     char* gb = smem + buf * STAGE;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int i = 0; i < GP; ++i) {
+      const int pi = wave * GP + i;
+      buf_lds16(rg, LDS_PTR(gb + (pi >> 4) * GH_BYTES + (pi & 15) * 1024), g_off[i], 0);
+    }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) buf_lds16(rg, LDS_PTR(gb + h * GH_BYTES + (wave * 4 + i) * 1024), g_off[h * 4 + i], 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) buf_lds16(rx, LDS_PTR(gb + G_BYTES + (wave * 2 + i) * 1024), x_off[i], 0);
+    for (int i = 0; i < XP; ++i) buf_lds16(rx, LDS_PTR(gb + G_BYTES + (wave * XP + i) * 1024), x_off[i], 0);
   };
 
-  // dgrad weights of this wave's 16 ci columns (MFMA A operand: row ci, 8 co per lane per k-step)
-  v8bf wa[8];
+  // dgrad roles: 16-column block cb of this half, co range kp * CO / KSPLIT ..; the weights of
+  // that block and range stay in registers (MFMA A operand: row ci, 8 co per lane per k-step)
+  const int cb = wave & 3, kp = wave >> 2;
+  v8bf wa[KS];
   {
-    const uint16_t* wr = p.wd + (long)(16 * wave + (lane & 15)) * p.ld_wd + 8 * (lane >> 4);
+    const uint16_t* wr = p.wd + (long)(half * CB + 16 * cb + (lane & 15)) * p.ld_wd + kp * (CO / KSPLIT) + 8 * (lane >> 4);
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) wa[ks] = *reinterpret_cast<const v8bf*>(wr + 32 * ks);
+    for (int ks = 0; ks < KS; ++ks) wa[ks] = *reinterpret_cast<const v8bf*>(wr + 32 * ks);
   }
 
   v4f accw[4][4];
@@ -104,46 +124,48 @@ __global__ void __launch_bounds__(256, 2) bwd1x1_kernel(Bwd1x1Params p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) accw[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int er = tid >> 3, ec = tid & 7;          // epilogue: rows er, er + 32; ci 8ec .. 8ec + 7
-  const int wm = wave & 1;                        // wgrad: co rows 64*wave .. +63 (half wave >> 1)
+  const int er = tid >> 3, ec = tid & 7;          // epilogue: rows er + NW * 8 * q; ci 8ec .. 8ec + 7
+  const int wm = wave & 1;                        // wgrad: co rows 64*wave .. +63 (image wave >> 1)
   const int Gq = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
 
-  uint32_t bt_next[2];
+  uint32_t bt_next[RPT];
   auto load_bits = [&](int tile) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {   // row clamped, value zeroed: no branch around the load
-      const long r = (long)tile * MT + er + 32 * q;
-      const uint32_t v = p.bits[(r < p.M ? r : p.M - 1) * (CI / 8) + ec];
+    for (int q = 0; q < RPT; ++q) {   // row clamped, value zeroed: no branch around the load
+      const long r = (long)tile * MT + er + NW * 8 * q;
+      const uint32_t v = p.bits[(r < p.M ? r : p.M - 1) * (CI / 8) + half * 8 + ec];
       bt_next[q] = r < p.M ? v : 0u;
     }
   };
   if (nit > 0) {
-    load_tile(b, 0);
-    load_bits(b);
+    load_tile(pid, 0);
+    load_bits(pid);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   for (int it = 0; it < nit; ++it) {
-    const int cur = it & 1, tile = b + it * G;
+    const int cur = it & 1, tile = pid + it * np;
     const long m0 = (long)tile * MT;
     // next tile (unconditional: past the last tile the descriptor is empty and the DMA writes
     // zeros into the idle buffer), then the next tile's ReLU bits into registers: both land by
     // the vmcnt(0) that ends this iteration, so no wait the compiler places for the bytes can
     // hold back a DMA (waiting for them here, before the GEMMs, drained the prefetch)
-    load_tile(tile + G, cur ^ 1);
-    const uint32_t bt[2] = {bt_next[0], bt_next[1]};
-    load_bits(tile + G);
+    load_tile(tile + np, cur ^ 1);
+    uint32_t bt[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) bt[q] = bt_next[q];
+    load_bits(tile + np);
     const char* gb = smem + cur * STAGE;
     const char* xb = gb + G_BYTES;
 
     // ---- data gradient: D[ci][m] = sum_co Wd[ci][co] g[m][co]; lane (grp, r): ci 4grp..4grp+3
-    // (of the wave's 16), m = 16i + r.  Reads of k-step ks + 1 are issued before the MFMAs of ks.
+    // of block cb, m = 16i + r.  Reads of k-step ks + 1 are issued before the MFMAs of ks.
     v4f accd[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) accd[i] = v4f{0.f, 0.f, 0.f, 0.f};
     b1_v4u ga[2][4];
     auto read_ks = [&](int ks, b1_v4u (&dst)[4]) {
-      const int c = 4 * ks + (lane >> 4);         // logical 16-byte chunk (8 co) of the k-step
+      const int c = 4 * (kp * KS + ks) + (lane >> 4);   // logical 16-byte chunk (8 co) of the k-step
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = 16 * i + (lane & 15);
@@ -152,8 +174,8 @@ __global__ void __launch_bounds__(256, 2) bwd1x1_kernel(Bwd1x1Params p) {
     };
     read_ks(0, ga[0]);
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      if (ks + 1 < 8) {
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
         read_ks(ks + 1, ga[(ks + 1) & 1]);
         asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
       } else {
@@ -201,49 +223,55 @@ __global__ void __launch_bounds__(256, 2) bwd1x1_kernel(Bwd1x1Params p) {
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- dgrad epilogue: fp32 tile staged over this buffer's g image (every wave is done with it)
+    // ---- dgrad epilogue: the KSPLIT partial fp32 tiles staged over this buffer's g images
+    // (every wave is done with them), summed on the read-back
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     char* st = smem + cur * STAGE;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = 16 * i + (lane & 15), col = 16 * wave + 4 * (lane >> 4);
-      const uint32_t a = (uint32_t)(uintptr_t)LDS_PTR(st + (row * LDF + col) * 4);
+      const int row = 16 * i + (lane & 15), col = 16 * cb + 4 * (lane >> 4);
+      const uint32_t a = (uint32_t)(uintptr_t)LDS_PTR(st + kp * PART + (row * LDF + col) * 4);
       asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(accd[i]) : "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    float w[2][8];
+    float w[RPT][8];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int row = er + 32 * q;
-      const uint32_t a = (uint32_t)(uintptr_t)LDS_PTR(st + (row * LDF + ec * 8) * 4);
-      float4 v0, v1;
-      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(v0), "=&v"(v1) : "v"(a) : "memory");
-      const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    for (int q = 0; q < RPT; ++q) {
+      const int row = er + NW * 8 * q;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KSPLIT; ++k) {
+        const uint32_t a = (uint32_t)(uintptr_t)LDS_PTR(st + k * PART + (row * LDF + ec * 8) * 4);
+        float4 v0, v1;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(v0), "=&v"(v1) : "v"(a) : "memory");
+        v[0] += v0.x; v[1] += v0.y; v[2] += v0.z; v[3] += v0.w; v[4] += v1.x; v[5] += v1.y; v[6] += v1.z; v[7] += v1.w;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         w[q][e] = ((bt[q] >> e) & 1u) ? v[e] : 0.f;
         csum[e] += w[q][e];
       }
     }
-    // (both rows' bits consumed before the first store: a store under a branch in between would
-    // make the compiler's wait for the second byte a vmcnt(0))
+    // (every row's bits consumed before the first store: a store under a branch in between would
+    // make the compiler's wait for the next byte a vmcnt(0))
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const long gm = m0 + er + 32 * q;
-      if (gm < p.M) *reinterpret_cast<uint4*>(p.out + gm * CI + ec * 8) = pack8(w[q]);
+    for (int q = 0; q < RPT; ++q) {
+      const long gm = m0 + er + NW * 8 * q;
+      if (gm < p.M) *reinterpret_cast<uint4*>(p.out + gm * CI + half * CB + ec * 8) = pack8(w[q]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile landed
     __syncthreads();                                    // ... and every wave is done with this buffer
   }
 
-  // per-wave partial column sums (one row per wave; the launch reports 4 x grid rows)
+  // per-wave partial column sums: row pid * NW + wave, this half's 64 columns (the launch
+  // reports np * NW rows of CI columns)
 #pragma unroll
   for (int o = 8; o < 64; o <<= 1)
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
   if (lane < 8) {
-    float4* dst = reinterpret_cast<float4*>(p.colsum + (long)(b * 4 + wave) * CI + ec * 8);
+    float4* dst = reinterpret_cast<float4*>(p.colsum + (long)(pid * NW + wave) * CI + half * CB + ec * 8);
     dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
     dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
   }
@@ -264,7 +292,7 @@ __global__ void __launch_bounds__(256, 2) bwd1x1_kernel(Bwd1x1Params p) {
     __syncthreads();
     for (int r = 0; r < 32; ++r) {
       const int co = 64 * wave + pass * 32 + r;
-      unsafeAtomicAdd(p.dw + (long)co * p.ld_dw + lane, stage[r * LDF + lane]);
+      unsafeAtomicAdd(p.dw + (long)co * p.ld_dw + half * CB + lane, stage[r * LDF + lane]);
     }
     __syncthreads();
   }
@@ -272,17 +300,35 @@ __global__ void __launch_bounds__(256, 2) bwd1x1_kernel(Bwd1x1Params p) {
 
 }  // namespace
 
-int bwd1x1_grid(int M) {
-  const long T = (M + B1_MT - 1) / B1_MT, G = 2L * num_cus();
-  return (int)(T < G ? T : G);
+// Launch geometry: (workgroups, pairs).  NW = 4 (CO 256): two per CU, one per tile column
+// block; NW = 8 (CO 512, CI 128): one per CU, as pairs (a multiple of 8 pairs: the XCD pairing).
+static void bwd1x1_geom(int M, int CO, int CI, int* grid, int* np) {
+  const long T = (M + B1_MT - 1) / B1_MT;
+  if (CO == 256) {
+    const long G = 2L * num_cus();
+    *np = *grid = (int)(T < G ? T : G);
+    return;
+  }
+  long P = (num_cus() / 2) / 8 * 8;
+  if (P < 8) P = 8;
+  *np = (int)P;
+  *grid = (int)(P * (CI / 64));
 }
-int bwd1x1_partial_rows(int M) { return 4 * bwd1x1_grid(M); }
+int bwd1x1_partial_rows(int M, int CO, int CI) {
+  int grid, np;
+  bwd1x1_geom(M, CO, CI, &grid, &np);
+  return np * (CO == 256 ? 4 : 8);
+}
 
 const char* bwd1x1_launch(const Bwd1x1Params& p, hipStream_t stream) {
   if (p.M <= 0) return "bwd1x1: empty problem";
-  if ((long)p.M * B1_CO >= (1L << 31)) return "bwd1x1: gradient has more than 2^31 elements";
-  if (p.ld_wd < B1_CO || p.ld_wd % 8 || p.ld_dw < B1_CI) return "bwd1x1: weight / gradient row strides";
-  hipLaunchKernelGGL(bwd1x1_kernel, dim3(bwd1x1_grid(p.M)), dim3(256), 0, stream, p);
+  if (!((p.CO == 256 && p.CI == 64) || (p.CO == 512 && p.CI == 128))) return "bwd1x1: (CO, CI) must be (256, 64) or (512, 128)";
+  if ((long)p.M * p.CO >= (1L << 31)) return "bwd1x1: gradient has more than 2^31 elements";
+  if (p.ld_wd < p.CO || p.ld_wd % 8 || p.ld_dw < p.CI) return "bwd1x1: weight / gradient row strides";
+  int grid, np;
+  bwd1x1_geom(p.M, p.CO, p.CI, &grid, &np);
+  if (p.CO == 256) hipLaunchKernelGGL((bwd1x1_kernel<256, 4>), dim3(grid), dim3(256), 0, stream, p);
+  else hipLaunchKernelGGL((bwd1x1_kernel<512, 8>), dim3(grid), dim3(512), 0, stream, p);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

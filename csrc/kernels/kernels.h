@@ -68,20 +68,21 @@ struct WgradParams {
 };
 const char* wgrad_launch(const WgradParams& p, hipStream_t stream);
 
-// Fused backward of a stride-1 1x1 conv with 256 output / 64 input channels (bwd1x1.hip):
-// out = bits * (g . Wd) with partial column sums, dw += g^T . x, from one read of g.
+// Fused backward of a stride-1 1x1 conv with (CO, CI) = (256, 64) or (512, 128) output / input
+// channels (bwd1x1.hip): out = bits * (g . Wd) with partial column sums, dw += g^T . x, from one
+// HBM read of g.
 struct Bwd1x1Params {
-  const uint16_t* g;                   // output gradient [M][256]
-  const uint16_t* x;                   // conv input [M][64]
-  const uint16_t* wd; int ld_wd;       // data-gradient weights [64][ld_wd >= 256]
-  const uint8_t* bits;                 // ReLU bits of x [M][8]
-  uint16_t* out;                       // input gradient [M][64]
-  float* colsum;                       // partial column sums [bwd1x1_partial_rows(M)][64]
-  float* dw; int ld_dw;                // fp32 [256][ld_dw >= 64], accumulated with atomics
-  int M;
+  const uint16_t* g;                   // output gradient [M][CO]
+  const uint16_t* x;                   // conv input [M][CI]
+  const uint16_t* wd; int ld_wd;       // data-gradient weights [CI][ld_wd >= CO]
+  const uint8_t* bits;                 // ReLU bits of x [M][CI / 8]
+  uint16_t* out;                       // input gradient [M][CI]
+  float* colsum;                       // partial column sums [bwd1x1_partial_rows(M, CO, CI)][CI]
+  float* dw; int ld_dw;                // fp32 [CO][ld_dw >= CI], accumulated with atomics
+  int M, CO, CI;
 };
 const char* bwd1x1_launch(const Bwd1x1Params& p, hipStream_t stream);
-int bwd1x1_partial_rows(int M);
+int bwd1x1_partial_rows(int M, int CO, int CI);
 
 // ---- fp32 convolution on the fp32 matrix cores (conv_f32.hip): the reference-precision path ----
 struct ConvF32Params {

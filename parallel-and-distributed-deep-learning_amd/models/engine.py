@@ -46,7 +46,7 @@ def _ceil(a, b):
 class HipEngine:
     BN_MODES = ("frozen",)   # HipEngineBNTrain (models/engine_bn.py) runs bn_mode="train"
     FUSE_PROJ_OK = True     # projection blocks: conv3 + shortcut conv as one dual-source GEMM
-    FUSE_BWD_OK = True      # stage-2 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
+    FUSE_BWD_OK = True      # stage-2/3 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
@@ -84,9 +84,10 @@ class HipEngine:
         # fused projection blocks (conv3 + shortcut conv as one dual-source GEMM, no shortcut
         # activation in HBM): their own folded affine slots (scale 1, shift b3 + b0)
         self.fuse_proj = self.FUSE_PROJ_OK and os.environ.get("PDDL_FUSE_PROJ", "1") != "0"
-        # stage-2 conv3 backward as one launch (bwd1x1.hip: data + weight gradient from one read
-        # of the 256-channel gradient; needs the ReLU bitmasks)
+        # stage-2/3 conv3 backward as one launch (bwd1x1.hip: data + weight gradient from one read
+        # of the 256 / 512-channel gradient; needs the ReLU bitmasks)
         self.fuse_bwd = self.FUSE_BWD_OK and self.bitmask and os.environ.get("PDDL_FUSE_BWD", "1") != "0"
+        self._fuse_bwd3 = os.environ.get("PDDL_FUSE_BWD", "1") != "2"
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -321,7 +322,7 @@ class HipEngine:
                 Hc = Ho // 2 + Ho % 2
                 Mc = B * Hc * Hc
             if self._bwd_fused(bi, b, s2):                                       # fused c3 backward -> g2
-                add(b.convs["2"].name, N.bwd1x1_partial_rows(M), f)
+                add(b.convs["2"].name, N.bwd1x1_partial_rows(M, 4 * f, f), f)
             else:
                 add(b.convs["2"].name, N.igemm_partial_rows(Mc, f, 4 * f), f)     # c3 dgrad -> g2
             add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)          # c2 dgrad -> g1
@@ -350,7 +351,8 @@ class HipEngine:
         return self.wbf[o:o + rows * k].view(rows, k)
 
     def _bwd_fused(self, bi, b, s2):
-        return self.fuse_bwd and b.filters == 64 and 4 * b.filters == 256 and bi not in s2
+        # stage 2 (256 <- 64 channels) and stage 3 (512 <- 128); PDDL_FUSE_BWD=2: stage 2 only
+        return self.fuse_bwd and bi not in s2 and (b.filters == 64 or (b.filters == 128 and self._fuse_bwd3))
 
     def _wdv(self, name, cin, k):
         o = self.wd[name]

@@ -8,7 +8,7 @@ b() { local n=$1; shift; timeout -k 10 300 python bench.py "$@" > gpurun_out/ab/
 true && \
 timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k bwd1x1 > gpurun_out/ab/t_kernel.log 2>&1 && \
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_engine.py tests/test_gpu_kernels.py > gpurun_out/ab/tests.log 2>&1 && \
-b w1 --batch 1024 && PDDL_FUSE_BWD=0 b w0 --batch 1024 && b w1_b2048 && PDDL_FUSE_BWD=0 b w0_b2048 && b w1b --batch 1024 && \
+b w1 --batch 1024 && PDDL_FUSE_BWD=2 b w2 --batch 1024 && b w1_b2048 && PDDL_FUSE_BWD=2 b w2_b2048 && b w1b --batch 1024 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab/prof_w1 -o run --output-format csv -- python bench.py --batch 1024 --steps 6 --warmup 3 > gpurun_out/ab/prof_w1.log 2>&1
 rc=$?
 tail -n 3 gpurun_out/ab/t_kernel.log gpurun_out/ab/tests.log 2>/dev/null

@@ -892,27 +892,30 @@ def test_igemm_pk_matches(case, nb):
     assert rel(outs[1], outs[0]) < 1e-5
 
 
-@pytest.mark.parametrize("M", [64 * 5 + 13, 64 * 1100 + 29])
-def test_bwd1x1_fused(M):
-    """Fused 1x1 backward (bwd1x1.hip: one read of the 256-channel gradient feeds the data
-    gradient with its ReLU bits and column sums AND the weight gradient) vs fp32 references:
+@pytest.mark.parametrize("co,ci,M", [(256, 64, 64 * 5 + 13), (256, 64, 64 * 1100 + 29), (512, 128, 64 * 3 + 7),
+                                     (512, 128, 64 * 700 + 45)])
+def test_bwd1x1_fused(co, ci, M):
+    """Fused 1x1 backward (bwd1x1.hip: one read of the output gradient feeds the data gradient
+    with its ReLU bits and column sums AND the weight gradient) vs fp32 references:
     out = bits(x) * (g . Wd^T), dw += g^T . x, sum of the partial column-sum rows = out.sum(0).
-    The second size gives every workgroup of the persistent grid several tiles and a ragged
-    last tile."""
+    Stage-2 shape (256 <- 64) and stage-3 shape (512 <- 128, run as XCD-paired workgroups, one
+    per 64-column half); the larger sizes give every workgroup several tiles and a ragged last
+    tile, the small ones leave most workgroups without a tile."""
     torch.manual_seed(11)
-    g = rnd(M, 256)
-    x = torch.relu(rnd(M, 64))
-    wd = rnd(64, 256, scale=0.05)
-    bits = ((x > 0).view(M, 8, 8).to(torch.int32) << torch.arange(8, device=dev, dtype=torch.int32)).sum(-1)
+    g = rnd(M, co)
+    x = torch.relu(rnd(M, ci))
+    wd = rnd(ci, co, scale=0.05)
+    nb = ci // 8
+    bits = ((x > 0).view(M, nb, 8).to(torch.int32) << torch.arange(8, device=dev, dtype=torch.int32)).sum(-1)
     bits = bits.to(torch.uint8).contiguous()
-    out = torch.full((M, 64), float("nan"), device=dev, dtype=torch.bfloat16)
-    rows = N().bwd1x1_partial_rows(M)
-    colsum = torch.full((rows * 64,), float("nan"), device=dev)
-    dw0 = torch.randn(256, 64, device=dev)
+    out = torch.full((M, ci), float("nan"), device=dev, dtype=torch.bfloat16)
+    rows = N().bwd1x1_partial_rows(M, co, ci)
+    colsum = torch.full((rows * ci,), float("nan"), device=dev)
+    dw0 = torch.randn(co, ci, device=dev)
     dw = dw0.clone()
     N().bwd1x1(g, x, wd, bits, out, colsum, dw)
     torch.cuda.synchronize()
     ref = (g.float() @ wd.float().t()) * (x > 0)
     assert rel(out, ref) < 1e-2
-    assert rel(colsum.view(rows, 64).sum(0), ref.sum(0)) < 1e-3
+    assert rel(colsum.view(rows, ci).sum(0), ref.sum(0)) < 1e-3
     assert rel(dw - dw0, g.float().t() @ x.float()) < 1e-3
