@@ -11,7 +11,7 @@
 
 Config: Keras-v1 ResNet-50 (25,636,712 params, random init), synthetic 3x224x224 uint8
 images + random labels, bf16 compute / fp32 master weights, frozen BN (the reference's
-`training=False`, Q3), Adam (the reference optimizer), per-GPU batch 2048 fixed (weak
+`training=False`, Q3), Adam (the reference optimizer), per-GPU batch 2560 fixed (weak
 scaling).  The step is the SAME strategy code the entry scripts run (parallel/strategies.py):
 
   horovod      imagenet-resnet50-hvd.py: 1 process per GPU, gradient buckets all-reduced by the
@@ -72,12 +72,13 @@ def parse(argv=None):
     ap.add_argument("--strategy", default="horovod", choices=["horovod", "mirrored", "multiworker", "ps"])
     ap.add_argument("--ps", type=int, default=None, help="ps: parameter-server roles (default gpus // 4, >= 1)")
     ap.add_argument("--local-gpus", type=int, default=1, help="multiworker: GPUs per worker process")
-    # Per-GPU batch sized for 288 GB HBM3E (BASELINE north star): b2048 holds 66 GB; its stage-1
-    # activations (3.3 GB) are reached through per-tile rebased buffer descriptors.  Measured on
+    # Per-GPU batch sized for 288 GB HBM3E (BASELINE north star): b2560 holds 75 GB; its stage-1
+    # activations (4.1 GB) are reached through per-tile rebased buffer descriptors.  Measured on
     # 1 MI355X, round 3: b512 20.6k, b1024 23.0-23.4k, b1536 24.3k, b2048 24.6k images/s
-    # (profiles/r3_batch_plateau.txt); the per-step fixed cost is ~4.4 ms, so larger batches
-    # add < 1 % (and b2675+ would exceed 2^31 elements in one activation).
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 2048; fp32 256; CPU 32)")
+    # (profiles/r3_batch_plateau.txt); after the fused kernels b2048 26.16-26.17k vs b2560
+    # 26.57-26.58k on one box (profiles/r3_b2560_ab.txt: the ~4.4 ms per-step fixed cost
+    # amortised further).  b2675+ would exceed 2^31 elements in conv1's output.
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 2560; fp32 256; CPU 32)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--crop", type=int, default=None, help="network input (default = image size)")
     ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
@@ -96,7 +97,7 @@ def parse(argv=None):
                          "rank dumps its stacks and the job exits non-zero")
     args = ap.parse_args(argv)
     if args.batch is None:
-        args.batch = 32 if args.device == "cpu" else (256 if args.precision == "fp32" else 2048)
+        args.batch = 32 if args.device == "cpu" else (256 if args.precision == "fp32" else 2560)
     if args.crop is None:
         args.crop = args.image_size
     if args.timeout is None:
