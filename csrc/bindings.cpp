@@ -254,14 +254,24 @@ void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
 // Fused stride-1 1x1 conv backward (bwd1x1.hip): g [.., CO], x [.., CI], wd [CI][>=CO] bf16,
 // bits [.., CI/8] uint8, out [.., CI] bf16, colsum fp32 >= partial rows x CI, dw fp32 [CO][>=CI];
 // (CO, CI) = (256, 64) or (512, 128).
-void bwd1x1(Tensor g, Tensor x, Tensor wd, Tensor bits, Tensor out, Tensor colsum, Tensor dw) {
+void bwd1x1(Tensor g, Tensor x, Tensor wd, Tensor bits, Tensor out, Tensor colsum, Tensor dw, OptT out2) {
   pddl::Bwd1x1Params p{};
   PCHECK(g.is_contiguous() && x.is_contiguous() && out.is_contiguous() && bits.is_contiguous(), "bwd1x1: contiguous operands");
   const int64_t CO = g.size(-1), CI = x.size(-1);
   PCHECK((CO == 256 && CI == 64) || (CO == 512 && CI == 128), "bwd1x1: (CO, CI) must be (256, 64) or (512, 128)");
   PCHECK(out.size(-1) == CI && bits.size(-1) == CI / 8, "bwd1x1: out / bits channel counts");
   const int64_t M = rows_of(g);
-  PCHECK(rows_of(x) == M && rows_of(out) == M && rows_of(bits) == M, "bwd1x1: row counts differ");
+  if (out2.has_value()) {   // stride-2 form: g / out2 on the compact grid of x / out / bits
+    PCHECK(g.dim() == 4 && x.dim() == 4 && out.sizes() == x.sizes() && out2->is_contiguous() && rows_of(*out2) == M &&
+               out2->size(-1) == CI && g.size(0) == x.size(0) && g.size(1) == (x.size(1) + 1) / 2 &&
+               g.size(2) == (x.size(2) + 1) / 2 && rows_of(bits) == rows_of(x),
+           "bwd1x1: stride-2 form needs g [N,Hc,Wc,CO], x / out [N,Hf,Wf,CI], bits [.., CI/8] at x's rows, out2 [N,Hc,Wc,CI]");
+    p.s2 = 1; p.N = (int)x.size(0); p.Hf = (int)x.size(1); p.Wf = (int)x.size(2); p.Hc = (int)g.size(1);
+    p.Wc = (int)g.size(2); p.out2 = bfpm(*out2);
+    PCHECK((int64_t)p.N * p.Hf * p.Wf * CI < (1LL << 31), "bwd1x1: more than 2^31 elements");
+  } else {
+    PCHECK(rows_of(x) == M && rows_of(out) == M && rows_of(bits) == M, "bwd1x1: row counts differ");
+  }
   PCHECK(bits.is_cuda() && bits.scalar_type() == torch::kUInt8, "bwd1x1: bits must be a uint8 GPU tensor");
   PCHECK(wd.dim() == 2 && wd.size(0) == CI && wd.size(1) >= CO, "bwd1x1: wd must be [CI][>=CO]");
   PCHECK(dw.dim() == 2 && dw.size(0) == CO && dw.size(1) >= CI, "bwd1x1: dw must be [CO][>=CI]");
@@ -591,7 +601,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply, REL);
   m.attr("BNSTAT_LAYER_BYTES") = (int)sizeof(pddl::BnStatLayer);
   m.def("wgrad", &wgrad, REL);
-  m.def("bwd1x1", &bwd1x1, REL);
+  m.def("bwd1x1", &bwd1x1, REL, py::arg("g"), py::arg("x"), py::arg("wd"), py::arg("bits"), py::arg("out"),
+        py::arg("colsum"), py::arg("dw"), py::arg("out2") = py::none());
   m.def("bwd1x1_partial_rows", &bwd1x1_partial_rows);
   m.def("conv_f32", &conv_f32, REL);
   m.def("conv_f32_epi", &conv_f32_epi, REL);

@@ -52,7 +52,7 @@ __device__ __forceinline__ b1_v4u b1_read16(const char* p) {
 // CI = 64 NH: with NH = 2 (stage 3: CI = 128 would need 272 registers per lane for the dW tile and
 // the weight fragments) the two halves of a tile run as a PAIR of workgroups b, b + 8 -- the same
 // XCD under the round-robin dispatch -- in lockstep, so the second read of each g tile hits L2.
-template <int CO, int NW>
+template <int CO, int NW, bool S2>
 __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1Params p) {
   constexpr int CB = 64, MT = B1_MT;
   constexpr int NIMG = CO / 128;                         // 128-co half images
@@ -94,18 +94,41 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1
     const int row = (wave * XP + i) * 8 + (lane >> 3);
     x_off[i] = (uint32_t)((row * CI + half * CB + ((lane & 7) ^ b1_swz128(row)) * 8) * 2);
   }
+  // S2 (the block feeds a stride-2 block): the gradient g and the compact copy out2 are on the
+  // stride-2 grid (M = N * Hc * Wc rows), x, out and the bits at full resolution Hf x Wf: compact
+  // row m is full-resolution pixel (n, 2i, 2j)
+  const int HWc = p.Hc * p.Wc;
+  auto full_row = [&](long m) -> long {
+    const int n = fdiv((int)m, p.mg_hwc), rem = (int)m - n * HWc, i = fdiv(rem, p.mg_wc), j = rem - i * p.Wc;
+    return ((long)n * p.Hf + 2 * i) * p.Wf + 2 * j;
+  };
   auto load_tile = [&](int tile, int buf) {
     const long m0 = (long)tile * MT;
     const __amdgpu_buffer_rsrc_t rg = make_rsrc_at(p.g, m0 * CO, (long)p.M * CO);   // rows >= M read zeros
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, m0 * CI, (long)p.M * CI);
     char* gb = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < GP; ++i) {
       const int pi = wave * GP + i;
       buf_lds16(rg, LDS_PTR(gb + (pi >> 4) * GH_BYTES + (pi & 15) * 1024), g_off[i], 0);
     }
+    if constexpr (S2) {   // x rows gathered at the grid pixels, descriptor rebased at the tile's first image
+      const int n_first = fdiv((int)(m0 < p.M ? m0 : 0), p.mg_hwc);
+      const long HWf = (long)p.Hf * p.Wf;
+      const __amdgpu_buffer_rsrc_t rx =
+          make_rsrc_at(p.x, m0 < p.M ? n_first * HWf * CI : 0, m0 < p.M ? (long)p.N * HWf * CI : 0);
 #pragma unroll
-    for (int i = 0; i < XP; ++i) buf_lds16(rx, LDS_PTR(gb + G_BYTES + (wave * XP + i) * 1024), x_off[i], 0);
+      for (int i = 0; i < XP; ++i) {
+        const int row = (wave * XP + i) * 8 + (lane >> 3);
+        const long m = m0 + row;
+        const long pf = full_row(m < p.M ? m : 0) - n_first * HWf;
+        const uint32_t off = m < p.M ? (uint32_t)((pf * CI + half * CB + ((lane & 7) ^ b1_swz128(row)) * 8) * 2) : OOB_OFF;
+        buf_lds16(rx, LDS_PTR(gb + G_BYTES + (wave * XP + i) * 1024), off, 0);
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, m0 * CI, (long)p.M * CI);
+#pragma unroll
+      for (int i = 0; i < XP; ++i) buf_lds16(rx, LDS_PTR(gb + G_BYTES + (wave * XP + i) * 1024), x_off[i], 0);
+    }
   };
 
   // dgrad roles: 16-column block cb of this half, co range kp * CO / KSPLIT ..; the weights of
@@ -133,7 +156,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {   // row clamped, value zeroed: no branch around the load
       const long r = (long)tile * MT + er + NW * 8 * q;
-      const uint32_t v = p.bits[(r < p.M ? r : p.M - 1) * (CI / 8) + half * 8 + ec];
+      const long rc = r < p.M ? r : p.M - 1;
+      const uint32_t v = p.bits[(S2 ? full_row(rc) : rc) * (CI / 8) + half * 8 + ec];
       bt_next[q] = r < p.M ? v : 0u;
     }
   };
@@ -258,7 +282,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const long gm = m0 + er + NW * 8 * q;
-      if (gm < p.M) *reinterpret_cast<uint4*>(p.out + gm * CI + half * CB + ec * 8) = pack8(w[q]);
+      if (gm < p.M) {
+        const uint4 pk = pack8(w[q]);
+        *reinterpret_cast<uint4*>(p.out + (S2 ? full_row(gm) : gm) * CI + half * CB + ec * 8) = pk;
+        if (S2) *reinterpret_cast<uint4*>(p.out2 + gm * CI + half * CB + ec * 8) = pk;   // compact copy
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next tile landed
     __syncthreads();                                    // ... and every wave is done with this buffer
@@ -327,8 +355,17 @@ const char* bwd1x1_launch(const Bwd1x1Params& p, hipStream_t stream) {
   if (p.ld_wd < p.CO || p.ld_wd % 8 || p.ld_dw < p.CI) return "bwd1x1: weight / gradient row strides";
   int grid, np;
   bwd1x1_geom(p.M, p.CO, p.CI, &grid, &np);
-  if (p.CO == 256) hipLaunchKernelGGL((bwd1x1_kernel<256, 4>), dim3(grid), dim3(256), 0, stream, p);
-  else hipLaunchKernelGGL((bwd1x1_kernel<512, 8>), dim3(grid), dim3(512), 0, stream, p);
+  if (p.s2 && (!p.out2 || p.Hc != (p.Hf + 1) / 2 || p.Wc != (p.Wf + 1) / 2 || (long)p.N * p.Hc * p.Wc != p.M))
+    return "bwd1x1: stride-2 grid geometry";
+  Bwd1x1Params q = p;
+  if (q.s2) { q.mg_hwc = fdiv_magic(q.Hc * q.Wc); q.mg_wc = fdiv_magic(q.Wc); }
+  if (q.CO == 256) {
+    if (q.s2) hipLaunchKernelGGL((bwd1x1_kernel<256, 4, true>), dim3(grid), dim3(256), 0, stream, q);
+    else hipLaunchKernelGGL((bwd1x1_kernel<256, 4, false>), dim3(grid), dim3(256), 0, stream, q);
+  } else {
+    if (q.s2) hipLaunchKernelGGL((bwd1x1_kernel<512, 8, true>), dim3(grid), dim3(512), 0, stream, q);
+    else hipLaunchKernelGGL((bwd1x1_kernel<512, 8, false>), dim3(grid), dim3(512), 0, stream, q);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

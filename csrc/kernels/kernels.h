@@ -80,6 +80,12 @@ struct Bwd1x1Params {
   float* colsum;                       // partial column sums [bwd1x1_partial_rows(M, CO, CI)][CI]
   float* dw; int ld_dw;                // fp32 [CO][ld_dw >= CI], accumulated with atomics
   int M, CO, CI;
+  // stride-2 form (the block feeds a downsampling block): g has the M = N * Hc * Wc compact rows,
+  // x / out / bits are full resolution N x Hf x Wf (out written at the grid pixels only, into a
+  // pre-zeroed tensor), out2 gets the compact copy
+  int s2, N, Hf, Wf, Hc, Wc;
+  uint16_t* out2;
+  uint64_t mg_hwc, mg_wc;              // set by bwd1x1_launch
 };
 const char* bwd1x1_launch(const Bwd1x1Params& p, hipStream_t stream);
 int bwd1x1_partial_rows(int M, int CO, int CI);

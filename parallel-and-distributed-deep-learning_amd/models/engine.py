@@ -88,6 +88,7 @@ class HipEngine:
         # of the 256 / 512-channel gradient; needs the ReLU bitmasks)
         self.fuse_bwd = self.FUSE_BWD_OK and self.bitmask and os.environ.get("PDDL_FUSE_BWD", "1") != "0"
         self._fuse_bwd3 = os.environ.get("PDDL_FUSE_BWD", "1") != "2"
+        self._fuse_bwd_s2 = os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0"
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -321,8 +322,8 @@ class HipEngine:
             if bi in s2:       # c3 dgrad runs on the compact stride-2 grid
                 Hc = Ho // 2 + Ho % 2
                 Mc = B * Hc * Hc
-            if self._bwd_fused(bi, b, s2):                                       # fused c3 backward -> g2
-                add(b.convs["2"].name, N.bwd1x1_partial_rows(M, 4 * f, f), f)
+            if self._bwd_fused(bi, b, s2) or self._bwd_fused_s2(bi, b, s2):     # fused c3 backward -> g2
+                add(b.convs["2"].name, N.bwd1x1_partial_rows(Mc, 4 * f, f), f)
             else:
                 add(b.convs["2"].name, N.igemm_partial_rows(Mc, f, 4 * f), f)     # c3 dgrad -> g2
             add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)          # c2 dgrad -> g1
@@ -349,6 +350,9 @@ class HipEngine:
     def _wf(self, name, rows, k):
         o = self.wf[name]
         return self.wbf[o:o + rows * k].view(rows, k)
+
+    def _bwd_fused_s2(self, bi, b, s2):   # the stride-2-grid form (block feeding a downsampling block)
+        return self.fuse_bwd and self._fuse_bwd_s2 and bi in s2 and (b.filters == 64 or (b.filters == 128 and self._fuse_bwd3))
 
     def _bwd_fused(self, bi, b, s2):
         # stage 2 (256 <- 64 channels) and stage 3 (512 <- 128); PDDL_FUSE_BWD=2: stage 2 only
@@ -516,9 +520,12 @@ class HipEngine:
                 Hc = Ho // 2 + Ho % 2
                 gc = self.gcbuf[: B * Hc * Hc * 4 * f].view(B, Hc, Hc, 4 * f)
                 g2c = self.g2cbuf[: B * Hc * Hc * f].view(B, Hc, Hc, f)
-                N.wgrad(y2, Ho, Ho, 1, 1, 2, 0, Hc, Hc, gc, None, 0, self._gview(c3n, 4 * f, f), f, 0)
-                N.igemm(gc, None, Hc, Hc, 1, 1, 1, 0, Hc, Hc, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
-                        None, g2, 0, g2c, 0, 0, 2, Ho, Ho, part(c2n), None)
+                if self._bwd_fused_s2(bi, b, s2):   # one read of gc: data + weight gradient
+                    N.bwd1x1(gc, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f), g2c)
+                else:
+                    N.wgrad(y2, Ho, Ho, 1, 1, 2, 0, Hc, Hc, gc, None, 0, self._gview(c3n, 4 * f, f), f, 0)
+                    N.igemm(gc, None, Hc, Hc, 1, 1, 1, 0, Hc, Hc, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
+                            None, g2, 0, g2c, 0, 0, 2, Ho, Ho, part(c2n), None)
                 N.wgrad(y1, Ho, Ho, 3, 3, 2, 1, Hc, Hc, g2c, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
             elif self._bwd_fused(bi, b, s2):
                 # conv3: data and weight gradient from one read of gout

@@ -13,7 +13,7 @@ import pddl  # noqa
 from pddl.models.resnet50 import ParamLayout
 
 
-def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True):
+def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True):
     L = ParamLayout()
     H1 = (crop + 6 - 7) // 2 + 1
     H2 = (H1 + 2 - 3) // 2 + 1
@@ -53,8 +53,8 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True):
         M = B * Ho * Ho
         # blocks feeding a stride-2 block: conv3 wgrad/dgrad and conv2 wgrad on the compact quarter
         Mc = B * (Ho // 2 + Ho % 2) ** 2 if bi in s2 else M
-        if fuse_bwd and (f == 64 or (f == 128 and fuse_bwd3)) and bi not in s2:   # bwd1x1: one read of g
-            ev.append(("bwd1x1", f"{b.name} c3 dgrad+wgrad", 4 * M * f * 4 * f, (M * 4 * f + 2 * M * f) * 2))
+        if fuse_bwd and (f == 64 or (f == 128 and fuse_bwd3)) and (bi not in s2 or fuse_s2):   # bwd1x1: one read of g
+            ev.append(("bwd1x1", f"{b.name} c3 dgrad+wgrad", 4 * Mc * f * 4 * f, (Mc * 4 * f + 2 * Mc * f) * 2))
         else:
             ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * Mc * f * 4 * f, (Mc * f + Mc * 4 * f) * 2))
             ev.append(("igemm", f"{b.name} c3 dgrad", 2 * Mc * f * 4 * f, (Mc * 4 * f + Mc * f + M * f) * 2,
@@ -92,7 +92,7 @@ def main():
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
     import os
     ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0", os.environ.get("PDDL_FUSE_BWD", "1") != "0",
-                  os.environ.get("PDDL_FUSE_BWD", "1") != "2")
+                  os.environ.get("PDDL_FUSE_BWD", "1") != "2", os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0")
     # a split launch (8-phase kernel for full rounds + 128x128 tail) is two dispatches of one layer
     try:
         from pddl.ops.native import require_native

@@ -919,3 +919,35 @@ def test_bwd1x1_fused(co, ci, M):
     assert rel(out, ref) < 1e-2
     assert rel(colsum.view(rows, ci).sum(0), ref.sum(0)) < 1e-3
     assert rel(dw - dw0, g.float().t() @ x.float()) < 1e-3
+
+
+@pytest.mark.parametrize("co,ci,B,H", [(256, 64, 3, 56), (512, 128, 5, 28), (256, 64, 2, 7)])
+def test_bwd1x1_fused_stride2(co, ci, B, H):
+    """Stride-2 form of the fused 1x1 backward (a block feeding a downsampling block): the output
+    gradient exists only on the stride-2 grid (compact [B, Hc, Wc, co]); x and its ReLU bits are
+    full resolution; the data gradient goes to the grid pixels of a pre-zeroed full-resolution
+    tensor plus a compact copy, the weight gradient reads x at the grid pixels.  Odd H = 7
+    checks the ceil grid (Hc = 4)."""
+    torch.manual_seed(12)
+    Hc = (H + 1) // 2
+    g = rnd(B, Hc, Hc, co)
+    x = torch.relu(rnd(B, H, H, ci))
+    wd = rnd(ci, co, scale=0.05)
+    nb = ci // 8
+    bits = ((x > 0).view(B, H, H, nb, 8).to(torch.int32) << torch.arange(8, device=dev, dtype=torch.int32)).sum(-1)
+    bits = bits.to(torch.uint8).contiguous()
+    out = torch.zeros(B, H, H, ci, device=dev, dtype=torch.bfloat16)
+    out2 = torch.full((B, Hc, Hc, ci), float("nan"), device=dev, dtype=torch.bfloat16)
+    M = B * Hc * Hc
+    rows = N().bwd1x1_partial_rows(M, co, ci)
+    colsum = torch.full((rows * ci,), float("nan"), device=dev)
+    dw = torch.zeros(co, ci, device=dev)
+    N().bwd1x1(g, x, wd, bits, out, colsum, dw, out2)
+    torch.cuda.synchronize()
+    xs = x[:, ::2, ::2, :]
+    refc = (g.float() @ wd.float().t()) * (xs > 0)
+    ref = torch.zeros(B, H, H, ci, device=dev)
+    ref[:, ::2, ::2, :] = refc
+    assert rel(out, ref) < 1e-2 and rel(out2, refc) < 1e-2
+    assert rel(colsum.view(rows, ci).sum(0), refc.sum((0, 1, 2))) < 1e-3
+    assert rel(dw, g.float().reshape(-1, co).t() @ xs.float().reshape(-1, ci)) < 1e-3
