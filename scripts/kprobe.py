@@ -16,7 +16,7 @@ from pddl.ops.native import require_native   # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", choices=["wgrad", "fwd", "fwdres", "dgrad_add"], default="wgrad")
+    ap.add_argument("--op", choices=["wgrad", "fwd", "fwdres", "dgrad_add", "bwd1x1"], default="wgrad")
     ap.add_argument("--shape", default="1024,14,256,256,3,1,1", help="N,H,Cin,Cout,R,stride,pad")
     ap.add_argument("--set", default="", help="knobs, e.g. wgrad8=1,igemm8=2")
     ap.add_argument("--iters", type=int, default=50)
@@ -46,8 +46,17 @@ def main():
     dx = torch.empty(n, h, h, c, dtype=torch.bfloat16, device=dev)
     part = torch.empty(N.igemm_partial_rows(n * h * h, c, co) * c, device=dev) if a.op == "dgrad_add" else None
 
+    if a.op == "bwd1x1":   # fused conv3 backward (bwd1x1.hip): shape N,H,CI,CO (1x1, stride 1)
+        gb = torch.randn(n, h, h, co, device=dev).to(torch.bfloat16)
+        wdb = (torch.randn(c, co, device=dev) * 0.05).to(torch.bfloat16)
+        outb = torch.empty(n, h, h, c, dtype=torch.bfloat16, device=dev)
+        partb = torch.empty(N.bwd1x1_partial_rows(n * h * h, co, c) * c, device=dev)
+        dwb = torch.zeros(co, c, device=dev)
+
     def step():
-        if a.op == "wgrad":
+        if a.op == "bwd1x1":
+            N.bwd1x1(gb, x, wdb, bits, outb, partb, dwb)
+        elif a.op == "wgrad":
             N.wgrad(x, h, h, r, r, st, pad, ho, ho, g, None, 0, dw, r * r * c, 0)
         elif a.op == "fwd":
             N.igemm(x, None, h, h, r, r, st, pad, ho, ho, w, 0, sc, sh, None, None, None, y, 1, None, 0, 0, 0, 0, 0,
@@ -70,7 +79,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.iters
-    flops = 2.0 * n * ho * ho * co * r * r * c
+    flops = 2.0 * n * ho * ho * co * r * r * c * (2 if a.op == "bwd1x1" else 1)
     print(json.dumps({"op": a.op, "shape": a.shape, "set": a.set, "drop": a.drop, "us": round(us, 1),
                       "tflops": round(flops / us / 1e6, 1)}), flush=True)
 

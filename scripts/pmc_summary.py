@@ -15,7 +15,7 @@ def main(root):
             name = r["Kernel_Name"]
             if "pddl::" not in name:
                 continue
-            key = name.split("(")[0].replace("void ", "").replace("pddl::", "") + f" grid={r['Grid_Size']}"
+            key = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("pddl::", "") + f" grid={r['Grid_Size']}"
             agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k in sorted(agg):
         c = {n: sum(v) / len(v) for n, v in agg[k].items()}
