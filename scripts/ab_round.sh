@@ -1,12 +1,11 @@
-# ad-hoc GPU session: end-of-round check -- the whole GPU suite, smoke, then the default bench
-# twice and b1024 once (final numbers for README / BASELINE)
+# ad-hoc GPU session: max-pool forward with two windows in flight per wave -> pool numerics,
+# then a b1024 kernel trace (maxpool_fwd was 532-534 us in every round-3 profile)
 set -o pipefail
-mkdir -p gpurun_out/fin
+mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
-bash scripts/gpu_round.sh gputests smoke && \
-timeout -k 10 300 python bench.py > gpurun_out/fin/d1.log 2>&1 && \
-timeout -k 10 300 python bench.py --batch 1024 > gpurun_out/fin/b1024.log 2>&1 && \
-timeout -k 10 300 python bench.py > gpurun_out/fin/d2.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "pool" > gpurun_out/ab/t_pool.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ab/prof_p -o run --output-format csv -- python bench.py --batch 1024 --steps 6 --warmup 3 > gpurun_out/ab/prof_p.log 2>&1
 rc=$?
-for f in gpurun_out/fin/*.log; do echo "$f $(grep -ho '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"peak_mem_gb": [0-9.]*' $f | tr '\n' ' ')"; done
+tail -2 gpurun_out/ab/t_pool.log
+grep -h '"value"' gpurun_out/ab/prof_p.log | grep -o '"value": [0-9.]*'
 exit $rc
