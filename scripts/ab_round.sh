@@ -1,8 +1,13 @@
-# ad-hoc GPU session: kernel trace of the default configuration (b2560) for the README step breakdown
+# ad-hoc GPU session: the K = 64 residual-gradient dgrad (conv2_block{2,3} c1 dgrad) on the persistent ring
+# kernel vs the per-tile kernel, standalone (scripts/kprobe.py), b1024 and b2560 shapes, alternating
 set -o pipefail
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/ab/prof_d -o run --output-format csv -- python bench.py --steps 4 --warmup 2 > gpurun_out/ab/prof_d.log 2>&1
+k() { timeout -k 10 120 python scripts/kprobe.py --op dgrad_add --iters 20 "$@" >> gpurun_out/ab/kp.log 2>&1; }
+k --shape 1024,56,256,64,1,1,0 --set igemm_pk=2 && k --shape 1024,56,256,64,1,1,0 --set igemm_pk=0 && \
+k --shape 1024,56,256,64,1,1,0 --set igemm_pk=2 && k --shape 1024,56,256,64,1,1,0 --set igemm_pk=0 && \
+k --shape 2560,56,256,64,1,1,0 --set igemm_pk=2 && k --shape 2560,56,256,64,1,1,0 --set igemm_pk=0 && \
+k --shape 1024,28,512,128,1,1,0 --set igemm_pk=2 && k --shape 1024,28,512,128,1,1,0 --set igemm_pk=0
 rc=$?
-grep -h '"value"' gpurun_out/ab/prof_d.log | grep -o '"value": [0-9.]*'
+grep '"op"' gpurun_out/ab/kp.log
 exit $rc
