@@ -65,12 +65,20 @@ class ReferenceResNet50:
     -- the preprocessed input, every fused conv+BN(+residual)+ReLU output, the GAP output, conv
     weights (straight-through: the weight gradient stays fp32), and the gradients stored at those
     points on the way back (dlogits, dpooled, every dgrad output) -- so an engine-vs-reference
-    comparison measures accumulation order, not bf16 storage."""
+    comparison measures accumulation order, not bf16 storage.
 
-    def __init__(self, layout: ParamLayout, bn_mode: str = "frozen", bf16_points: bool = False):
+    fused_proj=True (frozen BN): a projection block's conv3 and shortcut conv are
+    modelled as the engine's ONE dual-source GEMM (`prep_fuse_kernel`, csrc/kernels/eltwise.hip):
+    both frozen-BN scales are folded into the weights BEFORE the bf16 rounding,
+    `conv(y2, bf16(a3*W3)) + conv(x, bf16(a0*W0)) + (b3 + b0)`, and the shortcut activation is
+    never stored (no bf16 point on it)."""
+
+    def __init__(self, layout: ParamLayout, bn_mode: str = "frozen", bf16_points: bool = False,
+                 fused_proj: bool = False):
         self.L = layout
         self.bn_mode = bn_mode
         self.bf16 = bf16_points
+        self.fused_proj = fused_proj and bn_mode == "frozen"
         self.stats = None   # flat buffer holding the BN moving statistics (non-trainable)
         self._bound = None  # (flat tensor, {name: view}) of the last bind()
 
@@ -130,6 +138,21 @@ class ReferenceResNet50:
         inv = torch.rsqrt(var_ + BN_EPS)
         return (x - mu_.view(1, -1, 1, 1)) * (g * inv).view(1, -1, 1, 1) + be.view(1, -1, 1, 1)
 
+    def _folded_conv(self, params, x, c):
+        """Frozen-BN conv with the BN scale folded into bf16 weights (the fused projection GEMM):
+        returns (conv(x, bf16(a*W)), shift b) -- straight-through on the rounding, so W, gamma and
+        the bias get the fp32 gradients of the unrounded product."""
+        g = self._w(params, c.bn, "gamma")
+        be = self._w(params, c.bn, "beta")
+        mu = self._w(params, c.bn, "moving_mean").detach()
+        var = self._w(params, c.bn, "moving_variance").detach()
+        a = g * torch.rsqrt(var + BN_EPS)
+        w = self._w(params, c.name, "kernel").permute(0, 3, 1, 2) * a.view(-1, 1, 1, 1)
+        if self.bf16:
+            w = w + (w.to(torch.bfloat16).float() - w).detach()
+        b = (self._w(params, c.name, "bias") - mu) * a + be
+        return F.conv2d(x, w, None, stride=c.stride, padding=c.pad), b
+
     def features(self, params, x, training=True):
         L = self.L
         s = L.stem
@@ -140,6 +163,13 @@ class ReferenceResNet50:
         x = F.max_pool2d(x, 3, 2)
         for b in L.blocks:
             c = b.convs
+            if b.proj and self.fused_proj:
+                y = q(F.relu(self._bn(params, self._conv(params, x, c["1"]), c["1"], training)))
+                y = q(F.relu(self._bn(params, self._conv(params, y, c["2"]), c["2"], training)))
+                z3, b3 = self._folded_conv(params, y, c["3"])
+                z0, b0 = self._folded_conv(params, x, c["0"])
+                x = q(F.relu(z3 + z0 + (b3 + b0).view(1, -1, 1, 1)))
+                continue
             if b.proj:
                 sc = q(self._bn(params, self._conv(params, x, c["0"]), c["0"], training))
             else:
@@ -167,14 +197,14 @@ class TorchEngine:
     """
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, device="cpu", bn_mode="frozen",
-                 num_classes: int = 1000, bf16_points: bool = False):
+                 num_classes: int = 1000, bf16_points: bool = False, fused_proj: bool = False):
         self.L = layout
         self.device = torch.device(device)
         self.batch = batch
         self.crop = crop
         self.params = torch.zeros(layout.total, dtype=torch.float32, device=self.device)
         self.grads = torch.zeros(layout.n_trainable, dtype=torch.float32, device=self.device)
-        self.model = ReferenceResNet50(layout, bn_mode, bf16_points=bf16_points)
+        self.model = ReferenceResNet50(layout, bn_mode, bf16_points=bf16_points, fused_proj=fused_proj)
         self.num_classes = num_classes
         self._leaf = None
 

@@ -12,7 +12,9 @@ def _engines(B, crop, image_size, bf16_points=False):
     from pddl.models.resnet50 import ParamLayout
     L = ParamLayout()
     he = HipEngine(L, B, crop=crop, image_size=image_size)
-    te = TorchEngine(L, B, crop=crop, device="cuda", bf16_points=bf16_points)
+    # the bf16-point reference models the engine's fused projection GEMM (BN scales folded into
+    # the bf16 weights) when the engine runs it
+    te = TorchEngine(L, B, crop=crop, device="cuda", bf16_points=bf16_points, fused_proj=he.fuse_proj)
     he.init(seed=3)
     # perturb BN statistics / affine so the frozen-BN folding is exercised (not identity)
     g = torch.Generator(device="cpu").manual_seed(11)
@@ -83,12 +85,16 @@ def test_engine_matches_bf16_point_reference_within_its_noise_floor(crop, image_
     the engine's median error is at most 1.5 x the floor's.  (The factor 3 covers the engine's
     own run-to-run spread: its weight gradients are summed with fp32 atomics in no fixed order,
     which moves a cancellation-heavy BN-gamma gradient -- a dot product of W and dW -- by ~1 %
-    between runs, e.g. 3.3 % against a 1.1 % floor in one run and within 2x in the next.)"""
+    between runs, e.g. 3.3 % against a 1.1 % floor in one run and within 2x in the next.)
+    The reference models the fused projection GEMM (BN scales folded into bf16 weights,
+    models/reference.py fused_proj): without it the crop-244 median ratio sat at 1.52 and failed
+    on a fresh box (GPUTEST_r03); with it the ratios are 0.94 / 0.99 / 1.21 at crops 224 / 160 /
+    244 (profiles/r4_parity_ratios.txt)."""
     from pddl.models.reference import TorchEngine
     torch.manual_seed(0)
     B = 4
     L, he, te = _engines(B, crop, image_size, bf16_points=True)
-    tc = TorchEngine(L, B, crop=crop, device="cpu", bf16_points=True)
+    tc = TorchEngine(L, B, crop=crop, device="cpu", bf16_points=True, fused_proj=he.fuse_proj)
     tc.params.copy_(te.params.cpu())
     img = torch.randint(0, 256, (B, image_size, image_size, 3), dtype=torch.uint8, device="cuda")
     lab = torch.randint(0, 1000, (B,), device="cuda")
@@ -107,8 +113,9 @@ def test_engine_matches_bf16_point_reference_within_its_noise_floor(crop, image_
     over = [(n, round(r, 4), round(floor[n], 4)) for r, n in errs if r > 3 * floor[n] + 0.005]
     assert not over, over[:8]
     med = lambda v: sorted(v)[len(v) // 2]   # noqa: E731
-    assert med([r for r, _ in errs]) <= 1.5 * med(list(floor.values())), (med([r for r, _ in errs]),
-                                                                           med(list(floor.values())))
+    m_e, m_f = med([r for r, _ in errs]), med(list(floor.values()))
+    print(f"crop {crop}: engine median {m_e:.4f}, floor median {m_f:.4f}, ratio {m_e / m_f:.3f}")
+    assert m_e <= 1.5 * m_f, (m_e, m_f)
 
 
 def test_engine_loss_trajectory_20_steps():
@@ -124,7 +131,7 @@ def test_engine_loss_trajectory_20_steps():
     torch.manual_seed(0)
     B = 8
     L, he, te = _engines(B, 128, 128, bf16_points=True)
-    tc = TorchEngine(L, B, crop=128, device="cpu", bf16_points=True)
+    tc = TorchEngine(L, B, crop=128, device="cpu", bf16_points=True, fused_proj=he.fuse_proj)
     tc.params.copy_(te.params.cpu())
     opts = [make_optimizer("adam", e, lr=1e-4) for e in (he, te, tc)]
     img = torch.randint(0, 256, (B, 128, 128, 3), dtype=torch.uint8, device="cuda")
@@ -143,9 +150,8 @@ def test_engine_loss_trajectory_20_steps():
     dev_r = [abs(b - c) / abs(c) for b, c in zip(lt, lc)]                # GPU reference vs CPU reference
     print("losses engine / reference / cpu reference:", [(round(a, 4), round(b, 4), round(c, 4))
                                                         for a, b, c in zip(lh, lt, lc)])
-    # before the chaotic phase: within 3e-3, or 1.5x the GPU reference's own deviation there (the
-    # fused projection blocks round the BN-scaled weights to bf16, one rounding point the reference
-    # does not have: 2.1e-3 at step 3, where the GPU reference itself spans 1.1-1.8e-3 run to run)
+    # before the chaotic phase: within 3e-3, or 1.5x the GPU reference's own deviation there
+    # (both references model the fused projection blocks' bf16 rounding of the BN-scaled weights)
     assert max(dev_e[:4]) < max(3e-3, 1.5 * max(dev_r[:4])), (dev_e[:4], dev_r[:4])
     assert max(dev_e) < 0.10 and sum(dev_e) / len(dev_e) <= 2 * sum(dev_r) / len(dev_r) + 0.01, (dev_e, dev_r)
 

@@ -92,6 +92,34 @@ def test_reference_engine_grads_match_autograd_finite_difference():
     assert abs((lp - lm) / (2 * eps) - g.item()) < 2e-2 * max(1.0, abs(g.item()))
 
 
+def test_fused_projection_reference_is_the_same_function():
+    """The fused-projection form of the reference (BN scales folded into the conv3 / shortcut
+    weights, shifts summed: what the engine's dual-source GEMM computes) is the unfused Keras
+    graph in fp32 math -- loss and every gradient agree to fp32 rounding."""
+    from pddl.models.reference import TorchEngine
+    from pddl.models.resnet50 import ParamLayout
+    torch.manual_seed(0)
+    L = ParamLayout()
+    img = torch.randint(0, 256, (2, 32, 32, 3), dtype=torch.uint8)
+    lab = torch.tensor([3, 7])
+    out = []
+    for fused in (False, True):
+        e = TorchEngine(L, 2, crop=32, fused_proj=fused)
+        e.init(seed=1)
+        g = torch.Generator().manual_seed(4)
+        for ent in L.entries.values():   # non-identity BN so the fold is exercised
+            sl = e.params[ent.offset:ent.offset + ent.size]
+            if ent.kind in ("gamma", "moving_variance"):
+                sl.copy_(0.5 + torch.rand(ent.size, generator=g))
+            elif ent.kind in ("beta", "bias", "moving_mean"):
+                sl.copy_(0.1 * torch.randn(ent.size, generator=g))
+        s = e.forward_backward(img, lab, 0.5)
+        out.append((s[0].item(), e.grads.clone()))
+    (l0, g0), (l1, g1) = out
+    assert abs(l0 - l1) <= 1e-5 * abs(l0)
+    assert ((g0 - g1).norm() / g0.norm()).item() < 1e-5
+
+
 def test_frozen_bn_is_inference_mode():
     """training=False in the reference (Q3): BN uses moving stats, which never change."""
     L, e = _tiny_engine(2, 32)
