@@ -92,6 +92,9 @@ def parse(argv=None):
                     help="HIP graphs: 1 GPU = whole step; mirrored = per-device segments (default on)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: BASELINE config 1 plumbing (fp32 PyTorch reference engine, gloo ranks)")
+    ap.add_argument("--comm-proxy", default=None, metavar="SPEC",
+                    help="1 GPU: run a paced, CU-holding stand-in for each bucket's RCCL all-reduce on a side "
+                         "stream (e.g. 'world=8,busbw=350,nch=32'), to measure the backward under comm contention")
     ap.add_argument("--timeout", type=float, default=None,
                     help="job deadline in seconds (default: derived from steps + warmup); on expiry every "
                          "rank dumps its stacks and the job exits non-zero")
@@ -273,6 +276,10 @@ def run(args):
         strat_name = args.strategy
     if cpu:
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, world)))
+    if args.comm_proxy:
+        if args.gpus != 1 or cpu or args.strategy != "horovod":
+            fail("--comm-proxy models multi-GPU collectives on ONE GPU (horovod strategy)")
+        os.environ["PDDL_COMM_PROXY"] = args.comm_proxy
     cfg = build_cfg(args, strat_name)
     if strat_name == "horovod" and world == 1 and args.graph and not cpu:
         cfg = cfg.replace(strategy="single", graphs=True)   # whole-step HIP graph on one GPU
@@ -370,6 +377,12 @@ def run(args):
         out["comm"] = comm
         if rehearsing():
             out["rehearsal"] = True
+        if args.comm_proxy:
+            px = st.reducer
+            out["comm_proxy"] = {"spec": args.comm_proxy, "world": px.world, "busbw_gbs": px.busbw / 1e9,
+                                 "channels": px.nch, "buckets": len(px.buckets),
+                                 "modelled_ms_per_step": round(px.modelled_s * 1e3, 3),
+                                 "note": "1 GPU with paced stand-ins for the bucket all-reduces: NOT a multi-GPU number"}
         print(json.dumps(out), flush=True)
     progress("done")
     if world > 1:

@@ -593,6 +593,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                (int)r.size(0), scatter ? 1 : 0, cur_stream()),
        "range_copy");
   });
+  // bench.py --comm-proxy: a paced, CU-holding stand-in for one bucket's RCCL all-reduce
+  m.def("comm_proxy", [](Tensor src, Tensor scratch, int passes, int64_t ticks, int nch) {
+    PCHECK(src.is_cuda() && scratch.is_cuda() && src.scalar_type() == torch::kFloat32 &&
+               scratch.scalar_type() == torch::kFloat32 && src.is_contiguous() && scratch.is_contiguous() &&
+               scratch.numel() >= src.numel() && src.numel() % 4 == 0,
+           "comm_proxy: fp32 device tensors, scratch >= src, 4-element multiple");
+    ok(pddl::comm_proxy_launch(f32p(src), f32p(scratch), src.numel(), passes, ticks, nch, cur_stream()),
+       "comm_proxy");
+  }, REL);
   m.def("igemm", &igemm, REL);
   m.def("igemm_bn", &igemm_impl, REL);
   m.def("bn_stats", &bn_stats, REL);

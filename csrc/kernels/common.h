@@ -74,6 +74,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
 static __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
 __host__ __device__ __forceinline__ long lmin(long a, long b) { return a < b ? a : b; }
+__host__ __device__ __forceinline__ long lmax(long a, long b) { return a > b ? a : b; }
 
 // Descriptor over elements [e0, e_end) of a bf16 tensor, rebased at e0 with 64-bit pointer
 // arithmetic: a workgroup's lane offsets (relative to the first image / row its tile reads)

@@ -252,6 +252,8 @@ struct RangeRow { long flat, packed, len; };
 // scatter = 0: dst[packed + i] = src[flat + i]; 1: dst[flat + i] = src[packed + i].
 const char* range_copy_launch(const float* src, float* dst, const RangeRow* rows_dev, int nrows, int scatter,
                               hipStream_t s);
+const char* comm_proxy_launch(const float* src, float* scratch, long n, int passes, long ticks, int nch,
+                              hipStream_t s);
 
 // Deterministic synthetic images / labels for example ids idx[0..n) (uint8 [n][per], int64 [n]).
 const char* synth_launch(const int64_t* idx, int n, long per, int64_t seed, int ncls, uint8_t* img, int64_t* lab,

@@ -11,6 +11,9 @@
 // -- when `shutdown_s` > 0 -- terminates the process with exit status 124 once that grace has
 // also passed (Horovod's HOROVOD_STALL_SHUTDOWN_TIME_SECONDS; the reference's fail-fast intent,
 // imagenet-resnet50-ps.py:67-69).  `check()` rethrows the verdict on the caller thread.
+// The action runs on a thread of its own: an abort that blocks (on a lock held by a thread stuck
+// inside the collective, or inside ncclCommAbort itself) never delays the shutdown deadline,
+// which the watchdog loop keeps checking independently.
 #pragma once
 #include <atomic>
 #include <chrono>
@@ -36,8 +39,12 @@ class CommWatch {
   using Probe = std::function<bool()>;   // true once the collective completed (non-blocking)
   using Release = std::function<void()>; // frees the probe's resources (called by the watchdog)
 
-  CommWatch(double timeout_s, double shutdown_s, int rank, std::function<void(const std::string&)> on_stall)
-      : timeout_s_(timeout_s), shutdown_s_(shutdown_s), rank_(rank), on_stall_(std::move(on_stall)) {
+  // fatal = false: report only (Horovod's default stall check) -- each collective older than the
+  // timeout is reported once, nothing is aborted, check() never raises, and a late completion
+  // simply retires it; fatal = true: the verdict + action + shutdown deadline described above.
+  CommWatch(double timeout_s, double shutdown_s, int rank, std::function<void(const std::string&)> on_stall,
+            bool fatal = true)
+      : timeout_s_(timeout_s), shutdown_s_(shutdown_s), rank_(rank), on_stall_(std::move(on_stall)), fatal_(fatal) {
     th_ = std::thread([this] { loop(); });
   }
   ~CommWatch() { stop(); }
@@ -52,6 +59,7 @@ class CommWatch {
     }
     cv_.notify_all();
     if (th_.joinable()) th_.join();
+    if (act_th_.joinable()) act_th_.join();
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& e : q_)
       if (e.release) e.release();
@@ -60,7 +68,7 @@ class CommWatch {
 
   void add(std::string tag, Probe probe, Release release) {
     std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back({std::move(tag), std::move(probe), std::move(release), cw_now_s()});
+    q_.push_back({std::move(tag), std::move(probe), std::move(release), cw_now_s(), false});
     ++issued_;
   }
 
@@ -73,6 +81,7 @@ class CommWatch {
     std::lock_guard<std::mutex> lk(mu_);
     return stalled_;
   }
+  bool action_done() const { return act_done_.load(); }
   std::string message() const {
     std::lock_guard<std::mutex> lk(mu_);
     return msg_;
@@ -86,6 +95,7 @@ class CommWatch {
     return issued_;
   }
   int64_t retired() const { return retired_.load(); }
+  int64_t warnings() const { return warnings_.load(); }
 
  private:
   struct Entry {
@@ -93,6 +103,7 @@ class CommWatch {
     Probe probe;
     Release release;
     double t_issue;
+    bool warned;
   };
 
   void loop() {
@@ -107,7 +118,15 @@ class CommWatch {
         retired_++;
       }
       const double now = cw_now_s();
-      if (!stalled_ && timeout_s_ > 0 && !q_.empty() && now - q_.front().t_issue > timeout_s_) {
+      if (!fatal_ && timeout_s_ > 0 && !q_.empty() && !q_.front().warned && now - q_.front().t_issue > timeout_s_) {
+        q_.front().warned = true;
+        warnings_++;
+        std::fprintf(stderr, "[pddl comm watchdog] rank %d: %s issued %.1f s ago has not completed (%zu outstanding)"
+                     " - reporting only (set PDDL_STALL_SHUTDOWN > 0 or PDDL_STALL_ABORT=1 to abort)\n", rank_,
+                     q_.front().tag.c_str(), now - q_.front().t_issue, q_.size());
+        std::fflush(stderr);
+      }
+      if (fatal_ && !stalled_ && timeout_s_ > 0 && !q_.empty() && now - q_.front().t_issue > timeout_s_) {
         std::ostringstream os;
         os << "rank " << rank_ << ": " << q_.front().tag << " issued " << (now - q_.front().t_issue)
            << " s ago has not completed (" << q_.size() << " collective(s) outstanding) - a peer rank is"
@@ -119,9 +138,12 @@ class CommWatch {
         std::fflush(stderr);
         auto act = on_stall_;
         const std::string m = msg_;
-        lk.unlock();   // the action (communicator abort) may take a while; callers keep checking
-        if (act) act(m);
-        lk.lock();
+        // the action (communicator abort) may block; it runs beside this loop, which keeps
+        // enforcing the shutdown deadline below
+        act_th_ = std::thread([this, act, m] {
+          if (act) act(m);
+          act_done_ = true;
+        });
       }
       if (stalled_ && shutdown_s_ > 0 && now - t_stall_ > shutdown_s_) {
         std::fprintf(stderr, "[pddl comm watchdog] rank %d: still stalled %.1f s after the verdict; "
@@ -135,6 +157,7 @@ class CommWatch {
   const double timeout_s_, shutdown_s_;
   const int rank_;
   std::function<void(const std::string&)> on_stall_;
+  const bool fatal_;
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Entry> q_;
@@ -143,7 +166,9 @@ class CommWatch {
   std::string msg_;
   int64_t issued_ = 0;
   std::atomic<int64_t> retired_{0};
-  std::thread th_;
+  std::atomic<bool> act_done_{false};
+  std::atomic<int64_t> warnings_{0};
+  std::thread th_, act_th_;
 };
 
 }  // namespace pddl

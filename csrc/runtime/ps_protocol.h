@@ -133,10 +133,17 @@ inline void post(WorkerSlot& s, uint64_t seq, int op, float lr) {
 }
 
 // ... and wait for its completion (then the receive buffer holds the fresh shard).
-inline void wait_done(WorkerSlot& s, uint64_t seq, double timeout_s, int p) {
+// `failed` (optional): a local failure flag (e.g. the worker's poster thread could not post the
+// request) checked in the spin, so a failure that means no answer will ever come surfaces at
+// once instead of after the whole timeout as a misleading "did not answer".
+inline void wait_done(WorkerSlot& s, uint64_t seq, double timeout_s, int p,
+                      const std::atomic<bool>* failed = nullptr) {
   const double t0 = now_s();
   int spins = 0;
   while (s.done_seq.load(std::memory_order_acquire) != seq) {
+    if (failed && failed->load(std::memory_order_acquire))
+      throw std::runtime_error("pddl ps client: request to parameter server " + std::to_string(p) +
+                               " was never posted (local failure)");
     if (++spins > 64) {
       std::this_thread::sleep_for(std::chrono::microseconds(20));
       if (now_s() - t0 >= timeout_s)

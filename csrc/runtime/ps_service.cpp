@@ -381,7 +381,9 @@ class PSClient {
       std::lock_guard<std::mutex> lk(post_mu_);
       post_stop_ = true;
     }
+    post_stopping_.store(true);
     post_cv_.notify_all();
+    // bounded: the poster polls its event and leaves once stopping, even if the pack never ends
     if (poster_.joinable()) poster_.join();
     if (dev_ >= 0) {
       hipSetDevice(dev_);
@@ -473,7 +475,13 @@ class PSClient {
 
  private:
   void wait_done(Remote& r, int p) {
-    pddl::ps::wait_done(r.ctrl->slot[w_], r.seq, timeout_, p);
+    try {
+      pddl::ps::wait_done(r.ctrl->slot[w_], r.seq, timeout_, p, &post_failed_);
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> lk(post_mu_);
+      TORCH_CHECK(post_err_.empty(), "pddl ps client: ", post_err_);
+      throw;
+    }
     std::lock_guard<std::mutex> lk(post_mu_);
     TORCH_CHECK(post_err_.empty(), "pddl ps client: ", post_err_);
   }
@@ -490,11 +498,20 @@ class PSClient {
         job = post_job_;
         post_job_.valid = false;
       }
-      const hipError_t e = hipEventSynchronize(pack_ev_);
+      // poll (not hipEventSynchronize) so that a destructor can always stop this thread
+      hipError_t e;
+      int spins = 0;
+      while ((e = hipEventQuery(pack_ev_)) == hipErrorNotReady) {
+        if (post_stopping_.load()) return;
+        if (++spins > 256) std::this_thread::sleep_for(std::chrono::microseconds(10));
+      }
       if (e != hipSuccess) {
-        std::lock_guard<std::mutex> lk(post_mu_);
-        post_err_ = std::string("pack event: ") + hipGetErrorString(e);
-        continue;   // (end() reports it; the requests are never posted)
+        {
+          std::lock_guard<std::mutex> lk(post_mu_);
+          post_err_ = std::string("pack event: ") + hipGetErrorString(e);
+        }
+        post_failed_.store(true, std::memory_order_release);   // end()'s wait fails at once
+        continue;   // (the requests are never posted)
       }
       for (Remote& r : rem_) pddl::ps::post(r.ctrl->slot[w_], r.seq, job.op, job.lr);
     }
@@ -514,6 +531,7 @@ class PSClient {
   std::condition_variable post_cv_;
   PostJob post_job_;
   bool post_stop_ = false;
+  std::atomic<bool> post_stopping_{false}, post_failed_{false};
   std::string post_err_;
   int64_t flat_end_ = 0;
   std::vector<Remote> rem_;

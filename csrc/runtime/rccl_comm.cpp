@@ -26,9 +26,12 @@
 
 #include "runtime/comm_watch.h"
 
+#include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace py = pybind11;
@@ -75,24 +78,28 @@ class RcclComm {
     TORCH_CHECK(ranks_.size() == devs_.size() && !ranks_.empty(), "pddl rccl: ranks/devices mismatch");
     ncclUniqueId id;
     memcpy(&id, uid.data(), sizeof(id));
-    comms_.resize(devs_.size());
+    std::vector<ncclComm_t> cs(devs_.size(), nullptr);
     nck(ncclGroupStart(), "group start");
     for (size_t i = 0; i < devs_.size(); ++i) {
       c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
-      nck(ncclCommInitRank(&comms_[i], nranks_, id, ranks_[i]), "comm init rank");
+      nck(ncclCommInitRank(&cs[i], nranks_, id, ranks_[i]), "comm init rank");
     }
     nck(ncclGroupEnd(), "group end (init)");
+    set_comms(cs);
   }
   explicit RcclComm(std::vector<int> devices) : devs_(std::move(devices)) {
     nranks_ = (int)devs_.size();
-    comms_.resize(devs_.size());
+    std::vector<ncclComm_t> cs(devs_.size(), nullptr);
     for (int i = 0; i < nranks_; ++i) ranks_.push_back(i);
-    nck(ncclCommInitAll(comms_.data(), nranks_, devs_.data()), "comm init all");
+    nck(ncclCommInitAll(cs.data(), nranks_, devs_.data()), "comm init all");
+    set_comms(cs);
   }
   ~RcclComm() {
-    watch_.reset();
-    for (auto c : comms_)
+    watch_.reset();   // joins the watchdog (and a running abort) before the communicators go
+    for (size_t i = 0; i < ncomm_; ++i) {
+      ncclComm_t c = comms_[i].exchange(nullptr);
       if (c) ncclCommDestroy(c);
+    }
   }
 
   static py::bytes unique_id() {
@@ -104,9 +111,8 @@ class RcclComm {
   void all_reduce(std::vector<Tensor> ts, const std::string& op, const std::string& tag) {
     std::vector<hipStream_t> ss;
     for (auto& t : ts) ss.push_back(stream_of(t));
-    issue(ts, ss, tag.empty() ? "all_reduce" : tag, [&](size_t i) {
-      return ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), comms_[i],
-                           ss[i]);
+    issue(ts, ss, tag.empty() ? "all_reduce" : tag, [&](size_t i, ncclComm_t c) {
+      return ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), c, ss[i]);
     });
   }
 
@@ -117,17 +123,16 @@ class RcclComm {
     TORCH_CHECK(streams.size() == ts.size(), "pddl rccl: one stream per local rank");
     std::vector<hipStream_t> ss;
     for (auto s : streams) ss.push_back(reinterpret_cast<hipStream_t>(s));
-    issue(ts, ss, tag.empty() ? "all_reduce" : tag, [&](size_t i) {
-      return ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), comms_[i],
-                           ss[i]);
+    issue(ts, ss, tag.empty() ? "all_reduce" : tag, [&](size_t i, ncclComm_t c) {
+      return ncclAllReduce(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), op_of(op), c, ss[i]);
     });
   }
 
   void broadcast(std::vector<Tensor> ts, int root) {
     std::vector<hipStream_t> ss;
     for (auto& t : ts) ss.push_back(stream_of(t));
-    issue(ts, ss, "broadcast", [&](size_t i) {
-      return ncclBroadcast(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), root, comms_[i], ss[i]);
+    issue(ts, ss, "broadcast", [&](size_t i, ncclComm_t c) {
+      return ncclBroadcast(ts[i].data_ptr(), ts[i].data_ptr(), ts[i].numel(), dtype_of(ts[i]), root, c, ss[i]);
     });
   }
 
@@ -135,33 +140,48 @@ class RcclComm {
   void send(Tensor t, int peer, int li) {
     check();
     c10::hip::HIPGuardMasqueradingAsCUDA g(devs_.at(li));
-    nck(ncclSend(t.data_ptr(), t.numel(), dtype_of(t), peer, comms_.at(li), stream_of(t)), "send");
+    std::lock_guard<std::mutex> lk(issue_mu_);
+    nck(ncclSend(t.data_ptr(), t.numel(), dtype_of(t), peer, comm(li), stream_of(t)), "send");
   }
   void recv(Tensor t, int peer, int li) {
     check();
     c10::hip::HIPGuardMasqueradingAsCUDA g(devs_.at(li));
-    nck(ncclRecv(t.data_ptr(), t.numel(), dtype_of(t), peer, comms_.at(li), stream_of(t)), "recv");
-  }
-
-  // Failure path (stall watchdog / PS failure): abort every local communicator.
-  void abort() {
     std::lock_guard<std::mutex> lk(issue_mu_);
-    for (auto& c : comms_)
-      if (c) {
-        ncclCommAbort(c);
-        c = nullptr;
-      }
+    nck(ncclRecv(t.data_ptr(), t.numel(), dtype_of(t), peer, comm(li), stream_of(t)), "recv");
   }
 
-  void set_watchdog(double timeout_s, double shutdown_s, int rank) {
+  // Failure path (stall watchdog / PS failure): abort every local communicator.  The issue lock
+  // is taken when it comes free within 2 s; a thread stuck INSIDE a collective holds it, and
+  // ncclCommAbort is what unblocks that thread, so after the wait the abort goes ahead without
+  // it.  Each communicator handle is swapped out atomically, so a concurrent reader sees either
+  // the live handle or null (never a freed one it did not already hold under the lock).
+  void abort() {
+    std::unique_lock<std::mutex> lk(issue_mu_, std::defer_lock);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!lk.try_lock() && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    if (!lk.owns_lock())
+      std::fprintf(stderr, "[pddl rccl] collective issue lock held by a stuck thread; aborting without it\n");
+    for (size_t i = 0; i < ncomm_; ++i) {
+      ncclComm_t c = comms_[i].exchange(nullptr);
+      if (c) ncclCommAbort(c);
+    }
+  }
+
+  // abort_on_stall = false: report only (a slow but live peer does not end the job);
+  // true: ncclCommAbort on the verdict, the next call raises, exit 124 after shutdown_s.
+  void set_watchdog(double timeout_s, double shutdown_s, int rank, bool abort_on_stall) {
     watch_.reset();
     if (timeout_s <= 0) return;
-    watch_ = std::make_unique<pddl::CommWatch>(timeout_s, shutdown_s, rank, [this](const std::string&) {
-      const std::string e = async_error();
-      if (!e.empty()) std::fprintf(stderr, "[pddl comm watchdog] RCCL async error: %s\n", e.c_str());
-      std::fprintf(stderr, "[pddl comm watchdog] aborting %zu local RCCL communicator(s)\n", comms_.size());
-      abort();
-    });
+    watch_ = std::make_unique<pddl::CommWatch>(
+        timeout_s, shutdown_s, rank,
+        [this](const std::string&) {
+          const std::string e = async_error();
+          if (!e.empty()) std::fprintf(stderr, "[pddl comm watchdog] RCCL async error: %s\n", e.c_str());
+          std::fprintf(stderr, "[pddl comm watchdog] aborting %zu local RCCL communicator(s)\n", ncomm_);
+          abort();
+        },
+        abort_on_stall);
   }
   void check() const {
     if (watch_) watch_->check();
@@ -175,6 +195,7 @@ class RcclComm {
       d["issued"] = watch_->issued();
       d["retired"] = watch_->retired();
       d["outstanding"] = (int64_t)watch_->outstanding();
+      d["warnings"] = watch_->warnings();
     }
     return d;
   }
@@ -182,13 +203,14 @@ class RcclComm {
   // What RCCL built, per local communicator.
   py::list info() const {
     py::list out;
-    for (size_t i = 0; i < comms_.size(); ++i) {
+    std::lock_guard<std::mutex> lk(issue_mu_);
+    for (size_t i = 0; i < ncomm_; ++i) {
       py::dict d;
       int count = -1, urank = -1, dev = -1;
-      if (comms_[i]) {
-        nck(ncclCommCount(comms_[i], &count), "comm count");
-        nck(ncclCommUserRank(comms_[i], &urank), "comm user rank");
-        nck(ncclCommCuDevice(comms_[i], &dev), "comm device");
+      if (ncclComm_t c = comms_[i].load()) {
+        nck(ncclCommCount(c, &count), "comm count");
+        nck(ncclCommUserRank(c, &urank), "comm user rank");
+        nck(ncclCommCuDevice(c, &dev), "comm device");
       }
       char bus[64] = {0};
       if (hipDeviceGetPCIBusId(bus, sizeof(bus), devs_[i]) != hipSuccess) bus[0] = 0;
@@ -200,8 +222,10 @@ class RcclComm {
     }
     return out;
   }
+  // (called by the watchdog's abort action too: no issue lock, atomic handle reads)
   std::string async_error() {
-    for (auto c : comms_) {
+    for (size_t i = 0; i < ncomm_; ++i) {
+      ncclComm_t c = comms_[i].load();
       if (!c) continue;
       ncclResult_t e;
       if (ncclCommGetAsyncError(c, &e) == ncclSuccess && e != ncclSuccess) return ncclGetErrorString(e);
@@ -223,7 +247,7 @@ class RcclComm {
     nck(ncclGroupStart(), "group start");
     for (size_t i = 0; i < ts.size(); ++i) {
       c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
-      nck(op(i), tag.c_str());
+      nck(op(i, comm(i)), tag.c_str());
     }
     nck(ncclGroupEnd(), "group end");
     if (!watch_) return;
@@ -247,20 +271,32 @@ class RcclComm {
         });
   }
 
+  void set_comms(const std::vector<ncclComm_t>& cs) {
+    ncomm_ = cs.size();
+    comms_.reset(new std::atomic<ncclComm_t>[ncomm_]);
+    for (size_t i = 0; i < ncomm_; ++i) comms_[i].store(cs[i]);
+  }
+  ncclComm_t comm(size_t i) const {
+    TORCH_CHECK(i < ncomm_, "pddl rccl: local rank out of range");
+    ncclComm_t c = comms_[i].load();
+    TORCH_CHECK(c != nullptr, "pddl rccl: communicator aborted");
+    return c;
+  }
   void check_local(const std::vector<Tensor>& ts) {
-    TORCH_CHECK(ts.size() == comms_.size(), "pddl rccl: need one tensor per local rank");
+    TORCH_CHECK(ts.size() == ncomm_, "pddl rccl: need one tensor per local rank");
     for (size_t i = 0; i < ts.size(); ++i) {
       TORCH_CHECK(ts[i].is_cuda() && ts[i].device().index() == devs_[i], "pddl rccl: tensor ", i,
                   " must live on device ", devs_[i]);
       TORCH_CHECK(ts[i].is_contiguous(), "pddl rccl: contiguous tensors only");
       TORCH_CHECK(ts[i].numel() == ts[0].numel(), "pddl rccl: equal sizes across local ranks");
-      TORCH_CHECK(comms_[i] != nullptr, "pddl rccl: communicator aborted");
+      (void)comm(i);
     }
   }
   int nranks_;
   std::vector<int> ranks_, devs_;
-  std::vector<ncclComm_t> comms_;
-  std::mutex issue_mu_;   // collective issue vs. the watchdog's abort
+  std::unique_ptr<std::atomic<ncclComm_t>[]> comms_;
+  size_t ncomm_ = 0;
+  mutable std::mutex issue_mu_;   // collective issue vs. the watchdog's abort
   std::unique_ptr<pddl::CommWatch> watch_;
 };
 
@@ -282,7 +318,7 @@ void register_rccl(py::module& m) {
       .def("recv", &RcclComm::recv, py::call_guard<py::gil_scoped_release>())
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def("set_watchdog", &RcclComm::set_watchdog, py::arg("timeout_s"), py::arg("shutdown_s") = 0.0,
-           py::arg("rank") = 0)
+           py::arg("rank") = 0, py::arg("abort_on_stall") = true)
       .def("check", &RcclComm::check)
       .def("watchdog_state", &RcclComm::watchdog_state)
       .def("info", &RcclComm::info)

@@ -84,3 +84,50 @@ class BucketAllReducer:
     def broadcast_(self, t: torch.Tensor, src: int = 0):
         if self.world > 1:
             dist.broadcast(t, src, group=self.group)
+
+
+class CommProxy:
+    """1-GPU model of the multi-GPU gradient all-reduce's footprint (`bench.py --comm-proxy`,
+    PDDL_COMM_PROXY="world=8,busbw=350,nch=32"): at the moment the fusion engine would issue
+    bucket i's RCCL all-reduce (its readiness event on the compute stream), a paced copy kernel
+    with RCCL's channel count of workgroups (`comm_proxy`, csrc/kernels/pack.hip) runs on a side
+    stream for the collective's modelled duration -- bucket bytes x 2 (N-1)/N / bus bandwidth --
+    streaming the bucket through HBM as a ring would.  It touches no gradient.  The step then
+    shows what the backward kernels lose to CUs and HBM shared with the collectives
+    (imagenet-resnet50-hvd.py:101's all-reduce overlapped with backward), which one GPU cannot
+    otherwise measure."""
+
+    def __init__(self, grads: torch.Tensor, buckets: List[Tuple[int, int]], spec: str):
+        from ..ops.native import require_native
+        self.N = require_native()
+        kv = dict(p.split("=") for p in spec.split(",") if "=" in p) if spec not in ("1", "on") else {}
+        self.world = int(kv.get("world", 8))
+        self.busbw = float(kv.get("busbw", 350.0)) * 1e9     # bytes/s
+        self.nch = int(kv.get("nch", 32))
+        self.grads = grads
+        self.buckets = list(buckets)
+        dev = grads.device
+        self.stream = torch.cuda.Stream(dev)
+        self.scratch = torch.empty(max(e - s for s, e in self.buckets) + 8, dtype=torch.float32, device=dev)
+        self.passes = max(1, round(2 * (self.world - 1) / self.world))
+        self.modelled_s = 0.0
+
+    def begin(self):
+        self.modelled_s = 0.0
+
+    def on_bucket_ready(self, i: int):
+        s, e = self.buckets[i]
+        s4 = (s + 3) // 4 * 4
+        n = max(0, (e - s4) // 4 * 4)
+        if n == 0:
+            return
+        t = (e - s) * 4 * 2 * (self.world - 1) / self.world / self.busbw
+        self.modelled_s += t
+        ev = torch.cuda.Event()
+        ev.record()
+        self.stream.wait_event(ev)
+        with torch.cuda.stream(self.stream):
+            self.N.comm_proxy(self.grads[s4:s4 + n], self.scratch, self.passes, int(t * 1e8), self.nch)
+
+    def finish(self):
+        torch.cuda.current_stream().wait_stream(self.stream)

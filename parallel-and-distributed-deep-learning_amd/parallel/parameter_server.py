@@ -192,10 +192,15 @@ class _Heartbeat:
     loop marks each step with `step()` (compute + exchange) and each wait with `wait()` (epoch
     barrier, worker 0's validation, a drained ticket queue); a step that runs longer than
     `stall_s` (a GPU hang, a stuck exchange) stops the stamps, so a live but stalled worker is
-    declared dead and its ticket re-queued exactly like a crashed one."""
+    declared dead and its ticket re-queued exactly like a crashed one.  `stall_s` is its own
+    threshold (PDDL_PS_STEP_STALL), separate from and larger than the coordinator's liveness
+    timeout `hb_timeout`: a slow but healthy step (a cold first batch from real data, a PS slowed
+    by many workers) keeps beating.  A worker still stuck `stall_s + 2 * hb_timeout` into a step
+    -- its ticket re-queued by then -- ends itself."""
 
-    def __init__(self, store, rank: int, period: float, stall_s: float):
+    def __init__(self, store, rank: int, period: float, stall_s: float, hb_timeout: Optional[float] = None):
         self.store, self.rank, self.period, self.stall_s = store, rank, period, stall_s
+        self.hb_timeout = stall_s if hb_timeout is None else hb_timeout
         self._stop = threading.Event()
         self._lock = threading.Lock()
         self._state, self._since = "wait", time.time()
@@ -226,9 +231,10 @@ class _Heartbeat:
                 # push a stale gradient is worse than a dead one -- end the process (fail fast)
                 with self._lock:
                     stuck = time.time() - self._since
-                if stuck > 2 * self.stall_s:
+                if stuck > self.stall_s + 2 * self.hb_timeout:
                     sys.stderr.write(f"[ps worker rank {self.rank}] stuck in a step for {stuck:.0f} s "
-                                     f"(heartbeat timeout {self.stall_s:g} s): exiting\n")
+                                     f"(step stall {self.stall_s:g} s, heartbeat timeout {self.hb_timeout:g} s): "
+                                     "exiting\n")
                     sys.stderr.flush()
                     os._exit(18)
                 continue
@@ -260,6 +266,20 @@ def _missing_tickets(store, epoch: int, lo: int, hi: int) -> List[int]:
         return [lo]
     mid = (lo + hi) // 2
     return _missing_tickets(store, epoch, lo, mid) + _missing_tickets(store, epoch, mid, hi)
+
+
+def requeue_orphans_from(store, epoch: int, live_workers: List[int]) -> Dict[int, List[int]]:
+    """requeue_orphans over `epoch` and every later epoch that has claims: a worker killed
+    between its first claim of epoch e+1 and its `cur` write still reads e in `cur`, and its
+    e+1 ticket must not be missed."""
+    out = {}
+    e = epoch
+    while store.check([f"claim/{e}"]):
+        r = requeue_orphans(store, e, live_workers)
+        if r:
+            out[e] = r
+        e += 1
+    return out
 
 
 def requeue_orphans(store, epoch: int, live_workers: List[int]) -> List[int]:
@@ -370,9 +390,9 @@ class PSServer:
                     if cl.store.check([f"cur/{w}"]):
                         ep = int(cl.store.get(f"cur/{w}").decode().split(":")[0])
                     live = [r for r in range(cl.num_ps, cl.world) if r not in dead]
-                    req = requeue_orphans(cl.store, ep, live)
+                    req = requeue_orphans_from(cl.store, ep, live)
                     print(f"[coordinator] worker {w} missed heartbeats for {now - last:.1f}s: declared dead, "
-                          f"re-queued step(s) {req} of epoch {ep}", flush=True)
+                          f"re-queued step(s) {req or 'none'} (by epoch, scanned from epoch {ep})", flush=True)
 
 
 class NativePSServer(PSServer):
@@ -585,7 +605,8 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         spe = min(spe, cfg.max_steps)
     fault_at = _fault_step(widx)
     hb_timeout = float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30"))
-    hb = _Heartbeat(store, rank, max(0.05, hb_timeout / 6), hb_timeout)
+    step_stall = float(os.environ.get("PDDL_PS_STEP_STALL", str(max(300.0, 10 * hb_timeout))))
+    hb = _Heartbeat(store, rank, max(0.05, hb_timeout / 6), step_stall, hb_timeout)
     epoch_timeout = float(os.environ.get("PDDL_PS_EPOCH_TIMEOUT", str(max(600.0, 10 * hb_timeout))))
     it = pipe.iterate(device)
     from .strategies import Augment

@@ -51,6 +51,14 @@ def stall_shutdown() -> float:
     return float(os.environ.get("PDDL_STALL_SHUTDOWN", "0"))
 
 
+def stall_abort() -> bool:
+    """Whether the native RCCL watchdog aborts the communicators on a stall (irreversible).  Off
+    by default -- like Horovod's stall check it only reports, so a slow but live peer (a cold
+    input pipeline, a long validation or checkpoint) does not end the job; on with
+    PDDL_STALL_ABORT=1 or a PDDL_STALL_SHUTDOWN grace (bench.py sets 30 s)."""
+    return os.environ.get("PDDL_STALL_ABORT", "0") == "1" or stall_shutdown() > 0
+
+
 def collective_timeout():
     """c10d process-group timeout: ProcessGroupNCCL's own watchdog tears the process down when a
     collective exceeds it, so a dead peer cannot hang a rank inside a device synchronize."""
@@ -336,6 +344,10 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
             if self.fusion is None:
                 self.reducer = BucketAllReducer(self.engine.grads, self.buckets, comm_dtype=self.cfg.grad_dtype,
                                                 stall_timeout=stall_timeout())
+        elif os.environ.get("PDDL_COMM_PROXY") and self.device.type == "cuda":
+            # 1 GPU: paced CU-holding stand-ins for the buckets' RCCL all-reduces (bench --comm-proxy)
+            from .collectives import CommProxy
+            self.reducer = CommProxy(self.engine.grads, self.buckets, os.environ["PDDL_COMM_PROXY"])
 
     _TUNE_STEPS = int(os.environ.get("PDDL_AUTOTUNE_STEPS", "4"))   # per candidate: 1 discarded + rest timed
 
@@ -532,9 +544,10 @@ class _LocalReplicas:
                     dist.broadcast_object_list(obj, src=0)
                 self.comm = N.RcclComm(world_ranks, obj[0], [global_rank_base + i for i in range(self.R)],
                                        [d.index for d in self.devices])
-            # stall watchdog: a bucket collective not complete within the timeout aborts the
-            # communicators (blocked kernels exit) and the next step raises with the bucket id
-            self.comm.set_watchdog(stall_timeout(), stall_shutdown(), global_rank_base)
+            # stall watchdog: a bucket collective not complete within the timeout is reported;
+            # with stall_abort() the communicators are aborted (blocked kernels exit), the next
+            # step raises with the bucket id and the rank exits 124 after the shutdown grace
+            self.comm.set_watchdog(stall_timeout(), stall_shutdown(), global_rank_base, stall_abort())
         self.graph_mode = (self.comm is not None and hasattr(self.replicas[0][0], "wbf")
                            and (cfg.graphs if cfg.graphs is not None else True))
         self.graphs = None

@@ -90,6 +90,8 @@ def main():
     rows = [r for r in csv.DictReader(open(path))]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
+    proxy = [r for r in rows if "comm_proxy" in r["Kernel_Name"]]   # bench --comm-proxy stand-ins
+    rows = [r for r in rows if "comm_proxy" not in r["Kernel_Name"]]
     import os
     ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0", os.environ.get("PDDL_FUSE_BWD", "1") != "0",
                   os.environ.get("PDDL_FUSE_BWD", "1") != "2", os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0")
@@ -144,6 +146,12 @@ def main():
             meas = f"  {cn[:5]} {mb:8.1f} MB ({mb * 1e6 / t / 1e9:6.0f} GB/s)"
         print(f"{t*1e6:9.1f} us  {tf:7.1f} TF/s  {gb:7.0f} GB/s  grid={grid:>16}  {kn[:40]:40s} {name}{meas}")
     print(f"step total {tot*1e3:.2f} ms")
+    t_first, t_last = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
+    print(f"step span (first start -> last end) {(t_last - t_first) * 1e-6:.2f} ms")
+    px = [r for r in proxy if t_first <= int(r["Start_Timestamp"]) <= t_last]
+    if px:
+        print(f"comm proxy: {len(px)} launches in the step, "
+              f"{sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in px) * 1e-6:.2f} ms busy")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1]):
         print(f"  {k:24s} {v*1e3:8.3f} ms")
 

@@ -243,3 +243,72 @@ def test_bench_parameter_server_rehearsal_on_one_gpu():
                       {"PDDL_REHEARSE": "1", "PDDL_PS_IMPL": "native"})
     assert out["n_gpus"] == 3 and out["config"]["parallelism"] == "ps1+w2" and out["rehearsal"] is True
     assert out["steps_timed_epoch"] == 8 and out["value"] > 0
+
+
+_HUNG_RCCL = r"""
+import sys, time, torch
+sys.path.insert(0, sys.argv[1])
+import pddl
+from pddl.ops.native import require_native
+N = require_native()
+comm = N.RcclComm(1, N.RcclComm.unique_id(), [0], [0])
+comm.set_watchdog(0.5, 4.0, 0, True)      # abort on stall, exit 124 four seconds after the verdict
+t = torch.ones(1 << 20, device="cuda")
+torch.cuda.synchronize()
+torch.cuda._sleep(4_000_000_000)          # a bounded spin (~2 s) holds the stream: the collective
+comm.all_reduce([t], "sum", "bucket 7 all_reduce")   # queued behind it cannot complete in time
+t0 = time.time()
+while True:
+    try:
+        comm.check()
+    except RuntimeError as e:
+        print(f"verdict after {time.time() - t0:.2f} s: {e}", flush=True)
+        break
+    if time.time() - t0 > 10:
+        print("no verdict", flush=True)
+        sys.exit(3)
+    time.sleep(0.05)
+st = comm.watchdog_state()
+print("state", st, flush=True)
+time.sleep(30)                            # the watchdog's shutdown deadline ends the process
+sys.exit(4)
+"""
+
+
+def test_rccl_watchdog_aborts_a_hung_collective_and_exits_124(tmp_path):
+    """The native communicator's stall path on the GPU: a collective queued behind a
+    bounded spin kernel misses the 0.5 s stall timeout -> the verdict names its bucket, the
+    abort action (on its own thread, lock-bounded) aborts the communicator, and the watchdog's
+    shutdown deadline ends the rank with exit 124 in bounded time, whatever the main thread
+    is doing.  (Two RCCL ranks cannot share one GPU, so a hung PEER is modelled by the spin.)"""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "hung_rccl.py"
+    script.write_text(_HUNG_RCCL)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, str(script), root], cwd=root, capture_output=True, text=True, timeout=90)
+    dt = time.time() - t0
+    assert r.returncode == 124, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "verdict after" in r.stdout and "bucket 7 all_reduce" in r.stdout, r.stdout
+    assert "aborting 1 local RCCL communicator" in r.stderr, r.stderr[-2000:]
+    assert dt < 60, dt
+
+
+def test_comm_proxy_holds_its_duration_and_leaves_the_gradient():
+    """bench --comm-proxy's stand-in collective: the paced kernel runs for its modelled duration
+    (within launch overhead), streams the bucket into scratch, and never writes the gradient."""
+    import time
+    from pddl.ops.native import require_native
+    N = require_native()
+    g = torch.randn(1 << 22, device="cuda")
+    ref = g.clone()
+    scratch = torch.zeros_like(g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    N.comm_proxy(g, scratch, 2, 2_000_000, 32)      # 20 ms at 100 MHz
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert 0.019 < dt < 0.2, dt
+    assert torch.equal(g, ref) and torch.equal(scratch, g)

@@ -4,6 +4,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -202,10 +203,12 @@ def test_resume_continues_epochs_lr_and_callbacks(tmp_path):
 def test_ps_stalled_worker_declared_dead_and_requeued(monkeypatch):
     """A LIVE worker stuck inside a step (hang_worker) stops heartbeating (the beacon stamps
     only while the main loop makes progress), is declared dead, its ticket is re-queued and
-    the epoch completes; the stuck process ends itself after twice the timeout."""
+    the epoch completes; the stuck process ends itself after the step-stall threshold plus twice
+    the heartbeat timeout."""
     from pddl.parallel.parameter_server import run_ps_job
     monkeypatch.setenv("PDDL_FAULT", "hang_worker:1@1")
     monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
+    monkeypatch.setenv("PDDL_PS_STEP_STALL", "3")
     cfg = _cfg("ps", steps_per_epoch=6, batch_size=2, epochs=1)
     res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
     wk = [r for r in res if r[0] == "worker"]
@@ -228,6 +231,38 @@ def test_requeue_orphans_counts_each_lost_ticket_once():
     assert st.add("requeue/0", 0) == 1
     assert requeue_orphans(st, 0, [4]) == []  # a second scan does not count it again
     assert st.add("requeue/0", 0) == 1
+
+
+def test_requeue_orphans_scans_the_next_epoch():
+    """A worker killed between its first claim of epoch e+1 and its `cur` write still shows
+    `cur = e:-1`: the coordinator's scan starting at e must reach e+1's claims."""
+    import torch.distributed as dist
+    from pddl.parallel.parameter_server import requeue_orphans_from
+    st = dist.HashStore()
+    st.set("claim/0", "4/2")
+    for t in range(4):
+        st.set(f"tdone/0/{t}", "1")           # epoch 0 complete
+    st.set("claim/1", "1/3")                  # the dead worker claimed ticket 0 of epoch 1 ...
+    st.set("cur/3", "0:-1")                   # ... but its cur still names epoch 0
+    assert requeue_orphans_from(st, 0, [4]) == {1: [0]}
+    assert requeue_orphans_from(st, 0, [4]) == {}
+
+
+def test_heartbeat_keeps_beating_through_a_slow_step():
+    """The in-step stall threshold (PDDL_PS_STEP_STALL) is separate from the liveness timeout:
+    a step longer than the heartbeat timeout but shorter than the stall threshold keeps the
+    beacon stamping (a slow but healthy worker is not declared dead)."""
+    import torch.distributed as dist
+    from pddl.parallel.parameter_server import _Heartbeat
+    st = dist.HashStore()
+    hb = _Heartbeat(st, 5, 0.05, stall_s=5.0, hb_timeout=0.3)
+    try:
+        hb.step()
+        t0 = float(st.get("hb/5").decode())
+        time.sleep(0.8)                        # > hb_timeout, < stall_s
+        assert hb.healthy() and float(st.get("hb/5").decode()) > t0 + 0.5
+    finally:
+        hb.stop()
 
 
 def test_ps_resume_rejected(tmp_path):
