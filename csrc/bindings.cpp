@@ -466,6 +466,31 @@ void maxpool_fwd(Tensor x, Tensor y, Tensor idx, OptT bits) {
                               (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), cur_stream()),
      "maxpool_fwd");
 }
+// Fused stem: x2 [B,Hs,Ws,16] bf16, w [64,>=256] bf16 rows, scale/shift fp32 [>=64] ->
+// pool [B,H2,W2,64] bf16, idx uint8 same shape, bits (optional) [B,H2,W2,8] uint8.
+void stem_pool_fwd(Tensor x2, Tensor w, Tensor scale, Tensor shift, Tensor pool, Tensor idx, OptT bits,
+                   int64_t pool_rows) {
+  PCHECK(x2.dim() == 4 && x2.size(3) == 16 && x2.is_contiguous(), "stem_pool: x2 [B,Hs,Ws,16] contiguous");
+  PCHECK(w.dim() == 2 && w.size(0) == 64 && w.size(1) == 256 && w.stride(1) == 1 && w.stride(0) == 256,
+         "stem_pool: w [64,256] contiguous");
+  PCHECK(scale.numel() >= 64 && shift.numel() >= 64, "stem_pool: 64 scale / shift values");
+  PCHECK(pool.dim() == 4 && pool.size(3) == 64 && pool.is_contiguous() && pool.size(0) == x2.size(0),
+         "stem_pool: pool [B,H2,W2,64] contiguous");
+  PCHECK(idx.scalar_type() == torch::kUInt8 && idx.is_contiguous() && idx.numel() == pool.numel(),
+         "stem_pool: idx uint8 like pool");
+  if (bits.has_value())
+    PCHECK(bits->scalar_type() == torch::kUInt8 && bits->is_contiguous() && bits->numel() * 8 == pool.numel(),
+           "stem_pool: bits [B,H2,W2,8] uint8");
+  PCHECK((reinterpret_cast<uintptr_t>(scale.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(shift.data_ptr()) & 15) == 0,
+         "stem_pool: 16-byte aligned scale / shift");
+  pddl::StemPoolParams p{};
+  p.x2 = bfp(x2); p.w = bfp(w); p.scale = f32p(scale); p.shift = f32p(shift);
+  p.pool = bfpm(pool); p.idx = idx.data_ptr<uint8_t>(); p.bits = bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr;
+  p.B = (int)x2.size(0); p.Hs = (int)x2.size(1); p.Ws = (int)x2.size(2);
+  p.H1 = p.Hs - 3; p.W1 = p.Ws - 3; p.H2 = (int)pool.size(1); p.W2 = (int)pool.size(2);
+  p.PB = (int)pool_rows;
+  ok(pddl::stem_pool_fwd_launch(p, cur_stream()), "stem_pool_fwd");
+}
 void maxpool_bwd(Tensor gy, Tensor idx, OptT xmask, Tensor gx, OptT colsum) {
   ok(pddl::maxpool_bwd_launch(bfp(gy), idx.data_ptr<uint8_t>(), obfp(xmask), bfpm(gx), (int)gx.size(0),
                               (int)gx.size(1), (int)gx.size(2), (int)gx.size(3), (int)gy.size(1), (int)gy.size(2),
@@ -626,6 +651,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_s2d", &stem_s2d, REL);
   m.def("stem_wgrad_fold", &stem_wgrad_fold, REL);
   m.def("maxpool_fwd", &maxpool_fwd, REL);
+  m.def("stem_pool_fwd", &stem_pool_fwd, REL, py::arg("x2"), py::arg("w"), py::arg("scale"), py::arg("shift"),
+        py::arg("pool"), py::arg("idx"), py::arg("bits") = py::none(), py::arg("pool_rows") = 0);
   m.def("maxpool_bwd", &maxpool_bwd, REL);
   m.def("gap_fwd", &gap_fwd, REL);
   m.def("gap_bwd", &gap_bwd, REL);

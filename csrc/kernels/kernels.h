@@ -147,6 +147,20 @@ const char* stem_s2d_f32_launch(const StemParams& p, float* out, hipStream_t s);
 // Fold the s2d-domain stem weight gradient [64][256] back to [64][7][7][3] (added into dw).
 const char* stem_wgrad_fold_launch(const float* g2, float* dw, int cout, hipStream_t s);
 
+// Fused stem forward (stem.hip): conv1 on the s2d input + frozen BN + ReLU + the 3x3/s2 max-pool,
+// writing only the pool output, its argmax taps and (nullable) ReLU bits -- conv1's output never
+// reaches HBM.  PB = pool rows per workgroup (<= 0: chosen by the launcher; nblk is set by it).
+struct StemPoolParams {
+  const uint16_t* x2;                 // [B][Hs][Ws][16] space-to-depth input
+  const uint16_t* w;                  // [64][256] bf16 forward weights (s2d k order)
+  const float* scale; const float* shift;   // folded frozen BN of conv1 (64 each)
+  uint16_t* pool; uint8_t* idx; uint8_t* bits;   // [B][H2][W2][64], same, [B][H2][W2][8]
+  int B, Hs, Ws, H1, W1, H2, W2;
+  int PB, nblk;
+};
+const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s);
+int stem_pool_lds_bytes(int Ws, int W1);
+
 const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, uint8_t* bits, int B, int H, int W, int C,
                                int Ho, int Wo, hipStream_t s);
 const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uint16_t* xmask, uint16_t* gx,

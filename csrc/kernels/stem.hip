@@ -1,0 +1,205 @@
+// Fused stem forward (gfx950): conv1 (7x7/s2 as the 4x4/s1 space-to-depth window GEMM, K = 256)
+// + frozen BN + ReLU + ZeroPadding2D(1) + MaxPooling2D(3, 2), in one launch.  The conv output
+// (N x 112 x 112 x 64 bf16 at crop 224: 1.6 MB per image) never reaches HBM: the workgroup keeps
+// the three conv rows a pool row needs in LDS and writes only the pool output, its argmax taps
+// and its ReLU bits -- what the backward uses (the max-pool backward routes by the argmax tap,
+// and conv2_block1's dgrad masks with the pool output's bits).  Reference: the Keras ResNet50
+// stem behind imagenet-resnet50.py:56.
+//
+// Workgroup = (image, block of PB pool rows), 256 threads (4 waves), two workgroups per CU.
+// Per pool row p: conv rows 2p and 2p+1 (and 2p-1 for the block's first row) are computed as
+// 16-pixel x 64-channel MFMA tiles (v_mfma_f32_16x16x32_bf16 with the weights as the A operand,
+// held in registers for the whole launch, and the im2col pixels as the B operand, read from a
+// ring of eight space-to-depth input rows in LDS: 16 B per lane = 8 channels of one tap, rows of
+// a 16-pixel tile are consecutive pixels, conflict-free); the epilogue (scale / shift / ReLU /
+// bf16, exactly the igemm forward epilogue's expression) writes 4 channels x 1 pixel per lane
+// into a 3-row conv buffer (8-byte chunks XOR-swizzled by the pixel column so the stores and the
+// 16-byte pool reads are conflict-free).  After a barrier the workgroup pools row p (first
+// maximum in scan order, padding taps are zeros, as maxpool_fwd_kernel) while the next rows'
+// input is already in flight (global loads issued before the MFMA phase, written to the ring
+// after it).
+#include "common.h"
+#include "kernels.h"
+
+namespace pddl {
+
+namespace {
+
+constexpr int SP_THREADS = 256;
+
+__device__ __forceinline__ uint32_t swz_chunk(int chunk, int x) { return (uint32_t)(chunk ^ (x & 14)); }
+
+}  // namespace
+
+template <bool BITS>
+__global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int SLOT = p.Ws * 32;
+  const int CROW = p.W1 * 128;
+  uint8_t* ring = lds;
+  uint8_t* cbuf = lds + 8 * SLOT;
+  const int b = blockIdx.x / p.nblk;
+  const int blk = blockIdx.x - b * p.nblk;
+  const int P0 = blk * p.PB;
+  const int P1 = min(P0 + p.PB, p.H2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  // ---- weights as A fragments: co = 16 nt + lr, k = 32 t + 8 lg + j (held for the whole launch)
+  v8bf wa[4][8];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      wa[nt][t] = *reinterpret_cast<const v8bf*>(p.w + (16 * nt + lr) * 256 + 32 * t + 8 * lg);
+  // folded BN (scale | shift of the 64 output channels) in LDS: read per epilogue, so the
+  // weight fragments keep the register file
+  float* bn = reinterpret_cast<float*>(cbuf + 3 * CROW);
+  if (tid < 128) bn[tid] = tid < 64 ? p.scale[tid] : p.shift[tid - 64];
+
+  const uint4* x2b = reinterpret_cast<const uint4*>(p.x2 + (long)b * p.Hs * p.Ws * 16);
+  const int RCH = p.Ws * 2;   // 16-byte chunks per input row
+
+  // ---- initial ring fill: input rows [2 P0 - 1, 2 P0 + 5) (the first pool row's conv rows
+  //      2 P0 - 1 .. 2 P0 + 1 read input rows up to 2 P0 + 4)
+  for (int yy = max(2 * P0 - 1, 0); yy < min(2 * P0 + 5, p.Hs); ++yy) {
+    uint4* dst = reinterpret_cast<uint4*>(ring + (yy & 7) * SLOT);
+    for (int c = tid; c < RCH; c += SP_THREADS) dst[c] = x2b[(long)yy * RCH + c];
+  }
+  __syncthreads();
+
+  const int nct = (p.W1 + 15) >> 4;
+  for (int pr = P0; pr < P1; ++pr) {
+    // ---- prefetch the two input rows the next pool row adds (2 pr + 5, 2 pr + 6)
+    constexpr int PFN = 2;   // 2 rows x RCH chunks <= 2 x 256 for Ws <= 128 (checked by the launcher)
+    uint4 pf[PFN];
+    const bool more = pr + 1 < P1;
+#pragma unroll
+    for (int k = 0; k < PFN; ++k) {
+      const int c = tid + k * SP_THREADS;
+      const int yy = 2 * pr + 5 + (c >= RCH ? 1 : 0), cc = c >= RCH ? c - RCH : c;
+      pf[k] = make_uint4(0, 0, 0, 0);
+      if (more && c < 2 * RCH && yy < p.Hs) pf[k] = x2b[(long)yy * RCH + cc];
+    }
+    // ---- conv rows of this iteration: 2pr, 2pr+1 (and 2pr-1 on the block's first pool row)
+    const int ylo = (pr == P0 && pr > 0) ? 2 * pr - 1 : 2 * pr;
+    const int nrows = 2 * pr + 2 - ylo;
+    const int ntiles = nrows * nct;
+    for (int ti = wave; ti < ntiles; ti += SP_THREADS / 64) {
+      const int y = ylo + ti / nct, x0 = (ti % nct) * 16;
+      v4f acc[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = (v4f){0.f, 0.f, 0.f, 0.f};
+      const int xl = x0 + lr;   // this lane's pixel (B-operand column)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        // k = 32 t + 8 lg + j: tap (R, S) = (t >> 1, 2 (t & 1) + (lg >> 1)), channels 8 (lg & 1) + j
+        const int R = t >> 1, S = 2 * (t & 1) + (lg >> 1);
+        const uint8_t* src = ring + ((y + R) & 7) * SLOT + (xl + S) * 32 + (lg & 1) * 16;
+        const v8bf bx = *reinterpret_cast<const v8bf*>(src);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nt][t], bx, acc[nt], 0, 0, 0);
+      }
+      // epilogue: lane holds D[co = 16 nt + 4 lg + i][px = lr]
+      if (xl < p.W1) {
+        uint8_t* crow = cbuf + (y % 3) * CROW + xl * 128;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const float4 a = *reinterpret_cast<const float4*>(bn + 16 * nt + 4 * lg);
+          const float4 c = *reinterpret_cast<const float4*>(bn + 64 + 16 * nt + 4 * lg);
+          const float sc[4] = {a.x, a.y, a.z, a.w}, sh[4] = {c.x, c.y, c.z, c.w};
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = fmaxf(acc[nt][i] * sc[i] + sh[i], 0.f);
+          const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          *reinterpret_cast<uint2*>(crow + swz_chunk(4 * nt + lg, xl) * 8) = pk;
+        }
+      }
+    }
+    // ---- the prefetched rows into their ring slots (rows this iteration no longer reads)
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < PFN; ++k) {
+        const int c = tid + k * SP_THREADS;
+        if (c < 2 * RCH) {
+          const int yy = 2 * pr + 5 + (c >= RCH ? 1 : 0), cc = c >= RCH ? c - RCH : c;
+          if (yy < p.Hs) reinterpret_cast<uint4*>(ring + (yy & 7) * SLOT)[cc] = pf[k];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- pool row pr: window rows 2pr-1 .. 2pr+1, columns 2q-1 .. 2q+1; item = (q, 8-channel group)
+    const long orow = ((long)b * p.H2 + pr) * p.W2;
+    for (int it = tid; it < p.W2 * 8; it += SP_THREADS) {
+      const int q = it >> 3, cg = it & 7;
+      float best[8];
+      uint32_t code[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; code[e] = 0; }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int y = 2 * pr - 1 + r;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int x = 2 * q - 1 + s;
+          float v[8];
+          if (y >= 0 && x >= 0) {
+            const uint4 u = *reinterpret_cast<const uint4*>(cbuf + (y % 3) * CROW + x * 128 +
+                                                            swz_chunk(2 * cg, x) * 8);
+            unpack8(u, v);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (v[e] > best[e]) { best[e] = v[e]; code[e] = (uint32_t)(r * 3 + s); }
+        }
+      }
+      const long o = (orow + q) * 64 + cg * 8;
+      const uint4 yv = pack8(best);
+      *reinterpret_cast<uint4*>(p.pool + o) = yv;
+      if (BITS) p.bits[o >> 3] = (uint8_t)pos_bits8(yv);
+      *reinterpret_cast<uint2*>(p.idx + o) =
+          make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
+                     code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24));
+    }
+    __syncthreads();   // the next rows' epilogue overwrites conv rows 2pr-1 / 2pr
+  }
+}
+
+int stem_pool_lds_bytes(int Ws, int W1) { return 8 * Ws * 32 + 3 * W1 * 128 + 512; }
+
+const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s) {
+  if (p.H1 != p.Hs - 3 || p.W1 != p.Ws - 3) return "stem_pool: conv1 output must be the s2d input minus 3";
+  if (p.H1 % 2 || p.W1 % 2) return "stem_pool: even conv1 output (even crop) expected";
+  if (p.H2 != p.H1 / 2 || p.W2 != p.W1 / 2) return "stem_pool: pool output must be the pad-1 3x3/s2 size";
+  if (p.Ws > 128) return "stem_pool: input rows wider than the prefetch covers (crop <= 250)";
+  const int lds = stem_pool_lds_bytes(p.Ws, p.W1);
+  if (lds > 80 * 1024) return "stem_pool: LDS per workgroup above the two-per-CU budget";
+  if ((long)p.B * p.H2 * p.W2 * 64 >= (1L << 40)) return "stem_pool: output too large";
+  if (p.PB <= 0) {   // pool rows per workgroup: whole images when the batch fills the chip
+    const long want = 4L * num_cus();
+    int pb = p.H2;
+    while (pb > 2 && (long)p.B * ((p.H2 + pb - 1) / pb) < want) pb = (pb + 1) / 2;
+    p.PB = pb;
+  }
+  p.nblk = (p.H2 + p.PB - 1) / p.PB;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    attr = true;
+  }
+  const dim3 grid((unsigned)((long)p.B * p.nblk));
+  if (p.bits)
+    hipLaunchKernelGGL(stem_pool_fwd_kernel<true>, grid, dim3(SP_THREADS), lds, s, p);
+  else
+    hipLaunchKernelGGL(stem_pool_fwd_kernel<false>, grid, dim3(SP_THREADS), lds, s, p);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+}  // namespace pddl

@@ -47,6 +47,7 @@ class HipEngine:
     BN_MODES = ("frozen",)   # HipEngineBNTrain (models/engine_bn.py) runs bn_mode="train"
     FUSE_PROJ_OK = True     # projection blocks: conv3 + shortcut conv as one dual-source GEMM
     FUSE_BWD_OK = True      # stage-2/3 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
+    FUSE_STEM_OK = True     # stem conv + BN + ReLU + max-pool forward in one launch (stem.hip)
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
@@ -89,6 +90,8 @@ class HipEngine:
         self.fuse_bwd = self.FUSE_BWD_OK and self.bitmask and os.environ.get("PDDL_FUSE_BWD", "1") != "0"
         self._fuse_bwd3 = os.environ.get("PDDL_FUSE_BWD", "1") != "2"
         self._fuse_bwd_s2 = os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0"
+        # stem conv + max-pool forward as one launch (stem.hip): conv1's output never reaches HBM
+        self.fuse_stem = self.FUSE_STEM_OK and os.environ.get("PDDL_FUSE_STEM", "1") != "0" and crop <= 250
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -228,7 +231,8 @@ class HipEngine:
         self.Hs = (crop + 6) // 2
         assert crop % 2 == 0, "crop must be even (space-to-depth stem)"
         self.stem_x2 = torch.empty(B, self.Hs, self.Hs, 16, **bf)
-        self.c1 = torch.empty(B, H1, H1, 64, **bf)
+        # (the fused stem never materialises conv1's output)
+        self.c1 = None if self.fuse_stem else torch.empty(B, H1, H1, 64, **bf)
         self.pool = torch.empty(B, H2, H2, 64, **bf)
         self.pidx = torch.empty(B, H2, H2, 64, dtype=torch.uint8, device=dev)
         u8 = dict(dtype=torch.uint8, device=dev)
@@ -385,13 +389,18 @@ class HipEngine:
         N.stem_s2d(images, flip if training else None, mode, self.crop, self.crop, oy, ox, x2, crop_dev)
         H1, H2, Hs = self.H1, self.H2, self.Hs
         s = L.stem
-        c1 = self.c1[:B]
-        N.igemm(x2, None, Hs, Hs, 4, 4, 1, 0, H1, H1, self._wf(s.name, 64, STEM_K), 0,
-                self.scale[self.ch[s.name]:], self.shift[self.ch[s.name]:], None, None, None, c1, 1,
-                None, 0, 0, 0, 0, 0, None, None)
         pool = self.pool[:B]
         use_bits = training and self.bitmask
-        N.maxpool_fwd(c1, pool, self.pidx[:B], self.pool_bits[:B] if use_bits else None)
+        chs = self.ch[s.name]
+        if self.fuse_stem:
+            N.stem_pool_fwd(x2, self._wf(s.name, 64, STEM_K), self.scale[chs:chs + 64], self.shift[chs:chs + 64],
+                            pool, self.pidx[:B], self.pool_bits[:B] if use_bits else None)
+        else:
+            c1 = self.c1[:B]
+            N.igemm(x2, None, Hs, Hs, 4, 4, 1, 0, H1, H1, self._wf(s.name, 64, STEM_K), 0,
+                    self.scale[chs:], self.shift[chs:], None, None, None, c1, 1,
+                    None, 0, 0, 0, 0, 0, None, None)
+            N.maxpool_fwd(c1, pool, self.pidx[:B], self.pool_bits[:B] if use_bits else None)
         x = pool
         for b in L.blocks:
             a = self.acts[b.name]

@@ -37,6 +37,7 @@ class HipEngineBNTrain(HipEngine):
     BN_MODES = ("train",)
     FUSE_BWD_OK = False    # (its conv3 dgrad carries the fused BN-backward sums)
     FUSE_PROJ_OK = False   # (batch statistics: the shortcut's BN cannot be folded into weights)
+    FUSE_STEM_OK = False   # (conv1's batch statistics need its raw output)
 
     def __init__(self, layout: ParamLayout, batch: int, **kw):
         kw.setdefault("bn_mode", "train")

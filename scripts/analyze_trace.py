@@ -13,14 +13,18 @@ import pddl  # noqa
 from pddl.models.resnet50 import ParamLayout
 
 
-def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True):
+def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fuse_stem=True):
     L = ParamLayout()
     H1 = (crop + 6 - 7) // 2 + 1
     H2 = (H1 + 2 - 3) // 2 + 1
     ev = []
     ev.append(("stem_s2d", "stem", 0, B * H1 * H1 * 4 * 32))
-    ev.append(("igemm", "conv1 fwd", 2 * B * H1 * H1 * 256 * 64, B * H1 * H1 * 64 * 2, (B * H1 * H1, 64, 256)))
-    ev.append(("maxpool_fwd", "pool", 0, B * (H1 * H1 + H2 * H2) * 64 * 2))
+    if fuse_stem:   # conv1 + max-pool in one launch (stem.hip)
+        ev.append(("stem_pool", "conv1+pool fwd", 2 * B * H1 * H1 * 256 * 64,
+                   B * (H1 + 3) ** 2 * 32 + B * H2 * H2 * 64 * 3, None))
+    else:
+        ev.append(("igemm", "conv1 fwd", 2 * B * H1 * H1 * 256 * 64, B * H1 * H1 * 64 * 2, (B * H1 * H1, 64, 256)))
+        ev.append(("maxpool_fwd", "pool", 0, B * (H1 * H1 + H2 * H2) * 64 * 2))
     H = H2
     geo = []
     for b in L.blocks:
@@ -94,7 +98,8 @@ def main():
     rows = [r for r in rows if "comm_proxy" not in r["Kernel_Name"]]
     import os
     ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0", os.environ.get("PDDL_FUSE_BWD", "1") != "0",
-                  os.environ.get("PDDL_FUSE_BWD", "1") != "2", os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0")
+                  os.environ.get("PDDL_FUSE_BWD", "1") != "2", os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0",
+                  os.environ.get("PDDL_FUSE_STEM", "1") != "0")
     # a split launch (8-phase kernel for full rounds + 128x128 tail) is two dispatches of one layer
     try:
         from pddl.ops.native import require_native

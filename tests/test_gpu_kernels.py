@@ -951,3 +951,37 @@ def test_bwd1x1_fused_stride2(co, ci, B, H):
     assert rel(out, ref) < 1e-2 and rel(out2, refc) < 1e-2
     assert rel(colsum.view(rows, ci).sum(0), refc.sum((0, 1, 2))) < 1e-3
     assert rel(dw, g.float().reshape(-1, co).t() @ xs.float().reshape(-1, ci)) < 1e-3
+
+
+@pytest.mark.parametrize("B,crop,rows", [(2, 224, 0), (3, 244, 0), (2, 160, 1), (2, 96, 3), (1, 224, 56), (2, 244, 7)])
+def test_stem_pool_fused_matches_unfused(B, crop, rows):
+    """The fused stem (stem.hip: conv1 + BN + ReLU + max-pool, conv1's output only in LDS) equals
+    the unfused pair (igemm window GEMM -> bf16 conv1 output -> maxpool_fwd) bit for bit: pool
+    output, argmax taps and ReLU bits, for whole-image and row-block workgroups (the block's
+    first conv row recomputed) and the ragged 122-wide rows of crop 244."""
+    torch.manual_seed(crop + rows)
+    hs = (crop + 6) // 2
+    h1, h2 = hs - 3, (hs - 3) // 2
+    x2 = torch.rand(B, hs, hs, 16, device=dev).to(torch.bfloat16)
+    w2 = (torch.randn(64, 256, device=dev) * 0.08).to(torch.bfloat16)
+    scale = 0.5 + torch.rand(64, device=dev)
+    shift = 0.2 * torch.randn(64, device=dev)
+    c1 = torch.empty(B, h1, h1, 64, dtype=torch.bfloat16, device=dev)
+    N().igemm(x2, None, hs, hs, 4, 4, 1, 0, h1, h1, w2, 0, scale, shift, None, None, None, c1, 1, None, 0, 0, 0, 0, 0,
+              None, None)
+    pool_r = torch.empty(B, h2, h2, 64, dtype=torch.bfloat16, device=dev)
+    idx_r = torch.empty(B, h2, h2, 64, dtype=torch.uint8, device=dev)
+    bits_r = torch.empty(B, h2, h2, 8, dtype=torch.uint8, device=dev)
+    N().maxpool_fwd(c1, pool_r, idx_r, bits_r)
+    pool = torch.full_like(pool_r, 7.0)
+    idx = torch.full_like(idx_r, 99)
+    bits = torch.full_like(bits_r, 0x5a)
+    N().stem_pool_fwd(x2, w2, scale, shift, pool, idx, bits, rows)
+    torch.cuda.synchronize()
+    assert (pool.view(torch.int16) != pool_r.view(torch.int16)).sum().item() == 0, (pool.float() - pool_r.float()).abs().max()
+    assert torch.equal(idx, idx_r)
+    assert torch.equal(bits, bits_r)
+    # evaluation form (no bits)
+    pool2 = torch.empty_like(pool_r)
+    N().stem_pool_fwd(x2, w2, scale, shift, pool2, idx, None, rows)
+    assert torch.equal(pool2.view(torch.int16), pool_r.view(torch.int16))
