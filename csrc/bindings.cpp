@@ -618,6 +618,35 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                (int)r.size(0), scatter ? 1 : 0, cur_stream()),
        "range_copy");
   });
+  // bf16 wire of the PS data plane (tests): gather fp32 -> packed bf16 / scatter packed bf16 -> fp32
+  m.def("range_copy_cvt", [](Tensor src, Tensor dst, Tensor rows, bool scatter) {
+    PCHECK(!rows.is_cuda() && rows.scalar_type() == torch::kInt64 && rows.dim() == 2 && rows.size(1) == 3,
+           "range rows: host int64 [n, 3]");
+    PCHECK(src.is_cuda() && dst.is_cuda() && src.is_contiguous() && dst.is_contiguous(), "range_copy_cvt: GPU tensors");
+    PCHECK(scatter ? (src.scalar_type() == torch::kBFloat16 && dst.scalar_type() == torch::kFloat32)
+                   : (src.scalar_type() == torch::kFloat32 && dst.scalar_type() == torch::kBFloat16),
+           "range_copy_cvt: gather fp32 -> bf16, scatter bf16 -> fp32");
+    Tensor r = rows.contiguous();
+    const int64_t* q = r.data_ptr<int64_t>();
+    const int64_t flat_n = scatter ? dst.numel() : src.numel(), packed_n = scatter ? src.numel() : dst.numel();
+    for (int64_t i = 0; i < r.size(0); ++i)
+      PCHECK(q[3 * i] >= 0 && q[3 * i + 1] >= 0 && q[3 * i + 2] >= 0 && q[3 * i] + q[3 * i + 2] <= flat_n &&
+                 q[3 * i + 1] + q[3 * i + 2] <= packed_n,
+             "range out of bounds");
+    Tensor dev = r.to(src.device());
+    ok(pddl::range_copy_cvt_launch(src.data_ptr(), dst.data_ptr(), reinterpret_cast<const pddl::RangeRow*>(dev.data_ptr()),
+                                   (int)r.size(0), scatter ? 1 : 0, cur_stream()),
+       "range_copy_cvt");
+  });
+  m.def("adam_bf16_wire", [](Tensor p, Tensor g, Tensor m_, Tensor v, Tensor snap, double lr_t, double b1, double b2,
+                             double eps) {
+    PCHECK(g.scalar_type() == torch::kBFloat16 && snap.scalar_type() == torch::kBFloat16 && g.numel() == p.numel() &&
+               snap.numel() == p.numel() && m_.numel() == p.numel() && v.numel() == p.numel(),
+           "adam_bf16_wire: p/m/v fp32, g/snap bf16, equal sizes");
+    ok(pddl::adam_bf16_wire_launch(f32p(p), bfp(g), f32p(m_), f32p(v), bfpm(snap), p.numel(), (float)lr_t, (float)b1,
+                                   (float)b2, (float)eps, cur_stream()),
+       "adam_bf16_wire");
+  });
   // bench.py --comm-proxy: a paced, CU-holding stand-in for one bucket's RCCL all-reduce
   m.def("comm_proxy", [](Tensor src, Tensor scratch, int passes, int64_t ticks, int nch) {
     PCHECK(src.is_cuda() && scratch.is_cuda() && src.scalar_type() == torch::kFloat32 &&

@@ -266,6 +266,8 @@ struct RangeRow { long flat, packed, len; };
 // scatter = 0: dst[packed + i] = src[flat + i]; 1: dst[flat + i] = src[packed + i].
 const char* range_copy_launch(const float* src, float* dst, const RangeRow* rows_dev, int nrows, int scatter,
                               hipStream_t s);
+const char* range_copy_cvt_launch(const void* src, void* dst, const RangeRow* rows_dev, int nrows, int scatter,
+                                  hipStream_t s);   // gather: fp32 -> bf16 packed; scatter: bf16 packed -> fp32
 const char* comm_proxy_launch(const float* src, float* scratch, long n, int passes, long ticks, int nch,
                               hipStream_t s);
 
@@ -280,6 +282,8 @@ const char* adam_launch(float* p, const float* g, float* m, float* v, long n, fl
                         float eps, float gscale, const float* hs, hipStream_t s);
 const char* sgd_launch(float* p, const float* g, float* mom, long n, float lr, float momentum, float wd,
                        int nesterov, float gscale, const float* hs, hipStream_t s);
+const char* adam_bf16_wire_launch(float* p, const uint16_t* g, float* m, float* v, uint16_t* snap, long n, float lr_t,
+                                  float b1, float b2, float eps, hipStream_t s);
 const char* scale_launch(float* x, long n, float a, hipStream_t s);
 const char* cast_bf16_launch(const float* x, uint16_t* y, long n, hipStream_t s);
 const char* cast_f32_launch(const uint16_t* x, float* y, long n, hipStream_t s);

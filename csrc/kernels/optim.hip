@@ -46,6 +46,36 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+// Parameter-server form with the bf16 wire (--ps-wire bf16): the gradient arrives in bf16
+// (the worker's mailbox push) and the update also writes the bf16 snapshot of the new
+// parameters that the pulls copy (half the xGMI bytes both ways; the PS keeps fp32 master
+// weights and Adam slots).  Same arithmetic as adam_kernel.
+__global__ void adam_bf16_wire_kernel(float* __restrict__ p, const uint16_t* __restrict__ g, float* __restrict__ m,
+                                      float* __restrict__ v, uint16_t* __restrict__ snap, long n4, float lr_t,
+                                      float b1, float b2, float eps) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const uint2 gb = reinterpret_cast<const uint2*>(g)[i];
+    const float4 gg = make_float4(__uint_as_float(gb.x << 16), __uint_as_float(gb.x & 0xffff0000u),
+                                  __uint_as_float(gb.y << 16), __uint_as_float(gb.y & 0xffff0000u));
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+#define ADAM1(c)                                              \
+  {                                                           \
+    const float gr = gg.c;                                    \
+    mm.c = b1 * mm.c + (1.f - b1) * gr;                       \
+    vv.c = b2 * vv.c + (1.f - b2) * gr * gr;                  \
+    pp.c -= lr_t * mm.c / (sqrtf(vv.c) + eps);                \
+  }
+    ADAM1(x) ADAM1(y) ADAM1(z) ADAM1(w)
+#undef ADAM1
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    reinterpret_cast<uint2*>(snap)[i] = make_uint2(pack2(pp.x, pp.y), pack2(pp.z, pp.w));
+  }
+}
+
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ mom, long n4,
                            float lr, float mu, float wd, int nesterov, float gs, const float* __restrict__ hs) {
   if (hs) lr = hs[2];
@@ -104,6 +134,14 @@ const char* sgd_launch(float* p, const float* g, float* mom, long n, float lr, f
 const char* scale_launch(float* x, long n, float a, hipStream_t s) {
   hipLaunchKernelGGL(scale_kernel, dim3(grid_of(n)), dim3(256), 0, s, x, n, a);
   LAUNCH_RET
+}
+const char* adam_bf16_wire_launch(float* p, const uint16_t* g, float* m, float* v, uint16_t* snap, long n, float lr_t,
+                                  float b1, float b2, float eps, hipStream_t s) {
+  if (n % 4) return "adam_bf16_wire: n must be a multiple of 4";
+  hipLaunchKernelGGL(adam_bf16_wire_kernel, dim3(grid_of(n / 4)), dim3(256), 0, s, p, g, m, v, snap, n / 4, lr_t, b1,
+                     b2, eps);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 const char* cast_bf16_launch(const float* x, uint16_t* y, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_of(n)), dim3(256), 0, s, x, y, n);

@@ -31,6 +31,30 @@ const char* range_copy_launch(const float* src, float* dst, const RangeRow* rows
 }
 
 
+// bf16 wire of the parameter server (--ps-wire bf16): the same range gather / scatter with the
+// precision change fused in -- gather: flat fp32 -> packed bf16 (round to nearest even, the
+// worker's gradient push into a bf16 mailbox); scatter: packed bf16 -> flat fp32 (the pulled
+// bf16 shard snapshot into the worker's fp32 parameters).
+__global__ void range_copy_cvt_kernel(const void* __restrict__ src, void* __restrict__ dst,
+                                      const RangeRow* __restrict__ rows, int scatter) {
+  const RangeRow r = rows[blockIdx.y];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < r.len; i += (long)gridDim.x * blockDim.x) {
+    if (scatter)
+      static_cast<float*>(dst)[r.flat + i] = bf2f(static_cast<const uint16_t*>(src)[r.packed + i]);
+    else
+      static_cast<uint16_t*>(dst)[r.packed + i] = f2bf(static_cast<const float*>(src)[r.flat + i]);
+  }
+}
+
+const char* range_copy_cvt_launch(const void* src, void* dst, const RangeRow* rows_dev, int nrows, int scatter,
+                                  hipStream_t s) {
+  if (nrows <= 0) return nullptr;
+  if (nrows > 65535) return "range_copy_cvt: too many ranges";
+  hipLaunchKernelGGL(range_copy_cvt_kernel, dim3(32, nrows), dim3(256), 0, s, src, dst, rows_dev, scatter);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
 // ------------------------------------------------------------------------------ comm proxy
 // Stand-in for one RCCL ring all-reduce's footprint on THIS GPU (bench.py --comm-proxy): a 1-GPU
 // model of what a multi-GPU backward shares its CUs with.  `nch` workgroups (RCCL's channel

@@ -44,6 +44,7 @@ struct PSCtrl {
   int64_t n;            // shard elements (padded to a multiple of 4)
   int32_t workers;
   int32_t gpu;          // 1: data in GPU memory (IPC), 0: shared memory
+  int32_t wire;         // element type of mailboxes / snapshots: 0 fp32, 1 bf16 (GPU roles only)
   std::atomic<int32_t> ready;
   std::atomic<uint64_t> updates;
   unsigned char mailbox_handle[kIpcHandleBytes];

@@ -25,6 +25,10 @@
 //     buffers in shared memory and a host Adam loop.
 //   * The request / completion protocol and the service loop are in runtime/ps_protocol.h
 //     (torch-free; ThreadSanitizer drives it natively: csrc/tests/ps_protocol_test.cpp).
+//   * Wire precision (`wire` = 1, --ps-wire bf16): the worker's pack kernel rounds its gradient
+//     ranges to bf16 into a bf16 mailbox, the PS's fused Adam reads them and also writes a bf16
+//     snapshot of the updated shard, and the pull copies that snapshot: half the xGMI bytes in
+//     both directions; the PS keeps fp32 master weights and Adam slots.
 //   * Failure handling: a worker that dies never bumps its sequence number again (its
 //     half-written mailbox is never applied); the service loop treats a vanished worker pid
 //     as finished, and the coordinator re-queues its closure (parameter_server.py).  A worker
@@ -114,9 +118,11 @@ struct Shm {
 // ------------------------------------------------------------------------------ server
 class PSServer {
  public:
-  PSServer(const std::string& job, int p, Tensor init, int workers, int device, double b1, double b2, double eps)
-      : p_(p), W_(workers), dev_(device), b1_(b1), b2_(b2), eps_(eps) {
+  PSServer(const std::string& job, int p, Tensor init, int workers, int device, double b1, double b2, double eps,
+           int wire)
+      : p_(p), W_(workers), dev_(device), wire_(wire), b1_(b1), b2_(b2), eps_(eps) {
     TORCH_CHECK(workers >= 1 && workers <= kMaxWorkers, "pddl ps: 1..64 workers");
+    TORCH_CHECK(wire == 0 || (wire == 1 && device >= 0), "pddl ps: the bf16 wire needs GPU roles");
     TORCH_CHECK(init.scalar_type() == torch::kFloat32 && init.dim() == 1, "pddl ps: init must be a flat fp32 shard");
     n_real_ = init.numel();
     n_ = (n_real_ + 3) / 4 * 4;
@@ -126,6 +132,8 @@ class PSServer {
     ctrl_->n = n_;
     ctrl_->workers = W_;
     ctrl_->gpu = dev_ >= 0;
+    ctrl_->wire = wire_;
+    const size_t esz = wire_ ? 2 : 4;
     Tensor host = init.to(torch::kCPU).contiguous();
     if (dev_ >= 0) {
       hck(hipSetDevice(dev_), "set device");
@@ -135,8 +143,12 @@ class PSServer {
       v_ = params_ + 2 * n_;
       hck(hipMemset(params_, 0, 3 * n_ * sizeof(float)), "memset");
       hck(hipMemcpy(params_, host.data_ptr<float>(), n_real_ * sizeof(float), hipMemcpyHostToDevice), "init copy");
-      hck(hipMalloc(&mailbox_, (size_t)W_ * n_ * sizeof(float)), "malloc mailbox");
-      hck(hipMemset(mailbox_, 0, (size_t)W_ * n_ * sizeof(float)), "memset mailbox");
+      hck(hipMalloc(&mailbox_, (size_t)W_ * n_ * esz), "malloc mailbox");
+      hck(hipMemset(mailbox_, 0, (size_t)W_ * n_ * esz), "memset mailbox");
+      if (wire_) {   // the bf16 snapshot the pulls copy, kept current by every update
+        hck(hipMalloc(&snap_, n_ * sizeof(uint16_t)), "malloc snapshot");
+        kck(pddl::cast_bf16_launch(params_, snap_, n_, nullptr), "snapshot cast");
+      }
       hipIpcMemHandle_t mh;
       hck(hipIpcGetMemHandle(&mh, mailbox_), "ipc handle");
       std::memcpy(ctrl_->mailbox_handle, &mh, sizeof(mh));
@@ -152,7 +164,7 @@ class PSServer {
       params_ = host_.data(); m_ = params_ + n_; v_ = params_ + 2 * n_;
       mb_shm_.create(seg_name(job, p, "_mb"), (size_t)W_ * n_ * sizeof(float));
       rx_shm_.create(seg_name(job, p, "_rx"), (size_t)W_ * n_ * sizeof(float));
-      mailbox_ = static_cast<float*>(mb_shm_.ptr);
+      mailbox_ = mb_shm_.ptr;
     }
     ctrl_->ready.store(1, std::memory_order_release);
   }
@@ -161,10 +173,11 @@ class PSServer {
     if (thr_.joinable()) thr_.join();
     if (dev_ >= 0) {
       hipSetDevice(dev_);
-      for (float* r : rx_ptr_) if (r) hipIpcCloseMemHandle(r);
+      for (void* r : rx_ptr_) if (r) hipIpcCloseMemHandle(r);
       for (auto e : done_ev_) if (e) hipEventDestroy(e);
       for (auto e : start_ev_) if (e) hipEventDestroy(e);
       if (mailbox_) hipFree(mailbox_);
+      if (snap_) hipFree(snap_);
       if (params_) hipFree(params_);
       if (stream_) hipStreamDestroy(stream_);
     }
@@ -204,13 +217,18 @@ class PSServer {
   void apply_adam(int w, float lr) {
     ++t_;
     const double lr_t = lr * std::sqrt(1.0 - std::pow(b2_, t_)) / (1.0 - std::pow(b1_, t_));
-    const float* g = mailbox_ + (size_t)w * n_;
+    const float* g = static_cast<const float*>(mailbox_) + (size_t)w * n_;
     if (dev_ >= 0) {
       hck(hipEventRecord(start_ev_[w], stream_), "record start");
       started_[w] = true;
-      kck(pddl::adam_launch(params_, g, m_, v_, n_, (float)lr_t, (float)b1_, (float)b2_, (float)eps_, 1.f, nullptr,
-                            stream_),
-          "adam");
+      if (wire_)
+        kck(pddl::adam_bf16_wire_launch(params_, static_cast<const uint16_t*>(mailbox_) + (size_t)w * n_, m_, v_,
+                                        snap_, n_, (float)lr_t, (float)b1_, (float)b2_, (float)eps_, stream_),
+            "adam (bf16 wire)");
+      else
+        kck(pddl::adam_launch(params_, g, m_, v_, n_, (float)lr_t, (float)b1_, (float)b2_, (float)eps_, 1.f, nullptr,
+                              stream_),
+            "adam");
     } else {
       const float b1 = (float)b1_, b2 = (float)b2_, eps = (float)eps_, lt = (float)lr_t;
       for (int64_t i = 0; i < n_; ++i) {
@@ -229,11 +247,14 @@ class PSServer {
         hipIpcMemHandle_t h;
         std::memcpy(&h, s.rx_handle, sizeof(h));
         hck(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "open rx handle");
-        rx_ptr_[w] = static_cast<float*>(ptr);
+        rx_ptr_[w] = ptr;
       }
       if (!started_[w]) hck(hipEventRecord(start_ev_[w], stream_), "record start");   // (pull: copy only)
       started_[w] = false;
-      hck(hipMemcpyAsync(rx_ptr_[w], params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
+      if (wire_)
+        hck(hipMemcpyAsync(rx_ptr_[w], snap_, n_ * sizeof(uint16_t), hipMemcpyDeviceToDevice, stream_), "snapshot");
+      else
+        hck(hipMemcpyAsync(rx_ptr_[w], params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
       hck(hipEventRecord(done_ev_[w], stream_), "record done");
     } else {
       std::memcpy(static_cast<float*>(rx_shm_.ptr) + (size_t)w * n_, params_, n_ * sizeof(float));
@@ -274,7 +295,7 @@ class PSServer {
     }
   }
 
-  int p_, W_, dev_;
+  int p_, W_, dev_, wire_;
   double b1_, b2_, eps_;
   int64_t n_real_ = 0, n_ = 0, t_ = 0;
   Shm ctrl_shm_, mb_shm_, rx_shm_;
@@ -282,9 +303,10 @@ class PSServer {
   float* params_ = nullptr;
   float* m_ = nullptr;
   float* v_ = nullptr;
-  float* mailbox_ = nullptr;
+  void* mailbox_ = nullptr;            // [W][n] fp32 or (bf16 wire) bf16
+  uint16_t* snap_ = nullptr;           // bf16 wire: bf16 copy of params_
   std::vector<float> host_;
-  std::vector<float*> rx_ptr_;
+  std::vector<void*> rx_ptr_;
   std::vector<hipEvent_t> done_ev_;   // per worker: its request's Adam + snapshot copy finished
   std::vector<hipEvent_t> start_ev_;  // per worker: its request's work started (timing)
   std::vector<char> started_ = std::vector<char>(pddl::ps::kMaxWorkers, 0);
@@ -303,9 +325,10 @@ struct Remote {
   Shm ctrl_shm, mb_shm, rx_shm;
   PSCtrl* ctrl = nullptr;
   int64_t n = 0;
-  float* mailbox = nullptr;   // this worker's slot (peer GPU memory or shared memory)
+  int wire = 0;               // 1: bf16 mailbox / receive buffer
+  void* mailbox = nullptr;    // this worker's slot (peer GPU memory or shared memory)
   void* mb_base = nullptr;    // IPC mapping base (GPU)
-  float* rx = nullptr;        // this worker's receive buffer
+  void* rx = nullptr;         // this worker's receive buffer
   Tensor rows;                // device RangeRow table (GPU) / host (CPU)
   std::vector<pddl::RangeRow> host_rows;
   uint64_t seq = 0;
@@ -334,6 +357,8 @@ class PSClient {
       TORCH_CHECK(r.ctrl->magic == kMagic && w_ < r.ctrl->workers, "pddl ps client: bad control segment");
       TORCH_CHECK((r.ctrl->gpu != 0) == (dev_ >= 0), "pddl ps client: PS and worker must both be GPU or both CPU");
       r.n = r.ctrl->n;
+      r.wire = r.ctrl->wire;
+      const size_t esz = r.wire ? 2 : 4;
       int64_t packed = 0;
       for (auto& fr : ranges[p]) {
         TORCH_CHECK(fr.first >= 0 && fr.second >= 0, "pddl ps client: negative range");
@@ -348,12 +373,12 @@ class PSClient {
         hipIpcMemHandle_t mh;
         std::memcpy(&mh, r.ctrl->mailbox_handle, sizeof(mh));
         hck(hipIpcOpenMemHandle(&r.mb_base, mh, hipIpcMemLazyEnablePeerAccess), "open mailbox");
-        r.mailbox = static_cast<float*>(r.mb_base) + (size_t)w_ * r.n;
+        r.mailbox = static_cast<char*>(r.mb_base) + (size_t)w_ * r.n * esz;
         void* rx = nullptr;
-        hck(hipMalloc(&rx, r.n * sizeof(float)), "malloc rx");
-        hck(hipMemset(rx, 0, r.n * sizeof(float)), "memset rx");
+        hck(hipMalloc(&rx, r.n * esz), "malloc rx");
+        hck(hipMemset(rx, 0, r.n * esz), "memset rx");
         hck(hipDeviceSynchronize(), "rx sync");
-        r.rx = static_cast<float*>(rx);
+        r.rx = rx;
         hipIpcMemHandle_t rh;
         hck(hipIpcGetMemHandle(&rh, r.rx), "rx handle");
         std::memcpy(s.rx_handle, &rh, sizeof(rh));
@@ -418,14 +443,20 @@ class PSClient {
       WorkerSlot& s = r.ctrl->slot[w_];
       if (push) {
         TORCH_CHECK(grads.is_contiguous() && grads.scalar_type() == torch::kFloat32, "pddl ps: flat fp32 grads");
-        if (dev_ >= 0) {
-          kck(pddl::range_copy_launch(grads.data_ptr<float>(), r.mailbox,
+        if (dev_ >= 0 && r.wire) {
+          kck(pddl::range_copy_cvt_launch(grads.data_ptr<float>(), r.mailbox,
+                                          reinterpret_cast<const pddl::RangeRow*>(r.rows.data_ptr()),
+                                          (int)r.host_rows.size(), 0, st),
+              "pack (bf16)");
+        } else if (dev_ >= 0) {
+          kck(pddl::range_copy_launch(grads.data_ptr<float>(), static_cast<float*>(r.mailbox),
                                       reinterpret_cast<const pddl::RangeRow*>(r.rows.data_ptr()),
                                       (int)r.host_rows.size(), 0, st),
               "pack");
         } else {
           const float* g = grads.data_ptr<float>();
-          for (auto& row : r.host_rows) std::memcpy(r.mailbox + row.packed, g + row.flat, row.len * sizeof(float));
+          float* mb = static_cast<float*>(r.mailbox);
+          for (auto& row : r.host_rows) std::memcpy(mb + row.packed, g + row.flat, row.len * sizeof(float));
         }
       }
     }
@@ -454,14 +485,20 @@ class PSClient {
     for (size_t p = 0; p < rem_.size(); ++p) {
       Remote& r = rem_[p];
       wait_done(r, (int)p);
-      if (dev_ >= 0) {
-        kck(pddl::range_copy_launch(r.rx, params.data_ptr<float>(),
+      if (dev_ >= 0 && r.wire) {
+        kck(pddl::range_copy_cvt_launch(r.rx, params.data_ptr<float>(),
+                                        reinterpret_cast<const pddl::RangeRow*>(r.rows.data_ptr()),
+                                        (int)r.host_rows.size(), 1, st),
+            "unpack (bf16)");
+      } else if (dev_ >= 0) {
+        kck(pddl::range_copy_launch(static_cast<const float*>(r.rx), params.data_ptr<float>(),
                                     reinterpret_cast<const pddl::RangeRow*>(r.rows.data_ptr()),
                                     (int)r.host_rows.size(), 1, st),
             "unpack");
       } else {
         float* pp = params.data_ptr<float>();
-        for (auto& row : r.host_rows) std::memcpy(pp + row.flat, r.rx + row.packed, row.len * sizeof(float));
+        const float* rx = static_cast<const float*>(r.rx);
+        for (auto& row : r.host_rows) std::memcpy(pp + row.flat, rx + row.packed, row.len * sizeof(float));
       }
     }
   }
@@ -541,9 +578,9 @@ class PSClient {
 
 void register_ps(py::module& m) {
   py::class_<PSServer, std::shared_ptr<PSServer>>(m, "PSServer")
-      .def(py::init<const std::string&, int, Tensor, int, int, double, double, double>(), py::arg("job"),
+      .def(py::init<const std::string&, int, Tensor, int, int, double, double, double, int>(), py::arg("job"),
            py::arg("ps_index"), py::arg("init_shard"), py::arg("workers"), py::arg("device"), py::arg("beta1"),
-           py::arg("beta2"), py::arg("eps"))
+           py::arg("beta2"), py::arg("eps"), py::arg("wire") = 0)
       .def("start", &PSServer::start)
       .def("join", &PSServer::join, py::call_guard<py::gil_scoped_release>())
       .def("params", &PSServer::params)

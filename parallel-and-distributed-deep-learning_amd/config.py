@@ -65,6 +65,7 @@ class TrainConfig:
     min_shard_bytes: int = 256 << 10               # MinSizePartitioner (ps.py:77)
     shard_by: str = "batch"                        # hvd: batch-then-shard (hvd.py:77-78); mwms: element DATA
     ps_overlap: bool = True                        # PS: a worker's push/pull round trip overlaps its next step
+    ps_wire: str = "fp32"                          # PS: gradient push / parameter pull element type (bf16 halves xGMI bytes)
     # device / output
     device: str = "auto"                           # auto | cpu | cuda
     save: bool = True
@@ -156,6 +157,8 @@ def add_cli_args(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--no-graphs", action="store_false", dest="graphs", default=None)
     a("--roctx", action="store_true", default=None)
     a("--verbose", type=int)
+    a("--ps-wire", choices=["fp32", "bf16"], dest="ps_wire",
+      help="PS: element type of the gradient push and the parameter pull (GPU roles)")
     a("--ps-sync", action="store_false", dest="ps_overlap", default=None,
       help="PS: block on every push/pull round trip (no overlap with the next step)")
     return ap

@@ -48,6 +48,7 @@ class HipEngine:
     FUSE_PROJ_OK = True     # projection blocks: conv3 + shortcut conv as one dual-source GEMM
     FUSE_BWD_OK = True      # stage-2/3 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
     FUSE_STEM_OK = True     # stem conv + BN + ReLU + max-pool forward in one launch (stem.hip)
+    TWO_STREAM_MAX_BATCH = 1024
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
@@ -115,6 +116,13 @@ class HipEngine:
         # head), this engine's own (N.splitk_use makes it current for the launching thread)
         self.splitk_ws = torch.empty(self.N.splitk_default_floats(self.device.index or 0), dtype=torch.float32,
                                      device=dev)
+        # two-stream backward (small batches, where single kernels underfill the chip): the weight
+        # gradients run on a side stream concurrently with the data-gradient chain.
+        # PDDL_TWO_STREAM=1 / 0 forces it; default on up to TWO_STREAM_MAX_BATCH images.
+        ts = os.environ.get("PDDL_TWO_STREAM", "auto")
+        self.two_stream = (batch <= self.TWO_STREAM_MAX_BATCH) if ts == "auto" else ts == "1"
+        self.side = torch.cuda.Stream(dev) if self.two_stream and dev.type == "cuda" else None
+        self._pending, self._last_side = {}, None
 
     # ------------------------------------------------------------------ tables
     def _build_weight_tables(self):
@@ -456,6 +464,44 @@ class HipEngine:
         lab.copy_(labels, non_blocking=True)
         return lab
 
+    # ------------------------------------------------------------------ two-stream backward
+    def _side_run(self, fn, *args, reads=()):
+        """Launch a weight-gradient kernel on the side stream, ordered after everything enqueued
+        on the compute stream so far; `reads` names the gradient buffers it reads, which the
+        compute stream must not overwrite before it is done (see _before_write)."""
+        if self.side is None:
+            fn(*args)
+            return
+        main = torch.cuda.current_stream(self.device)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            fn(*args)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        for r in reads:
+            self._pending[r] = done
+        self._last_side = done
+
+    def _before_write(self, *bufs):
+        """The compute stream is about to overwrite these gradient buffers: wait for the side
+        stream's last reader of each."""
+        if self.side is None:
+            return
+        main = torch.cuda.current_stream(self.device)
+        for b in bufs:
+            ev = self._pending.pop(b, None)
+            if ev is not None:
+                main.wait_event(ev)
+
+    def _join_side(self):
+        if self.side is None or self._last_side is None:
+            return
+        torch.cuda.current_stream(self.device).wait_event(self._last_side)
+        self._pending.clear()
+        self._last_side = None
+
     # ------------------------------------------------------------------ train step
     def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0),
                          bucket_cb: Optional[Callable[[int], None]] = None, buckets=None):
@@ -475,17 +521,20 @@ class HipEngine:
         # bucket readiness tracking (kernels region is filled in layout order)
         bks = buckets if buckets is not None else []
         nb = [0]
+        self._pending, self._last_side = {}, None
+        W = self._side_run
 
         def done_upto(off):
             while bucket_cb is not None and nb[0] < len(bks) - 1 and bks[nb[0]][1] <= off:
+                self._join_side()   # the bucket's weight gradients ran on the side stream
                 bucket_cb(nb[0])
                 nb[0] += 1
 
         # ---- head
         pooled = self.pooled[:B]
         chd = self.ch["dense"]
-        N.wgrad(pooled.view(B, 1, 1, 2048), 1, 1, 1, 1, 1, 0, 1, 1, dl, None, 0,
-                self._gview("dense", self.num_classes, 2048), 2048, 0)
+        W(N.wgrad, pooled.view(B, 1, 1, 2048), 1, 1, 1, 1, 1, 0, 1, 1, dl, None, 0,
+          self._gview("dense", self.num_classes, 2048), 2048, 0)
         N.colsum(dl, self.num_classes, self.colsum[chd:])
         dpooled = self.dpooled[:B]
         N.igemm(dl.view(B, 1, 1, self.ncls_pad), None, 1, 1, 1, 1, 1, 0, 1, 1,
@@ -502,6 +551,7 @@ class HipEngine:
 
         def part(layer):
             return cp[coffs[layer]:]
+        self._before_write("gbuf0")
         N.gap_bwd(dpooled, x5, gout, part(blocks[-1].convs["3"].name))
         s2 = self._s2_fed()
         # ---- blocks (column sums of every produced gradient are fused into its producer)
@@ -521,8 +571,10 @@ class HipEngine:
             cs_in = part(blocks[bi - 1].convs["3"].name) if bi > 0 else None
             y1, y2 = a["y1"][:B], a["y2"][:B]
             gout = (self.s2full[bi] if bi in s2 else self.gbuf[cur])[: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
+            gout_n = f"s2f{bi}" if bi in s2 else f"gbuf{cur}"
             c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
             g2 = (self.s2g2full[bi] if bi in s2 else self.g2buf)[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            g2_n = f"s2g2f{bi}" if bi in s2 else "g2"
             if bi in s2:
                 # gout is zero off the stride-2 grid (the next block reads only even rows /
                 # columns); its compact copy `gc` came from that block's dgrad epilogue
@@ -530,45 +582,61 @@ class HipEngine:
                 gc = self.gcbuf[: B * Hc * Hc * 4 * f].view(B, Hc, Hc, 4 * f)
                 g2c = self.g2cbuf[: B * Hc * Hc * f].view(B, Hc, Hc, f)
                 if self._bwd_fused_s2(bi, b, s2):   # one read of gc: data + weight gradient
+                    self._before_write(g2_n, "g2c")
                     N.bwd1x1(gc, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f), g2c)
                 else:
-                    N.wgrad(y2, Ho, Ho, 1, 1, 2, 0, Hc, Hc, gc, None, 0, self._gview(c3n, 4 * f, f), f, 0)
+                    W(N.wgrad, y2, Ho, Ho, 1, 1, 2, 0, Hc, Hc, gc, None, 0, self._gview(c3n, 4 * f, f), f, 0,
+                      reads=("gc",))
+                    self._before_write(g2_n, "g2c")
                     N.igemm(gc, None, Hc, Hc, 1, 1, 1, 0, Hc, Hc, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
                             None, g2, 0, g2c, 0, 0, 2, Ho, Ho, part(c2n), None)
-                N.wgrad(y1, Ho, Ho, 3, 3, 2, 1, Hc, Hc, g2c, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
+                W(N.wgrad, y1, Ho, Ho, 3, 3, 2, 1, Hc, Hc, g2c, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0,
+                  reads=("g2c",))
             elif self._bwd_fused(bi, b, s2):
                 # conv3: data and weight gradient from one read of gout
+                self._before_write(g2_n)
                 N.bwd1x1(gout, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f))
-                N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
+                W(N.wgrad, y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0,
+                  reads=(g2_n,))
             else:
                 # conv3
-                N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0)
+                W(N.wgrad, y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0,
+                  reads=(gout_n,))
+                self._before_write(g2_n)
                 N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
                         None, g2, 0, None, 0, 0, 0, 0, 0, part(c2n), None)
                 # conv2 (3x3)
-                N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0)
+                W(N.wgrad, y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0,
+                  reads=(g2_n,))
             g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            self._before_write("g1")
             N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1m, None,
                     g1, 0, None, 0, 0, 0, 0, 0, part(c1n), None)
             # conv1 (+ conv0)
             nxt = 1 - cur
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+            gx_n = [f"gbuf{nxt}"]
             if b.proj:
-                N.wgrad(x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0)
-                N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
+                W(N.wgrad, x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0,
+                  reads=("g1", gout_n))
+                W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
                 gxc, up2 = None, 1 if b.stride == 2 else 0
                 if bi - 1 in s2:   # compact copy for the previous block's stride-2-grid passes
                     gxc = self.gcbuf[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
                     # grid positions only, into the pre-zeroed full-resolution buffer (saves the
                     # 3/4 zero-fill writes: conv3_block1 c1 dgrad 942 -> 681 us at b1024)
                     gx = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin)
+                    gx_n = [f"s2f{bi - 1}", "gc"]
                     up2 = 2
+                self._before_write(*gx_n)
                 N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, 5 * f), 1, None, None, None,
                         mask_in, None, gx, 0, gxc, 0, 0, up2, H, H, cs_in, None)
                 last = L.entry(b.convs["0"].name, "kernel")
             else:
-                N.wgrad(x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0)
-                N.wgrad_finalize(self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
+                W(N.wgrad, x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0,
+                  reads=("g1",))
+                W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
+                self._before_write(*gx_n)
                 N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, f), 1, None, None, None,
                         mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0, cs_in, None)
                 last = L.entry(c1n, "kernel")
@@ -579,10 +647,12 @@ class HipEngine:
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
         gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
         s = L.stem
+        self._before_write(f"gbuf{1 - cur}")
         N.maxpool_bwd(gpool, self.pidx[:B], None, gc1, part(s.name))
-        N.wgrad(self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
-        N.stem_wgrad_fold(self.stem_dw2, self._gview(s.name, 64, 147), 64)
-        N.wgrad_finalize(self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)
+        W(N.wgrad, self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
+        W(N.stem_wgrad_fold, self.stem_dw2, self._gview(s.name, 64, 147), 64)
+        W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)
+        self._join_side()
         done_upto(L.kernels_end)
         N.colsum_reduce(cp, ctab, cn, self.colsum)
         N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)

@@ -405,8 +405,9 @@ class NativePSServer(PSServer):
         cfg = cl.cfg
         shard = _gather(init_params, cl.ranges[cl.rank]).contiguous()
         dev = cl.device.index if cl.device.type == "cuda" else -1
+        wire = 1 if getattr(cfg, "ps_wire", "fp32") == "bf16" and dev >= 0 else 0
         self.srv = require_native().PSServer(cl.job, cl.rank, shard, cl.num_workers, dev, cfg.beta1, cfg.beta2,
-                                             cfg.adam_eps)
+                                             cfg.adam_eps, wire)
         self.updates = 0
         self.dead = set()
 

@@ -284,3 +284,39 @@ def test_fused_conv3_backward_matches_unfused(monkeypatch):
     (l1, g1), (l0, g0) = res
     assert abs(l1 - l0) < 1e-4 * abs(l0)
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_two_stream_backward_matches_one_stream(monkeypatch, graphed):
+    """Small-batch backward with the weight gradients on a side stream (PDDL_TWO_STREAM=1, the
+    default up to 1024 images) against the single-stream schedule: same loss and gradients to
+    fp32-atomic order, eager and captured in a HIP graph (the side stream forks from and joins
+    the capture)."""
+    from pddl.models.engine import HipEngine
+    from pddl.models.resnet50 import ParamLayout
+    from pddl.train.graph import GraphedTrainStep
+    from pddl.train.optim import make_optimizer
+    L = ParamLayout()
+    B = 8
+    img = torch.randint(0, 256, (B, 112, 112, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(3)).cuda()
+    lab = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(4)).cuda()
+    flips = torch.zeros(B, dtype=torch.uint8, device="cuda")
+    res = []
+    for two in ("1", "0"):
+        monkeypatch.setenv("PDDL_TWO_STREAM", two)
+        he = HipEngine(L, B, crop=112, image_size=112)
+        assert he.two_stream == (two == "1")
+        he.init(seed=7)
+        if graphed:
+            opt = make_optimizer("adam", he, lr=1e-3)
+            gs = GraphedTrainStep(he, opt, B, (112, 112), 1.0 / B)
+            for _ in range(3):
+                st = gs(img, lab, flips, (0, 0))
+            res.append((st[0].item(), he.params.clone()))
+        else:
+            st = he.forward_backward(img, lab, 1.0 / B)
+            torch.cuda.synchronize()
+            res.append((st[0].item(), he.grads.clone()))
+    (l1, g1), (l0, g0) = res
+    assert abs(l1 - l0) <= 1e-3 * abs(l0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < (2e-3 if graphed else 1e-3)
