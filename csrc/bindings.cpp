@@ -491,6 +491,25 @@ void stem_pool_fwd(Tensor x2, Tensor w, Tensor scale, Tensor shift, Tensor pool,
   p.PB = (int)pool_rows;
   ok(pddl::stem_pool_fwd_launch(p, cur_stream()), "stem_pool_fwd");
 }
+// Fused stem backward: gpool / idx [B,H2,W2,64], x2 [B,Hs,Ws,16] -> dw [64,256] fp32 (added),
+// colsum partial rows [stem_pool_bwd_partial_rows, 64].
+void stem_pool_bwd(Tensor x2, Tensor gpool, Tensor idx, Tensor dw, Tensor colsum, int64_t pool_rows) {
+  PCHECK(x2.dim() == 4 && x2.size(3) == 16 && x2.is_contiguous(), "stem_pool_bwd: x2 [B,Hs,Ws,16] contiguous");
+  PCHECK(gpool.dim() == 4 && gpool.size(3) == 64 && gpool.is_contiguous() && gpool.size(0) == x2.size(0),
+         "stem_pool_bwd: gpool [B,H2,W2,64] contiguous");
+  PCHECK(idx.scalar_type() == torch::kUInt8 && idx.is_contiguous() && idx.numel() == gpool.numel(),
+         "stem_pool_bwd: idx uint8 like gpool");
+  PCHECK(dw.is_contiguous() && dw.numel() >= 64 * 256, "stem_pool_bwd: dw [64,256] fp32");
+  pddl::StemPoolBwdParams p{};
+  p.x2 = bfp(x2); p.gpool = bfp(gpool); p.idx = idx.data_ptr<uint8_t>(); p.dw = f32p(dw);
+  p.B = (int)x2.size(0); p.Hs = (int)x2.size(1); p.Ws = (int)x2.size(2);
+  p.H1 = p.Hs - 3; p.W1 = p.Ws - 3; p.H2 = (int)gpool.size(1); p.W2 = (int)gpool.size(2);
+  p.PB = (int)pool_rows;
+  PCHECK(colsum.numel() >= (int64_t)pddl::stem_pool_bwd_partial_rows(p.B, p.H2, p.PB) * 64,
+         "stem_pool_bwd: colsum needs stem_pool_bwd_partial_rows x 64 floats");
+  p.colsum = f32p(colsum);
+  ok(pddl::stem_pool_bwd_launch(p, cur_stream()), "stem_pool_bwd");
+}
 void maxpool_bwd(Tensor gy, Tensor idx, OptT xmask, Tensor gx, OptT colsum) {
   ok(pddl::maxpool_bwd_launch(bfp(gy), idx.data_ptr<uint8_t>(), obfp(xmask), bfpm(gx), (int)gx.size(0),
                               (int)gx.size(1), (int)gx.size(2), (int)gx.size(3), (int)gy.size(1), (int)gy.size(2),
@@ -680,6 +699,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_s2d", &stem_s2d, REL);
   m.def("stem_wgrad_fold", &stem_wgrad_fold, REL);
   m.def("maxpool_fwd", &maxpool_fwd, REL);
+  m.def("stem_pool_bwd", &stem_pool_bwd, REL, py::arg("x2"), py::arg("gpool"), py::arg("idx"), py::arg("dw"),
+        py::arg("colsum"), py::arg("pool_rows") = 0);
+  m.def("stem_pool_bwd_partial_rows", [](int B, int H2, int PB) { return pddl::stem_pool_bwd_partial_rows(B, H2, PB); },
+        py::arg("B"), py::arg("H2"), py::arg("pool_rows") = 0);
   m.def("stem_pool_fwd", &stem_pool_fwd, REL, py::arg("x2"), py::arg("w"), py::arg("scale"), py::arg("shift"),
         py::arg("pool"), py::arg("idx"), py::arg("bits") = py::none(), py::arg("pool_rows") = 0);
   m.def("maxpool_bwd", &maxpool_bwd, REL);
@@ -711,6 +734,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm_pk") { TORCH_CHECK(v == 0 || (v >= 2 && v <= 4), "igemm_pk: 0 or ring depth 2-4"); pddl::g_igemm_pk = v; }
     else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
+    else if (which == "conv_f32") pddl::g_conv_f32_variant = v;
     else if (which == "igemm8_ragged") pddl::g_igemm8_ragged = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;

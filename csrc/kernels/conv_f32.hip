@@ -330,6 +330,329 @@ __global__ void __launch_bounds__(256) wgrad_f32_kernel(ConvF32Params p, int m_p
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// 128 x 128 tiles (round 4): 4 waves of 64 x 64 (4 x 4 MFMA tiles of 16x16x4 f32), reduction
+// step 16 floats, a 3-stage LDS pipeline fed by buffer LDS-DMA (16 B per lane straight from HBM /
+// L2 into LDS, no register staging).  The gather geometry of each tile row (image, top-left input
+// pixel, bitmask of its in-bounds taps) is computed once per tile; the k walk (tap r, s and
+// channel offset: C % 16 == 0, so a 16-wide step never crosses a tap) is scalar, so the k loop
+// carries no divides.  LDS images are chunk-major ([4 chunks][128 rows][16 B]: one DMA piece =
+// one chunk column of 64 rows), which makes every ds_read_b128 fragment read conflict-free.
+// The epilogue is the 64 x 64 kernel's, run over the tile's two 64-row halves through the
+// pipeline's LDS (partial column sums: one row per 64-row half, the same layout).
+namespace {
+constexpr int G_BM = 128, G_BN = 128, G_STAGE = 16384, G_CLD = G_BN + 4;
+
+__device__ __forceinline__ v4f mfma4v(const float4& a, const float4& b, v4f c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+  return c;
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * G_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int mt = (p.M + G_BM - 1) / G_BM, nt = (p.Cout + G_BN - 1) / G_BN;
+  const int wg = xcd_remap(blockIdx.x, mt * nt);
+  const int tn = wg % nt, tm = wg / nt;
+  const int m0 = tm * G_BM, n0 = tn * G_BN;
+  const int HoWo = p.Ho * p.Wo;
+  // descriptors: A from the first image of the tile (lane offsets span a few images at any batch)
+  const int n_first = fdiv(m0, p.mg_howo);
+  const long HWC = (long)p.H * p.W * p.C;
+  const __amdgpu_buffer_rsrc_t ra =
+      make_rsrc(p.x + n_first * HWC, (int)lmin((long)(p.N - n_first) * HWC * 4, 0x7fffffffL));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.w, (int)lmin((long)p.Cout * p.K * 4, 0x7fffffffL));
+  // this lane's two A rows (pieces rh = 0, 1: rows rh * 64 + lane) and two B rows, chunk = wave
+  uint32_t a_off[2], a_taps[2], b_off[2];
+#pragma unroll
+  for (int rh = 0; rh < 2; ++rh) {
+    const int m = m0 + rh * 64 + lane;
+    a_off[rh] = OOB_OFF;
+    a_taps[rh] = 0;
+    if (m < p.M) {
+      const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
+      const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
+      const int hi = ho * p.stride - p.pad, wi = wo * p.stride - p.pad;
+      const int pix = ((n - n_first) * p.H + hi) * p.W + wi;
+      a_off[rh] = (uint32_t)((pix * p.C + 4 * wave) * 4);
+      uint32_t t = 0;
+      for (int r = 0; r < p.R; ++r)
+        for (int s2 = 0; s2 < p.S; ++s2)
+          if ((unsigned)(hi + r) < (unsigned)p.H && (unsigned)(wi + s2) < (unsigned)p.W) t |= 1u << (r * p.S + s2);
+      a_taps[rh] = t;
+    }
+    const int nn = n0 + rh * 64 + lane;
+    b_off[rh] = nn < p.Cout ? (uint32_t)((nn * p.K + 4 * wave) * 4) : OOB_OFF;
+  }
+  int ld_r = 0, ld_s = 0, ld_c0 = 0, ld_k = 0;
+  auto load_step = [&](int buf) {
+    char* base = smem + buf * G_STAGE;
+    const int tap = ld_r * p.S + ld_s;
+    const int delta = ((ld_r * p.W + ld_s) * p.C + ld_c0) * 4;
+#pragma unroll
+    for (int rh = 0; rh < 2; ++rh) {
+      const uint32_t off = ((a_taps[rh] >> tap) & 1u) ? a_off[rh] + (uint32_t)delta : OOB_OFF;
+      buf_lds16(ra, LDS_PTR(base + wave * 2048 + rh * 1024), off, 0);
+    }
+#pragma unroll
+    for (int rh = 0; rh < 2; ++rh) buf_lds16(rb, LDS_PTR(base + 8192 + wave * 2048 + rh * 1024), b_off[rh], ld_k * 4);
+    ld_k += 16;
+    ld_c0 += 16;
+    if (ld_c0 == p.C) {
+      ld_c0 = 0;
+      if (++ld_s == p.S) { ld_s = 0; ++ld_r; }
+    }
+  };
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int KT = p.K / 16;
+  load_step(0);
+  if (KT > 1) load_step(1);
+  const int fr = lane & 15, g = lane >> 4;
+  const int a_rd = g * 2048 + (wm * 64 + fr) * 16, b_rd = 8192 + g * 2048 + (wn * 64 + fr) * 16;
+  for (int t = 0; t < KT; ++t) {
+    // step t landed (step t+1 stays in flight across the raw barrier), and every wave finished
+    // step t-1, whose buffer takes step t+2
+    if (t + 1 < KT) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int cur = t % 3;
+    if (t + 2 < KT) load_step((t + 2) % 3);
+    const char* st = smem + cur * G_STAGE;
+    float4 af[4], bf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const float4*>(st + a_rd + i * 256);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const float4*>(st + b_rd + j * 256);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma4v(af[i], bf[j], acc[i][j]);
+  }
+  __syncthreads();   // every fragment read done: the epilogue reuses the pipeline's LDS
+
+  float* Cs = reinterpret_cast<float*>(smem);
+  const int c4 = (tid & 31) * 4, col = n0 + c4;
+  const bool vec = col + 3 < p.Cout;
+  float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (col + e < p.Cout) {
+      if (p.epi == F32_EPI_FWD) { sc[e] = p.scale[col + e]; sh[e] = p.shift[col + e]; }
+      else if (p.epi == F32_EPI_PLAIN && p.bias) sh[e] = p.bias[col + e];
+    }
+  }
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) Cs[(i * 16 + 4 * g + e) * G_CLD + wn * 64 + j * 16 + fr] = acc[i][j][e];
+    }
+    __syncthreads();
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int rl = (tid >> 5) + 8 * it, row = m0 + h * 64 + rl;
+      if (row >= p.M || col >= p.Cout) continue;
+      const float4 q = *reinterpret_cast<const float4*>(&Cs[rl * G_CLD + c4]);
+      float v[4] = {q.x, q.y, q.z, q.w};
+      long orow = row;
+      if (p.epi == F32_EPI_DGRAD && p.up2) {
+        const int nn = fdiv(row, p.mg_howo), rem = row - nn * HoWo, ii = fdiv(rem, p.mg_wo), jj = rem - ii * p.Wo;
+        orow = ((long)nn * p.Hf + 2 * ii) * p.Wf + 2 * jj;
+      }
+      const long o = orow * p.Cout + col;
+      const long oa = p.up2 ? (long)row * p.Cout + col : o;
+      if (vec) {
+        if (p.epi == F32_EPI_FWD) {
+          float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (p.res) r = *reinterpret_cast<const float4*>(p.res + o);
+          const float rv[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = v[e] * sc[e] + sh[e] + rv[e];
+            if (p.relu) v[e] = fmaxf(v[e], 0.f);
+          }
+        } else if (p.epi == F32_EPI_DGRAD) {
+          float4 a = make_float4(0.f, 0.f, 0.f, 0.f), mk = make_float4(1.f, 1.f, 1.f, 1.f);
+          if (p.add) a = *reinterpret_cast<const float4*>(p.add + oa);
+          if (p.mask) mk = *reinterpret_cast<const float4*>(p.mask + o);
+          const float av[4] = {a.x, a.y, a.z, a.w}, mv[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = mv[e] > 0.f ? v[e] + av[e] : 0.f;
+            cs[e] += v[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += sh[e];
+        }
+        *reinterpret_cast<float4*>(p.y + o) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (col + e >= p.Cout) break;
+          float x = v[e];
+          if (p.epi == F32_EPI_FWD) {
+            x = x * sc[e] + sh[e] + (p.res ? p.res[o + e] : 0.f);
+            if (p.relu) x = fmaxf(x, 0.f);
+          } else if (p.epi == F32_EPI_DGRAD) {
+            x = (!p.mask || p.mask[o + e] > 0.f) ? x + (p.add ? p.add[oa + e] : 0.f) : 0.f;
+            cs[e] += x;
+          } else {
+            x += sh[e];
+          }
+          p.y[o + e] = x;
+        }
+      }
+    }
+    if (p.epi == F32_EPI_DGRAD && p.colsum) {
+      // fold the 8 row groups of each 4-column group: lanes l, l + 32 of a wave, then the 4 waves
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
+      __syncthreads();
+      if (lane < 32) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Cs[wave * G_CLD + c4 + e] = cs[e];
+      }
+      __syncthreads();
+      if (tid < 32 && m0 + h * 64 < p.M) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = Cs[c4 + e] + Cs[G_CLD + c4 + e] + Cs[2 * G_CLD + c4 + e] + Cs[3 * G_CLD + c4 + e];
+          if (col + e < p.Cout) p.colsum[(long)(tm * 2 + h) * p.Cout + col + e] = t;
+        }
+      }
+    }
+    __syncthreads();   // (the next half overwrites Cs)
+  }
+}
+int g_conv_f32_variant = 1;   // 1: 128 x 128 LDS-DMA kernels where they apply (C % 16 == 0), 0: 64 x 64 only
+
+// Weight gradient on 128 (Cout) x 128 (K) tiles, reduction over m in steps of 16 rows, the same
+// 3-stage LDS-DMA pipeline.  Both operands arrive row-major ([m][n] / [m][k] rows of 128 floats,
+// one DMA piece = 2 m-rows, pieces padded by 64 B so the fragment reads spread over the banks) and
+// are read as single floats (ds_read_b32: the MFMA reduction index is m, which is the row).  The
+// k geometry of a lane's 16-byte chunk (tap r, s and channel) is fixed for the tile; the pixel
+// of its m-row is recomputed per step (magic-number division).  dW accumulates in registers over
+// the workgroup's m range and is added once with fp32 atomics.
+namespace {
+constexpr int W_PIECE = 1024 + 64, W_TILE = 8 * W_PIECE, W_STAGE = 2 * W_TILE;
+}
+__global__ void __launch_bounds__(256, 2) wgrad_f32_big_kernel(ConvF32Params p, int m_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * W_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tnn = (p.Cout + 127) / 128, tkk = (p.K + 127) / 128, ntiles = tnn * tkk;
+  const int splits = (p.M + m_per_split - 1) / m_per_split;
+  const int wg = xcd_remap(blockIdx.x, ntiles * splits);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int n0 = (tile % tnn) * 128, k0 = (tile / tnn) * 128;
+  const int mbeg = split * m_per_split, mend = min(p.M, mbeg + m_per_split);
+  const int nsteps = (mend - mbeg + 15) / 16;
+  if (nsteps <= 0) return;   // (block-uniform, before any barrier)
+  const int HoWo = p.Ho * p.Wo;
+  // descriptors over the whole tensors (offsets of one split stay below 2 GiB: the launcher
+  // bounds a split's span), rebased at the split's first image for x
+  const int n_first = fdiv(mbeg, p.mg_howo);
+  const long HWC = (long)p.H * p.W * p.C;
+  const __amdgpu_buffer_rsrc_t rx =
+      make_rsrc(p.x + n_first * HWC, (int)lmin((long)(p.N - n_first) * HWC * 4, 0x7fffffffL));
+  const __amdgpu_buffer_rsrc_t rg =
+      make_rsrc(p.y + (long)mbeg * p.Cout, (int)lmin((long)(mend - mbeg) * p.Cout * 4, 0x7fffffffL));
+  // this lane's chunk: 4 consecutive columns (n for the gradient, k for x) of m-row (lane >> 5)
+  // of every piece; each wave issues pieces 2 wave, 2 wave + 1 of both tiles
+  const int cc = (lane & 31) * 4;
+  const int gcol = n0 + cc;
+  const bool g_ok = gcol < p.Cout;   // (Cout % 4 == 0: checked by the launcher)
+  const int kq = k0 + cc;
+  const bool k_ok = kq < p.K;
+  int kr = 0, ks = 0, kc = 0;
+  if (k_ok) {
+    const int rs = kq / p.C;
+    kc = kq - rs * p.C;
+    kr = rs / p.S;
+    ks = rs - kr * p.S;
+  }
+  auto load_step = [&](int buf, int mb) {
+    char* base = smem + buf * W_STAGE;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int piece = 2 * wave + q;
+      const int m = mb + 2 * piece + (lane >> 5);
+      const bool ok = m < mend;
+      const uint32_t goff = (ok && g_ok) ? (uint32_t)(((m - mbeg) * p.Cout + gcol) * 4) : OOB_OFF;
+      buf_lds16(rg, LDS_PTR(base + piece * W_PIECE), goff, 0);
+      uint32_t xoff = OOB_OFF;
+      if (ok && k_ok) {
+        const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
+        const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
+        const int hi = ho * p.stride - p.pad + kr, wi = wo * p.stride - p.pad + ks;
+        if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+          xoff = (uint32_t)(((((n - n_first) * p.H + hi) * p.W + wi) * p.C + kc) * 4);
+      }
+      buf_lds16(rx, LDS_PTR(base + W_TILE + piece * W_PIECE), xoff, 0);
+    }
+  };
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  load_step(0, mbeg);
+  if (nsteps > 1) load_step(1, mbeg + 16);
+  const int fr = lane & 15, g = lane >> 4;
+  // fragment element e of lane (fr, g): m-row 4 g + e = piece 2 g + (e >> 1), half e & 1
+  const int a_rd = 2 * g * W_PIECE + (wm * 64 + fr) * 4, b_rd = W_TILE + 2 * g * W_PIECE + (wn * 64 + fr) * 4;
+  for (int t = 0; t < nsteps; ++t) {
+    if (t + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int cur = t % 3;
+    if (t + 2 < nsteps) load_step((t + 2) % 3, mbeg + (t + 2) * 16);
+    const char* st = smem + cur * W_STAGE;
+    float4 af[4], bf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* a = reinterpret_cast<const float*>(st + a_rd + i * 64);
+      af[i] = make_float4(a[0], a[128], a[W_PIECE / 4], a[W_PIECE / 4 + 128]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* b = reinterpret_cast<const float*>(st + b_rd + j * 64);
+      bf[j] = make_float4(b[0], b[128], b[W_PIECE / 4], b[W_PIECE / 4 + 128]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma4v(af[i], bf[j], acc[i][j]);
+  }
+  // dW[n][k] += D: lane holds D[n = 16 i + 4 g + e][k = 16 j + fr] of the wave's 64 x 64
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = k0 + wn * 64 + j * 16 + fr;
+    if (col >= p.K) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = n0 + wm * 64 + i * 16 + 4 * g + e;
+        if (row < p.Cout) unsafeAtomicAdd(p.dw + (long)row * p.K + col, acc[i][j][e]);
+      }
+  }
+}
+
 static const char* check_f32(const ConvF32Params& p) {
   if (p.M <= 0 || p.Cout <= 0 || p.K <= 0) return "conv_f32: empty problem";
   if (p.epi == F32_EPI_FWD && (!p.scale || !p.shift)) return "conv_f32: forward epilogue needs scale and shift";
@@ -346,6 +669,12 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (const char* e = check_f32(p)) return e;
   p.mg_howo = fdiv_magic(p.Ho * p.Wo);
   p.mg_wo = fdiv_magic(p.Wo);
+  if (g_conv_f32_variant == 1 && p.C % 16 == 0 && p.R * p.S <= 32) {
+    const int grid = ((p.M + G_BM - 1) / G_BM) * ((p.Cout + G_BN - 1) / G_BN);
+    hipLaunchKernelGGL(conv_f32_big_kernel, dim3(grid), dim3(256), 0, stream, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? nullptr : hipGetErrorString(e);
+  }
   const int grid = ((p.M + F_BM - 1) / F_BM) * ((p.Cout + F_BN - 1) / F_BN);
   if (p.C % 4 == 0) hipLaunchKernelGGL(conv_f32_kernel<true>, dim3(grid), dim3(256), 0, stream, p);
   else hipLaunchKernelGGL(conv_f32_kernel<false>, dim3(grid), dim3(256), 0, stream, p);
@@ -365,6 +694,17 @@ const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (splits < 1) splits = 1;
   int mps = ((p.M + splits - 1) / splits + F_BK - 1) / F_BK * F_BK;
   splits = (p.M + mps - 1) / mps;
+  if (g_conv_f32_variant == 1 && p.C % 4 == 0 && p.Cout % 4 == 0) {
+    const int bt = ((p.Cout + 127) / 128) * ((p.K + 127) / 128);
+    int bs = (3 * num_cus() + bt - 1) / bt;                  // ~3 workgroups per CU
+    const int bcap = (p.M + 511) / 512;                      // each reducing >= 512 rows of m
+    bs = bs > bcap ? bcap : (bs < 1 ? 1 : bs);
+    const int bmps = ((p.M + bs - 1) / bs + 15) / 16 * 16;
+    bs = (p.M + bmps - 1) / bmps;
+    hipLaunchKernelGGL(wgrad_f32_big_kernel, dim3(bt * bs), dim3(256), 0, stream, p, bmps);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? nullptr : hipGetErrorString(e);
+  }
   if (p.C % 4 == 0) hipLaunchKernelGGL(wgrad_f32_kernel<true>, dim3(ntiles * splits), dim3(256), 0, stream, p, mps);
   else hipLaunchKernelGGL(wgrad_f32_kernel<false>, dim3(ntiles * splits), dim3(256), 0, stream, p, mps);
   hipError_t e = hipGetLastError();

@@ -114,6 +114,7 @@ struct ConvF32Params {
 };
 enum { F32_EPI_PLAIN = 0, F32_EPI_FWD = 1, F32_EPI_DGRAD = 2 };
 const char* conv_f32_launch(ConvF32Params p, hipStream_t stream);
+extern int g_conv_f32_variant;   // 1: 128 x 128 LDS-DMA fp32 kernels (default), 0: the 64 x 64 register-staged ones
 const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream);
 // fp32 elementwise kernels of the fp32 engine (f32.hip)
 const char* maxpool_fwd_f32_launch(const float* x, float* y, uint8_t* idx, int B, int H, int W, int C, int Ho, int Wo,
@@ -159,6 +160,20 @@ struct StemPoolParams {
   int PB, nblk;
 };
 const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s);
+// Fused stem backward (stem.hip): max-pool backward into LDS + conv1 weight gradient
+// dw[64][256] += sum gc1^T im2col(x2) (fp32 atomics) + per-workgroup partial column sums of gc1
+// ([stem_pool_bwd_partial_rows][64]); conv1's output gradient never reaches HBM.
+struct StemPoolBwdParams {
+  const uint16_t* x2;                 // [B][Hs][Ws][16]
+  const uint16_t* gpool;              // [B][H2][W2][64] pool-output gradient
+  const uint8_t* idx;                 // [B][H2][W2][64] argmax taps of the forward
+  float* dw;                          // [64][256] s2d-domain weight gradient (accumulated)
+  float* colsum;                      // partial rows [grid][64]
+  int B, Hs, Ws, H1, W1, H2, W2;
+  int PB, nblk;
+};
+const char* stem_pool_bwd_launch(StemPoolBwdParams p, hipStream_t s);
+int stem_pool_bwd_partial_rows(int B, int H2, int PB);
 int stem_pool_lds_bytes(int Ws, int W1);
 
 const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, uint8_t* bits, int B, int H, int W, int C,

@@ -168,6 +168,227 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused stem backward: max-pool backward (route each pool-output gradient to its argmax tap) +
+// conv1 weight gradient dW2[co][k] = sum_px gc1[px][co] * im2col(x2)[px][k] (s2d domain, K = 256)
+// + the stem's per-channel gradient sums, in one launch.  conv1's output gradient gc1 (4.1 GB at
+// b2560) never reaches HBM: per conv row pair (2p, 2p+1) -- fed by pool rows p (taps r = 1, 2)
+// and p+1 (tap r = 0), so pool-row blocks partition the conv rows with no halo -- the workgroup
+// routes the pool gradient into an LDS image [2 rows][128 px][64 ch] (16-byte chunks XOR-swizzled
+// by the pixel), then runs the weight-gradient MFMAs with BOTH operands read back transposed by
+// ds_read_b64_tr_b16 (the reduction runs over pixels): A = gc1^T (co x px) from that image, B =
+// the im2col pixels from the ring of space-to-depth input rows.  Each wave owns 4 taps (64 of the
+// 256 k columns) x all 64 output channels in registers for the whole launch and adds them once at
+// the end with row-contiguous fp32 atomics.  Padding pixels of a 32-pixel step carry zero
+// gradient and read a clamped (finite) input pixel.
+__device__ __forceinline__ v4bf sp_tr_read(const uint8_t* p) {
+  v4bf r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
+  return r;
+}
+// gc1 image: pixel x of row a at a * 128 * 128 + x * 128; its 8-channel chunk c at (c ^ swz(x)) * 16
+__device__ __forceinline__ int gimg_off(int a, int x, int chunk) {
+  return a * 16384 + x * 128 + ((chunk ^ (x & 7) ^ ((x >> 3) & 1) * 4) << 4);
+}
+
+__global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_bwd_kernel(StemPoolBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int SLOT = p.Ws * 32;
+  uint8_t* ring = lds;
+  uint8_t* gimg = lds + 8 * SLOT;                              // 2 x 128 px x 128 B
+  float* csum = reinterpret_cast<float*>(gimg + 2 * 16384);   // [4 waves][64]
+  const int b = blockIdx.x / p.nblk;
+  const int blk = blockIdx.x - b * p.nblk;
+  const int P0 = blk * p.PB;
+  const int P1 = min(P0 + p.PB, p.H2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int W1 = p.W1;
+  const int nst = (W1 + 31) >> 5;                              // 32-pixel steps per conv row
+
+  // zero the image's padding pixels [W1, 32 nst) once (never written by the router)
+  for (int i = tid; i < 2 * (32 * nst - W1) * 8; i += SP_THREADS) {
+    const int a = i / ((32 * nst - W1) * 8), r = i - a * (32 * nst - W1) * 8;
+    const int x = W1 + (r >> 3), c = r & 7;
+    *reinterpret_cast<uint4*>(gimg + gimg_off(a, x, c)) = make_uint4(0, 0, 0, 0);
+  }
+  const uint4* x2b = reinterpret_cast<const uint4*>(p.x2 + (long)b * p.Hs * p.Ws * 16);
+  const int RCH = p.Ws * 2;
+  for (int yy = 2 * P0; yy < min(2 * P0 + 5, p.Hs); ++yy) {
+    uint4* dst = reinterpret_cast<uint4*>(ring + (yy & 7) * SLOT);
+    for (int c = tid; c < RCH; c += SP_THREADS) dst[c] = x2b[(long)yy * RCH + c];
+  }
+
+  v4f acc[4][4];   // [co16 tile][tap of this wave]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = (v4f){0.f, 0.f, 0.f, 0.f};
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // ds_read_b64_tr_b16: lane 4 q + pp of each 16-lane group addresses block row q, columns 4 pp .. +3
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const long gbase = (long)b * p.H2 * p.W2;
+  const int Wq = W1 / 2;   // conv column pairs (= W2)
+  __syncthreads();
+
+  for (int rp = P0; rp < P1; ++rp) {
+    // ---- prefetch the input rows the next row pair adds (2 rp + 5, 2 rp + 6)
+    constexpr int PFN = 2;
+    uint4 pf[PFN];
+    const bool more = rp + 1 < P1;
+#pragma unroll
+    for (int k = 0; k < PFN; ++k) {
+      const int c = tid + k * SP_THREADS;
+      const int yy = 2 * rp + 5 + (c >= RCH ? 1 : 0), cc = c >= RCH ? c - RCH : c;
+      pf[k] = make_uint4(0, 0, 0, 0);
+      if (more && c < 2 * RCH && yy < p.Hs) pf[k] = x2b[(long)yy * RCH + cc];
+    }
+    // ---- route pool rows rp (taps r = 1, 2) and rp + 1 (tap r = 0) into conv rows 2rp, 2rp+1:
+    //      item = (column pair qq, 8-channel group cg), as maxpool_bwd_stream_kernel
+    for (int it = tid; it < Wq * 8; it += SP_THREADS) {
+      const int qq = it >> 3, cg = it & 7;
+      uint4 gv[2][2];
+      uint2 iv[2][2];
+#pragma unroll
+      for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+        for (int dc = 0; dc < 2; ++dc) {
+          const int pr = rp + dr, pc = qq + dc;
+          const bool ok = pr < p.H2 && pc < p.W2;
+          const long o = (gbase + (long)(ok ? pr : 0) * p.W2 + (ok ? pc : 0)) * 64 + cg * 8;
+          const uint4 gl = *reinterpret_cast<const uint4*>(p.gpool + o);
+          const uint2 il = *reinterpret_cast<const uint2*>(p.idx + o);
+          gv[dr][dc] = ok ? gl : make_uint4(0, 0, 0, 0);
+          iv[dr][dc] = ok ? il : make_uint2(0xffffffffu, 0xffffffffu);
+        }
+      float ga[8], gb[8], gc[8], gd[8];
+      unpack8(gv[0][0], ga); unpack8(gv[0][1], gb); unpack8(gv[1][0], gc); unpack8(gv[1][1], gd);
+      auto tap = [](const uint2& v, int e) { return ((e < 4 ? v.x : v.y) >> (8 * (e & 3))) & 0xffu; };
+      float o4[2][2][8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t ta = tap(iv[0][0], e), tb = tap(iv[0][1], e), tc = tap(iv[1][0], e), td = tap(iv[1][1], e);
+        o4[0][0][e] = ta == 4u ? ga[e] : 0.f;
+        o4[0][1][e] = (ta == 5u ? ga[e] : 0.f) + (tb == 3u ? gb[e] : 0.f);
+        o4[1][0][e] = (ta == 7u ? ga[e] : 0.f) + (tc == 1u ? gc[e] : 0.f);
+        o4[1][1][e] = (ta == 8u ? ga[e] : 0.f) + (tb == 6u ? gb[e] : 0.f) + (tc == 2u ? gc[e] : 0.f) +
+                      (td == 0u ? gd[e] : 0.f);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += o4[a][c][e];   // (fp32, as maxpool_bwd's fused sums)
+          *reinterpret_cast<uint4*>(gimg + gimg_off(a, 2 * qq + c, cg)) = pack8(o4[a][c]);
+        }
+    }
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < PFN; ++k) {
+        const int c = tid + k * SP_THREADS;
+        if (c < 2 * RCH) {
+          const int yy = 2 * rp + 5 + (c >= RCH ? 1 : 0), cc = c >= RCH ? c - RCH : c;
+          if (yy < p.Hs) reinterpret_cast<uint4*>(ring + (yy & 7) * SLOT)[cc] = pf[k];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- weight-gradient MFMAs over the row pair: 2 rows x nst steps of 32 pixels
+    for (int a = 0; a < 2; ++a) {
+      const int y = 2 * rp + a;
+      for (int st = 0; st < nst; ++st) {
+        const int x0 = 32 * st;
+        v8bf af[4], bfr[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int px = x0 + 8 * g + 4 * h + q;   // this lane's block row (pixel)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            // A block: pixels px0..px0+3 x channels 16 i + 4 pp .. +3 -> chunk 2 i + (pp >> 1), half pp & 1
+            const v4bf r = sp_tr_read(gimg + gimg_off(a, px, 2 * i + (pp >> 1)) + (pp & 1) * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) af[i][4 * h + j] = r[j];
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int T = 4 * wave + t, R = T >> 2, S = T & 3;
+            const int xs = min(px + S, p.Ws - 1);
+            const v4bf r = sp_tr_read(ring + ((y + R) & 7) * SLOT + xs * 32 + pp * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[t][4 * h + j] = r[j];
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the asm fragment reads)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[t], acc[i][t], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // the next row pair's router overwrites the image and ring slots
+  }
+  // ---- dW2 += acc: lane holds D[co = 16 i + 4 g + e][k = 16 T + (lane & 15)]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = 16 * i + 4 * g + e, k = 16 * (4 * wave + t) + (lane & 15);
+        unsafeAtomicAdd(p.dw + co * 256 + k, acc[i][t][e]);
+      }
+  // ---- the workgroup's partial column sums: thread (it & 7) owns channels 8 (it & 7) .. +7
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] += __shfl_xor(cs[e], 8, 64);
+    cs[e] += __shfl_xor(cs[e], 16, 64);
+    cs[e] += __shfl_xor(cs[e], 32, 64);
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[wave * 64 + lane * 8 + e] = cs[e];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const float t = csum[tid] + csum[64 + tid] + csum[128 + tid] + csum[192 + tid];
+    p.colsum[(long)blockIdx.x * 64 + tid] = t;
+  }
+}
+
+int stem_pool_bwd_lds_bytes(int Ws) { return 8 * Ws * 32 + 2 * 16384 + 4 * 64 * 4; }
+
+static int stem_pool_rows(int B, int H2, int PB) {
+  if (PB > 0) return PB;
+  const long want = 4L * num_cus();
+  int pb = H2;
+  while (pb > 1 && (long)B * ((H2 + pb - 1) / pb) < want) pb = (pb + 1) / 2;
+  return pb;
+}
+int stem_pool_bwd_partial_rows(int B, int H2, int PB) {
+  const int pb = stem_pool_rows(B, H2, PB);
+  return B * ((H2 + pb - 1) / pb);
+}
+
+const char* stem_pool_bwd_launch(StemPoolBwdParams p, hipStream_t s) {
+  if (p.H1 != p.Hs - 3 || p.W1 != p.Ws - 3) return "stem_pool_bwd: conv1 output must be the s2d input minus 3";
+  if (p.H1 % 2 || p.W1 % 2) return "stem_pool_bwd: even conv1 output (even crop) expected";
+  if (p.H2 != p.H1 / 2 || p.W2 != p.W1 / 2) return "stem_pool_bwd: pool output must be the pad-1 3x3/s2 size";
+  if (p.Ws > 128 || p.W1 > 128) return "stem_pool_bwd: rows wider than the image / prefetch cover (crop <= 250)";
+  const int lds = stem_pool_bwd_lds_bytes(p.Ws);
+  if (lds > 80 * 1024) return "stem_pool_bwd: LDS per workgroup above the two-per-CU budget";
+  p.PB = stem_pool_rows(p.B, p.H2, p.PB);
+  p.nblk = (p.H2 + p.PB - 1) / p.PB;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_bwd_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(stem_pool_bwd_kernel, dim3((unsigned)((long)p.B * p.nblk)), dim3(SP_THREADS), lds, s, p);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
 int stem_pool_lds_bytes(int Ws, int W1) { return 8 * Ws * 32 + 3 * W1 * 128 + 512; }
 
 const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s) {

@@ -48,7 +48,10 @@ class HipEngine:
     FUSE_PROJ_OK = True     # projection blocks: conv3 + shortcut conv as one dual-source GEMM
     FUSE_BWD_OK = True      # stage-2/3 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
     FUSE_STEM_OK = True     # stem conv + BN + ReLU + max-pool forward in one launch (stem.hip)
+    TWO_STREAM_OK = True
     TWO_STREAM_MAX_BATCH = 1024
+    GRAD_RING = 3           # two-stream: gradient buffers per kind, so the data-gradient chain can run
+                            # two blocks ahead of the weight gradients still reading older ones
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
@@ -119,8 +122,7 @@ class HipEngine:
         # two-stream backward (small batches, where single kernels underfill the chip): the weight
         # gradients run on a side stream concurrently with the data-gradient chain.
         # PDDL_TWO_STREAM=1 / 0 forces it; default on up to TWO_STREAM_MAX_BATCH images.
-        ts = os.environ.get("PDDL_TWO_STREAM", "auto")
-        self.two_stream = (batch <= self.TWO_STREAM_MAX_BATCH) if ts == "auto" else ts == "1"
+        self.two_stream = self._two_stream_wanted(batch)
         self.side = torch.cuda.Stream(dev) if self.two_stream and dev.type == "cuda" else None
         self._pending, self._last_side = {}, None
 
@@ -270,9 +272,12 @@ class HipEngine:
             outer = max(outer, B * H * H * b.cin, B * Ho * Ho * 4 * f)
             H = Ho
         self.H5 = H
-        self.gbuf = [torch.empty(outer, **bf), torch.empty(outer, **bf)]
-        self.g1buf = torch.empty(inner, **bf)
-        self.g2buf = torch.empty(inner, **bf)
+        # (set before _alloc_acts runs; the subclasses' engines keep one stream)
+        ring = self.GRAD_RING if self._two_stream_wanted(B) else 1
+        self.gbuf = [torch.empty(outer, **bf) for _ in range(max(2, ring))]
+        self.g1bufs = [torch.empty(inner, **bf) for _ in range(ring)]
+        self.g2bufs = [torch.empty(inner, **bf) for _ in range(ring)]
+        self.g1buf, self.g2buf = self.g1bufs[0], self.g2bufs[0]
         # compact (stride-2 grid) copies of the output gradient / conv2-output gradient of every
         # block feeding a downsampling block (see _s2_fed)
         gc, g2c = 1, 1
@@ -341,7 +346,10 @@ class HipEngine:
             add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)          # c2 dgrad -> g1
             if bi > 0:                                                           # c1 dgrad -> g_out(prev)
                 add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin, 5 * f if b.proj else f), b.cin)
-        add(L.stem.name, N.maxpool_bwd_partial_rows(B, self.H1, self.H1, 64), 64)
+        if self.fuse_stem:   # (fused pool backward + conv1 weight gradient: one partial row per workgroup)
+            add(L.stem.name, N.stem_pool_bwd_partial_rows(B, self.H2), 64)
+        else:
+            add(L.stem.name, N.maxpool_bwd_partial_rows(B, self.H1, self.H1, 64), 64)
         res = (offs, self._dev_table(rows), off, len(rows))
         self._cred[B] = res
         return res
@@ -465,6 +473,10 @@ class HipEngine:
         return lab
 
     # ------------------------------------------------------------------ two-stream backward
+    def _two_stream_wanted(self, batch) -> bool:
+        ts = os.environ.get("PDDL_TWO_STREAM", "auto")
+        return self.TWO_STREAM_OK and ((batch <= self.TWO_STREAM_MAX_BATCH) if ts == "auto" else ts == "1")
+
     def _side_run(self, fn, *args, reads=()):
         """Launch a weight-gradient kernel on the side stream, ordered after everything enqueued
         on the compute stream so far; `reads` names the gradient buffers it reads, which the
@@ -494,6 +506,27 @@ class HipEngine:
             ev = self._pending.pop(b, None)
             if ev is not None:
                 main.wait_event(ev)
+
+    def _bucket_ready(self, cb, i):
+        """Report bucket i complete.  Two streams: its gradients come from both streams, so the
+        side stream first waits for the compute stream and the callback runs with the SIDE stream
+        current -- whatever it enqueues or records (an all-reduce, an optimizer update) is
+        ordered after both, and the compute stream never blocks on the side stream."""
+        if self.side is None:
+            cb(i)
+            return
+        if getattr(cb, "needs_join", False):   # (e.g. a graph capture cut at the bucket boundary)
+            self._join_side()
+            cb(i)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            cb(i)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        self._last_side = done
 
     def _join_side(self):
         if self.side is None or self._last_side is None:
@@ -526,8 +559,7 @@ class HipEngine:
 
         def done_upto(off):
             while bucket_cb is not None and nb[0] < len(bks) - 1 and bks[nb[0]][1] <= off:
-                self._join_side()   # the bucket's weight gradients ran on the side stream
-                bucket_cb(nb[0])
+                self._bucket_ready(bucket_cb, nb[0])
                 nb[0] += 1
 
         # ---- head
@@ -573,8 +605,9 @@ class HipEngine:
             gout = (self.s2full[bi] if bi in s2 else self.gbuf[cur])[: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
             gout_n = f"s2f{bi}" if bi in s2 else f"gbuf{cur}"
             c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
-            g2 = (self.s2g2full[bi] if bi in s2 else self.g2buf)[: B * Ho * Ho * f].view(B, Ho, Ho, f)
-            g2_n = f"s2g2f{bi}" if bi in s2 else "g2"
+            rk = bi % len(self.g2bufs)
+            g2 = (self.s2g2full[bi] if bi in s2 else self.g2bufs[rk])[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            g2_n = f"s2g2f{bi}" if bi in s2 else f"g2_{rk}"
             if bi in s2:
                 # gout is zero off the stride-2 grid (the next block reads only even rows /
                 # columns); its compact copy `gc` came from that block's dgrad epilogue
@@ -608,17 +641,17 @@ class HipEngine:
                 # conv2 (3x3)
                 W(N.wgrad, y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0,
                   reads=(g2_n,))
-            g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
-            self._before_write("g1")
+            g1 = self.g1bufs[rk][: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            self._before_write(f"g1_{rk}")
             N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1m, None,
                     g1, 0, None, 0, 0, 0, 0, 0, part(c1n), None)
             # conv1 (+ conv0)
-            nxt = 1 - cur
+            nxt = (cur + 1) % len(self.gbuf)
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
             gx_n = [f"gbuf{nxt}"]
             if b.proj:
                 W(N.wgrad, x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0,
-                  reads=("g1", gout_n))
+                  reads=(f"g1_{rk}", gout_n))
                 W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
                 gxc, up2 = None, 1 if b.stride == 2 else 0
                 if bi - 1 in s2:   # compact copy for the previous block's stride-2-grid passes
@@ -634,7 +667,7 @@ class HipEngine:
                 last = L.entry(b.convs["0"].name, "kernel")
             else:
                 W(N.wgrad, x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0,
-                  reads=("g1",))
+                  reads=(f"g1_{rk}",))
                 W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
                 self._before_write(*gx_n)
                 N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, f), 1, None, None, None,
@@ -645,12 +678,18 @@ class HipEngine:
         # ---- stem (space-to-depth wgrad, folded back to 7x7x3)
         H1, H2, Hs = self.H1, self.H2, self.Hs
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
-        gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
         s = L.stem
-        self._before_write(f"gbuf{1 - cur}")
-        N.maxpool_bwd(gpool, self.pidx[:B], None, gc1, part(s.name))
-        W(N.wgrad, self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
-        W(N.stem_wgrad_fold, self.stem_dw2, self._gview(s.name, 64, 147), 64)
+        if self.fuse_stem:
+            # pool backward + conv1 weight gradient in one launch: conv1's gradient stays in LDS
+            N.stem_pool_bwd(self.stem_x2[:B], gpool, self.pidx[:B], self.stem_dw2, part(s.name))
+            W(N.stem_wgrad_fold, self.stem_dw2, self._gview(s.name, 64, 147), 64)
+        else:
+            gcn = (cur + 1) % len(self.gbuf)
+            gc1 = self.gbuf[gcn][: B * H1 * H1 * 64].view(B, H1, H1, 64)
+            self._before_write(f"gbuf{gcn}")
+            N.maxpool_bwd(gpool, self.pidx[:B], None, gc1, part(s.name))
+            W(N.wgrad, self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
+            W(N.stem_wgrad_fold, self.stem_dw2, self._gview(s.name, 64, 147), 64)
         W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)
         self._join_side()
         done_upto(L.kernels_end)
@@ -659,7 +698,7 @@ class HipEngine:
         prof.pop()
         if bucket_cb is not None:
             while nb[0] < len(bks):
-                bucket_cb(nb[0])
+                self._bucket_ready(bucket_cb, nb[0])
                 nb[0] += 1
         return self.stats
 

@@ -38,6 +38,7 @@ class HipEngineBNTrain(HipEngine):
     FUSE_BWD_OK = False    # (its conv3 dgrad carries the fused BN-backward sums)
     FUSE_PROJ_OK = False   # (batch statistics: the shortcut's BN cannot be folded into weights)
     FUSE_STEM_OK = False   # (conv1's batch statistics need its raw output)
+    TWO_STREAM_OK = False  # (its own backward schedule runs on one stream)
 
     def __init__(self, layout: ParamLayout, batch: int, **kw):
         kw.setdefault("bn_mode", "train")

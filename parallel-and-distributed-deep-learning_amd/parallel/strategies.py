@@ -66,6 +66,25 @@ def collective_timeout():
     return datetime.timedelta(seconds=float(os.environ.get("PDDL_COLLECTIVE_TIMEOUT", "600")))
 
 
+def overlap_buckets(engine):
+    """Gradient slices whose optimizer update can start as soon as backward completes them
+    (8 MiB: fine enough that only the last stage-2 / stem slice and the per-channel tail wait
+    for the end of backward)."""
+    if not hasattr(engine, "_ov_buckets"):
+        engine._ov_buckets = engine.L.buckets(8.0)
+    return engine._ov_buckets
+
+
+def overlap_stream(engine):
+    """The stream the overlapped optimizer updates run on: the engine's weight-gradient side
+    stream when it has one, else a stream of their own."""
+    if getattr(engine, "side", None) is not None:
+        return engine.side
+    if not hasattr(engine, "_opt_stream"):
+        engine._opt_stream = torch.cuda.Stream(engine.params.device)
+    return engine._opt_stream
+
+
 def gpu_available() -> bool:
     return torch.cuda.is_available() and torch.cuda.device_count() > 0
 
@@ -262,9 +281,17 @@ class SingleStrategy(Strategy):
         if self.graphed is not None and B == self.graphed.B and tuple(images.shape[1:3]) == self.graphed.images.shape[1:3]:
             return self.graphed(images.to(self.device, non_blocking=True), labels.to(self.device, non_blocking=True),
                                 flip, off).clone()
-        s = self.engine.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off).clone()
-        self.opt.step()
-        self.engine.after_update()
+        eng = self.engine
+        if eng.params.is_cuda and hasattr(eng, "wbf") and os.environ.get("PDDL_OVERLAP_OPT", "1") != "0":
+            bks = overlap_buckets(eng)       # optimizer bucket updates under the rest of backward
+            self.opt.overlap_begin(bks, overlap_stream(eng))
+            s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off,
+                                     bucket_cb=self.opt.overlap_bucket, buckets=bks).clone()
+            self.opt.overlap_finish()
+        else:
+            s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off).clone()
+            self.opt.step()
+        eng.after_update()
         return s
 
 
@@ -383,15 +410,25 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
             return self._autotune_step(images, labels)
         return self._step(images, labels)
 
+    def _overlap_opt(self) -> bool:
+        """One replica on the GPU: the optimizer's bucket updates run under the rest of backward
+        (PDDL_OVERLAP_OPT=0 turns it off).  With collectives the update waits for the all-reduce."""
+        return (self.world == 1 and self.fusion is None and self.reducer is None and self.device.type == "cuda"
+                and hasattr(self.engine, "wbf") and os.environ.get("PDDL_OVERLAP_OPT", "1") != "0")
+
     def _step(self, images, labels):
-        s = self.compute_gradients(images, labels)
+        ov = self._overlap_opt()
+        s = self.compute_gradients(images, labels, overlap_opt=ov)
         prof.push("step/optimizer")
-        self.opt.step()
+        if ov:
+            self.opt.overlap_finish()
+        else:
+            self.opt.step()
         self.engine.after_update()
         prof.pop()
         return s
 
-    def compute_gradients(self, images, labels):
+    def compute_gradients(self, images, labels, overlap_opt: bool = False):
         """Forward + backward + the bucketed all-reduce, without applying the update
         (Optimizer.compute_gradients of the reference's DistributedOptimizer,
         imagenet-resnet50-hvd.py:101): afterwards `engine.grads` holds the global-batch mean
@@ -400,14 +437,19 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
         flip, off = self.aug(B)
         gscale = 1.0 / (B * self.world)
         cb = None
+        bks = self.buckets
         if self.fusion is not None:
             self.fusion.begin_step()
             cb = self.fusion.bucket_ready
         elif self.reducer is not None:
             self.reducer.begin()
             cb = self.reducer.on_bucket_ready
+        elif overlap_opt:   # (the caller finishes the step with opt.overlap_finish())
+            bks = overlap_buckets(self.engine)
+            self.opt.overlap_begin(bks, overlap_stream(self.engine))
+            cb = self.opt.overlap_bucket
         s = self.engine.forward_backward(images, labels, gscale, flip=flip, crop_offset=off, bucket_cb=cb,
-                                         buckets=self.buckets).clone()
+                                         buckets=bks).clone()
         prof.push("step/allreduce")
         if self.fusion is not None:
             self.fusion.finish()

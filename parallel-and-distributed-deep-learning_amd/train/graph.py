@@ -20,6 +20,8 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import os
+
 import torch
 
 
@@ -51,6 +53,16 @@ class GraphedTrainStep:
 
     def _body(self):
         eng = self.engine
+        if self.with_optimizer and os.environ.get("PDDL_OVERLAP_OPT", "1") != "0":
+            # the optimizer's bucket updates run under the rest of backward (one replica)
+            from ..parallel.strategies import overlap_buckets, overlap_stream
+            bks = overlap_buckets(eng)
+            self.opt.overlap_begin(bks, overlap_stream(eng))
+            stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip, crop_offset=self.crop,
+                                         bucket_cb=self.opt.overlap_bucket, buckets=bks)
+            self.opt.overlap_finish()
+            eng.after_update()
+            return stats
         stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip, crop_offset=self.crop)
         if self.with_optimizer:
             self.opt.step()
@@ -144,6 +156,7 @@ class SegmentedStepGraphs(GraphedTrainStep):
             segs[-1].capture_end()
             if i < nb - 1:
                 begin()
+        cut.needs_join = True   # (a two-stream engine joins its side stream before each cut)
 
         with torch.cuda.device(dev):
             s = torch.cuda.Stream(device=dev)

@@ -74,8 +74,11 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         ev.append(("wgrad_finalize", b.name, 0, 0))
         ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2, (M, cin, n1),
                    "dual" if b.proj else ""))
-    ev.append(("maxpool_bwd", "pool", 0, 0))
-    ev.append(("wgrad", "conv1 wgrad", 2 * B * H1 * H1 * 256 * 64, 0))
+    if fuse_stem:   # pool backward + conv1 weight gradient in one launch (stem.hip)
+        ev.append(("stem_pool", "pool bwd + conv1 wgrad", 2 * B * H1 * H1 * 256 * 64, 0))
+    else:
+        ev.append(("maxpool_bwd", "pool", 0, 0))
+        ev.append(("wgrad", "conv1 wgrad", 2 * B * H1 * H1 * 256 * 64, 0))
     ev.append(("stem_wgrad_fold", "fold", 0, 0))
     ev.append(("wgrad_finalize", "stem", 0, 0))
     ev.append(("colsum_reduce", "cred", 0, 0))

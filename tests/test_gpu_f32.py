@@ -319,3 +319,46 @@ def test_f32_pool_gap_softmax_kernels():
     (loss * 0.5).backward()
     assert abs(ls.item() - loss.item()) < 1e-4 and rel(dl, lr.grad) < 1e-6
     assert cr.item() == (logits.argmax(1) == lab).sum().item()
+
+
+@pytest.mark.parametrize("case", [(4, 28, 64, 128, 3, 1, 1), (2, 30, 16, 64, 4, 1, 0), (2, 14, 256, 1024, 1, 1, 0),
+                                  (8, 7, 512, 512, 3, 1, 1), (3, 15, 128, 200, 1, 2, 0)])
+def test_conv_f32_128_tile_kernels_match_64_and_fp64(case):
+    """The 128 x 128 LDS-DMA fp32 kernels (conv_f32_big_kernel / wgrad_f32_big_kernel, knob
+    conv_f32 = 1, the default for C % 16 == 0) against float64 and against the 64 x 64 kernels
+    (knob 0): forward with the fused frozen-BN epilogue, data-gradient epilogue with column sums,
+    and the weight gradient, over multi-tile shapes incl. the stem's 4x4 window (C = 16) and a
+    ragged Cout."""
+    torch.manual_seed(1)
+    n, h, c, co, r, st, pad = case
+    ho = (h + 2 * pad - r) // st + 1
+    x = torch.randn(n, h, h, c, device=dev)
+    w = torch.randn(co, r, r, c, device=dev) * 0.1
+    sc, sh = torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev)
+    res = torch.randn(n, ho, ho, co, device=dev)
+    g = torch.randn(n, ho, ho, co, device=dev)
+    outs = []
+    for v in (1, 0):
+        N().set_variant("conv_f32", v)
+        try:
+            y = torch.empty(n, ho, ho, co, device=dev)
+            N().conv_f32_epi(x, r, r, st, pad, ho, ho, w.view(co, -1), 1, sc, sh, res, 1, None, None, 0, y, None)
+            yd = torch.empty(n, ho, ho, co, device=dev)
+            cs = torch.zeros((n * ho * ho + 63) // 64, co, device=dev)
+            N().conv_f32_epi(x, r, r, st, pad, ho, ho, w.view(co, -1), 2, None, None, None, 0, res, g, 0, yd, cs)
+            dw = torch.zeros(co, r * r * c, device=dev)
+            N().wgrad_f32(x, r, r, st, pad, g, dw)
+            torch.cuda.synchronize()
+            outs.append((y, yd, cs.sum(0), dw))
+        finally:
+            N().set_variant("conv_f32", 1)
+    conv = F.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), stride=st,
+                    padding=pad).permute(0, 2, 3, 1)
+    ref_y = torch.relu(conv * sc.double() + sh.double() + res.double())
+    ref_yd = torch.where(g > 0, conv + res.double(), torch.zeros_like(conv))
+    ref_dw = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (co, c, r, r), g.double().permute(0, 3, 1, 2),
+                                         stride=st, padding=pad).permute(0, 2, 3, 1).reshape(co, -1)
+    (y1, yd1, cs1, dw1), (y0, yd0, cs0, dw0) = outs
+    assert rel(y1, ref_y) < 1e-5 and rel(yd1, ref_yd) < 1e-5 and rel(dw1, ref_dw) < 1e-5
+    assert rel(cs1, ref_yd.reshape(-1, co).sum(0)) < 1e-5
+    assert rel(y1, y0) < 1e-5 and rel(dw1, dw0) < 1e-5

@@ -985,3 +985,37 @@ def test_stem_pool_fused_matches_unfused(B, crop, rows):
     pool2 = torch.empty_like(pool_r)
     N().stem_pool_fwd(x2, w2, scale, shift, pool2, idx, None, rows)
     assert torch.equal(pool2.view(torch.int16), pool_r.view(torch.int16))
+
+
+@pytest.mark.parametrize("B,crop,rows", [(2, 224, 0), (3, 244, 0), (2, 160, 1), (2, 96, 5), (1, 224, 56)])
+def test_stem_pool_bwd_fused_matches_unfused(B, crop, rows):
+    """Fused stem backward (stem.hip: max-pool backward routed into LDS + conv1 weight gradient
+    from transposed LDS reads + the stem's column sums) against the unfused pair (maxpool_bwd ->
+    bf16 conv1 gradient -> wgrad) and an fp32 reference of the routed gradient's weight gradient."""
+    torch.manual_seed(crop + rows + 1)
+    hs = (crop + 6) // 2
+    h1, h2 = hs - 3, (hs - 3) // 2
+    x2 = torch.rand(B, hs, hs, 16, device=dev).to(torch.bfloat16)
+    # forward taps from a real pool so the routing is exercised with valid argmax codes
+    c1 = torch.relu(torch.randn(B, h1, h1, 64, device=dev)).to(torch.bfloat16)
+    pool = torch.empty(B, h2, h2, 64, dtype=torch.bfloat16, device=dev)
+    idx = torch.empty(B, h2, h2, 64, dtype=torch.uint8, device=dev)
+    N().maxpool_fwd(c1, pool, idx, None)
+    gpool = rnd(B, h2, h2, 64)
+    gc1 = torch.empty(B, h1, h1, 64, dtype=torch.bfloat16, device=dev)
+    prow = N().maxpool_bwd_partial_rows(B, h1, h1, 64)
+    cs_r = torch.zeros(prow, 64, device=dev)
+    N().maxpool_bwd(gpool, idx, None, gc1, cs_r)
+    dw_r = torch.zeros(64, 256, device=dev)
+    N().wgrad(x2, hs, hs, 4, 4, 1, 0, h1, h1, gc1, None, 0, dw_r, 256, 0)
+    dw = torch.zeros(64, 256, device=dev)
+    cs = torch.zeros(N().stem_pool_bwd_partial_rows(B, h2, rows), 64, device=dev)
+    N().stem_pool_bwd(x2, gpool, idx, dw, cs, rows)
+    torch.cuda.synchronize()
+    # fp32 reference: window GEMM of the (bf16) routed gradient
+    xw = x2.float().unfold(1, 4, 1).unfold(2, 4, 1)              # [B, h1, h1, 16, 4(R), 4(S)]
+    xw = xw.permute(0, 1, 2, 4, 5, 3).reshape(B * h1 * h1, 256)   # k = (R*4 + S)*16 + c
+    ref = gc1.float().reshape(-1, 64).t() @ xw
+    assert rel(dw, ref) < 1e-5, rel(dw, ref)
+    assert rel(dw, dw_r) < 1e-5
+    assert torch.allclose(cs.sum(0), cs_r.sum(0), rtol=1e-4, atol=1e-3)
