@@ -39,8 +39,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--knob", default="igemm_big", help="igemm knob to A/B (igemm_big, igemm_il, ...)")
-    ap.add_argument("--variants", default="0,3", help="comma-separated knob values")
+    ap.add_argument("--knob", default="igemm8", help="igemm knob to A/B (igemm8, igemm, igemm_pf, igemm_pk, ...)")
+    ap.add_argument("--variants", default="0,2", help="comma-separated knob values")
     ap.add_argument("--wgrad-knob", default="wgrad8", help="wgrad knob to A/B")
     ap.add_argument("--wgrad-variants", default="0,2", help="comma-separated wgrad knob values")
     ap.add_argument("--skip-lib", action="store_true", help="skip the MIOpen / hipBLASLt yardsticks")

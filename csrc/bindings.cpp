@@ -714,28 +714,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_variant", [](const std::string& which, int v) {
     if (which == "igemm") pddl::g_igemm_variant = v;
     else if (which == "igemm_deep") pddl::g_igemm_deep = v;
-    else if (which == "igemm_big") pddl::g_igemm_big = v;
     else if (which == "igemm_pf") pddl::g_igemm_pf = v;
-    else if (which == "igemm_il") pddl::g_igemm_il = v;
     else if (which == "igemm8") pddl::g_igemm8 = v;
     else if (which == "igemm8_min_tiles") pddl::g_igemm8_min_tiles = v;
     else if (which == "wgrad8") pddl::g_wgrad8 = v;
-    else if (which == "igemm8_expand") pddl::g_igemm8_expand = v;
     else if (which == "igemm_ns1_kt") pddl::g_igemm_ns1_kt = v;
     else if (which == "igemm8_min_n") pddl::g_igemm8_min_n = v;
     else if (which == "wgrad1") pddl::g_wgrad1 = v;
     else if (which == "wgrad") pddl::g_wgrad_variant = v;
-    else if (which == "pool") pddl::g_pool_variant = v;
     else if (which == "igemm_n64") pddl::g_igemm_n64 = v;
     else if (which == "igemm_splitk") pddl::g_igemm_splitk = v;
-    else if (which == "igemm_epf") pddl::g_igemm_epf = v;
-    else if (which == "igemm_rd") pddl::g_igemm_rd = v;
     else if (which == "igemm_pk_all") pddl::g_igemm_pk_all = v;
     else if (which == "igemm_pk") { TORCH_CHECK(v == 0 || (v >= 2 && v <= 4), "igemm_pk: 0 or ring depth 2-4"); pddl::g_igemm_pk = v; }
     else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
     else if (which == "conv_f32") pddl::g_conv_f32_variant = v;
-    else if (which == "igemm8_ragged") pddl::g_igemm8_ragged = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;

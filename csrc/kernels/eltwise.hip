@@ -229,156 +229,6 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
   }
 }
 
-// Strip form (knob pool = 2 / 3; measured slower, see g_pool_variant): a thread owns PH vertically adjacent outputs of one column and
-// channel group, so it streams the 2 * PH + 1 input rows of their windows once (15 loads for
-// 2 outputs instead of 18) and the row shared by two strips is the only one fetched twice.
-// Rows are visited in order and, within a row, taps left to right, so each output still sees
-// its taps in scan order (the first maximum wins, as in the per-output form above).
-template <int PH>
-__global__ void __launch_bounds__(256) maxpool_fwd_strip_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                         uint8_t* __restrict__ idx, uint8_t* __restrict__ bits, int B, int H, int W,
-                                         int C, int Ho, int Wo, PoolDiv dv) {
-  const int cg = C / 8, Hq = (Ho + PH - 1) / PH;
-  const int total = B * Hq * Wo * cg;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int pix = fdiv(t, dv.cg);
-    const int g = t - pix * cg;
-    const int t2 = fdiv(pix, dv.w);
-    const int wo = pix - t2 * Wo;
-    const int b = fdiv(t2, dv.h);
-    const int hq = t2 - b * Hq;
-    const int ho0 = hq * PH, hi0 = 2 * ho0 - 1, wi0 = 2 * wo - 1;
-    float best[PH][8];
-    uint32_t bi[PH][2];
-#pragma unroll
-    for (int j = 0; j < PH; ++j) {
-      bi[j][0] = bi[j][1] = 0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) best[j][e] = -INFINITY;
-    }
-    const bf16_t* xb = x + (long)b * H * W * C + g * 8;
-#pragma unroll
-    for (int ri = 0; ri < 2 * PH + 1; ++ri) {
-      const int hi = hi0 + ri;
-      const bool row_ok = hi >= 0 && hi < H;
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const int wi = wi0 + s;
-        float v[8];
-        if (row_ok && wi >= 0 && wi < W) {
-          unpack8(*reinterpret_cast<const uint4*>(xb + ((long)hi * W + wi) * C), v);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < PH; ++j) {
-          const int r = ri - 2 * j;   // compile-time after unrolling
-          if (r < 0 || r > 2) continue;
-          const uint32_t code = (uint32_t)(r * 3 + s);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (v[e] > best[j][e]) {
-              best[j][e] = v[e];
-              bi[j][e >> 2] = (bi[j][e >> 2] & ~(0xffu << (8 * (e & 3)))) | (code << (8 * (e & 3)));
-            }
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < PH; ++j) {
-      if (ho0 + j >= Ho) break;
-      const long o = (((long)b * Ho + ho0 + j) * Wo + wo) * C + g * 8;
-      const uint4 yv = pack8(best[j]);
-      *reinterpret_cast<uint4*>(y + o) = yv;
-      if (bits) bits[o >> 3] = (uint8_t)pos_bits8(yv);
-      *reinterpret_cast<uint2*>(idx + o) = make_uint2(bi[j][0], bi[j][1]);
-    }
-  }
-}
-
-// Block form of the backward (default, 24% faster than the per-pixel form): a thread owns the 2 x 2 input block (2q..2q+1,
-// 2p..2p+1) of one channel group.  Exactly the outputs (q..q+1, p..p+1) can route gradient
-// into it, each through a fixed tap per block position, so the thread reads 4 (gy, idx)
-// pairs for 4 written pixels with no data-dependent loop bounds.
-__global__ void maxpool_bwd_block_kernel(const bf16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
-                                         const bf16_t* __restrict__ xmask, bf16_t* __restrict__ gx, int B, int H,
-                                         int W, int C, int Ho, int Wo, float* __restrict__ colsum, PoolDiv dv) {
-  const int cg = C / 8, Hq = (H + 1) / 2, Wq = (W + 1) / 2;
-  const int total = B * Hq * Wq * cg;
-  float cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int pix = fdiv(t, dv.cg);
-    const int g = t - pix * cg;
-    const int t2 = fdiv(pix, dv.w);
-    const int p = pix - t2 * Wq;
-    const int b = fdiv(t2, dv.h);
-    const int q = t2 - b * Hq;
-    float acc[2][2][8];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[a][c][e] = 0.f;
-    // output (q + dq, p + dp) covers input rows 2(q+dq)-1 .. 2(q+dq)+1: block row a (input
-    // row 2q + a) is its tap r = a + 1 - 2 dq (valid when 0 <= r <= 2); likewise columns.
-#pragma unroll
-    for (int dq = 0; dq < 2; ++dq)
-#pragma unroll
-      for (int dp = 0; dp < 2; ++dp) {
-        const int ho = q + dq, wo = p + dp;
-        if (ho >= Ho || wo >= Wo) continue;
-        const long o = (((long)b * Ho + ho) * Wo + wo) * C + g * 8;
-        const uint2 pk = *reinterpret_cast<const uint2*>(idx + o);
-        float gv[8];
-        unpack8(*reinterpret_cast<const uint4*>(gy + o), gv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t id = ((e < 4 ? pk.x : pk.y) >> (8 * (e & 3))) & 0xffu;
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              const int r = a + 1 - 2 * dq, sc = c + 1 - 2 * dp;   // compile-time tap
-              if (r < 0 || sc < 0) continue;
-              if (id == (uint32_t)(r * 3 + sc)) acc[a][c][e] += gv[e];
-            }
-        }
-      }
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int h = 2 * q + a, w = 2 * p + c;
-        if (h >= H || w >= W) continue;
-        const long o = (((long)b * H + h) * W + w) * C + g * 8;
-        if (xmask) {
-          float mv[8];
-          unpack8(*reinterpret_cast<const uint4*>(xmask + o), mv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[a][c][e] = mv[e] > 0.f ? acc[a][c][e] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) cs[e] += acc[a][c][e];
-        *reinterpret_cast<uint4*>(gx + o) = pack8(acc[a][c]);
-      }
-  }
-  if (colsum) {  // one partial row of C sums per wave (plain stores)
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = cg; o < 64; o <<= 1)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) cs[e] += __shfl_xor(cs[e], o, 64);
-    if (lane < cg) {
-      const long wave = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
-      float4* dst = reinterpret_cast<float4*>(colsum + wave * C + lane * 8);
-      dst[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
-      dst[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
-    }
-  }
-}
-
 // Column sums of the output are accumulated per thread: with a grid stride that is a
 // multiple of C/8 every thread keeps one channel group, folded across the wave at the end.
 __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ gy, const uint8_t* __restrict__ idx,
@@ -626,21 +476,17 @@ __global__ void __launch_bounds__(256) maxpool_bwd_stream_kernel(const bf16_t* _
   }
 }
 
-// Max-pool kernels (bench/pool.py, b1024 @ 112x112x64; profiles/r1_pool_ab.json):
-//   0 = per-output forward (740 us) + 2x2-block backward (628 us, was 827 us per input pixel)
-//   1 = per-output forward + per-input-pixel backward
-//   2 / 3 = 2- / 4-output strip forward (796 / 1000 us: the register-held strip costs more
-//           occupancy than the saved re-reads return) + block backward
-//   4 = row-streaming forward and backward (one wave per image x column band)
-int g_pool_variant = 4;
-static bool pool_stream(int C) { return g_pool_variant == 4 && (C == 64 || C == 128 || C == 256); }
+// Max-pool kernels: row-streaming forward and backward (one wave per image x column band) for
+// the ResNet widths C = 64 / 128 / 256; the per-output forward and per-input-pixel backward
+// for any other C % 8 == 0.  (Rejected after bench/pool.py A/B at b1024 @ 112x112x64,
+// profiles/r1_pool_ab.json, and removed: 2- / 4-output strip forwards, 796 / 1000 us, and a
+// 2x2-block backward, 628 us, against the streaming pair.)
+static bool pool_stream(int C) { return C == 64 || C == 128 || C == 256; }
 static long pool_stream_waves(int B, int cols, int C) {
   const int WL = 64 / (C / 8);
   return (long)B * ((cols + WL - 1) / WL);
 }
-static long pool_bwd_items(int B, int H, int W, int C) {
-  return g_pool_variant == 1 ? (long)B * H * W * C / 8 : (long)B * ((H + 1) / 2) * ((W + 1) / 2) * C / 8;
-}
+static long pool_bwd_items(int B, int H, int W, int C) { return (long)B * H * W * C / 8; }
 int maxpool_bwd_partial_rows(int B, int H, int W, int C) {
   if (pool_stream(C)) return (int)pool_stream_waves(B, (W + 1) / 2, C);
   return grid_for(pool_bwd_items(B, H, W, C)) * 4;
@@ -656,19 +502,10 @@ const char* maxpool_fwd_launch(const uint16_t* x, uint16_t* y, uint8_t* idx, uin
 #define POOL_F(CG_) hipLaunchKernelGGL(maxpool_fwd_stream_kernel<CG_>, dim3(grid), dim3(256), 0, s, x, y, idx, bits, B, H, W, Ho, Wo)
     if (C == 64) POOL_F(8); else if (C == 128) POOL_F(16); else POOL_F(32);
 #undef POOL_F
-  } else if (g_pool_variant <= 1) {
+  } else {
     const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic(Wo), fdiv_magic(Ho)};
     hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)B * Ho * Wo * C / 8)), dim3(256), 0, s, x, y, idx,
                        bits, B, H, W, C, Ho, Wo, dv);
-  } else {
-    const int ph = g_pool_variant == 3 ? 4 : 2;
-    const int Hq = (Ho + ph - 1) / ph;
-    const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic(Wo), fdiv_magic(Hq)};
-    const int grid = grid_for((long)B * Hq * Wo * C / 8);
-    if (ph == 4)
-      hipLaunchKernelGGL(maxpool_fwd_strip_kernel<4>, dim3(grid), dim3(256), 0, s, x, y, idx, bits, B, H, W, C, Ho, Wo, dv);
-    else
-      hipLaunchKernelGGL(maxpool_fwd_strip_kernel<2>, dim3(grid), dim3(256), 0, s, x, y, idx, bits, B, H, W, C, Ho, Wo, dv);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
@@ -686,14 +523,10 @@ const char* maxpool_bwd_launch(const uint16_t* gy, const uint8_t* idx, const uin
   hipLaunchKernelGGL(maxpool_bwd_stream_kernel<CG_>, dim3(sgrid), dim3(256), 0, s, gy, idx, xmask, gx, B, H, W, Ho, Wo, colsum)
     if (C == 64) POOL_B(8); else if (C == 128) POOL_B(16); else POOL_B(32);
 #undef POOL_B
-  } else if (g_pool_variant == 1) {
+  } else {
     const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic(W), fdiv_magic(H)};
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid), dim3(256), 0, s, gy, idx, xmask, gx, B, H, W, C, Ho, Wo,
                        colsum, dv);
-  } else {
-    const PoolDiv dv{fdiv_magic(C / 8), fdiv_magic((W + 1) / 2), fdiv_magic((H + 1) / 2)};
-    hipLaunchKernelGGL(maxpool_bwd_block_kernel, dim3(grid), dim3(256), 0, s, gy, idx, xmask, gx, B, H, W, C, Ho,
-                       Wo, colsum, dv);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);

@@ -119,13 +119,9 @@ __device__ __forceinline__ void igemm_epi_load(const IgemmParams& p, int mb, int
     }
 }
 
-// EARLY: the caller loaded the whole sub-tile's operand (igemm_epi_load) before its K loop and
-// passes it in `epre` / `ebits` (the short-K layers: their HBM latency then overlaps the
-// operand loads instead of following the MFMAs).
-template <int TM, int TN, bool PF, bool BNZ = false, bool EARLY = false>
+template <int TM, int TN, bool PF, bool BNZ = false>
 __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
-                                               float* stage, int lane, const uint4* epre = nullptr,
-                                               const uint32_t* ebits = nullptr) {
+                                               float* stage, int lane) {
   constexpr int WTN = 16 * TN;
   constexpr int EPI_LD = WTN + 4;
   const int HoWo = p.Ho * p.Wo;
@@ -161,17 +157,16 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
   // 32-row pass at a time at the top of the pass.  (Loaded inside the store loop, each load
   // would wait behind the previous iteration's store -- `out` may alias `add` as far as the
   // compiler knows -- and the pass would pay NIT serialised HBM round trips.)
-  constexpr bool WHOLE = PF && !EARLY;
-  uint4 pre[WHOLE ? (TM / 2) * NIT : (EARLY ? 1 : NIT)];
-  uint32_t pre_bits[WHOLE ? (TM / 2) * NIT : (EARLY ? 1 : NIT)];
+  uint4 pre[PF ? (TM / 2) * NIT : NIT];
+  uint32_t pre_bits[PF ? (TM / 2) * NIT : NIT];
   const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
   const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
-  if (WHOLE && (pre_on || pf_bits)) igemm_epi_load<TM, TN>(p, mb, nb, lane, 0, TM / 2, pre, pre_bits);
+  if (PF && (pre_on || pf_bits)) igemm_epi_load<TM, TN>(p, mb, nb, lane, 0, TM / 2, pre, pre_bits);
 #pragma unroll
   for (int pass = 0; pass < TM / 2; ++pass) {
-    if (!PF && !EARLY && (pre_on || pf_bits)) igemm_epi_load<TM, TN>(p, mb, nb, lane, pass, 1, pre, pre_bits);
-    const uint4* ppre = EARLY ? epre + pass * NIT : (PF ? pre + pass * NIT : pre);
-    const uint32_t* pbits = EARLY ? ebits + pass * NIT : (PF ? pre_bits + pass * NIT : pre_bits);
+    if (!PF && (pre_on || pf_bits)) igemm_epi_load<TM, TN>(p, mb, nb, lane, pass, 1, pre, pre_bits);
+    const uint4* ppre = PF ? pre + pass * NIT : pre;
+    const uint32_t* pbits = PF ? pre_bits + pass * NIT : pre_bits;
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -321,239 +316,33 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
   }
 }
 
-// Register-direct (RD) epilogue.  The K loop ran with the MFMA operands swapped (weights as the
-// MFMA's A operand, activations as its B), so lane l = 16g + r of every 16x16 accumulator block
-// [i][j] holds FOUR CONSECUTIVE COLUMNS of one row: D[n = 16j + 4g + jj][m = 16i + r].
-//  1. One v_permlane16_swap per register pair of the column blocks (2q, 2q+1) (odd 16-lane rows
-//     of the first operand <-> even rows of the second) turns the 4-column runs into 8-column
-//     (16-byte) runs: lane (g, r) then holds columns 32q + cb(g) + 0..7 of row 16i + r,
-//     cb(g) = 16(g&1) + 8(g>>1), in acc[i][2q][0..3], acc[i][2q+1][0..3].
-//  2. One DPP row_ror:8 move per value exchanges run q = 1 of lane r < 8 with run q = 0 of lane
-//     r + 8: afterwards lane (g, r) holds run q = r >> 3 of rows 16i + (r & 7) and 16i + 8 + (r & 7)
-//     (acc[i][0..1] and acc[i][2..3]), so every store instruction writes 8 rows x 128 contiguous
-//     bytes (8 lanes per row: 4 groups x 2 runs) -- the store shape of the LDS-staged epilogue.
-//     (Without it, 16 rows x 64 B per instruction: measured 25-35 % slower on the short-K layers.)
-// Each lane then has ONE column set (8 scale / shift values, 8 column sums), and every chunk goes
-// through the same fused operations as the LDS-staged epilogue, stored straight from registers:
-// no LDS staging (64 ds_write_b32 + 16 ds_read_b128 per lane), no barriers, no epilogue LDS.
-// 4-wave tiles with 64-column wave tiles only (TN = 4); not for the train-mode BN sums.
-// Epilogue operands of the RD chunk layout: per-element operand (forward residual / dgrad
-// residual-gradient) and ReLU bits of chunk (i, h) = row 16i + 8h + r8 at this lane's 8 columns.
-// Branch-free and unconditional: exactly 2 * TM 16-byte + 2 * TM 1-byte loads per lane (row /
-// column clamped into the tensor, value zeroed; an unused operand reads the output's first
-// element), so a caller that counts its vector-memory operations (igemm_pk_kernel) can rely
-// on the number.
-template <int TM>
-__device__ __forceinline__ void igemm_rd_prefetch(const IgemmParams& p, int mb, int nb, int lane, uint4 (&pre)[TM][2],
-                                                  uint32_t (&pbits)[TM][2]) {
-  const int g = lane >> 4, r = lane & 15, r8 = r & 7;
-  const int gn = nb + 32 * (r >> 3) + 16 * (g & 1) + 8 * (g >> 1);
-  const bool col_ok = gn < p.Nn;
-  const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
-  const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
-  const bf16_t* psrc = pre_on ? (p.mode == EPI_FWD ? p.res : p.add) : reinterpret_cast<const bf16_t*>(p.out);
-  const long pld = pre_on ? (p.mode == EPI_FWD ? p.ld_res : p.ld_add) : 0;
-  const uint8_t* bsrc = pf_bits ? p.bits_mask : reinterpret_cast<const uint8_t*>(p.out);
-  const long bld = pf_bits ? p.ld_bits_mask : 0;
-  const int gc = col_ok ? gn : 0;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int gm = mb + 16 * i + 8 * h + r8;
-      const bool ok = gm < p.M && col_ok;
-      const long gr = gm < p.M ? gm : p.M - 1;
-      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + (pre_on ? gc : 0));
-      const uint32_t b = bsrc[gr * bld + (pf_bits ? (gc >> 3) : 0)];
-      pre[i][h] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
-      pbits[i][h] = (ok && pf_bits) ? b : 0u;
-    }
-}
-
-// EXT: the caller already prefetched the epilogue operands (igemm_rd_prefetch) into pre / pbits;
-// otherwise they are loaded here, after the shuffles.
-template <int TM, int TN, bool EXT = false>
-__device__ __forceinline__ void igemm_epilogue_rd(const IgemmParams& p, v4f (&acc)[TM][TN], int mb, int nb, int prow,
-                                                  int lane, uint4 (&pre)[TM][2], uint32_t (&pbits)[TM][2]) {
-  static_assert(TN == 4, "the RD epilogue exchanges the two 32-column runs of a 64-column wave tile");
-  const int g = lane >> 4, r = lane & 15, r8 = r & 7;
-  const int gn = nb + 32 * (r >> 3) + 16 * (g & 1) + 8 * (g >> 1);   // this lane's 8 columns
-  const bool col_ok = gn < p.Nn;
-  const int HoWo = p.Ho * p.Wo;
-  // rows of chunk (i, h): 16i + 8h + r8
-  const bool pf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
-  const bool pre_on = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * q][jj]),
-                                                         __float_as_uint(acc[i][2 * q + 1][jj]), false, false);
-        acc[i][2 * q][jj] = __uint_as_float(sw[0]);
-        acc[i][2 * q + 1][jj] = __uint_as_float(sw[1]);
-      }
-    // run q0 = acc[i][0..1], run q1 = acc[i][2..3]: lanes r >= 8 take run q1 of lane r - 8 into
-    // their first chunk, lanes r < 8 take run q0 of lane r + 8 into their second (DPP row_ror:8
-    // with the bank mask selecting the written half of each 16-lane row; the other half keeps
-    // its own value -- no selects, no extra live registers)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int c0 = __float_as_int(acc[i][j][jj]), c1 = __float_as_int(acc[i][2 + j][jj]);
-        acc[i][j][jj] = __int_as_float(__builtin_amdgcn_update_dpp(c0, c1, 0x128, 0xf, 0xc, false));      // row 16i + r8
-        acc[i][2 + j][jj] = __int_as_float(__builtin_amdgcn_update_dpp(c1, c0, 0x128, 0xf, 0x3, false));  // row 16i + 8 + r8
-      }
-  }
-  if constexpr (!EXT) {
-    if (pre_on || pf_bits) igemm_rd_prefetch<TM>(p, mb, nb, lane, pre, pbits);
-  }
-  float sc[8], sh[8];
-  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-  int ldo = p.ldo, col = gn;
-  bool relu = p.relu != 0, seg0 = true;
-  if (p.mode != EPI_DGRAD && col_ok) {
-    const float4* s4 = reinterpret_cast<const float4*>(p.scale + gn);
-    const float4* h4 = reinterpret_cast<const float4*>(p.shift + gn);
-    const float4 a = s4[0], b = s4[1], c = h4[0], d = h4[1];
-    sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
-    sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
-    if (p.out2 && gn >= p.n_split) {
-      out = reinterpret_cast<bf16_t*>(p.out2); ldo = p.ldo2; relu = p.relu2 != 0; col = gn - p.n_split;
-      seg0 = false;
-    }
-  }
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int gm = mb + 16 * i + 8 * h + r8;
-      if (gm >= p.M || !col_ok) continue;
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] = acc[i][2 * h][e]; v[4 + e] = acc[i][2 * h + 1][e]; }
-      if (p.mode == EPI_FWD) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
-        if (p.res) {
-          float rv[8];
-          unpack8(pre[i][h], rv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += rv[e];
-        }
-        if (relu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        const uint4 pk = pack8(v);
-        *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pk;
-        if (p.bits_out && seg0) p.bits_out[(long)gm * p.ld_bits_out + (col >> 3)] = (uint8_t)pos_bits8(pk);
-      } else if (p.mode == EPI_F32) {
-        float* o = reinterpret_cast<float*>(p.out) + (long)gm * p.ldo + gn;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
-        reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
-        reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
-      } else {  // EPI_DGRAD (same operations as igemm_epilogue)
-        long row = gm;
-        int n = 0, ii = 0, jw = 0;
-        if (p.up2) {
-          n = fdiv(gm, p.mg_howo); const int rem = gm - n * HoWo; ii = fdiv(rem, p.mg_wo); jw = rem - ii * p.Wo;
-          row = ((long)n * p.Hf + 2 * ii) * p.Wf + 2 * jw;
-        }
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          long rq = row;
-          if (qq > 0) {
-            if (p.up2 != 1) break;
-            const int hh = 2 * ii + (qq >> 1), ww = 2 * jw + (qq & 1);
-            if (hh >= p.Hf || ww >= p.Wf) continue;
-            rq = ((long)n * p.Hf + hh) * p.Wf + ww;
-          }
-          float w[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) w[e] = (qq == 0) ? v[e] : 0.f;
-          if (p.add) {
-            float av[8];
-            uint4 a4;
-            if (!p.up2) a4 = pre[i][h];
-            else a4 = *reinterpret_cast<const uint4*>(p.add + rq * p.ld_add + gn);
-            unpack8(a4, av);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) w[e] += av[e];
-          }
-          if (p.mask) {
-            float mv[8];
-            unpack8(*reinterpret_cast<const uint4*>(p.mask + rq * p.ld_mask + gn), mv);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
-          } else if (p.bits_mask) {
-            uint32_t byte;
-            if (pf_bits) byte = pbits[i][h];
-            else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
-          }
-          const uint4 pk = pack8(w);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) csum[e] += w[e];
-          *reinterpret_cast<uint4*>(out + rq * p.ldo + gn) = pk;
-          if (qq == 0 && p.up2 && p.out2)
-            *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out2) + (long)gm * p.ldo2 + gn) = pk;
-        }
-      }
-    }
-  // partial column sums: fold the 8 lanes (r8) sharing this lane's columns, then lane r8 == 0 of
-  // each (group, run) stores its 8 columns into the wave's partial row
-  if (p.colsum) {
-#pragma unroll
-    for (int o = 1; o < 8; o <<= 1)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) csum[e] += __shfl_xor(csum[e], o, 64);
-    if (r8 == 0 && col_ok) {
-      float4* dst = reinterpret_cast<float4*>(p.colsum + (long)prow * p.Nn + gn);
-      dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
-      dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
-    }
-  }
-}
-
-// Block tile BM x BN of NW waves, each wave a 64x64 tile of 16x16x32 MFMAs.
-//   NW = 4, NSTAGE 1/2: 2 blocks per CU, the next k-tile's LDS-DMA overlaps this tile's MFMAs.
-//   NW = 8 (256x128), NSTAGE 3: one 144 KiB block per CU, 2 waves per SIMD; a 3-deep LDS ring
-//   keeps two k-tiles in flight (counted vmcnt across a raw barrier) for compute-bound layers.
-//   NSTAGE 4: the 2-stage pipeline with the next tile's LDS-DMA issue spread over the MFMA
-//   groups (one piece per TN-MFMA group, pinned by sched barriers) instead of a burst of AI+BI
-//   issues at the top of the tile, during which the barrier-aligned waves of a SIMD all stall
-//   the matrix pipe together.
+// Block tile BM x BN (128x128 or 256x64) of 4 waves, each wave a 64x64 tile of 16x16x32 MFMAs.
+//   NSTAGE 1: one LDS buffer, 3 resident blocks per CU overlap each other's load and MFMA phases.
+//   NSTAGE 2: double buffer, the next k-tile's LDS-DMA overlaps this tile's MFMAs.
+// (Rejected and removed after per-layer A/B: an 8-wave 256x128 3-stage ring, an 8-wave 256x256
+// 2-stage tile, a 2-stage pipeline with the next tile's LDS-DMA interleaved into the MFMA groups,
+// an early epilogue-operand prefetch and a register-direct epilogue -- all neutral or slower,
+// profiles/r1_kbench_b1024_interleaved_issue.json, profiles/r3_hbm_bytes_per_layer.txt.  The
+// wide long-K layers run on igemm8_kernel below.)
 // PF: the epilogue's per-element operand (forward residual / dgrad residual-gradient `add`,
 // plus the dgrad ReLU bitmask) of the whole wave tile is loaded into registers before the
 // accumulators are staged through LDS, so its HBM latency overlaps the staging instead of
 // stalling every store iteration (short-K 1x1 layers are epilogue-bound).
-// WTM_: wave-tile rows (64, or 128 for the 256x256 tile: 8 waves as 2 x 4, 128x64 each).
 // SK: split-K slice instantiation (separate, so the unsplit kernels keep their register budget:
 // the slice bookkeeping compiled into every instantiation cost 33 VGPRs, occupancy 3 -> 2).
-// EPF: early epilogue-operand prefetch (igemm_epi_load issued right after the first k-tile's
-// LDS-DMA, so the residual / residual-gradient round trip overlaps the operand round trip).
-// RD: register-direct epilogue (igemm_epilogue_rd; MFMA operands swapped in the K loop).
-template <int BM, int BN, int NW, int NSTAGE, int AM, bool PF = false, int WTM_ = 64, bool BNZ = false, bool SK = false,
-          bool EPF = false, bool RD = false>
-__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParams p) {
-  constexpr int WTM = WTM_, WTN = 64;
+template <int BM, int BN, int NSTAGE, int AM, bool PF = false, bool BNZ = false, bool SK = false>
+__global__ void __launch_bounds__(256, IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParams p) {
+  constexpr int NW = 4, WTM = 64, WTN = 64;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int WAVES_N = BN / WTN;
   static_assert((BM / WTM) * (BN / WTN) == NW, "wave grid must cover the block tile");
-  static_assert(NSTAGE >= 1 && NSTAGE <= 4, "1- to 3-stage LDS pipeline (4: interleaved 2-stage)");
-  constexpr bool IL = NSTAGE == 4;
-  constexpr int NS = IL ? 2 : NSTAGE;   // LDS buffers
+  static_assert(NSTAGE == 1 || NSTAGE == 2, "1- or 2-stage LDS pipeline");
+  constexpr int NS = NSTAGE;   // LDS buffers
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // 1 KiB LDS-DMA pieces per wave per tile
   static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows must split evenly over the waves");
   constexpr int EPI_LD = WTN + 4;
-  constexpr int EPI_BYTES = RD ? 0 : NW * 32 * EPI_LD * 4;
+  constexpr int EPI_BYTES = NW * 32 * EPI_LD * 4;
   constexpr int SMEM = (NS * STAGE > EPI_BYTES) ? NS * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -673,7 +462,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
     for (int j = 0; j < AI + BI; ++j) load_piece(buf, j, delta);
     advance();
   };
-  constexpr int PPG = (AI + BI + 2 * TM - 1) / (2 * TM);   // IL: pieces issued per MFMA group
 
   v4f acc[TM][TN];
 #pragma unroll
@@ -684,31 +472,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
   const int a_off = (wm * WTM + (lane & 15)) * 128;
   const int b_off = (wn * WTN + (lane & 15)) * 128;
   load_tile(0);
-  constexpr int ENIT = 32 / (64 / (WTN / 8));
-  uint4 epre[EPF ? (TM / 2) * ENIT : 1];
-  uint32_t ebits[EPF ? (TM / 2) * ENIT : 1];
-  if constexpr (EPF) igemm_epi_load<TM, TN>(p, m0 + wm * WTM, n0 + wn * WTN, lane, 0, TM / 2, epre, ebits);
-  if (NSTAGE == 3) {
-    if (KT > 1) load_tile(1);
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int t = 0; t < KT; ++t) {
-    int cur;
-    if (NSTAGE == 3) {
-      // tile t landed (tile t+1 stays in flight across the raw barrier: a __syncthreads()
-      // would drain vmcnt), and every wave finished tile t-1, whose buffer takes tile t+2
-      if (t + 1 < KT) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(AI + BI) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      cur = t % 3;
-      if (t + 2 < KT) load_tile((t + 2) % 3);
-    } else {
-      cur = NS == 2 ? (t & 1) : 0;
-      if (NSTAGE == 2 && t + 1 < KT) load_tile(cur ^ 1);
-    }
-    const bool il_next = IL && t + 1 < KT;
-    const int il_delta = IL ? tile_delta() : 0;
+    const int cur = NS == 2 ? (t & 1) : 0;
+    if (NSTAGE == 2 && t + 1 < KT) load_tile(cur ^ 1);
     const char* As = smem + cur * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -720,33 +488,18 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const v8bf*>(Bs + b_off + j * 16 * 128 + pos);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (RD) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
-        if (IL) {
-#pragma unroll
-          for (int q = 0; q < PPG; ++q) {
-            const int jp = (kh * TM + i) * PPG + q;
-            if (jp < AI + BI && il_next) load_piece(cur ^ 1, jp, il_delta);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (il_next) advance();
     if (NSTAGE == 1 && t + 1 < KT) {
       __syncthreads();            // every wave is done reading the single buffer
       load_tile(0);
     }
-    if (NSTAGE != 3) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  if (NSTAGE == 3) __syncthreads();   // all fragment reads done before the epilogue reuses LDS
 
   if constexpr (SK) {   // split-K slice: the fp32 partial tile in fragment order (16-byte coalesced stores)
     float4* dst = reinterpret_cast<float4*>(p.slab) + ((long)(wg * ks + slice) * NW + wave) * (TM * TN) * 64 + lane;
@@ -758,17 +511,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : IGEMM_MIN_BLOCKS) igemm
     return;
   }
 
-  if constexpr (RD) {
-    uint4 pre[TM][2];
-    uint32_t pbits[TM][2];
-    igemm_epilogue_rd<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, lane, pre,
-                              pbits);
-    return;
-  }
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
   float* stage = reinterpret_cast<float*>(smem) + wave * (32 * (WTN + 4));
-  igemm_epilogue<TM, TN, PF || EPF, BNZ, EPF>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm,
-                                              stage, lane, epre, ebits);
+  igemm_epilogue<TM, TN, PF, BNZ>(p, acc, m0 + wm * WTM, n0 + wn * WTN, p.prow_begin + tm * (BM / WTM) + wm, stage,
+                                  lane);
 }
 
 
@@ -1404,9 +1150,6 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
 }
 
 int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wave tiles)
-int g_igemm_big = 0;       // 8-wave 256x128 3-stage tile: 0 never (default: measured slower on every
-                           // ResNet-50 layer, kbench A/B), 1 heuristic, 2 always (Nn > 64);
-                           // 256x256 8-wave tile: 3 heuristic (Nn, K >= 256), 4 always (Nn > 128)
 int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
 int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 layers with a residual / add
 int g_igemm8 = 2;          // 8-phase 256x256 kernel (igemm8_kernel) for Nn >= 256, K >= 256, Nn < 4K:
@@ -1416,17 +1159,10 @@ int g_igemm_ns1_kt = 1000; // single-stage tile for K <= 64 * this (default: eve
                            // end 2/4/8/16/36 -> 20.11k/20.42k/20.53k/20.76k/20.87k img/s: three
                            // resident single-buffer blocks per CU overlap each other's load and MFMA
                            // phases better than one block's double buffer does
-int g_igemm8_expand = 0;
 int g_igemm8_min_n = 512;  // ... and only for GEMM widths Nn >= this (with single-stage 128x128
-                           // tiles the 8-phase kernel wins only the stage-5 layers, kbench)  // A/B: also run the expansion 1x1s (Nn >= 4K) on the 8-phase kernel
+                           // tiles the 8-phase kernel wins only the stage-5 layers, kbench)
 int g_igemm8_min_tiles = 128;   // ... when the problem has at least this many 256x256 tiles
-int g_igemm8_ragged = 0;   // 1: 8-phase tiles also for widths that are not a multiple of 256 (conv3_block1
-                           // c1+shortcut, Nn = 640: 680 us vs 588 us on five 128-wide tiles; not kept)
 int g_igemm_n64 = 1;       // see igemm_config (1: conv2_block1 c1+c0 fwd 831 -> 765 us; 2: no further gain)
-int g_igemm_il = 0;        // 2-stage tiles issue the next tile's LDS-DMA interleaved with the MFMAs:
-                           // off (measured -3..-12% on the compute-bound layers, -2.5% end to end;
-                           // profiles/r1_kbench_b1024_interleaved_issue.json) -- the later issue
-                           // shortens each piece's latency window more than the burst costs
 
 static bool igemm_no_halo(const IgemmParams& p) {
   return p.pad == 0 && (p.Ho - 1) * p.stride + p.R <= p.H && (p.Wo - 1) * p.stride + p.S <= p.W;
@@ -1465,8 +1201,7 @@ static bool igemm_check(const IgemmParams& p, const char** why) {
 }
 
 // Tile configuration of a problem: 0 = 256x64 / 4 waves (Nn <= 64), 1 = 128x128 / 4 waves,
-// 2 = 256x128 / 8 waves / 3-stage ring, 3 = 256x256 / 8 waves of 128x64 / 2-stage (half the
-// LDS-DMA pieces per MFMA of the 128x128 tile; for wide, long-K layers).
+// 4 = the 8-phase 256x256 kernel (igemm8_kernel; wide, long-K layers).
 static int igemm_config(int M, int Nn, int K) {
   if (Nn <= 64) return 0;
   // A/B knob: 256x64 tiles for widths that are not a multiple of 128 (1: conv2_block1's
@@ -1478,22 +1213,19 @@ static int igemm_config(int M, int Nn, int K) {
   // conv1 dgrad), whose short K loop is dominated by an epilogue that streams a residual /
   // residual gradient: measured 30-40% slower there than the 2-block 128x128 tile with the
   // epilogue-operand prefetch (per-layer A/B, profiles/r2_igemm8_per_layer_ab.txt)
-  if (g_igemm8 && Nn >= g_igemm8_min_n && K >= 256 && (Nn < 4 * K || g_igemm8_expand) &&
-      (g_igemm8_ragged || Nn % 256 == 0) &&
+  // (widths that are not a multiple of 256 stay on the 128x128 tile: conv3_block1 c1 + shortcut,
+  // Nn = 640, measured 680 us on 8-phase tiles vs 588 us on five 128-wide tiles)
+  if (g_igemm8 && Nn >= g_igemm8_min_n && K >= 256 && Nn < 4 * K && Nn % 256 == 0 &&
       (long)((M + 255) / 256) * ((Nn + 255) / 256) >= g_igemm8_min_tiles)
     return 4;
-  if (g_igemm_big == 4 && Nn > 128) return 3;   // forced (equivalence tests)
-  if (g_igemm_big == 3 && Nn >= 256 && K >= 256 && (long)((M + 255) / 256) * ((Nn + 255) / 256) >= 256) return 3;
-  const long big_tiles = (long)((M + 255) / 256) * ((Nn + 127) / 128);
-  if (g_igemm_big == 2 || (g_igemm_big == 1 && K >= 256 && big_tiles >= 512)) return 2;
   return 1;
 }
 static int igemm_bm(int cfg) { return cfg == 1 ? 128 : 256; }
-static int igemm_wtm(int cfg) { return cfg == 3 ? 128 : 64; }   // (cfg 4: 64-row partial-row groups)
 
+// partial column-sum rows of m output rows: one per 64-row wave group (cfg 4: 64-row groups too)
 static int igemm_rows_of(int cfg, int m) {
   const int BM = igemm_bm(cfg);
-  return ((m + BM - 1) / BM) * (BM / igemm_wtm(cfg));
+  return ((m + BM - 1) / BM) * (BM / 64);
 }
 
 int num_cus() {
@@ -1516,18 +1248,12 @@ int num_cus() {
 struct IgemmPlan { int cfg, split, ks; };
 
 int g_igemm_splitk = 1;
-int g_igemm_epf = 0;       // early epilogue-operand prefetch for the short-K single-stage tiles (A/B knob)
 int g_igemm_pk = 2;        // persistent ring kernel (igemm_pk_kernel) for the short-K 1x1 layers:
                            // 0 off, else the ring depth NB (2: two 68 KiB blocks per CU; 3, 4: one
                            // 128 KiB+ block per CU, measured 5-7 % slower end to end)
 int g_igemm_pk_all = 0;    // 0: only where it measured faster (dgrads with a residual-gradient add:
                            // -10..-18 % per layer; forwards with a residual and K >= 128: -4..-10 %);
                            // 1: every eligible layer (K = 64 forwards +5 %, no-residual ones +5..8 %)
-int g_igemm_rd = 0;        // register-direct epilogue on the 4-wave tiles (igemm_epilogue_rd): 0 off,
-                           // 1 on (every unsplit cfg 0 / 1 launch without train-BN sums).  Off: its
-                           // stores put consecutive lanes on different rows, and the resulting 16 B
-                           // partial-line writes cost a second read + write of the output through
-                           // the fabric (WRITE_SIZE / FETCH_SIZE, profiles/r3_hbm_bytes_per_layer.txt)
 
 // Split-K for layers with too few output tiles to fill the chip (small batches, small spatial
 // stages: stage 5 at batch 32-256, crop 160): the 4-wave tiles stay resident 2-3 per CU, so a
@@ -1680,19 +1406,18 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
   const int KT = p.K / 64;
   int ns = g_igemm_variant;
   if (ns == 0) ns = KT <= g_igemm_ns1_kt ? 1 : 2;
-  const bool il = g_igemm_il && ns == 2;
   const int am = p.a2 ? AM_DUAL : (igemm_no_halo(p) ? AM_DIRECT : AM_HALO);
   // (explicit launches per instantiation: taking kernel addresses through a conditional
   // expression leaves the host stubs uninstantiated with this compiler)
-#define IG_GO(BM_, BN_, NW_, NS_, AM_) \
-  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, NW_, NS_, AM_>), dim3(nwg), dim3(NW_ * 64), 0, stream, p)
-#define IG_MODES(BM_, BN_, NW_, NS_)                                 \
-  {                                                                  \
-    if (am == AM_DIRECT) IG_GO(BM_, BN_, NW_, NS_, AM_DIRECT);       \
-    else if (am == AM_HALO) IG_GO(BM_, BN_, NW_, NS_, AM_HALO);      \
-    else IG_GO(BM_, BN_, NW_, NS_, AM_DUAL);                         \
+#define IG_GO(BM_, BN_, NS_, AM_) \
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, NS_, AM_>), dim3(nwg), dim3(256), 0, stream, p)
+#define IG_MODES(BM_, BN_, NS_)                                 \
+  {                                                             \
+    if (am == AM_DIRECT) IG_GO(BM_, BN_, NS_, AM_DIRECT);       \
+    else if (am == AM_HALO) IG_GO(BM_, BN_, NS_, AM_HALO);      \
+    else IG_GO(BM_, BN_, NS_, AM_DUAL);                         \
   }
-  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : (cfg >= 3 ? 256 : 128);
+  const int BM = igemm_bm(cfg), BN = cfg == 0 ? 64 : (cfg == 4 ? 256 : 128);
   const int nwg = ((p.M - p.m_begin + BM - 1) / BM) * ((p.Nn + BN - 1) / BN) * (p.ksplit > 1 ? p.ksplit : 1);
   // PF where the prefetched operand exists for every element (forward residual; dgrad
   // residual-gradient without the stride-2 scatter).  Measured (bench/epilogue.py, b1024,
@@ -1701,7 +1426,7 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
   // VGPRs cut from 3 to 2 waves per SIMD -- so dgrad uses it only on 2-stage tiles.
   if (p.ksplit > 1) {   // split-K slices (cfg 0 / 1, single source; igemm_launch)
 #define IG_SK(BM_, BN_, NS_, AM_) \
-  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_, false, 64, false, true>), dim3(nwg), dim3(256), 0, stream, p)
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, NS_, AM_, false, false, true>), dim3(nwg), dim3(256), 0, stream, p)
     if (cfg == 1) {
       if (ns == 1) { if (am == AM_DIRECT) IG_SK(128, 128, 1, AM_DIRECT); else IG_SK(128, 128, 1, AM_HALO); }
       else { if (am == AM_DIRECT) IG_SK(128, 128, 2, AM_DIRECT); else IG_SK(128, 128, 2, AM_HALO); }
@@ -1712,42 +1437,11 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
 #undef IG_SK
     return;
   }
-  if (g_igemm_rd && cfg <= 1 && !p.stats && !p.bn_z && !il && !g_igemm_epf) {
-#define IG_RD(BM_, BN_, NS_, AM_) \
-  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_, false, 64, false, false, false, true>), dim3(nwg), dim3(256), 0, \
-                     stream, p)
-#define IG_RD_MODES(BM_, BN_, NS_)                              \
-  {                                                             \
-    if (am == AM_DIRECT) IG_RD(BM_, BN_, NS_, AM_DIRECT);       \
-    else if (am == AM_HALO) IG_RD(BM_, BN_, NS_, AM_HALO);      \
-    else IG_RD(BM_, BN_, NS_, AM_DUAL);                         \
-  }
-    if (cfg == 1) {
-      if (ns == 1) IG_RD_MODES(128, 128, 1) else IG_RD_MODES(128, 128, 2)
-    } else {
-      if (ns == 1) IG_RD_MODES(256, 64, 1) else IG_RD_MODES(256, 64, 2)
-    }
-#undef IG_RD_MODES
-#undef IG_RD
-    return;
-  }
-  // early prefetch (knob igemm_epf: 1 = single-stage tiles with a residual / residual-gradient
-  // operand, K <= 256; 2 = also the ReLU-bits-only dgrads)
-  const bool epf_op = (p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2);
-  const bool epf_bits = p.mode == EPI_DGRAD && !p.up2 && !p.mask && p.bits_mask;
-  if (g_igemm_epf && am == AM_DIRECT && cfg <= 1 && ns == 1 && KT <= 4 && (epf_op || (g_igemm_epf == 2 && epf_bits))) {
-#define IG_EPF(BM_, BN_) \
-  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, 1, AM_DIRECT, false, 64, false, false, true>), dim3(nwg), dim3(256), 0, \
-                     stream, p)
-    if (cfg == 1) IG_EPF(128, 128); else IG_EPF(256, 64);
-#undef IG_EPF
-    return;
-  }
   const bool pf = g_igemm_pf && am == AM_DIRECT && cfg <= 1 &&
                   ((p.mode == EPI_FWD && p.res) || (p.mode == EPI_DGRAD && p.add && !p.up2 && (ns == 2 || g_igemm_pf == 2)));
   if (p.bn_z) {   // (igemm_check: DGRAD, no dual source; plan: cfg 0 / 1)
 #define IG_Z(BM_, BN_, AM_) \
-  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, 1, AM_, false, 64, true>), dim3(nwg), dim3(256), 0, stream, p)
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 1, AM_, false, true>), dim3(nwg), dim3(256), 0, stream, p)
     if (cfg == 0) {
       if (am == AM_DIRECT) IG_Z(256, 64, AM_DIRECT); else IG_Z(256, 64, AM_HALO);
     } else {
@@ -1766,26 +1460,17 @@ static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream) 
 #undef IG_8
   } else if (pf) {
 #define IG_PF(BM_, BN_, NS_) \
-  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, 4, NS_, AM_DIRECT, true>), dim3(nwg), dim3(256), 0, stream, p)
+  hipLaunchKernelGGL((igemm_kernel<BM_, BN_, NS_, AM_DIRECT, true>), dim3(nwg), dim3(256), 0, stream, p)
     if (cfg == 1) {
-      if (ns == 1) IG_PF(128, 128, 1); else if (il) IG_PF(128, 128, 4); else IG_PF(128, 128, 2);
+      if (ns == 1) IG_PF(128, 128, 1); else IG_PF(128, 128, 2);
     } else {
-      if (ns == 1) IG_PF(256, 64, 1); else if (il) IG_PF(256, 64, 4); else IG_PF(256, 64, 2);
+      if (ns == 1) IG_PF(256, 64, 1); else IG_PF(256, 64, 2);
     }
 #undef IG_PF
-  } else if (cfg == 3) {
-#define IG_W(AM_) \
-  hipLaunchKernelGGL((igemm_kernel<256, 256, 8, 2, AM_, false, 128>), dim3(nwg), dim3(512), 0, stream, p)
-    if (am == AM_DIRECT) IG_W(AM_DIRECT);
-    else if (am == AM_HALO) IG_W(AM_HALO);
-    else IG_W(AM_DUAL);
-#undef IG_W
-  } else if (cfg == 2) {
-    IG_MODES(256, 128, 8, 3)
   } else if (cfg == 1) {
-    if (ns == 1) IG_MODES(128, 128, 4, 1) else if (il) IG_MODES(128, 128, 4, 4) else IG_MODES(128, 128, 4, 2)
+    if (ns == 1) IG_MODES(128, 128, 1) else IG_MODES(128, 128, 2)
   } else {
-    if (ns == 1) IG_MODES(256, 64, 4, 1) else if (il) IG_MODES(256, 64, 4, 4) else IG_MODES(256, 64, 4, 2)
+    if (ns == 1) IG_MODES(256, 64, 1) else IG_MODES(256, 64, 2)
   }
 #undef IG_MODES
 #undef IG_GO

@@ -51,10 +51,10 @@ int igemm_partial_rows(int M, int Nn, int K, bool bnz = false);   // rows of the
 void igemm_plan_query(int M, int Nn, int K, int* cfg, int* split, int* ksplit = nullptr);   // tile config;
                                                     // rows >= split: 128x128 tail; ksplit: K slices (split-K)
 long igemm_splitk_floats(int M, int Nn, int K);     // split-K workspace a problem wants (0: no split)
-extern int g_igemm8, g_igemm8_min_tiles, g_igemm8_expand, g_igemm8_min_n, g_igemm_ns1_kt, g_wgrad8, g_wgrad1;
+extern int g_igemm8, g_igemm8_min_tiles, g_igemm8_min_n, g_igemm_ns1_kt, g_wgrad8, g_wgrad1;
 int num_cus();   // compute units of the current device (cached)
-extern int g_igemm_splitk, g_wgrad8_min_rows, g_igemm_epf, g_igemm_rd, g_igemm_pk, g_igemm_pk_all;   // split-K: 0 off, 1 heuristic (default), >= 2 forced slices (where legal)
-extern int g_igemm8_ragged, g_stem_variant, g_igemm_n64, g_igemm_variant, g_igemm_deep, g_igemm_big, g_igemm_pf, g_igemm_il, g_wgrad_variant, g_pool_variant, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
+extern int g_igemm_splitk, g_wgrad8_min_rows, g_igemm_pk, g_igemm_pk_all;   // split-K: 0 off, 1 heuristic (default), >= 2 forced slices (where legal)
+extern int g_stem_variant, g_igemm_n64, g_igemm_variant, g_igemm_deep, g_igemm_pf, g_wgrad_variant, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
 
 struct WgradParams {
   const uint16_t* x; int N, H, W, C;   // conv input, NHWC (or [M][ldx] rows for 1x1/s1)

@@ -52,7 +52,7 @@ def _load():
 
 
 def _apply_knobs(mod):
-    """PDDL_KNOBS="igemm_il=1,igemm_big=3": kernel tuning knobs for A/B runs of whole
+    """PDDL_KNOBS="igemm8=1,igemm_pk=0": kernel tuning knobs for A/B runs of whole
     programs (bench.py, the entry scripts) without code changes."""
     spec = os.environ.get("PDDL_KNOBS", "").strip()
     for item in filter(None, (x.strip() for x in spec.split(","))):

@@ -82,9 +82,10 @@ class FlatOptimizer:
         if s != ov["upto"] or s % 4 or (e - s) % 4 or e > self.n:
             return                       # (not contiguous / not 16-byte aligned: left for the end)
         main = torch.cuda.current_stream(self.params.device)
-        ev = torch.cuda.Event()
-        ev.record(main)
-        ov["stream"].wait_event(ev)
+        if main != ov["stream"]:   # (a two-stream engine runs the callback on the update stream
+            ev = torch.cuda.Event()  # itself; a self-wait inside a graph capture crashes capture_end)
+            ev.record(main)
+            ov["stream"].wait_event(ev)
         with torch.cuda.stream(ov["stream"]):
             self._update_range(s, e)
         ov["upto"] = e

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/ov
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -k "stem_pool" > $OUT/kt.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread > $OUT/kt.log 2>&1
 rc=$?; grep -E "FAIL|Error|passed|failed|assert" $OUT/kt.log | tail -8
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32.py -x -v --timeout 120 --timeout-method thread > $OUT/f32.log 2>&1
@@ -37,6 +37,4 @@ run b1024 X=1 -- --batch 1024 --steps 12 --warmup 4 && \
 run b2560 X=1 -- --steps 12 --warmup 4 && \
 run b2560_ov0 PDDL_OVERLAP_OPT=0 -- --steps 12 --warmup 4
 rc=$?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof2560 -o run --output-format csv -- python bench.py --steps 3 --warmup 2 > $OUT/prof2560.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof32 -o run --output-format csv -- python bench.py --batch 32 --steps 10 --warmup 5 > $OUT/prof32.log 2>&1
 exit $rc

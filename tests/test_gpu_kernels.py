@@ -145,19 +145,16 @@ def test_igemm_dgrad(case):
     assert rel(cs, ref.sum((0, 1, 2))) < 1e-2
 
 
-KNOB_DEFAULTS = {"igemm_pk": 2}
+KNOB_DEFAULTS = {"igemm_pk": 2, "igemm_pf": 1}
 
 
-@pytest.mark.parametrize("knob,big", [("igemm_big", 2), ("igemm_big", 4), ("igemm_il", 1), ("igemm8", 1),
-                                      ("igemm8", 2), ("igemm", 2), ("igemm_epf", 1), ("igemm_epf", 2),
-                                      ("igemm_rd", 1)])
+@pytest.mark.parametrize("knob,big", [("igemm8", 1), ("igemm8", 2), ("igemm", 2), ("igemm_pf", 2)])
 @pytest.mark.parametrize("kind", ["fwd3x3", "fwd1x1res", "dgrad_up2_dual", "fwd1x1resid", "dgrad1x1add"])
 def test_igemm_big_tile_matches(kind, knob, big):
-    """The 8-wave 256x128 3-stage (igemm_big 2) and 256x256 2-stage (igemm_big 4)
-    configurations, the interleaved-issue 2-stage pipeline (igemm_il 1) and the 8-phase
-    256x256 kernel (igemm8 1, with the wave-row stagger 2) compute the same result (same k
-    order) as the 4-wave 128x128 one, including the fused epilogues and the per-wave
-    column-sum rows."""
+    """The 8-phase 256x256 kernel (igemm8 1, with the wave-row stagger 2), the forced 2-stage
+    pipeline (igemm 2) and the epilogue-operand prefetch on single-stage dgrads (igemm_pf 2)
+    compute the same result (same k order) as the default 4-wave 128x128 tile, including the
+    fused epilogues and the per-wave column-sum rows."""
     torch.manual_seed(12)
     n, h, ho = 3, 14, 7
     if kind == "fwd3x3":
@@ -501,18 +498,13 @@ def test_operands_beyond_2gib(case):
     assert rel(dw, ref.permute(0, 2, 3, 1).reshape(co, -1)) < 5e-3
 
 
-@pytest.mark.parametrize("variant,h,c", [(0, 12, 64), (0, 13, 64), (1, 12, 64), (1, 13, 64), (2, 13, 64),
-                                         (3, 12, 64), (3, 18, 64), (4, 12, 64), (4, 13, 64), (4, 35, 64),
-                                         (4, 13, 128), (4, 18, 256)])
-def test_maxpool_and_gap(variant, h, c):
-    """Max pool (pad 1, 3x3/s2; row-streaming, strip / block kernels and the per-pixel ones)
-    against PyTorch, including odd sizes, partial column bands and a partial last strip, then GAP."""
+@pytest.mark.parametrize("h,c", [(12, 64), (13, 64), (35, 64), (13, 128), (18, 256), (12, 32), (13, 8)])
+def test_maxpool_and_gap(h, c):
+    """Max pool (pad 1, 3x3/s2; the row-streaming kernels for C = 64 / 128 / 256, the per-output
+    and per-pixel ones otherwise) against PyTorch, including odd sizes and partial column bands,
+    then GAP."""
     torch.manual_seed(6)
-    N().set_variant("pool", variant)
-    try:
-        _maxpool_gap(h, c)
-    finally:
-        N().set_variant("pool", 4)
+    _maxpool_gap(h, c)
 
 
 def _maxpool_gap(h, c):
