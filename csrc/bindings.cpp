@@ -510,6 +510,56 @@ void stem_pool_bwd(Tensor x2, Tensor gpool, Tensor idx, Tensor dw, Tensor colsum
   p.colsum = f32p(colsum);
   ok(pddl::stem_pool_bwd_launch(p, cur_stream()), "stem_pool_bwd");
 }
+// 3x3 / pad 1 / stride 1 convolution 64 -> 64 on the persistent pixel-ring kernel.
+// mode 0 (forward): out = relu(conv(x, w) * scale + shift), bits = its ReLU bits (optional);
+// mode 1 (data gradient): out = conv(x, w) masked by `bits` (input ReLU bits, required),
+// colsum = partial rows [conv3x3c64_partial_rows(M), 64] of out's column sums (optional).
+void conv3x3c64(Tensor x, Tensor w, int64_t mode, Tensor out, OptT scale, OptT shift, OptT bits, OptT colsum) {
+  PCHECK(x.dim() == 4 && x.size(3) == 64 && x.is_contiguous() && x.scalar_type() == torch::kBFloat16,
+         "conv3x3c64: x [N,H,W,64] bf16 contiguous");
+  PCHECK(out.sizes() == x.sizes() && out.is_contiguous() && out.scalar_type() == torch::kBFloat16,
+         "conv3x3c64: out like x");
+  PCHECK(w.dim() == 2 && w.size(0) == 64 && w.size(1) == 576 && w.stride(1) == 1 && w.stride(0) == 576,
+         "conv3x3c64: w [64,576] contiguous rows");
+  pddl::C64Params p{};
+  p.x = bfp(x); p.w = bfp(w); p.out = bfpm(out);
+  p.N = (int)x.size(0); p.H = (int)x.size(1); p.W = (int)x.size(2);
+  PCHECK((int64_t)p.N * p.H * p.W < (1LL << 30), "conv3x3c64: too many pixels");
+  p.M = p.N * p.H * p.W;
+  if (bits.has_value())
+    PCHECK(bits->scalar_type() == torch::kUInt8 && bits->is_contiguous() && bits->numel() == (int64_t)p.M * 8,
+           "conv3x3c64: bits [N,H,W,8] uint8");
+  if (mode == pddl::C64_FWD) {
+    PCHECK(scale.has_value() && shift.has_value() && scale->numel() >= 64 && shift->numel() >= 64,
+           "conv3x3c64: forward needs 64 scale / shift values");
+    PCHECK((reinterpret_cast<uintptr_t>(scale->data_ptr()) & 15) == 0 &&
+           (reinterpret_cast<uintptr_t>(shift->data_ptr()) & 15) == 0, "conv3x3c64: 16-byte aligned scale / shift");
+    p.scale = f32p(*scale); p.shift = f32p(*shift);
+    p.bits_out = bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr;
+  } else {
+    PCHECK(mode == pddl::C64_DGRAD && bits.has_value(), "conv3x3c64: mode 1 needs the ReLU bits");
+    p.bits_mask = bits->data_ptr<uint8_t>();
+    if (colsum.has_value()) {
+      PCHECK(colsum->numel() >= (int64_t)pddl::conv3x3c64_partial_rows(p.M) * 64,
+             "conv3x3c64: colsum needs conv3x3c64_partial_rows x 64 floats");
+      p.colsum = f32p(*colsum);
+    }
+  }
+  ok(pddl::conv3x3c64_launch(p, (int)mode, cur_stream()), "conv3x3c64");
+}
+// Weight gradient of the 64 -> 64 3x3 / pad 1 conv: dw [64, >=576] fp32 += (x, g) correlation.
+void conv3x3c64_wgrad(Tensor x, Tensor g, Tensor dw) {
+  PCHECK(x.dim() == 4 && x.size(3) == 64 && x.is_contiguous() && x.scalar_type() == torch::kBFloat16,
+         "conv3x3c64_wgrad: x [N,H,W,64] bf16 contiguous");
+  PCHECK(g.sizes() == x.sizes() && g.is_contiguous() && g.scalar_type() == torch::kBFloat16,
+         "conv3x3c64_wgrad: g like x");
+  PCHECK(dw.dim() == 2 && dw.size(0) == 64 && dw.size(1) >= 576 && dw.stride(1) == 1 &&
+         dw.scalar_type() == torch::kFloat32, "conv3x3c64_wgrad: dw [64, >=576] fp32 rows");
+  pddl::C64WgradParams p{};
+  p.x = bfp(x); p.g = bfp(g); p.dw = f32p(dw); p.ld_dw = (int)dw.stride(0);
+  p.N = (int)x.size(0); p.H = (int)x.size(1); p.W = (int)x.size(2);
+  ok(pddl::conv3x3c64_wgrad_launch(p, cur_stream()), "conv3x3c64_wgrad");
+}
 void maxpool_bwd(Tensor gy, Tensor idx, OptT xmask, Tensor gx, OptT colsum) {
   ok(pddl::maxpool_bwd_launch(bfp(gy), idx.data_ptr<uint8_t>(), obfp(xmask), bfpm(gx), (int)gx.size(0),
                               (int)gx.size(1), (int)gx.size(2), (int)gx.size(3), (int)gy.size(1), (int)gy.size(2),
@@ -706,6 +756,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_pool_fwd", &stem_pool_fwd, REL, py::arg("x2"), py::arg("w"), py::arg("scale"), py::arg("shift"),
         py::arg("pool"), py::arg("idx"), py::arg("bits") = py::none(), py::arg("pool_rows") = 0);
   m.def("maxpool_bwd", &maxpool_bwd, REL);
+  m.def("conv3x3c64", &conv3x3c64, REL, py::arg("x"), py::arg("w"), py::arg("mode"), py::arg("out"),
+        py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("bits") = py::none(),
+        py::arg("colsum") = py::none());
+  m.def("conv3x3c64_wgrad", &conv3x3c64_wgrad, REL, py::arg("x"), py::arg("g"), py::arg("dw"));
+  m.def("conv3x3c64_partial_rows", [](int64_t M) { return pddl::conv3x3c64_partial_rows((int)M); });
   m.def("gap_fwd", &gap_fwd, REL);
   m.def("gap_bwd", &gap_bwd, REL);
   m.def("colsum", &colsum, REL);
@@ -729,6 +784,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
     else if (which == "conv_f32") pddl::g_conv_f32_variant = v;
+    else if (which == "c64_grid") pddl::g_c64_grid = v;
+    else if (which == "c64w_grid") pddl::g_c64w_grid = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;

@@ -1,0 +1,467 @@
+// Persistent pixel-ring 3x3 convolution for the 64-channel stage (ResNet-50 conv2_block*_2:
+// 56x56x64 -> 64, pad 1, stride 1), forward and data gradient (gfx950).
+//
+// The generic implicit GEMM (igemm.hip) gathers every one of the nine taps of a 256-row tile
+// from L2: 9 x 32 KiB of A per tile for 2 x 256 x 64 x 576 FLOP, plus the 72 KiB weight matrix
+// per tile, and runs these layers at 620-690 TF/s (0.87 / 0.95 ms at b2560, forward / dgrad)
+// while their HBM floor -- read 1 GB, write 1 GB -- is ~0.4 ms.  Here:
+//   * one workgroup per CU owns a contiguous range of 256-pixel tiles; the whole 64 x 576
+//     weight matrix stays resident in LDS (72 KiB, loaded once per workgroup);
+//   * the input pixels stream through a 640-pixel LDS ring (80 KiB): a tile at m0 reads pixels
+//     [m0 - W - 1, m0 + 256 + W + 1) -- every tap of every row is a shifted view of the ring, so
+//     each input pixel crosses L2 -> LDS once instead of nine times; the next tile's 256 new
+//     pixels are LDS-DMA'd while this tile computes (ring slots [m0 + 320, m0 + 576));
+//   * taps that fall outside the image (padding) are zeroed by a per-row 9-bit tap mask on the
+//     fragment, the ring read itself is always in range;
+//   * the MFMAs run with the weights as the A operand, so a lane ends with 4 consecutive output
+//     channels of one pixel: the epilogue (BN scale/shift + ReLU + ReLU bits forward; ReLU-bit
+//     mask + per-channel column sums for the data gradient) runs in fp32 registers and is staged
+//     as bf16 through a 2 KiB per-wave LDS slice into 1 KiB fully contiguous row stores.
+// LDS: 73,728 (weights) + 81,920 (ring) + 8,192 (epilogue slices) = 163,840 B, one 256-thread
+// workgroup per CU (one wave per SIMD).
+// Reference: the Keras Conv2D(64, 3, padding='same') of every conv2 bottleneck block behind
+// keras.applications.ResNet50 (imagenet-resnet50.py:56).
+#include "common.h"
+#include "kernels.h"
+
+namespace pddl {
+
+namespace {
+constexpr int C64_BM = 256;                 // output pixels per tile (4 waves x 64)
+constexpr int C64_RING = 640;               // ring slots (pixels); 128 B each
+constexpr int C64_AHEAD = 64;               // >= W + 1, multiple of 8
+constexpr int C64_W_BYTES = 9 * 64 * 128;   // 73,728
+constexpr int C64_RING_BYTES = C64_RING * 128;
+constexpr int C64_STAGE_BYTES = 2048;       // per wave
+constexpr int C64_LDS = C64_W_BYTES + C64_RING_BYTES + 4 * C64_STAGE_BYTES;
+static_assert(C64_LDS <= 163840, "LDS budget");
+// the current window [m0 - AHEAD, m0 + BM + AHEAD) plus the next tile's new pixels
+static_assert(C64_RING >= 2 * C64_BM + 2 * C64_AHEAD, "ring too small");
+}  // namespace
+
+// Logical 16-byte chunk `c` of LDS row `row` ([rows][128 B] images) sits at chunk c ^ f(row):
+// 16 consecutive rows at one logical chunk hit 16 distinct 16-B slots (igemm.hip sw_chunk).
+__device__ __forceinline__ int c64_sw(int row) { return (row >> 1) & 7; }
+
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) conv3x3c64_kernel(C64Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wl = smem;
+  char* ring = smem + C64_W_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* stage = smem + C64_W_BYTES + C64_RING_BYTES + wave * C64_STAGE_BYTES;
+  const int T = (p.M + C64_BM - 1) / C64_BM;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int t_begin = (int)((long)g * T / G), t_end = (int)((long)(g + 1) * T / G);
+  if (t_begin >= t_end) return;   // (whole workgroup; the host sizes G <= T)
+  const int m_start = t_begin * C64_BM;
+  const int rb = m_start - C64_AHEAD;   // pixel held by ring slot 0
+  const long pbase = rb > 0 ? rb : 0;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, pbase * 64, (long)p.M * 64);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, 64 * 576 * 2);
+  const int HW = p.H * p.W;
+
+  // ---- weights -> LDS, tap-major images [tap][n][128 B] (72 pieces of 8 rows, 18 per wave)
+#pragma unroll
+  for (int q = 0; q < 18; ++q) {
+    const int pc = wave * 18 + q;              // piece: tap = pc / 8, rows n = 8 (pc % 8) + lane / 8
+    const int tap = pc >> 3, n = (pc & 7) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ c64_sw(n);     // logical chunk carried by this lane-linear slot
+    buf_lds16(rw, LDS_PTR(wl + pc * 1024), (uint32_t)((n * 576 + tap * 64 + ch * 8) * 2), 0);
+  }
+  // ring piece: 8 pixels [p0, p0 + 8) (p0 - rb a multiple of 8) into their ring slots
+  auto ring_piece = [&](int p0) {
+    int slot0 = (p0 - rb) % C64_RING;
+    const int pix = p0 + (lane >> 3);
+    const int slot = slot0 + (lane >> 3);
+    const int ch = (lane & 7) ^ c64_sw(slot);
+    const uint32_t off = (pix >= 0 && pix < p.M) ? (uint32_t)(((long)(pix - pbase) * 64 + ch * 8) * 2) : OOB_OFF;
+    buf_lds16(rx, LDS_PTR(ring + slot0 * 128), off, 0);
+  };
+  // first window: pixels [m_start - 64, m_start + 320): 48 pieces, 12 per wave
+#pragma unroll
+  for (int q = 0; q < 12; ++q) ring_piece(rb + (wave * 12 + q) * 8);
+
+  // epilogue constants: this lane's 4 channels in each 16-channel block jb: 16 jb + 4 (lane>>4) + e
+  const int cq = 4 * (lane >> 4);
+  float sc[4][4], sh[4][4];
+  if (MODE == C64_FWD) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      const float4 a = *reinterpret_cast<const float4*>(p.scale + 16 * jb + cq);
+      const float4 b = *reinterpret_cast<const float4*>(p.shift + 16 * jb + cq);
+      sc[jb][0] = a.x; sc[jb][1] = a.y; sc[jb][2] = a.z; sc[jb][3] = a.w;
+      sh[jb][0] = b.x; sh[jb][1] = b.y; sh[jb][2] = b.z; sh[jb][3] = b.w;
+    }
+  }
+  float csum[4][4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[jb][e] = 0.f;
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int r16 = lane & 15;
+  const int kq = lane >> 4;
+  // tap offsets (pixels) of (r, s): (r - 1) W + (s - 1)
+  const int dW = p.W;
+  // vmcnt younger than a tile's ring pieces when the next tile starts: the previous tile's
+  // stores, 2 row stores (+ 2 ReLU-bit stores) per 16-row block
+  const bool bits_st = MODE == C64_FWD && p.bits_out != nullptr;
+  int slot_m0 = C64_AHEAD;   // ring slot of this tile's pixel m0
+  for (int t = t_begin; t < t_end; ++t) {
+    const int m0 = t * C64_BM;
+    if (t > t_begin) {
+      // this tile's ring pieces landed (only the previous tile's stores may be outstanding),
+      // and every wave finished the previous tile, whose slots the next DMA overwrites
+      if (bits_st) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // DGRAD: this tile's ReLU-bit rows (pixel 16 i + r16 of the wave, 8 bytes = 64 channels)
+    uint2 mbits[4];
+    if (MODE == C64_DGRAD) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wave * 64 + 16 * i + r16;
+        const int mc = m < p.M ? m : p.M - 1;
+        mbits[i] = *reinterpret_cast<const uint2*>(p.bits_mask + (long)mc * 8);
+      }
+    }
+    // next tile's new pixels [m0 + 320, m0 + 576): 8 pieces per wave, always issued (past the
+    // range they load zeros into slots nobody reads) so the vmcnt counts stay constant
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ring_piece(m0 + C64_BM + C64_AHEAD + (wave * 8 + q) * 8);
+
+    // per-row ring slot and tap mask
+    int rslot[4];
+    uint32_t taps[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int s = slot_m0 + wave * 64 + 16 * i + r16;
+      if (s >= C64_RING) s -= C64_RING;
+      rslot[i] = s;
+      const int m = m0 + wave * 64 + 16 * i + r16;
+      const int n = fdiv(m, p.mg_hw), rem = m - n * HW;
+      const int h = fdiv(rem, p.mg_w), w = rem - h * p.W;
+      const uint32_t cols = (w > 0 ? 1u : 0u) | 2u | (w + 1 < p.W ? 4u : 0u);
+      taps[i] = (h > 0 ? cols : 0u) | (cols << 3) | (h + 1 < p.H ? cols << 6 : 0u);
+    }
+
+    v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) acc[i][jb] = v4f{0.f, 0.f, 0.f, 0.f};
+    // 18 steps (tap, 32-channel half kh) of 16 MFMAs, software-pipelined over two fragment sets:
+    // step st + 1's LDS reads are issued before step st's MFMAs (one wave per SIMD: nothing else
+    // hides the LDS latency); the padding-tap zeroing is applied at the MFMA phase so no VALU op
+    // waits on a read in flight.
+    v8bf ra[2][4], rw[2][4];
+    auto load_step = [&](int st, int set) {
+      const int tap = st >> 1, kh = st & 1;
+      const int delta = (tap / 3 - 1) * dW + (tap % 3 - 1);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const int n = 16 * jb + r16;
+        rw[set][jb] = *reinterpret_cast<const v8bf*>(wl + tap * 8192 + n * 128 + (((kh * 4 + kq) ^ c64_sw(n)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int sl = rslot[i] + delta;
+        sl = sl < 0 ? sl + C64_RING : (sl >= C64_RING ? sl - C64_RING : sl);
+        ra[set][i] = *reinterpret_cast<const v8bf*>(ring + sl * 128 + (((kh * 4 + kq) ^ c64_sw(sl)) << 4));
+      }
+    };
+    auto mfma_step = [&](int st, int set) {
+      const int tap = st >> 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = (taps[i] >> tap) & 1u;
+        const v8bf a = ok ? ra[set][i] : v8bf{};
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[set][jb], a, acc[i][jb], 0, 0, 0);
+      }
+    };
+    load_step(0, 0);
+#pragma unroll
+    for (int st = 0; st < 18; st += 2) {
+      load_step(st + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_step(st, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 2 < 18) load_step(st + 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_step(st + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- epilogue: acc[i][jb][e] = out[pixel 16 i + r16][channel 16 jb + cq + e]
+    if (MODE == C64_DGRAD) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // mbits (ring DMA may fly)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wave * 64 + 16 * i + r16;
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = acc[i][jb][e];
+          if (MODE == C64_FWD) {
+            x = fmaxf(x * sc[jb][e] + sh[jb][e], 0.f);
+          } else {
+            const int c = 16 * jb + cq + e;
+            const uint32_t word = c < 32 ? mbits[i].x : mbits[i].y;
+            x = ((word >> (c & 31)) & 1u) ? x : 0.f;
+            if (m < p.M) csum[jb][e] += x;
+          }
+          v[e] = x;
+        }
+        const int chunk = 2 * jb + (kq >> 1);
+        *reinterpret_cast<uint2*>(stage + r16 * 128 + ((chunk ^ c64_sw(r16)) << 4) + 8 * (kq & 1)) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = (lane >> 3) + 8 * hh, c = lane & 7;
+        const uint4 pk = *reinterpret_cast<const uint4*>(stage + r * 128 + ((c ^ c64_sw(r)) << 4));
+        const int mo = m0 + wave * 64 + 16 * i + r;
+        if (mo < p.M) {
+          *reinterpret_cast<uint4*>(p.out + (long)mo * 64 + c * 8) = pk;
+          if (bits_st) p.bits_out[(long)mo * 8 + c] = (uint8_t)pos_bits8(pk);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slice reads done before the next i rewrites it
+    }
+    slot_m0 += C64_BM;
+    if (slot_m0 >= C64_RING) slot_m0 -= C64_RING;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (MODE == C64_DGRAD && p.colsum) {
+    // one partial row per wave: fold the 16 lanes (r16) sharing this lane's channels
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csum[jb][e] += __shfl_xor(csum[jb][e], o, 64);
+    if (r16 == 0) {
+      float* row = p.colsum + (long)(g * 4 + wave) * 64;
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+        *reinterpret_cast<float4*>(row + 16 * jb + cq) = make_float4(csum[jb][0], csum[jb][1], csum[jb][2], csum[jb][3]);
+    }
+  }
+}
+
+int g_c64_grid = 0;   // test knob: cap on the workgroup count (0: one per CU), so that small
+                      // problems still run many tiles per workgroup through the ring
+int conv3x3c64_grid(int M) {
+  const int T = (M + C64_BM - 1) / C64_BM;
+  int C = num_cus();
+  if (g_c64_grid > 0 && g_c64_grid < C) C = g_c64_grid;
+  return T < C ? T : C;
+}
+int conv3x3c64_partial_rows(int M) { return conv3x3c64_grid(M) * 4; }
+
+const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
+  C64Params p = p_in;
+  if (p.M <= 0 || p.M != p.N * p.H * p.W) return "conv3x3c64: M must be N * H * W";
+  if (p.W + 1 > C64_AHEAD) return "conv3x3c64: image rows wider than 63 pixels";
+  if ((long)p.M * 64 >= (1L << 40)) return "conv3x3c64: too many pixels";
+  if (mode == C64_FWD && (!p.scale || !p.shift)) return "conv3x3c64: forward needs scale / shift";
+  if (mode == C64_DGRAD && !p.bits_mask) return "conv3x3c64: data gradient needs the ReLU bits";
+  p.mg_hw = fdiv_magic(p.H * p.W);
+  p.mg_w = fdiv_magic(p.W);
+  const int G = conv3x3c64_grid(p.M);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv3x3c64_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, C64_LDS);
+    (void)hipFuncSetAttribute((const void*)conv3x3c64_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, C64_LDS);
+    attr = true;
+  }
+  if (mode == C64_FWD) hipLaunchKernelGGL(conv3x3c64_kernel<C64_FWD>, dim3(G), dim3(256), C64_LDS, s, p);
+  else hipLaunchKernelGGL(conv3x3c64_kernel<C64_DGRAD>, dim3(G), dim3(256), C64_LDS, s, p);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient of the same conv: dW[co][tap][ci] = sum_m g[m][co] x[m + tap][ci].
+// Row tiles: a tile is 4 output rows (h0 .. h0 + 3) of one image, each as 64 pixel slots (slot w,
+// w >= W zero): 256 slots of g (32 KiB) and the 6 x 64 zero-padded input rows h0 - 1 .. h0 + 4
+// (slot j <-> w = j - 1; padding rows / columns are zeros straight from the LDS-DMA's out-of-range
+// loads), so every tap of every slot is a plain shifted read -- no tap masks.  Two such buffers
+// (2 x 80 KiB) alternate: tile t + 1 is DMA'd while tile t computes.  Wave w owns input channels
+// 16 w .. 16 w + 15 for all 9 taps x 64 output channels (acc[9][4]: 144 accumulators) for the
+// workgroup's whole range and adds them once at the end (row-contiguous fp32 atomics).  The
+// reduction runs over pixels, so both operands are read with ds_read_b64_tr_b16.
+// Reference: the Conv2D kernel gradient of conv2_block*_2 (tf.GradientTape in model.fit,
+// imagenet-resnet50.py:67).
+namespace {
+constexpr int CW_XS = 6 * 64;                       // input-window slots
+constexpr int CW_BUF = (CW_XS + 256) * 128;         // 81,920 B per buffer
+constexpr int CW_LDS = 2 * CW_BUF;
+static_assert(CW_LDS <= 163840, "LDS budget");
+}  // namespace
+
+// 16-channel pair-preserving swizzle: chunk pairs (2c, 2c + 1) move together, so a 4-row x 32-B
+// transposed read of 8 consecutive slots hits 8 distinct 32-B bank segments
+__device__ __forceinline__ int cw_sw(int slot) { return ((slot >> 1) & 3) << 1; }
+// Inline asm, not the builtin: with the builtin the compiler drains the next tile's LDS-DMA
+// (vmcnt(0)) before every read (wgrad.hip).  The asm results are invisible to its wait insertion,
+// so the loop waits itself (lgkmcnt(0)) and pins the MFMAs behind that wait with a scheduling
+// barrier -- without it an MFMA consuming a fragment can be hoisted above the wait.
+__device__ __forceinline__ v4bf cw_tr(const char* p) {
+  v4bf r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
+  return r;
+}
+
+__global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int RT = (p.H + 3) / 4;                 // row tiles per image
+  const int T = p.N * RT;
+  const int G = gridDim.x, gb = blockIdx.x;
+  const int t_begin = (int)((long)gb * T / G), t_end = (int)((long)(gb + 1) * T / G);
+  if (t_begin >= t_end) return;
+  const long img = (long)p.H * p.W * 64;        // elements per image
+
+  // DMA of tile t into buffer b: 48 x-window pieces then 32 g pieces (8 slots each), 20 per wave
+  auto load_tile = [&](int t, int b) {
+    const bool live = t < t_end;
+    const int tt = live ? t : t_begin;
+    const int n = tt / RT, h0 = (tt - n * RT) * 4;
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, n * img, (n + 1) * img);
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc_at(p.g, n * img, (n + 1) * img);
+    char* base = smem + b * CW_BUF;
+#pragma unroll
+    for (int q = 0; q < 20; ++q) {
+      const int pc = wave * 20 + q;             // 0..79
+      const bool isx = pc < 48;
+      const int sp0 = (isx ? pc : pc - 48) * 8;                 // first slot of the piece
+      const int slot = sp0 + (lane >> 3);
+      const int rr = slot >> 6, j = slot & 63;
+      const int h = isx ? h0 - 1 + rr : h0 + rr;
+      const int w = isx ? j - 1 : j;
+      const bool ok = live && h >= 0 && h < p.H && w >= 0 && w < p.W;
+      const int ch = (lane & 7) ^ cw_sw(slot);
+      const uint32_t off = ok ? (uint32_t)(((h * p.W + w) * 64 + ch * 8) * 2) : OOB_OFF;
+      char* dst = base + (isx ? 0 : CW_XS * 128) + sp0 * 128;
+      buf_lds16(isx ? rx : rg, LDS_PTR(dst), off, 0);
+    }
+  };
+
+  v4f acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[t][i] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // ds_read_b64_tr_b16: lane 4 q + pp of each 16-lane group addresses slot row q, channels 4 pp .. +3
+  // of a 16-channel block; lane i of the group then holds channel i for the 4 slots
+  const int gq = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  load_tile(t_begin, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = t_begin; t < t_end; ++t) {
+    const int b = (t - t_begin) & 1;
+    load_tile(t + 1, b ^ 1);                    // (past the range: zeros into the idle buffer)
+    const char* xw = smem + b * CW_BUF;
+    const char* gt = xw + CW_XS * 128;
+    // 8 k-steps of 32 slots; each step's 26 transposed reads (4 g + 9 x fragments, two halves)
+    // are issued during the previous step's MFMAs, in two batches of 13 (the LDS counter tracks
+    // at most 15 reads in flight), behind explicit waits and scheduling barriers (asm reads)
+    v8bf af[2][4], bfr[2][9];
+    auto rd_a = [&](int ks, int set) {
+      const int rl = ks >> 1, w0 = (ks & 1) * 32;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int sg = rl * 64 + w0 + 8 * gq + 4 * hh + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const v4bf r = cw_tr(gt + sg * 128 + (((2 * i + (pp >> 1)) ^ cw_sw(sg)) << 4) + (pp & 1) * 8);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[set][i][4 * hh + e] = r[e];
+        }
+      }
+    };
+    auto rd_b = [&](int ks, int set, int t0, int t1) {
+      const int rl = ks >> 1, w0 = (ks & 1) * 32;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int ws = w0 + 8 * gq + 4 * hh + q;
+#pragma unroll
+        for (int tap = t0; tap < t1; ++tap) {
+          const int sx = (rl + tap / 3) * 64 + ws + tap % 3;
+          const v4bf r = cw_tr(xw + sx * 128 + (((2 * wave + (pp >> 1)) ^ cw_sw(sx)) << 4) + (pp & 1) * 8);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[set][tap][4 * hh + e] = r[e];
+        }
+      }
+    };
+    auto mm = [&](int set, int t0, int t1) {
+#pragma unroll
+      for (int tap = t0; tap < t1; ++tap)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[set][i], bfr[set][tap], acc[tap][i], 0, 0, 0);
+    };
+    rd_a(0, 0);
+    rd_b(0, 0, 0, 9);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int cs = ks & 1, ns = cs ^ 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step ks's fragments
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < 8) { rd_a(ks + 1, ns); rd_b(ks + 1, ns, 0, 3); }   // 8 + 6 reads
+      __builtin_amdgcn_sched_barrier(0);
+      mm(cs, 0, 5);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < 8) rd_b(ks + 1, ns, 3, 9);                         // 12 reads
+      __builtin_amdgcn_sched_barrier(0);
+      mm(cs, 5, 9);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // tile t + 1 landed; every wave is done with buffer b (tile t + 2 goes there next)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // D[co][ci] of tap: co = 16 i + 4 (lane >> 4) + e, ci = 16 wave + (lane & 15)
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = 16 * i + 4 * gq + e, ci = 16 * wave + (lane & 15);
+        atomicAdd(p.dw + (long)co * p.ld_dw + tap * 64 + ci, acc[tap][i][e]);
+      }
+}
+
+int g_c64w_grid = 0;   // test knob: workgroup cap of the weight-gradient kernel (0: one per CU)
+const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s) {
+  if (p.N <= 0 || p.H <= 0 || p.W <= 0) return "conv3x3c64_wgrad: empty";
+  if (p.W + 2 > 64) return "conv3x3c64_wgrad: image rows wider than 62 pixels";
+  if ((long)p.H * p.W * 64 * 2 >= (1L << 31)) return "conv3x3c64_wgrad: image too large";
+  if (p.ld_dw < 576) return "conv3x3c64_wgrad: ld_dw";
+  const int T = p.N * ((p.H + 3) / 4);
+  int G = num_cus();
+  if (g_c64w_grid > 0 && g_c64w_grid < G) G = g_c64w_grid;
+  if (G > T) G = T;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv3x3c64_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CW_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(conv3x3c64_wgrad_kernel, dim3(G), dim3(256), CW_LDS, s, p);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+}  // namespace pddl

@@ -172,6 +172,30 @@ struct StemPoolBwdParams {
   int B, Hs, Ws, H1, W1, H2, W2;
   int PB, nblk;
 };
+// Persistent pixel-ring 3x3 / pad 1 / stride 1 convolution, 64 -> 64 channels (conv3x3c64.hip).
+enum { C64_FWD = 0, C64_DGRAD = 1 };
+struct C64Params {
+  const uint16_t* x;          // [M][64] NHWC input (forward) / output gradient (dgrad)
+  const uint16_t* w;          // [64][576] OHWI weights (dgrad: transposed + flipped, as igemm's B)
+  const float* scale;         // forward: folded BN scale / shift (ReLU always applied)
+  const float* shift;
+  const uint8_t* bits_mask;   // dgrad: [M][8] ReLU bits of the layer input
+  uint16_t* out;              // [M][64]
+  uint8_t* bits_out;          // forward, optional: [M][8] ReLU bits of out
+  float* colsum;              // dgrad, optional: partial rows [grid * 4][64]
+  int N, H, W, M;
+  uint64_t mg_hw, mg_w;
+};
+const char* conv3x3c64_launch(const C64Params& p, int mode, hipStream_t s);
+int conv3x3c64_partial_rows(int M);
+extern int g_c64_grid, g_c64w_grid;
+struct C64WgradParams {
+  const uint16_t* x;          // [N][H][W][64] conv input
+  const uint16_t* g;          // [N][H][W][64] output gradient
+  float* dw; int ld_dw;       // [64][ld_dw >= 576] fp32, accumulated with atomics
+  int N, H, W;
+};
+const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s);
 const char* stem_pool_bwd_launch(StemPoolBwdParams p, hipStream_t s);
 int stem_pool_bwd_partial_rows(int B, int H2, int PB);
 int stem_pool_lds_bytes(int Ws, int W1);

@@ -181,10 +181,10 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
 // 256 k columns) x all 64 output channels in registers for the whole launch and adds them once at
 // the end with row-contiguous fp32 atomics.  Padding pixels of a 32-pixel step carry zero
 // gradient and read a clamped (finite) input pixel.
+// (the builtin, not inline asm: with asm the compiler may schedule an MFMA that consumes the
+// result before a hand-placed s_waitcnt lgkmcnt)
 __device__ __forceinline__ v4bf sp_tr_read(const uint8_t* p) {
-  v4bf r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
-  return r;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(p));
 }
 // gc1 image: pixel x of row a at a * 128 * 128 + x * 128; its 8-channel chunk c at (c ^ swz(x)) * 16
 __device__ __forceinline__ int gimg_off(int a, int x, int chunk) {
@@ -318,7 +318,6 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_bwd_kernel(StemPoolBw
             for (int j = 0; j < 4; ++j) bfr[t][4 * h + j] = r[j];
           }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the asm fragment reads)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll

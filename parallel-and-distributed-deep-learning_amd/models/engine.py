@@ -49,6 +49,8 @@ class HipEngine:
     FUSE_BWD_OK = True      # stage-2/3 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
     FUSE_STEM_OK = True     # stem conv + BN + ReLU + max-pool forward in one launch (stem.hip)
     TWO_STREAM_OK = True
+    C64_OK = True           # stage-2 3x3 convs on the persistent pixel-ring kernel (conv3x3c64.hip)
+    C64_MIN_M = 262144      # ... from 4 x 256 CUs x 256-pixel tiles up (b >= 84 at 56 x 56)
     TWO_STREAM_MAX_BATCH = 1024
     GRAD_RING = 3           # two-stream: gradient buffers per kind, so the data-gradient chain can run
                             # two blocks ahead of the weight gradients still reading older ones
@@ -96,6 +98,10 @@ class HipEngine:
         self._fuse_bwd_s2 = os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0"
         # stem conv + max-pool forward as one launch (stem.hip): conv1's output never reaches HBM
         self.fuse_stem = self.FUSE_STEM_OK and os.environ.get("PDDL_FUSE_STEM", "1") != "0" and crop <= 250
+        # stage-2 3x3 convs (64 -> 64) on the persistent pixel-ring kernel (conv3x3c64.hip) at
+        # batches where every CU streams several tiles through its ring
+        self.c64 = self.C64_OK and os.environ.get("PDDL_C64", "1") != "0"
+        self.c64w = self.c64 and os.environ.get("PDDL_C64W", "0") != "0"
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -343,7 +349,10 @@ class HipEngine:
                 add(b.convs["2"].name, N.bwd1x1_partial_rows(Mc, 4 * f, f), f)
             else:
                 add(b.convs["2"].name, N.igemm_partial_rows(Mc, f, 4 * f), f)     # c3 dgrad -> g2
-            add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)          # c2 dgrad -> g1
+            if self._use_c64(f, M, Ho, self.bitmask):                           # c2 dgrad -> g1
+                add(b.convs["1"].name, N.conv3x3c64_partial_rows(M), f)
+            else:
+                add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)
             if bi > 0:                                                           # c1 dgrad -> g_out(prev)
                 add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin, 5 * f if b.proj else f), b.cin)
         if self.fuse_stem:   # (fused pool backward + conv1 weight gradient: one partial row per workgroup)
@@ -377,6 +386,17 @@ class HipEngine:
     def _bwd_fused(self, bi, b, s2):
         # stage 2 (256 <- 64 channels) and stage 3 (512 <- 128); PDDL_FUSE_BWD=2: stage 2 only
         return self.fuse_bwd and bi not in s2 and (b.filters == 64 or (b.filters == 128 and self._fuse_bwd3))
+
+    def _use_c64(self, f, M, W, bits=True) -> bool:
+        return self.c64 and f == 64 and W + 1 <= 64 and M >= self.C64_MIN_M and bits
+
+    def _c2_wgrad(self, W, y1, g2, c2n, f, B, Ho, g2_n):
+        """Weight gradient of a bottleneck's stride-1 3x3 conv (on the side stream when two-stream)."""
+        if self.c64w and self._use_c64(f, B * Ho * Ho, Ho) and Ho + 2 <= 64:
+            W(self.N.conv3x3c64_wgrad, y1, g2, self._gview(c2n, f, 9 * f), reads=(g2_n,))
+        else:
+            W(self.N.wgrad, y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0,
+              reads=(g2_n,))
 
     def _wdv(self, name, cin, k):
         o = self.wd[name]
@@ -445,9 +465,13 @@ class HipEngine:
                         bt.get("y1"))
                 res = x
             c2 = b.convs["2"].name
-            N.igemm(y1, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wf(c2, f, 9 * f), 0,
-                    self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0, 0, 0,
-                    None, bt.get("y2"))
+            if self._use_c64(f, B * Ho * Ho, Ho):
+                N.conv3x3c64(y1, self._wf(c2, f, 9 * f), 0, y2, scale=self.scale[self.ch[c2]:],
+                             shift=self.shift[self.ch[c2]:], bits=bt.get("y2"))
+            else:
+                N.igemm(y1, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wf(c2, f, 9 * f), 0,
+                        self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0,
+                        0, 0, None, bt.get("y2"))
             c3 = b.convs["3"].name
             if b.proj and self.fuse_proj:
                 fz = "fuse:" + b.name
@@ -629,8 +653,7 @@ class HipEngine:
                 # conv3: data and weight gradient from one read of gout
                 self._before_write(g2_n)
                 N.bwd1x1(gout, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f))
-                W(N.wgrad, y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0,
-                  reads=(g2_n,))
+                self._c2_wgrad(W, y1, g2, c2n, f, B, Ho, g2_n)
             else:
                 # conv3
                 W(N.wgrad, y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, gout, None, 0, self._gview(c3n, 4 * f, f), f, 0,
@@ -639,12 +662,14 @@ class HipEngine:
                 N.igemm(gout, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c3n, f, 4 * f), 1, None, None, None, y2m,
                         None, g2, 0, None, 0, 0, 0, 0, 0, part(c2n), None)
                 # conv2 (3x3)
-                W(N.wgrad, y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2n, f, 9 * f), 9 * f, 0,
-                  reads=(g2_n,))
+                self._c2_wgrad(W, y1, g2, c2n, f, B, Ho, g2_n)
             g1 = self.g1bufs[rk][: B * Ho * Ho * f].view(B, Ho, Ho, f)
             self._before_write(f"g1_{rk}")
-            N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1m, None,
-                    g1, 0, None, 0, 0, 0, 0, 0, part(c1n), None)
+            if self._use_c64(f, B * Ho * Ho, Ho, self.bitmask):
+                N.conv3x3c64(g2, self._wdv(c2n, f, 9 * f), 1, g1, bits=y1m, colsum=part(c1n))
+            else:
+                N.igemm(g2, None, Ho, Ho, 3, 3, 1, 1, Ho, Ho, self._wdv(c2n, f, 9 * f), 1, None, None, None, y1m,
+                        None, g1, 0, None, 0, 0, 0, 0, 0, part(c1n), None)
             # conv1 (+ conv0)
             nxt = (cur + 1) % len(self.gbuf)
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)

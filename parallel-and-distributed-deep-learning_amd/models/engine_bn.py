@@ -39,6 +39,7 @@ class HipEngineBNTrain(HipEngine):
     FUSE_PROJ_OK = False   # (batch statistics: the shortcut's BN cannot be folded into weights)
     FUSE_STEM_OK = False   # (conv1's batch statistics need its raw output)
     TWO_STREAM_OK = False  # (its own backward schedule runs on one stream)
+    C64_OK = False         # (train-mode BN needs the batch statistics from the conv epilogue)
 
     def __init__(self, layout: ParamLayout, batch: int, **kw):
         kw.setdefault("bn_mode", "train")

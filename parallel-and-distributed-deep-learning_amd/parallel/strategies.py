@@ -75,6 +75,15 @@ def overlap_buckets(engine):
     return engine._ov_buckets
 
 
+def overlap_opt_wanted() -> bool:
+    """Optimizer bucket updates overlapped with backward: opt-in (PDDL_OVERLAP_OPT=1).  Measured
+    no gain on one GPU -- the fused Adam is 0.11 ms of a 92 ms b2560 step, and at b32 the side-
+    stream updates cost 2.7 % (4.36 vs 4.24 ms, profiles/r4_ovopt_ab.txt) -- and inside a HIP
+    graph capture together with the two-stream backward the replayed updates diverge from the
+    eager ones, so GraphedTrainStep never overlaps."""
+    return os.environ.get("PDDL_OVERLAP_OPT", "0") == "1"
+
+
 def overlap_stream(engine):
     """The stream the overlapped optimizer updates run on: the engine's weight-gradient side
     stream when it has one, else a stream of their own."""
@@ -282,7 +291,7 @@ class SingleStrategy(Strategy):
             return self.graphed(images.to(self.device, non_blocking=True), labels.to(self.device, non_blocking=True),
                                 flip, off).clone()
         eng = self.engine
-        if eng.params.is_cuda and hasattr(eng, "wbf") and os.environ.get("PDDL_OVERLAP_OPT", "1") != "0":
+        if eng.params.is_cuda and hasattr(eng, "wbf") and overlap_opt_wanted():
             bks = overlap_buckets(eng)       # optimizer bucket updates under the rest of backward
             self.opt.overlap_begin(bks, overlap_stream(eng))
             s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off,
@@ -412,9 +421,9 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
 
     def _overlap_opt(self) -> bool:
         """One replica on the GPU: the optimizer's bucket updates run under the rest of backward
-        (PDDL_OVERLAP_OPT=0 turns it off).  With collectives the update waits for the all-reduce."""
+        (PDDL_OVERLAP_OPT=1 turns it on).  With collectives the update waits for the all-reduce."""
         return (self.world == 1 and self.fusion is None and self.reducer is None and self.device.type == "cuda"
-                and hasattr(self.engine, "wbf") and os.environ.get("PDDL_OVERLAP_OPT", "1") != "0")
+                and hasattr(self.engine, "wbf") and overlap_opt_wanted())
 
     def _step(self, images, labels):
         ov = self._overlap_opt()

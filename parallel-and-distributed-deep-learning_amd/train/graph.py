@@ -20,8 +20,6 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
-import os
-
 import torch
 
 
@@ -53,16 +51,6 @@ class GraphedTrainStep:
 
     def _body(self):
         eng = self.engine
-        if self.with_optimizer and os.environ.get("PDDL_OVERLAP_OPT", "1") != "0":
-            # the optimizer's bucket updates run under the rest of backward (one replica)
-            from ..parallel.strategies import overlap_buckets, overlap_stream
-            bks = overlap_buckets(eng)
-            self.opt.overlap_begin(bks, overlap_stream(eng))
-            stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip, crop_offset=self.crop,
-                                         bucket_cb=self.opt.overlap_bucket, buckets=bks)
-            self.opt.overlap_finish()
-            eng.after_update()
-            return stats
         stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip, crop_offset=self.crop)
         if self.with_optimizer:
             self.opt.step()

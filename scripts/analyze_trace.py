@@ -6,6 +6,7 @@ Pairs the last complete step's dispatches with the engine's fixed launch schedul
 prints time, TFLOP/s and effective GB/s per launch.
 """
 import csv
+import os
 import sys
 
 sys.path.insert(0, ".")
@@ -34,7 +35,9 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         n1 = 5 * f if b.proj and not fuse else f
         ev.append(("igemm", f"{b.name} c1{'+c0' if n1 > f else ''} fwd", 2 * M * cin * n1, (B * H * H * cin + M * n1) * 2,
                    (M, n1, cin)))
-        ev.append(("igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2, (M, f, 9 * f)))
+        c64 = f == 64 and M >= 262144 and Ho + 1 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
+        ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2,
+                   (M, f, 9 * f)))
         if b.proj and fuse:   # conv3 + the shortcut conv as one dual-source GEMM (K = f + cin)
             ev.append(("igemm", f"{b.name} c3+c0 fwd", 2 * M * (f + cin) * 4 * f, (M * f + M * cin + M * 4 * f) * 2,
                        (M, 4 * f, f + cin), "dual"))
@@ -63,8 +66,12 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
             ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * Mc * f * 4 * f, (Mc * f + Mc * 4 * f) * 2))
             ev.append(("igemm", f"{b.name} c3 dgrad", 2 * Mc * f * 4 * f, (Mc * 4 * f + Mc * f + M * f) * 2,
                        (Mc, f, 4 * f)))
-        ev.append(("wgrad", f"{b.name} c2 wgrad", 2 * Mc * 9 * f * f, (Mc + M) * f * 2))
-        ev.append(("igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2, (M, f, 9 * f)))
+        c64w = f == 64 and M >= 262144 and Ho + 2 <= 64 and Mc == M and os.environ.get("PDDL_C64", "1") != "0" \
+            and os.environ.get("PDDL_C64W", "0") != "0"
+        ev.append(("conv3x3c64" if c64w else "wgrad", f"{b.name} c2 wgrad", 2 * Mc * 9 * f * f, (Mc + M) * f * 2))
+        c64 = f == 64 and M >= 262144 and Ho + 1 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
+        ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2,
+                   (M, f, 9 * f)))
         n1 = 5 * f if b.proj else f
         if b.proj:   # conv1 and the shortcut conv: one wgrad launch per gradient source
             ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * f, (M * f + B * H * H * cin) * 2))

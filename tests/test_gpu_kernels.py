@@ -1011,3 +1011,69 @@ def test_stem_pool_bwd_fused_matches_unfused(B, crop, rows):
     assert rel(dw, ref) < 1e-5, rel(dw, ref)
     assert rel(dw, dw_r) < 1e-5
     assert torch.allclose(cs.sum(0), cs_r.sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,h,grid", [(24, 56, 0), (6, 56, 4), (50, 13, 3), (3, 17, 0)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_conv3x3c64_ring_matches_reference(mode, n, h, grid):
+    """Persistent pixel-ring 3x3 conv (conv3x3c64.hip), forward (BN + ReLU + bits) and data
+    gradient (ReLU-bit mask + column sums), against the fp32 PyTorch conv of the same bf16
+    operands and against the generic implicit GEMM (same k order).  `grid` caps the workgroup
+    count so each workgroup streams many tiles through the ring (wrap-around, tile tails)."""
+    torch.manual_seed(40 + mode)
+    x = rnd(n, h, h, 64)
+    w = rnd(64, 576, scale=0.05)
+    wr = w.float().view(64, 3, 3, 64).permute(0, 3, 1, 2)
+    conv = F.conv2d(x.float().permute(0, 3, 1, 2), wr, padding=1).permute(0, 2, 3, 1)
+    out = torch.empty_like(x)
+    ref_ig = torch.empty_like(x)
+    M = n * h * h
+    N().set_variant("c64_grid", grid)
+    try:
+        if mode == 0:
+            sc, sh = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.1
+            bits = torch.zeros(n, h, h, 8, dtype=torch.uint8, device=dev)
+            N().conv3x3c64(x, w, 0, out, scale=sc, shift=sh, bits=bits)
+            ref = torch.relu(conv * sc + sh)
+            bits_ig = torch.zeros_like(bits)
+            N().igemm(x, None, h, h, 3, 3, 1, 1, h, h, w, 0, sc, sh, None, None, None, ref_ig, 1, None, 0, 0, 0, 0,
+                      0, None, bits_ig)
+            assert torch.equal(bits, bits_ig) or (bits != bits_ig).float().mean().item() < 1e-4
+        else:
+            mask = rnd(n, h, h, 64)
+            mbits = pack_bits(mask)
+            rows = N().conv3x3c64_partial_rows(M)
+            part = torch.full((rows * 64,), float("nan"), device=dev)
+            N().conv3x3c64(x, w, 1, out, bits=mbits, colsum=part)
+            ref = conv * (mask.float() > 0)
+            assert rel(_fold(part, rows, 64), ref.sum((0, 1, 2))) < 1e-3
+            N().igemm(x, None, h, h, 3, 3, 1, 1, h, h, w, 1, None, None, None, mbits, None, ref_ig, 0, None, 0, 0,
+                      0, 0, 0, None, None)
+    finally:
+        N().set_variant("c64_grid", 0)
+    assert rel(out, ref) < 1e-2
+    d = (out.float() - ref_ig.float()).abs().max().item()
+    print(f"conv3x3c64 mode {mode}: max |ring - igemm| = {d}")
+    assert rel(out, ref_ig) < 2e-3
+
+
+@pytest.mark.parametrize("n,h,grid", [(24, 56, 0), (5, 56, 3), (7, 13, 2), (3, 61, 0)])
+def test_conv3x3c64_wgrad_matches_reference(n, h, grid):
+    """Row-tile weight gradient of the 64 -> 64 3x3 conv (conv3x3c64.hip) against the fp32
+    PyTorch weight gradient of the same bf16 operands and against the generic wgrad kernel;
+    accumulates into dw (atomics) like the engine's zeroed gradient buffer."""
+    torch.manual_seed(44)
+    x = rnd(n, h, h, 64)
+    g = rnd(n, h, h, 64)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 64, 3, 3), g.float().permute(0, 3, 1, 2),
+                                      padding=1).permute(0, 2, 3, 1).reshape(64, 576)
+    dw = torch.full((64, 576), 0.5, device=dev)
+    N().set_variant("c64w_grid", grid)
+    try:
+        N().conv3x3c64_wgrad(x, g, dw)
+    finally:
+        N().set_variant("c64w_grid", 0)
+    assert rel(dw - 0.5, ref) < 1e-3
+    dw2 = torch.zeros(64, 576, device=dev)
+    N().wgrad(x, h, h, 3, 3, 1, 1, h, h, g, None, 0, dw2, 576, 0)
+    assert rel(dw - 0.5, dw2) < 1e-3
