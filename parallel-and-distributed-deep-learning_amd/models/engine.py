@@ -101,7 +101,7 @@ class HipEngine:
         # stage-2 3x3 convs (64 -> 64) on the persistent pixel-ring kernel (conv3x3c64.hip) at
         # batches where every CU streams several tiles through its ring
         self.c64 = self.C64_OK and os.environ.get("PDDL_C64", "1") != "0"
-        self.c64w = self.c64 and os.environ.get("PDDL_C64W", "0") != "0"
+        self.c64w = self.c64 and os.environ.get("PDDL_C64W", "1") != "0"
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off

@@ -67,7 +67,7 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
             ev.append(("igemm", f"{b.name} c3 dgrad", 2 * Mc * f * 4 * f, (Mc * 4 * f + Mc * f + M * f) * 2,
                        (Mc, f, 4 * f)))
         c64w = f == 64 and M >= 262144 and Ho + 2 <= 64 and Mc == M and os.environ.get("PDDL_C64", "1") != "0" \
-            and os.environ.get("PDDL_C64W", "0") != "0"
+            and os.environ.get("PDDL_C64W", "1") != "0"
         ev.append(("conv3x3c64" if c64w else "wgrad", f"{b.name} c2 wgrad", 2 * Mc * 9 * f * f, (Mc + M) * f * 2))
         c64 = f == 64 and M >= 262144 and Ho + 1 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
         ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2,
@@ -91,7 +91,8 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
     ev.append(("colsum_reduce", "cred", 0, 0))
     ev.append(("bn_grad", "bn", 0, 0))
     ev.append(("opt_hparams", "hparams", 0, 0))
-    ev.append(("adam", "adam", 0, 0))
+    if os.environ.get("NO_ADAM") is None:
+        ev.append(("adam", "adam", 0, 0))
     ev.append(("prep", "prep", 0, 0))
     return ev
 
