@@ -787,6 +787,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "c64_grid") pddl::g_c64_grid = v;
     else if (which == "c64w_grid") pddl::g_c64w_grid = v;
     else if (which == "stem_pool") pddl::g_stem_pool_variant = v;
+    else if (which == "c64") pddl::g_c64_variant = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;

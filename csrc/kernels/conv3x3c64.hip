@@ -258,15 +258,242 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_kernel(C64Params p) {
   }
 }
 
+// Row-tile form of the same forward / data-gradient conv (knob c64 = 2, default): a tile is 4 output
+// rows of one image, wave w computing row h0 + w as 64 pixel slots (slots >= W are padding and are
+// not stored); its input is the zero-padded 6 x 64-slot window of rows h0 - 1 .. h0 + 4 (48 KiB,
+// the wgrad kernel's x image: padding taps read zeros the LDS-DMA wrote, so no tap masks and no
+// ring wrap), double-buffered so tile t + 1 loads while tile t computes.  The whole 64 x 576 weight
+// matrix lives in registers as MFMA A fragments (288 VGPRs, one wave per SIMD), so the k loop reads
+// only the pixel fragments, at addresses precomputed per lane (the window row of tap r is an
+// immediate offset).  (All nine taps in registers -- 288 VGPRs -- spill: the last four taps' weights
+// sit in LDS, read like the igemm B images.)
+namespace {
+constexpr int CR_WIN = 6 * 64 * 128;                // 49,152 B per window
+constexpr int CR_TR = 5;                            // taps 0..4: weights in registers; 5..8: in LDS
+constexpr int CR_WL = (9 - CR_TR) * 8192;           // LDS weight images [tap - TR][n][128 B]
+constexpr int CR_LDS = 2 * CR_WIN + CR_WL + 4 * C64_STAGE_BYTES;
+static_assert(CR_LDS <= 163840, "LDS budget");
+}  // namespace
+
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* wl = smem + 2 * CR_WIN;
+  char* stage = smem + 2 * CR_WIN + CR_WL + wave * C64_STAGE_BYTES;
+  const int RT = (p.H + 3) / 4;
+  const int T = p.N * RT;
+  const int G = gridDim.x, gb = blockIdx.x;
+  const int t_begin = (int)((long)gb * T / G), t_end = (int)((long)(gb + 1) * T / G);
+  if (t_begin >= t_end) return;
+  const long img = (long)p.H * p.W * 64;
+  const int r16 = lane & 15, kq = lane >> 4, cq = 4 * kq;
+
+  // window DMA of tile t into buffer b: 6 rows x 8 pieces, 12 per wave
+  auto load_tile = [&](int t, int b) {
+    const bool live = t < t_end;
+    const int tt = live ? t : t_begin;
+    const int n = tt / RT, h0 = (tt - n * RT) * 4;
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, n * img, (n + 1) * img);
+    char* base = smem + b * CR_WIN;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      const int pc = wave * 12 + q;
+      const int slot = pc * 8 + (lane >> 3);
+      const int rr = slot >> 6, j = slot & 63;
+      const int h = h0 - 1 + rr, w = j - 1;
+      const bool ok = live && h >= 0 && h < p.H && w >= 0 && w < p.W;
+      const int ch = (lane & 7) ^ c64_sw(slot);
+      buf_lds16(rx, LDS_PTR(base + pc * 1024), ok ? (uint32_t)(((h * p.W + w) * 64 + ch * 8) * 2) : OOB_OFF, 0);
+    }
+  };
+
+  // weights of taps >= TR -> LDS ([tap - TR][n][128 B], chunk swizzled by n): 32 pieces, 8 per wave
+  {
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, 64 * 576 * 2);
+#pragma unroll
+    for (int q = 0; q < (9 - CR_TR) * 2; ++q) {
+      const int pc = wave * ((9 - CR_TR) * 2) + q;
+      const int tl = pc >> 3, nn = (pc & 7) * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ c64_sw(nn);
+      buf_lds16(rw, LDS_PTR(wl + pc * 1024), (uint32_t)((nn * 576 + (CR_TR + tl) * 64 + ch * 8) * 2), 0);
+    }
+  }
+  // weights of taps < TR as A fragments: wf[tap][kh][jb] = W[16 jb + r16][tap * 64 + kh * 32 + 8 kq .. + 7]
+  v8bf wf[CR_TR][2][4];
+#pragma unroll
+  for (int tap = 0; tap < CR_TR; ++tap)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+        wf[tap][kh][jb] = *reinterpret_cast<const v8bf*>(p.w + (16 * jb + r16) * 576 + tap * 64 + kh * 32 + 8 * kq);
+  // per-lane fragment offsets within a window row: pixel slot 16 i + r16 + s, chunk kh * 4 + kq
+  // (the swizzle depends on the slot only through (slot >> 1) & 7, which a row offset of 64 keeps)
+  int aoff[4][3][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int sx = 0; sx < 3; ++sx)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int sl = 16 * i + r16 + sx;
+        aoff[i][sx][kh] = sl * 128 + (((kh * 4 + kq) ^ c64_sw(sl)) << 4);
+      }
+  float sc[4][4], sh[4][4];
+  if (MODE == C64_FWD) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      const float4 a = *reinterpret_cast<const float4*>(p.scale + 16 * jb + cq);
+      const float4 b = *reinterpret_cast<const float4*>(p.shift + 16 * jb + cq);
+      sc[jb][0] = a.x; sc[jb][1] = a.y; sc[jb][2] = a.z; sc[jb][3] = a.w;
+      sh[jb][0] = b.x; sh[jb][1] = b.y; sh[jb][2] = b.z; sh[jb][3] = b.w;
+    }
+  }
+  float csum[4][4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[jb][e] = 0.f;
+  const bool bits_st = MODE == C64_FWD && p.bits_out != nullptr;
+
+  load_tile(t_begin, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = t_begin; t < t_end; ++t) {
+    const int b = (t - t_begin) & 1;
+    if (t > t_begin) {
+      // this tile's window landed (only the previous tile's stores may be outstanding), and every
+      // wave finished the previous tile (its window buffer takes tile t + 1)
+      if (bits_st) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const int n = t / RT, h = (t - n * RT) * 4 + wave;   // this wave's output row
+    const bool row_ok = h < p.H;
+    const long mrow = ((long)n * p.H + (row_ok ? h : 0)) * p.W;   // pixel index of (n, h, 0)
+    uint2 mbits[4];
+    if (MODE == C64_DGRAD) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int wpx = 16 * i + r16;
+        const long m = mrow + (wpx < p.W ? wpx : p.W - 1);
+        mbits[i] = *reinterpret_cast<const uint2*>(p.bits_mask + m * 8);
+      }
+    }
+    load_tile(t + 1, b ^ 1);                     // (past the range: zeros into the idle buffer)
+    const char* xw = smem + b * CR_WIN + wave * 8192;   // window row of tap r = 0 for this wave
+
+    v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) acc[i][jb] = v4f{0.f, 0.f, 0.f, 0.f};
+    v8bf ra[2][4], rwt[2][4];
+    auto load_step = [&](int st, int set) {
+      const int tap = st >> 1, kh = st & 1, r = tap / 3, sx = tap % 3;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ra[set][i] = *reinterpret_cast<const v8bf*>(xw + r * 8192 + aoff[i][sx][kh]);
+      if (tap >= CR_TR) {
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const int nn = 16 * jb + r16;
+          rwt[set][jb] = *reinterpret_cast<const v8bf*>(wl + (tap - CR_TR) * 8192 + nn * 128 +
+                                                         (((kh * 4 + kq) ^ c64_sw(nn)) << 4));
+        }
+      }
+    };
+    auto mfma_step = [&](int st, int set) {
+      const int tap = st >> 1, kh = st & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+          acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tap < CR_TR ? wf[tap < CR_TR ? tap : 0][kh][jb] : rwt[set][jb],
+                                                               ra[set][i], acc[i][jb], 0, 0, 0);
+    };
+    load_step(0, 0);
+#pragma unroll
+    for (int st = 0; st < 18; st += 2) {
+      load_step(st + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_step(st, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 2 < 18) load_step(st + 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_step(st + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- epilogue: acc[i][jb][e] = out[pixel slot 16 i + r16 of row h][channel 16 jb + cq + e]
+    if (MODE == C64_DGRAD) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // mbits (the window DMA may fly)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool px_ok = row_ok && 16 * i + r16 < p.W;
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = acc[i][jb][e];
+          if (MODE == C64_FWD) {
+            x = fmaxf(x * sc[jb][e] + sh[jb][e], 0.f);
+          } else {
+            const int c = 16 * jb + cq + e;
+            const uint32_t word = c < 32 ? mbits[i].x : mbits[i].y;
+            x = ((word >> (c & 31)) & 1u) ? x : 0.f;
+            if (px_ok) csum[jb][e] += x;
+          }
+          v[e] = x;
+        }
+        const int chunk = 2 * jb + (kq >> 1);
+        *reinterpret_cast<uint2*>(stage + r16 * 128 + ((chunk ^ c64_sw(r16)) << 4) + 8 * (kq & 1)) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int rr = (lane >> 3) + 8 * hh, c = lane & 7;
+        const uint4 pk = *reinterpret_cast<const uint4*>(stage + rr * 128 + ((c ^ c64_sw(rr)) << 4));
+        const int wpx = 16 * i + rr;
+        if (row_ok && wpx < p.W) {
+          const long mo = mrow + wpx;
+          *reinterpret_cast<uint4*>(p.out + mo * 64 + c * 8) = pk;
+          if (bits_st) p.bits_out[mo * 8 + c] = (uint8_t)pos_bits8(pk);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (MODE == C64_DGRAD && p.colsum) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csum[jb][e] += __shfl_xor(csum[jb][e], o, 64);
+    if (r16 == 0) {
+      float* rowp = p.colsum + (long)(gb * 4 + wave) * 64;
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+        *reinterpret_cast<float4*>(rowp + 16 * jb + cq) = make_float4(csum[jb][0], csum[jb][1], csum[jb][2], csum[jb][3]);
+    }
+  }
+}
+
+int g_c64_variant = 2;   // 2: row-tile kernel (weights in registers); 1: pixel-ring kernel
 int g_c64_grid = 0;   // test knob: cap on the workgroup count (0: one per CU), so that small
                       // problems still run many tiles per workgroup through the ring
+// workgroups: one per CU (capped by the tile count); the partial column-sum rows are 4 per
+// workgroup for either form, so a caller sizes them from the pixel count alone
 int conv3x3c64_grid(int M) {
   const int T = (M + C64_BM - 1) / C64_BM;
   int C = num_cus();
   if (g_c64_grid > 0 && g_c64_grid < C) C = g_c64_grid;
   return T < C ? T : C;
 }
-int conv3x3c64_partial_rows(int M) { return conv3x3c64_grid(M) * 4; }
+int conv3x3c64_partial_rows(int M) { return num_cus() * 4; }
 
 const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
   C64Params p = p_in;
@@ -277,13 +504,29 @@ const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
   if (mode == C64_DGRAD && !p.bits_mask) return "conv3x3c64: data gradient needs the ReLU bits";
   p.mg_hw = fdiv_magic(p.H * p.W);
   p.mg_w = fdiv_magic(p.W);
-  const int G = conv3x3c64_grid(p.M);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, C64_LDS);
     (void)hipFuncSetAttribute((const void*)conv3x3c64_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, C64_LDS);
+    (void)hipFuncSetAttribute((const void*)conv3x3c64_row_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, CR_LDS);
+    (void)hipFuncSetAttribute((const void*)conv3x3c64_row_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, CR_LDS);
     attr = true;
   }
+  if (g_c64_variant == 2 && p.W + 2 <= 64) {
+    const int T = p.N * ((p.H + 3) / 4);
+    int G = num_cus();
+    if (g_c64_grid > 0 && g_c64_grid < G) G = g_c64_grid;
+    if (G > T) G = T;
+    if (p.colsum)   // (rows of workgroups the grid leaves out stay zero for the reduction)
+      (void)hipMemsetAsync(p.colsum + (long)G * 4 * 64, 0, (size_t)(num_cus() - G) * 4 * 64 * sizeof(float), s);
+    if (mode == C64_FWD) hipLaunchKernelGGL(conv3x3c64_row_kernel<C64_FWD>, dim3(G), dim3(256), CR_LDS, s, p);
+    else hipLaunchKernelGGL(conv3x3c64_row_kernel<C64_DGRAD>, dim3(G), dim3(256), CR_LDS, s, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? nullptr : hipGetErrorString(e);
+  }
+  const int G = conv3x3c64_grid(p.M);
+  if (p.colsum && G < num_cus())
+    (void)hipMemsetAsync(p.colsum + (long)G * 4 * 64, 0, (size_t)(num_cus() - G) * 4 * 64 * sizeof(float), s);
   if (mode == C64_FWD) hipLaunchKernelGGL(conv3x3c64_kernel<C64_FWD>, dim3(G), dim3(256), C64_LDS, s, p);
   else hipLaunchKernelGGL(conv3x3c64_kernel<C64_DGRAD>, dim3(G), dim3(256), C64_LDS, s, p);
   hipError_t e = hipGetLastError();

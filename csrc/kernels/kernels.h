@@ -188,7 +188,7 @@ struct C64Params {
 };
 const char* conv3x3c64_launch(const C64Params& p, int mode, hipStream_t s);
 int conv3x3c64_partial_rows(int M);
-extern int g_c64_grid, g_c64w_grid, g_stem_pool_variant;
+extern int g_c64_grid, g_c64w_grid, g_stem_pool_variant, g_c64_variant;
 struct C64WgradParams {
   const uint16_t* x;          // [N][H][W][64] conv input
   const uint16_t* g;          // [N][H][W][64] output gradient

@@ -102,6 +102,7 @@ class HipEngine:
         # batches where every CU streams several tiles through its ring
         self.c64 = self.C64_OK and os.environ.get("PDDL_C64", "1") != "0"
         self.c64w = self.c64 and os.environ.get("PDDL_C64W", "1") != "0"
+        self.c64_min_m = int(os.environ.get("PDDL_C64_MIN_M", self.C64_MIN_M))
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -388,7 +389,7 @@ class HipEngine:
         return self.fuse_bwd and bi not in s2 and (b.filters == 64 or (b.filters == 128 and self._fuse_bwd3))
 
     def _use_c64(self, f, M, W, bits=True) -> bool:
-        return self.c64 and f == 64 and W + 1 <= 64 and M >= self.C64_MIN_M and bits
+        return self.c64 and f == 64 and W + 1 <= 64 and M >= self.c64_min_m and bits
 
     def _c2_wgrad(self, W, y1, g2, c2n, f, B, Ho, g2_n):
         """Weight gradient of a bottleneck's stride-1 3x3 conv (on the side stream when two-stream)."""

@@ -286,6 +286,37 @@ def test_fused_conv3_backward_matches_unfused(monkeypatch):
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_c64_kernels_in_engine_match_generic(monkeypatch, variant):
+    """The stage-2 3x3 convs on conv3x3c64.hip (forward, data gradient -- 1: pixel ring, 2: row
+    tiles -- and the row-tile weight gradient; the engine enables them from b >= 84 at 224, here
+    forced on with PDDL_C64_MIN_M) against the generic implicit GEMM / wgrad kernels: same loss,
+    flat gradients to fp32 accumulation order."""
+    from pddl.models.engine import HipEngine
+    from pddl.models.resnet50 import ParamLayout
+    L = ParamLayout()
+    B = 8
+    res = []
+    monkeypatch.setenv("PDDL_C64_MIN_M", "1")
+    N_ = None
+    for on in ("1", "0"):
+        monkeypatch.setenv("PDDL_C64", on)
+        he = HipEngine(L, B, crop=224, image_size=224)
+        he.N.set_variant("c64", int(variant))
+        he.init(seed=7)
+        assert he.c64 == (on == "1") and he._use_c64(64, B * 56 * 56, 56) == (on == "1")
+        img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(1)).cuda()
+        lab = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(2)).cuda()
+        st = he.forward_backward(img, lab, 1.0 / B)
+        torch.cuda.synchronize()
+        res.append((st[0].item() / B, he.grads.clone()))
+        N_ = he.N
+    N_.set_variant("c64", 2)
+    (l1, g1), (l0, g0) = res
+    assert abs(l1 - l0) < 1e-3 * abs(l0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
+
+
 @pytest.mark.parametrize("graphed", [False, True])
 def test_two_stream_backward_matches_one_stream(monkeypatch, graphed):
     """Small-batch backward with the weight gradients on a side stream (PDDL_TWO_STREAM=1, the

@@ -1013,13 +1013,23 @@ def test_stem_pool_bwd_fused_matches_unfused(B, crop, rows):
     assert torch.allclose(cs.sum(0), cs_r.sum(0), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("n,h,grid", [(24, 56, 0), (6, 56, 4), (50, 13, 3), (3, 17, 0)])
+@pytest.mark.parametrize("n,h,grid", [(24, 56, 0), (6, 56, 4), (50, 13, 3), (3, 17, 0), (4, 61, 0)])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_conv3x3c64_ring_matches_reference(mode, n, h, grid):
-    """Persistent pixel-ring 3x3 conv (conv3x3c64.hip), forward (BN + ReLU + bits) and data
-    gradient (ReLU-bit mask + column sums), against the fp32 PyTorch conv of the same bf16
-    operands and against the generic implicit GEMM (same k order).  `grid` caps the workgroup
-    count so each workgroup streams many tiles through the ring (wrap-around, tile tails)."""
+@pytest.mark.parametrize("variant", [1, 2])
+def test_conv3x3c64_ring_matches_reference(variant, mode, n, h, grid):
+    """The 64-channel 3x3 conv kernels (conv3x3c64.hip: 1 = persistent pixel ring, 2 = row tiles
+    with register-resident weights), forward (BN + ReLU + bits) and data gradient (ReLU-bit mask +
+    column sums), against the fp32 PyTorch conv of the same bf16 operands and against the generic
+    implicit GEMM (same k order).  `grid` caps the workgroup count so each workgroup streams many
+    tiles (ring wrap-around, window double-buffering, tile tails, partial last row tile)."""
+    N().set_variant("c64", variant)
+    try:
+        _c64_case(mode, n, h, grid)
+    finally:
+        N().set_variant("c64", 2)
+
+
+def _c64_case(mode, n, h, grid):
     torch.manual_seed(40 + mode)
     x = rnd(n, h, h, 64)
     w = rnd(64, 576, scale=0.05)
