@@ -538,7 +538,10 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
     __syncthreads();   // (the next half overwrites Cs)
   }
 }
-int g_conv_f32_variant = 1;   // 1: 128 x 128 LDS-DMA kernels where they apply (C % 16 == 0), 0: 64 x 64 only
+int g_conv_f32_variant = 1;   // 1: 128 x 128 LDS-DMA kernels where they apply (C % 16 == 0) and, for the
+                              // forward / dgrad, where the problem has >= 4 tiles per CU (fewer: the
+                              // 2-per-CU 128 x 128 tiles leave a half-empty last round -- b256 stage
+                              // 4/5: 784 / 392 tiles on 512 slots); 2: wherever they apply; 0: 64 x 64 only
 
 // Weight gradient on 128 (Cout) x 128 (K) tiles, reduction over m in steps of 16 rows, the same
 // 3-stage LDS-DMA pipeline.  Both operands arrive row-major ([m][n] / [m][k] rows of 128 floats,
@@ -669,8 +672,10 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (const char* e = check_f32(p)) return e;
   p.mg_howo = fdiv_magic(p.Ho * p.Wo);
   p.mg_wo = fdiv_magic(p.Wo);
-  if (g_conv_f32_variant == 1 && p.C % 16 == 0 && p.R * p.S <= 32) {
-    const int grid = ((p.M + G_BM - 1) / G_BM) * ((p.Cout + G_BN - 1) / G_BN);
+  const int big_grid = ((p.M + G_BM - 1) / G_BM) * ((p.Cout + G_BN - 1) / G_BN);
+  if (g_conv_f32_variant >= 1 && p.C % 16 == 0 && p.R * p.S <= 32 &&
+      (g_conv_f32_variant == 2 || big_grid >= 4 * num_cus())) {
+    const int grid = big_grid;
     hipLaunchKernelGGL(conv_f32_big_kernel, dim3(grid), dim3(256), 0, stream, p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? nullptr : hipGetErrorString(e);
@@ -694,7 +699,7 @@ const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (splits < 1) splits = 1;
   int mps = ((p.M + splits - 1) / splits + F_BK - 1) / F_BK * F_BK;
   splits = (p.M + mps - 1) / mps;
-  if (g_conv_f32_variant == 1 && p.C % 4 == 0 && p.Cout % 4 == 0) {
+  if (g_conv_f32_variant >= 1 && p.C % 4 == 0 && p.Cout % 4 == 0) {
     const int bt = ((p.Cout + 127) / 128) * ((p.K + 127) / 128);
     int bs = (3 * num_cus() + bt - 1) / bt;                  // ~3 workgroups per CU
     const int bcap = (p.M + 511) / 512;                      // each reducing >= 512 rows of m

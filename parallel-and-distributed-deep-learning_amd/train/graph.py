@@ -128,6 +128,12 @@ class SegmentedStepGraphs(GraphedTrainStep):
         eng, opt = self.engine, self.opt
         dev = eng.params.device
         nb = len(self.buckets)
+        # one stream: the two-stream backward's side stream forked across the segment cuts
+        # captured fine but its replay segfaulted inside hipGraphLaunch in a long-lived process
+        # (tests/test_gpu_runtime.py::test_mirrored_graphed_step_matches_eager after the rest of
+        # the GPU suite; alone it passed), so segmented replicas run the single-stream schedule
+        if getattr(eng, "side", None) is not None:
+            eng.side = None
         opt.sync_hparams()
         torch.cuda.synchronize(dev)
         it = opt._iterations
