@@ -196,6 +196,24 @@ struct C64WgradParams {
   int N, H, W;
 };
 const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s);
+
+// Fused 64-channel bottleneck boundary (c3c1.hip): block b's conv3 (+ residual, or the fused
+// projection with a second A source) and block b + 1's conv1, one launch.
+struct C3C1Params {
+  const uint16_t* a;           // [M][64] conv3 input (block b's conv2 output)
+  const uint16_t* a2;          // optional [M][64] second K source (fused projection: block input)
+  const uint16_t* w3;          // [256][64 or 128] conv3 (+ shortcut) weights, BN scale folded or not
+  const float* scale3; const float* shift3;   // [256]
+  const uint16_t* res;         // optional [M][256] residual (plain blocks)
+  uint16_t* out;               // [M][256] block-b output
+  uint8_t* bits3;              // optional [M][32] its ReLU bits
+  const uint16_t* w1;          // [64][256] block b+1 conv1 weights
+  const float* scale1; const float* shift1;   // [64]
+  uint16_t* y1;                // [M][64] block b+1 conv1 output
+  uint8_t* bits1;              // optional [M][8]
+  int M;
+};
+const char* c3c1_launch(const C3C1Params& p, hipStream_t s);
 const char* stem_pool_bwd_launch(StemPoolBwdParams p, hipStream_t s);
 int stem_pool_bwd_partial_rows(int B, int H2, int PB);
 int stem_pool_lds_bytes(int Ws, int W1);

@@ -51,6 +51,7 @@ class HipEngine:
     TWO_STREAM_OK = True
     C64_OK = True           # stage-2 3x3 convs on the persistent pixel-ring kernel (conv3x3c64.hip)
     C64_MIN_M = 262144      # ... from 4 x 256 CUs x 256-pixel tiles up (b >= 84 at 56 x 56)
+    C3C1_OK = True          # stage-2 boundaries: conv3 + next conv1 fused (c3c1.hip)
     TWO_STREAM_MAX_BATCH = 1024
     GRAD_RING = 3           # two-stream: gradient buffers per kind, so the data-gradient chain can run
                             # two blocks ahead of the weight gradients still reading older ones
@@ -103,6 +104,8 @@ class HipEngine:
         self.c64 = self.C64_OK and os.environ.get("PDDL_C64", "1") != "0"
         self.c64w = self.c64 and os.environ.get("PDDL_C64W", "1") != "0"
         self.c64_min_m = int(os.environ.get("PDDL_C64_MIN_M", self.C64_MIN_M))
+        # stage-2 block boundaries: conv3 + the next block's conv1 in one launch (c3c1.hip)
+        self.c3c1 = int(os.environ.get("PDDL_C3C1", "1")) if self.C3C1_OK else 0
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -391,6 +394,16 @@ class HipEngine:
     def _use_c64(self, f, M, W, bits=True) -> bool:
         return self.c64 and f == 64 and W + 1 <= 64 and M >= self.c64_min_m and bits
 
+    def _c3c1_ok(self, b, nb) -> bool:
+        """Fuse block b's conv3 with block nb's conv1 (c3c1.hip): 64-channel stride-1 boundaries
+        (stage 2: conv2_block1 -> 2 with the fused projection, 2 -> 3), not into a projection block."""
+        if not self.c3c1 or nb is None or b.filters != 64 or nb.filters != 64 or nb.proj or nb.stride != 1:
+            return False
+        if b.proj:   # the fused-projection form (K = 128, two A tiles) measured no gain: 2.77 ms fused vs
+            # 1.87 + 0.90 ms separate at b2560 (profiles/r4_c3c1.txt); opt in with PDDL_C3C1=2
+            return self.c3c1 == 2 and self.fuse_proj and b.stride == 1 and b.cin == 64
+        return True
+
     def _c2_wgrad(self, W, y1, g2, c2n, f, B, Ho, g2_n):
         """Weight gradient of a bottleneck's stride-1 3x3 conv (on the side stream when two-stream)."""
         if self.c64w and self._use_c64(f, B * Ho * Ho, Ho) and Ho + 2 <= 64:
@@ -439,7 +452,8 @@ class HipEngine:
                     None, 0, 0, 0, 0, 0, None, None)
             N.maxpool_fwd(c1, pool, self.pidx[:B], self.pool_bits[:B] if use_bits else None)
         x = pool
-        for b in L.blocks:
+        c1_done = False   # this block's conv1 already ran inside the previous block's c3c1 launch
+        for bi, b in enumerate(L.blocks):
             a = self.acts[b.name]
             bt = {k: v[:B] for k, v in self.bits[b.name].items()} if use_bits else {}
             H, Ho = self.geo[b.name]
@@ -447,7 +461,9 @@ class HipEngine:
             y1, y2, out = a["y1"][:B], a["y2"][:B], a["out"][:B]
             c1n = b.convs["1"].name
             ch1 = self.ch[c1n]
-            if b.proj and self.fuse_proj:
+            if c1_done:
+                res = x
+            elif b.proj and self.fuse_proj:
                 # conv1 alone; the shortcut conv runs inside conv3's GEMM (second A source = the block
                 # input at the block's stride, K = f + cin, both BN scales folded into the weights), so
                 # the shortcut activation is never written and re-read as a residual
@@ -474,7 +490,24 @@ class HipEngine:
                         self.scale[self.ch[c2]:], self.shift[self.ch[c2]:], None, None, None, y2, 1, None, 0, 0, 0,
                         0, 0, None, bt.get("y2"))
             c3 = b.convs["3"].name
-            if b.proj and self.fuse_proj:
+            nb = L.blocks[bi + 1] if bi + 1 < len(L.blocks) else None
+            c1_done = False
+            if self._c3c1_ok(b, nb):
+                # conv3 of this block + conv1 of the next in one launch: the next conv1 reads this
+                # block's output from LDS (c3c1.hip)
+                an = self.acts[nb.name]
+                btn = {k: v[:B] for k, v in self.bits[nb.name].items()} if use_bits else {}
+                c1x = nb.convs["1"].name
+                if b.proj:
+                    fz = "fuse:" + b.name
+                    w3, k3, a2, rs = self._wf(fz, 4 * f, f + cin), self.ch[fz], x, None
+                else:
+                    w3, k3, a2, rs = self._wf(c3, 4 * f, f), self.ch[c3], None, res
+                N.c3c1(y2, a2, w3, self.scale[k3:], self.shift[k3:], rs, out, bt.get("out"),
+                       self._wf(c1x, nb.filters, nb.cin), self.scale[self.ch[c1x]:], self.shift[self.ch[c1x]:],
+                       an["y1"][:B], btn.get("y1"))
+                c1_done = True
+            elif b.proj and self.fuse_proj:
                 fz = "fuse:" + b.name
                 N.igemm(y2, x, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(fz, 4 * f, f + cin), 0,
                         self.scale[self.ch[fz]:], self.shift[self.ch[fz]:], None, None, None, out, 1, None, 0, 0, 0,

@@ -28,17 +28,32 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         ev.append(("maxpool_fwd", "pool", 0, B * (H1 * H1 + H2 * H2) * 64 * 2))
     H = H2
     geo = []
-    for b in L.blocks:
+    c3c1_on = int(os.environ.get("PDDL_C3C1", "1"))
+    blocks = list(L.blocks)
+
+    def c3c1(b, nb):   # engine._c3c1_ok
+        if not c3c1_on or nb is None or b.filters != 64 or nb.filters != 64 or nb.proj or nb.stride != 1:
+            return False
+        return not b.proj or (c3c1_on == 2 and fuse and b.stride == 1 and b.cin == 64)
+    c1_done = False
+    for bi, b in enumerate(blocks):
         f, cin = b.filters, b.cin
         Ho = (H - 1) // b.stride + 1
         M = B * Ho * Ho
         n1 = 5 * f if b.proj and not fuse else f
-        ev.append(("igemm", f"{b.name} c1{'+c0' if n1 > f else ''} fwd", 2 * M * cin * n1, (B * H * H * cin + M * n1) * 2,
-                   (M, n1, cin)))
+        nb = blocks[bi + 1] if bi + 1 < len(blocks) else None
+        if not c1_done:
+            ev.append(("igemm", f"{b.name} c1{'+c0' if n1 > f else ''} fwd", 2 * M * cin * n1,
+                       (B * H * H * cin + M * n1) * 2, (M, n1, cin)))
         c64 = f == 64 and M >= 262144 and Ho + 1 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
         ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2,
                    (M, f, 9 * f)))
-        if b.proj and fuse:   # conv3 + the shortcut conv as one dual-source GEMM (K = f + cin)
+        c1_done = c3c1(b, nb)
+        if c1_done:   # conv3 (+ shortcut) and the next block's conv1 in one launch
+            k3 = f + cin if b.proj else f
+            ev.append(("c3c1", f"{b.name} c3 + {nb.name} c1 fwd", 2 * M * k3 * 4 * f + 2 * M * 4 * f * f,
+                       (M * k3 + (0 if b.proj else M * 4 * f) + M * 4 * f + M * f) * 2))
+        elif b.proj and fuse:   # conv3 + the shortcut conv as one dual-source GEMM (K = f + cin)
             ev.append(("igemm", f"{b.name} c3+c0 fwd", 2 * M * (f + cin) * 4 * f, (M * f + M * cin + M * 4 * f) * 2,
                        (M, 4 * f, f + cin), "dual"))
         else:

@@ -324,6 +324,33 @@ def test_c64_kernels_in_engine_match_generic(monkeypatch, variant):
     assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
 
 
+def test_c3c1_boundary_fusion_in_engine(monkeypatch):
+    """Stage-2 block boundaries with conv3 + the next conv1 in one launch (c3c1.hip, PDDL_C3C1=1,
+    the default) against separate launches: same loss, flat gradients to fp32 order; and the
+    engine with the fusion stays within the fp32 reference's bf16-point noise floor."""
+    from pddl.models.engine import HipEngine
+    from pddl.models.resnet50 import ParamLayout
+    L = ParamLayout()
+    B = 8
+    res = []
+    for on in ("2", "0"):   # (2: also the fused-projection boundary conv2_block1 -> 2)
+        monkeypatch.setenv("PDDL_C3C1", on)
+        he = HipEngine(L, B, crop=224, image_size=224)
+        assert he.c3c1 == int(on)
+        he.init(seed=7)
+        img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(1)).cuda()
+        lab = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(2)).cuda()
+        st = he.forward_backward(img, lab, 1.0 / B)
+        torch.cuda.synchronize()
+        res.append((st[0].item() / B, he.grads.clone()))
+    (l1, g1), (l0, g0) = res
+    print(f"c3c1: loss rel {abs(l1 - l0) / abs(l0):.2e}, grad rel {((g1 - g0).norm() / g0.norm()).item():.3e}")
+    assert abs(l1 - l0) < 1e-4 * abs(l0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
+    monkeypatch.setenv("PDDL_C3C1", "1")
+    test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
+
+
 @pytest.mark.parametrize("variant", ["1", "2"])
 def test_c64_engine_within_noise_floor(monkeypatch, variant):
     """The engine with the stage-2 3x3 convs forced onto conv3x3c64.hip is as close to the fp32
