@@ -403,12 +403,15 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_bwd_kernel(StemPoolBw
 
 int stem_pool_bwd_lds_bytes(int Ws) { return 8 * Ws * 32 + 2 * 16384 + 4 * 64 * 4; }
 
+// Pool rows per backward workgroup: whole images at large batches; at small ones the largest block
+// that still gives ~2 workgroups per CU.  Every workgroup ends with 64 x 256 fp32 atomics into dW,
+// so the one-row blocks of the forward heuristic (4 per CU) cost b32 1,792 x 16 Ki atomics: 150 us
+// of a 4.2 ms step (profiles/r4_b32_timeline.txt).
 static int stem_pool_rows(int B, int H2, int PB) {
   if (PB > 0) return PB;
-  const long want = 4L * num_cus();
-  int pb = H2;
-  while (pb > 1 && (long)B * ((H2 + pb - 1) / pb) < want) pb = (pb + 1) / 2;
-  return pb;
+  const long want = 2L * num_cus();
+  long pb = (long)B * H2 / want;
+  return (int)(pb < 1 ? 1 : (pb > H2 ? H2 : pb));
 }
 int stem_pool_bwd_partial_rows(int B, int H2, int PB) {
   const int pb = stem_pool_rows(B, H2, PB);
