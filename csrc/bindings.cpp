@@ -254,8 +254,22 @@ void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
 // Fused stride-1 1x1 conv backward (bwd1x1.hip): g [.., CO], x [.., CI], wd [CI][>=CO] bf16,
 // bits [.., CI/8] uint8, out [.., CI] bf16, colsum fp32 >= partial rows x CI, dw fp32 [CO][>=CI];
 // (CO, CI) = (256, 64) or (512, 128).
-void bwd1x1(Tensor g, Tensor x, Tensor wd, Tensor bits, Tensor out, Tensor colsum, Tensor dw, OptT out2) {
+void bwd1x1(Tensor g, Tensor x, Tensor wd, Tensor bits, Tensor out, Tensor colsum, Tensor dw, OptT out2, OptT g1,
+            OptT w1d, OptT gmask, OptT gx, OptT colsum_gx) {
   pddl::Bwd1x1Params p{};
+  if (g1.has_value()) {   // pre form: g = bit(gmask) * (g1 . w1d^T + g) computed per tile, written to gx
+    PCHECK(!out2.has_value() && w1d.has_value() && gmask.has_value() && gx.has_value() && colsum_gx.has_value(),
+           "bwd1x1 pre form: g1, w1d, gmask, gx, colsum_gx together, stride-1 only");
+    PCHECK(g.size(-1) == 256 && g1->size(-1) == 64 && g1->is_contiguous() && rows_of(*g1) == rows_of(g),
+           "bwd1x1 pre form: g1 [M,64] next to g [M,256]");
+    PCHECK(w1d->dim() == 2 && w1d->size(0) == 256 && w1d->size(1) == 64 && w1d->is_contiguous(), "bwd1x1: w1d [256,64]");
+    PCHECK(gmask->scalar_type() == torch::kUInt8 && gmask->numel() == rows_of(g) * 32, "bwd1x1: gmask [M,32] uint8");
+    PCHECK(gx->sizes() == g.sizes() && gx->is_contiguous() && gx->scalar_type() == torch::kBFloat16, "bwd1x1: gx like g");
+    PCHECK(colsum_gx->numel() >= (int64_t)pddl::bwd1x1_partial_rows((int)rows_of(g), 256, 64) * 256,
+           "bwd1x1: colsum_gx too small");
+    p.g1 = bfp(*g1); p.w1d = bfp(*w1d); p.gmask = gmask->data_ptr<uint8_t>(); p.gx = bfpm(*gx);
+    p.colsum_gx = f32p(*colsum_gx);
+  }
   PCHECK(g.is_contiguous() && x.is_contiguous() && out.is_contiguous() && bits.is_contiguous(), "bwd1x1: contiguous operands");
   const int64_t CO = g.size(-1), CI = x.size(-1);
   PCHECK((CO == 256 && CI == 64) || (CO == 512 && CI == 128), "bwd1x1: (CO, CI) must be (256, 64) or (512, 128)");
@@ -764,7 +778,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("BNSTAT_LAYER_BYTES") = (int)sizeof(pddl::BnStatLayer);
   m.def("wgrad", &wgrad, REL);
   m.def("bwd1x1", &bwd1x1, REL, py::arg("g"), py::arg("x"), py::arg("wd"), py::arg("bits"), py::arg("out"),
-        py::arg("colsum"), py::arg("dw"), py::arg("out2") = py::none());
+        py::arg("colsum"), py::arg("dw"), py::arg("out2") = py::none(), py::arg("g1") = py::none(),
+        py::arg("w1d") = py::none(), py::arg("gmask") = py::none(), py::arg("gx") = py::none(),
+        py::arg("colsum_gx") = py::none());
   m.def("bwd1x1_partial_rows", &bwd1x1_partial_rows);
   m.def("conv_f32", &conv_f32, REL);
   m.def("conv_f32_epi", &conv_f32_epi, REL);

@@ -52,13 +52,37 @@ __device__ __forceinline__ b1_v4u b1_read16(const char* p) {
 // CI = 64 NH: with NH = 2 (stage 3: CI = 128 would need 272 registers per lane for the dW tile and
 // the weight fragments) the two halves of a tile run as a PAIR of workgroups b, b + 8 -- the same
 // XCD under the round-robin dispatch -- in lockstep, so the second read of each g tile hits L2.
-template <int CO, int NW, bool S2>
-__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1Params p) {
+__device__ __forceinline__ uint2 b1_read8(const char* p) {
+  uint2 r;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
+  return r;
+}
+__device__ __forceinline__ void b1_write8(char* p, uint2 v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"((uint32_t)(uintptr_t)LDS_PTR(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t b1_read_u8(const char* p) {
+  uint32_t r;
+  asm volatile("ds_read_u8 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
+  return r;
+}
+
+// PRE (stage 2 only): the g tile is computed in LDS from the next block's conv1 gradient instead
+// of read -- the next block's conv1 data gradient fused in front (one 4.1 GB read of g fewer per
+// stage-2 block boundary at b2560): the shortcut gradient is DMA'd into the g images, the next
+// block's conv1 gradient g1 and this block's output ReLU bits into two small images, and
+//   g = bit * (g1 . w1d^T + shortcut gradient)
+// overwrites the images in place (each lane reads its 8 bytes of the shortcut gradient where it
+// writes its 8 bytes of g), is stored to HBM and summed per channel, then both GEMMs below run
+// on it unchanged.  One 100 KiB workgroup per CU.
+template <int CO, int NW, bool S2, bool PRE = false>
+__global__ void __launch_bounds__(NW * 64, (NW == 8 || PRE) ? 1 : 2) bwd1x1_kernel(Bwd1x1Params p) {
   constexpr int CB = 64, MT = B1_MT;
   constexpr int NIMG = CO / 128;                         // 128-co half images
   constexpr int GH_BYTES = MT * 256;                     // one image: 16 KiB
   constexpr int G_BYTES = NIMG * GH_BYTES, X_BYTES = MT * CB * 2;
-  constexpr int STAGE = G_BYTES + X_BYTES;               // 40 KiB (256) / 72 KiB (512); two stages
+  constexpr int G1_BYTES = PRE ? MT * 128 : 0, GM_BYTES = PRE ? MT * CO / 8 : 0;
+  constexpr int STAGE = G_BYTES + X_BYTES + G1_BYTES + GM_BYTES;   // 40 KiB (256; PRE 50) / 72 KiB (512)
+  static_assert(!PRE || (CO == 256 && NW == 4 && !S2), "the pre form is the stage-2 stride-1 kernel");
   constexpr int GP = NIMG * 16 / NW, XP = 8 / NW;        // LDS-DMA pieces per wave per tile
   constexpr int KSPLIT = NW / 4;                         // waves per 16-column dgrad block (co split)
   constexpr int KS = CO / 32 / KSPLIT;                   // dgrad k-steps per wave
@@ -129,6 +153,23 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1
 #pragma unroll
       for (int i = 0; i < XP; ++i) buf_lds16(rx, LDS_PTR(gb + G_BYTES + (wave * XP + i) * 1024), x_off[i], 0);
     }
+    if constexpr (PRE) {
+      // g1 tile [64 m][64 ch] (chunk ^ ((row >> 1) & 7)): 8 pieces, 2 per wave; the output's ReLU
+      // bits [64 m][32 B] lane-linear: 2 pieces (waves 0, 1)
+      const __amdgpu_buffer_rsrc_t r1 = make_rsrc_at(p.g1, m0 * 64, (long)p.M * 64);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pc = wave * 2 + i, row = pc * 8 + (lane >> 3);
+        buf_lds16(r1, LDS_PTR(gb + G_BYTES + X_BYTES + pc * 1024),
+                  (uint32_t)((row * 64 + ((lane & 7) ^ ((row >> 1) & 7)) * 8) * 2), 0);
+      }
+      if (wave < 2) {
+        const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(p.gmask) + m0 * (CO / 8), (short)0,
+            (int)(m0 < p.M ? lmin(((long)p.M - m0) * (CO / 8), 0x7fffffffL) : 0), 0x00020000);
+        buf_lds16(rm, LDS_PTR(gb + G_BYTES + X_BYTES + G1_BYTES + wave * 1024), (uint32_t)((wave * 64 + lane) * 16), 0);
+      }
+    }
   };
 
   // dgrad roles: 16-column block cb of this half, co range kp * CO / KSPLIT ..; the weights of
@@ -139,6 +180,20 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1
     const uint16_t* wr = p.wd + (long)(half * CB + 16 * cb + (lane & 15)) * p.ld_wd + kp * (CO / KSPLIT) + 8 * (lane >> 4);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) wa[ks] = *reinterpret_cast<const v8bf*>(wr + 32 * ks);
+  }
+
+  // PRE: the next block's conv1 data-gradient weights as MFMA A fragments: rows co = 64 wave +
+  // 16 jb + (lane & 15), k = 32 kh + 8 (lane >> 4) .. + 7 (the g tile's 64 co columns of this wave)
+  v8bf w1f[PRE ? 4 : 1][2];
+  float csx[PRE ? 16 : 1];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+        w1f[jb][kh] = *reinterpret_cast<const v8bf*>(p.w1d + (64 * wave + 16 * jb + (lane & 15)) * 64 + 32 * kh + 8 * (lane >> 4));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) csx[e] = 0.f;
   }
 
   v4f accw[4][4];
@@ -181,6 +236,81 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1
     load_bits(tile + np);
     const char* gb = smem + cur * STAGE;
     const char* xb = gb + G_BYTES;
+
+    if constexpr (PRE) {
+      // ---- g = bit * (g1 . w1d^T + shortcut gradient), in place in the g images
+      const char* g1b = gb + G_BYTES + X_BYTES;
+      const char* gmb = g1b + G1_BYTES;
+      v4f acc1[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) acc1[i][jb] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        b1_v4u bx[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * i + (lane & 15), ch = kh * 4 + (lane >> 4);
+          bx[i] = b1_read16(g1b + row * 128 + ((ch ^ ((row >> 1) & 7)) << 4));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jb = 0; jb < 4; ++jb)
+            acc1[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[jb][kh], __builtin_bit_cast(v8bf, bx[i]), acc1[i][jb], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // lane: co = 64 wave + 16 jb + 4 kq + e (image wave >> 1), row 16 i + (lane & 15)
+      const int kq = lane >> 4;
+      char* gw = const_cast<char*>(gb) + (wave >> 1) * GH_BYTES;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * i + (lane & 15);
+        uint2 ad[4];
+        uint32_t mb[4];
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const int cc = 64 * (wave & 1) + 16 * jb + 4 * kq;   // column within the 128-co image
+          ad[jb] = b1_read8(gw + row * 256 + (((cc >> 3) ^ b1_swz256(row)) << 4) + 8 * (kq & 1));
+          mb[jb] = b1_read_u8(gmb + row * (CO / 8) + ((64 * wave + 16 * jb + 4 * kq) >> 3));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);   // (the asm reads' results: nothing may move above the wait)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const int cc = 64 * (wave & 1) + 16 * jb + 4 * kq;
+          const float a4[4] = {__uint_as_float(ad[jb].x << 16), __uint_as_float(ad[jb].x & 0xffff0000u),
+                               __uint_as_float(ad[jb].y << 16), __uint_as_float(ad[jb].y & 0xffff0000u)};
+          const int sh = (kq & 1) * 4;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = ((mb[jb] >> (sh + e)) & 1u) ? acc1[i][jb][e] + a4[e] : 0.f;
+            if (m0 + row < p.M) csx[4 * jb + e] += v[e];
+          }
+          b1_write8(gw + row * 256 + (((cc >> 3) ^ b1_swz256(row)) << 4) + 8 * (kq & 1),
+                    make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3])));
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // g tile -> HBM (256 threads x 8 x 16 B, 512-byte rows)
+      b1_v4u gv[8];
+#pragma unroll
+      for (int it2 = 0; it2 < 8; ++it2) {
+        const int idx = it2 * 256 + tid, row = idx >> 5, c32 = idx & 31;
+        gv[it2] = b1_read16(gb + (c32 >> 4) * GH_BYTES + row * 256 + (((c32 & 15) ^ b1_swz256(row)) << 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int it2 = 0; it2 < 8; ++it2) {
+        const int idx = it2 * 256 + tid, row = idx >> 5, c32 = idx & 31;
+        if (m0 + row < p.M) *reinterpret_cast<b1_v4u*>(p.gx + (m0 + row) * CO + c32 * 8) = gv[it2];
+      }
+    }
 
     // ---- data gradient: D[ci][m] = sum_co Wd[ci][co] g[m][co]; lane (grp, r): ci 4grp..4grp+3
     // of block cb, m = 16i + r.  Reads of k-step ks + 1 are issued before the MFMAs of ks.
@@ -303,6 +433,18 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) bwd1x1_kernel(Bwd1x1
     dst[0] = make_float4(csum[0], csum[1], csum[2], csum[3]);
     dst[1] = make_float4(csum[4], csum[5], csum[6], csum[7]);
   }
+  if constexpr (PRE) {   // g's per-channel partial sums: row pid * NW + wave, this wave's 64 columns
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) csx[e] += __shfl_xor(csx[e], o, 64);
+    if ((lane & 15) == 0) {
+      float* row = p.colsum_gx + (long)(pid * NW + wave) * CO + 64 * wave + 4 * (lane >> 4);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+        *reinterpret_cast<float4*>(row + 16 * jb) = make_float4(csx[4 * jb], csx[4 * jb + 1], csx[4 * jb + 2], csx[4 * jb + 3]);
+    }
+  }
   if (nit == 0) return;
 
   // dW: per-wave 32-row fp32 staging, then one 256-byte row-contiguous atomic per row
@@ -359,7 +501,13 @@ const char* bwd1x1_launch(const Bwd1x1Params& p, hipStream_t stream) {
     return "bwd1x1: stride-2 grid geometry";
   Bwd1x1Params q = p;
   if (q.s2) { q.mg_hwc = fdiv_magic(q.Hc * q.Wc); q.mg_wc = fdiv_magic(q.Wc); }
-  if (q.CO == 256) {
+  if (q.g1) {
+    if (q.CO != 256 || q.s2 || !q.w1d || !q.gmask || !q.gx || !q.colsum_gx) return "bwd1x1: pre form operands";
+    // (partial rows of other waves' columns stay zero: every row is written by exactly one wave's
+    // 64 columns)
+    (void)hipMemsetAsync(q.colsum_gx, 0, (size_t)np * 4 * 256 * sizeof(float), stream);
+    hipLaunchKernelGGL((bwd1x1_kernel<256, 4, false, true>), dim3(grid), dim3(256), 0, stream, q);
+  } else if (q.CO == 256) {
     if (q.s2) hipLaunchKernelGGL((bwd1x1_kernel<256, 4, true>), dim3(grid), dim3(256), 0, stream, q);
     else hipLaunchKernelGGL((bwd1x1_kernel<256, 4, false>), dim3(grid), dim3(256), 0, stream, q);
   } else {

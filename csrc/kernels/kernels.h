@@ -86,6 +86,14 @@ struct Bwd1x1Params {
   int s2, N, Hf, Wf, Hc, Wc;
   uint16_t* out2;
   uint64_t mg_hwc, mg_wc;              // set by bwd1x1_launch
+  // "pre" form (stage 2, not stride-2): g is not read from HBM but computed per tile from the next
+  // block's conv1 gradient -- g = bit(gmask) * (g1 . w1d^T + g) with g the shortcut gradient --
+  // and written out (gx) with its per-channel partial sums (colsum_gx, rows as colsum, CO columns)
+  const uint16_t* g1;                  // [M][64] gradient of the next block's conv1 output
+  const uint16_t* w1d;                 // [CO][64] its data-gradient weights
+  const uint8_t* gmask;                // [M][CO / 8] ReLU bits of this block's output
+  uint16_t* gx;                        // [M][CO]
+  float* colsum_gx;                    // [bwd1x1_partial_rows][CO]
 };
 const char* bwd1x1_launch(const Bwd1x1Params& p, hipStream_t stream);
 int bwd1x1_partial_rows(int M, int CO, int CI);

@@ -107,6 +107,9 @@ class HipEngine:
         self.c64_min_m = int(os.environ.get("PDDL_C64_MIN_M", self.C64_MIN_M))
         # stage-2 block boundaries: conv3 + the next block's conv1 in one launch (c3c1.hip)
         self.c3c1 = int(os.environ.get("PDDL_C3C1", "1")) if self.C3C1_OK else 0
+        # stage-2 backward boundaries: the next block's conv1 data gradient computed inside this
+        # block's fused conv3 backward (bwd1x1 pre form), its 256-channel result never re-read
+        self.c1pre = self.C3C1_OK and os.environ.get("PDDL_C1PRE", "1") != "0"
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -359,7 +362,10 @@ class HipEngine:
             else:
                 add(b.convs["1"].name, N.igemm_partial_rows(M, f, 9 * f), f)
             if bi > 0:                                                           # c1 dgrad -> g_out(prev)
-                add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin, 5 * f if b.proj else f), b.cin)
+                if self._pre_fused(bi, s2):   # (computed inside block bi-1's fused conv3 backward)
+                    add(blocks[bi - 1].convs["3"].name, N.bwd1x1_partial_rows(M, 256, 64), b.cin)
+                else:
+                    add(blocks[bi - 1].convs["3"].name, N.igemm_partial_rows(M, b.cin, 5 * f if b.proj else f), b.cin)
         if self.fuse_stem:   # (fused pool backward + conv1 weight gradient: one partial row per workgroup)
             add(L.stem.name, N.stem_pool_bwd_partial_rows(B, self.H2), 64)
         else:
@@ -387,6 +393,17 @@ class HipEngine:
 
     def _bwd_fused_s2(self, bi, b, s2):   # the stride-2-grid form (block feeding a downsampling block)
         return self.fuse_bwd and self._fuse_bwd_s2 and bi in s2 and (b.filters == 64 or (b.filters == 128 and self._fuse_bwd3))
+
+    def _pre_fused(self, bi, s2) -> bool:
+        """Block bi's conv1 data gradient runs inside block bi-1's fused conv3 backward (bwd1x1 pre
+        form): both stage-2 (64-channel), block bi not a projection block, block bi-1 on the
+        stride-1 fused conv3 backward."""
+        L = self.L
+        if not self.c1pre or bi < 1 or not self.bitmask:
+            return False
+        b, pb = L.blocks[bi], L.blocks[bi - 1]
+        return (b.filters == 64 and pb.filters == 64 and not b.proj and b.stride == 1 and bi - 1 not in s2
+                and self._bwd_fused(bi - 1, pb, s2))
 
     def _bwd_fused(self, bi, b, s2):
         # stage 2 (256 <- 64 channels) and stage 3 (512 <- 128); PDDL_FUSE_BWD=2: stage 2 only
@@ -645,6 +662,7 @@ class HipEngine:
         self._before_write("gbuf0")
         N.gap_bwd(dpooled, x5, gout, part(blocks[-1].convs["3"].name))
         s2 = self._s2_fed()
+        pre = None   # the previous (deeper) block's deferred conv1 data gradient (bwd1x1 pre form)
         # ---- blocks (column sums of every produced gradient are fused into its producer)
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
@@ -667,6 +685,8 @@ class HipEngine:
             rk = bi % len(self.g2bufs)
             g2 = (self.s2g2full[bi] if bi in s2 else self.g2bufs[rk])[: B * Ho * Ho * f].view(B, Ho, Ho, f)
             g2_n = f"s2g2f{bi}" if bi in s2 else f"g2_{rk}"
+            assert pre is None or self._bwd_fused(bi, b, s2)
+            pre_next = None
             if bi in s2:
                 # gout is zero off the stride-2 grid (the next block reads only even rows /
                 # columns); its compact copy `gc` came from that block's dgrad epilogue
@@ -687,7 +707,13 @@ class HipEngine:
             elif self._bwd_fused(bi, b, s2):
                 # conv3: data and weight gradient from one read of gout
                 self._before_write(g2_n)
-                N.bwd1x1(gout, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f))
+                if pre is not None:
+                    # gout itself is computed per tile from the next block's conv1 gradient
+                    # (pre form): this block's output gradient is written once, never re-read
+                    N.bwd1x1(pre["add"], y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f),
+                             g1=pre["g1"], w1d=pre["w1d"], gmask=pre["gmask"], gx=gout, colsum_gx=pre["cs"])
+                else:
+                    N.bwd1x1(gout, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f))
                 self._c2_wgrad(W, y1, g2, c2n, f, B, Ho, g2_n)
             else:
                 # conv3
@@ -730,11 +756,15 @@ class HipEngine:
                   reads=(f"g1_{rk}",))
                 W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
                 self._before_write(*gx_n)
-                N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, f), 1, None, None, None,
-                        mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0, cs_in, None)
+                if self._pre_fused(bi, s2):   # deferred into block bi-1's fused conv3 backward
+                    pre_next = {"add": gout, "g1": g1, "w1d": self._wdv(c1n, cin, f), "gmask": mask_in, "cs": cs_in}
+                else:
+                    N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, f), 1, None, None, None,
+                            mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0, cs_in, None)
                 last = L.entry(c1n, "kernel")
             done_upto(last.offset + last.size)
             cur = nxt
+            pre, pre_next = pre_next, None
         # ---- stem (space-to-depth wgrad, folded back to 7x7x3)
         H1, H2, Hs = self.H1, self.H2, self.Hs
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)

@@ -69,13 +69,25 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
     ev.append(("gap_bwd", "gap", 0, 0))
     blocks = L.blocks
     s2 = {i for i in range(len(blocks) - 1) if blocks[i + 1].proj and blocks[i + 1].stride == 2}
+    c1pre_on = os.environ.get("PDDL_C1PRE", "1") != "0" and c3c1_on != 0
+
+    def fused_c3(i):
+        fi = blocks[i].filters
+        return fuse_bwd and (fi == 64 or (fi == 128 and fuse_bwd3)) and i not in s2
+
+    def pre_fused(i):   # engine._pre_fused: block i's conv1 dgrad inside block i-1's fused conv3 backward
+        return (c1pre_on and i >= 1 and blocks[i].filters == 64 and blocks[i - 1].filters == 64 and not blocks[i].proj
+                and blocks[i].stride == 1 and fused_c3(i - 1))
     for bi in range(len(geo) - 1, -1, -1):
         b, H, Ho = geo[bi]
         f, cin = b.filters, b.cin
         M = B * Ho * Ho
         # blocks feeding a stride-2 block: conv3 wgrad/dgrad and conv2 wgrad on the compact quarter
         Mc = B * (Ho // 2 + Ho % 2) ** 2 if bi in s2 else M
-        if fuse_bwd and (f == 64 or (f == 128 and fuse_bwd3)) and (bi not in s2 or fuse_s2):   # bwd1x1: one read of g
+        if bi + 1 < len(geo) and pre_fused(bi + 1):
+            ev.append(("bwd1x1", f"{blocks[bi + 1].name} c1 dgrad + {b.name} c3 dgrad+wgrad",
+                       4 * Mc * f * 4 * f + 2 * M * 4 * f * f, (M * f + 3 * M * 4 * f + 2 * Mc * f) * 2))
+        elif fuse_bwd and (f == 64 or (f == 128 and fuse_bwd3)) and (bi not in s2 or fuse_s2):   # bwd1x1: one read of g
             ev.append(("bwd1x1", f"{b.name} c3 dgrad+wgrad", 4 * Mc * f * 4 * f, (Mc * 4 * f + 2 * Mc * f) * 2))
         else:
             ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * Mc * f * 4 * f, (Mc * f + Mc * 4 * f) * 2))
@@ -94,6 +106,8 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         else:
             ev.append(("wgrad", f"{b.name} c1 wgrad", 2 * M * cin * n1, (M * n1 + B * H * H * cin) * 2))
         ev.append(("wgrad_finalize", b.name, 0, 0))
+        if pre_fused(bi):
+            continue
         ev.append(("igemm", f"{b.name} c1 dgrad", 2 * M * cin * n1, (M * n1 + 3 * B * H * H * cin) * 2, (M, cin, n1),
                    "dual" if b.proj else ""))
     if fuse_stem:   # pool backward + conv1 weight gradient in one launch (stem.hip)

@@ -913,6 +913,48 @@ def test_bwd1x1_fused(co, ci, M):
     assert rel(dw - dw0, g.float().t() @ x.float()) < 1e-3
 
 
+@pytest.mark.parametrize("M", [64 * 1000 + 37, 3 * 56 * 56, 200])
+def test_bwd1x1_pre_form_matches_two_launches(M):
+    """bwd1x1 pre form: the next block's conv1 data gradient computed per tile in front of the fused
+    conv3 backward -- g = bit(gmask) * (g1 . w1d^T + shortcut gradient), written to gx with its
+    column sums -- against the igemm dgrad launch followed by the plain bwd1x1 launch."""
+    torch.manual_seed(13)
+    g1 = rnd(M, 64)
+    w1d = rnd(256, 64, scale=0.05)
+    add = rnd(M, 256)
+    ox = rnd(M, 256)
+    gmask = pack_bits(ox)
+    x = torch.relu(rnd(M, 64))
+    wd = rnd(64, 256, scale=0.05)
+    bits = pack_bits(x)
+    rows = N().bwd1x1_partial_rows(M, 256, 64)
+    # pre form
+    gx = torch.full((M, 256), float("nan"), device=dev, dtype=torch.bfloat16)
+    csx = torch.full((rows * 256,), float("nan"), device=dev)
+    out = torch.full((M, 64), float("nan"), device=dev, dtype=torch.bfloat16)
+    cs = torch.full((rows * 64,), float("nan"), device=dev)
+    dw = torch.zeros(256, 64, device=dev)
+    N().bwd1x1(add, x, wd, bits, out, cs, dw, g1=g1, w1d=w1d, gmask=gmask, gx=gx, colsum_gx=csx)
+    # two launches
+    gx_r = torch.empty(M, 256, device=dev, dtype=torch.bfloat16)
+    prow = N().igemm_partial_rows(M, 256, 64)
+    csx_r = torch.full((prow * 256,), float("nan"), device=dev)
+    N().igemm(g1.view(1, 1, M, 64), None, 1, M, 1, 1, 1, 0, 1, M, w1d, 1, None, None, None, gmask.view(1, 1, M, 32),
+              add.view(1, 1, M, 256), gx_r.view(1, 1, M, 256), 0, None, 0, 0, 0, 0, 0, csx_r, None)
+    out_r = torch.empty(M, 64, device=dev, dtype=torch.bfloat16)
+    cs_r = torch.full((rows * 64,), float("nan"), device=dev)
+    dw_r = torch.zeros(256, 64, device=dev)
+    N().bwd1x1(gx_r, x, wd, bits, out_r, cs_r, dw_r)
+    torch.cuda.synchronize()
+    ref_gx = (g1.float() @ w1d.float().t() + add.float()) * (ox.float() > 0)
+    assert rel(gx, ref_gx) < 1e-2
+    assert rel(gx, gx_r) < 2e-3
+    assert rel(csx.view(rows, 256).sum(0), ref_gx.sum(0)) < 1e-3
+    assert rel(out, out_r) < 5e-3
+    assert rel(cs.view(rows, 64).sum(0), cs_r.view(rows, 64).sum(0)) < 5e-3
+    assert rel(dw, dw_r) < 5e-3
+
+
 @pytest.mark.parametrize("co,ci,B,H", [(256, 64, 3, 56), (512, 128, 5, 28), (256, 64, 2, 7)])
 def test_bwd1x1_fused_stride2(co, ci, B, H):
     """Stride-2 form of the fused 1x1 backward (a block feeding a downsampling block): the output
