@@ -331,17 +331,21 @@ __global__ void __launch_bounds__(256) wgrad_f32_kernel(ConvF32Params p, int m_p
 }
 
 // ------------------------------------------------------------------------------------------
-// 128 x 128 tiles (round 4): 4 waves of 64 x 64 (4 x 4 MFMA tiles of 16x16x4 f32), reduction
-// step 16 floats, a 3-stage LDS pipeline fed by buffer LDS-DMA (16 B per lane straight from HBM /
-// L2 into LDS, no register staging).  The gather geometry of each tile row (image, top-left input
-// pixel, bitmask of its in-bounds taps) is computed once per tile; the k walk (tap r, s and
-// channel offset: C % 16 == 0, so a 16-wide step never crosses a tap) is scalar, so the k loop
-// carries no divides.  LDS images are chunk-major ([4 chunks][128 rows][16 B]: one DMA piece =
-// one chunk column of 64 rows), which makes every ds_read_b128 fragment read conflict-free.
+// 128 x BN tiles (round 4; BN = 128, or 64 for the 64-channel layers and small grids): 4 waves
+// as 2 x 2 wave tiles of 64 x BN/2 (4 x BN/32 MFMA tiles of 16x16x4 f32), reduction step 16
+// floats, a 3-stage LDS pipeline fed by buffer LDS-DMA (16 B per lane straight from HBM / L2 into
+// LDS, no register staging).  The gather geometry of each tile row (image, top-left input pixel,
+// bitmask of its in-bounds taps) is computed once per tile; the k walk (tap r, s and channel
+// offset: C % 16 == 0, so a 16-wide step never crosses a tap) is scalar, so the k loop carries no
+// divides.  LDS images are chunk-major ([4 chunks][rows][16 B]: one DMA piece = one chunk column
+// of 64 rows), which makes every ds_read_b128 fragment read conflict-free.  The fragment reads
+// are inline asm: the compiler's own LDS loads after an LDS-DMA make it drain every DMA in flight
+// (s_waitcnt vmcnt(0)), which would serialise the pipeline; the asm reads wait on lgkmcnt only,
+// behind a scheduling barrier so no MFMA is hoisted above the wait.
 // The epilogue is the 64 x 64 kernel's, run over the tile's two 64-row halves through the
 // pipeline's LDS (partial column sums: one row per 64-row half, the same layout).
 namespace {
-constexpr int G_BM = 128, G_BN = 128, G_STAGE = 16384, G_CLD = G_BN + 4;
+constexpr int G_BM = 128;
 
 __device__ __forceinline__ v4f mfma4v(const float4& a, const float4& b, v4f c) {
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
@@ -350,17 +354,30 @@ __device__ __forceinline__ v4f mfma4v(const float4& a, const float4& b, v4f c) {
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
   return c;
 }
+
+__device__ __forceinline__ float4 f32_read16(const char* p) {
+  float4 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
+  return r;
+}
 }  // namespace
 
+template <int BN>
 __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * G_STAGE];
+  constexpr int A_CH = G_BM * 16, B_CH = BN * 16;   // bytes of one 16-byte chunk column
+  constexpr int B_BASE = 4 * A_CH, STAGE = 4 * (A_CH + B_CH);
+  constexpr int NB = BN / 64;                        // B DMA pieces per lane per step
+  constexpr int TJ = BN / 32;                        // MFMA column tiles per wave
+  constexpr int CLD = BN + 4;
+  static_assert(64 * CLD * 4 <= 3 * STAGE, "epilogue tile must fit the pipeline's LDS");
+  __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int mt = (p.M + G_BM - 1) / G_BM, nt = (p.Cout + G_BN - 1) / G_BN;
+  const int mt = (p.M + G_BM - 1) / G_BM, nt = (p.Cout + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, mt * nt);
   const int tn = wg % nt, tm = wg / nt;
-  const int m0 = tm * G_BM, n0 = tn * G_BN;
+  const int m0 = tm * G_BM, n0 = tn * BN;
   const int HoWo = p.Ho * p.Wo;
   // descriptors: A from the first image of the tile (lane offsets span a few images at any batch)
   const int n_first = fdiv(m0, p.mg_howo);
@@ -368,8 +385,8 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
   const __amdgpu_buffer_rsrc_t ra =
       make_rsrc(p.x + n_first * HWC, (int)lmin((long)(p.N - n_first) * HWC * 4, 0x7fffffffL));
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.w, (int)lmin((long)p.Cout * p.K * 4, 0x7fffffffL));
-  // this lane's two A rows (pieces rh = 0, 1: rows rh * 64 + lane) and two B rows, chunk = wave
-  uint32_t a_off[2], a_taps[2], b_off[2];
+  // this lane's two A rows (pieces rh = 0, 1: rows rh * 64 + lane) and NB B rows, chunk = wave
+  uint32_t a_off[2], a_taps[2], b_off[NB];
 #pragma unroll
   for (int rh = 0; rh < 2; ++rh) {
     const int m = m0 + rh * 64 + lane;
@@ -387,21 +404,24 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
           if ((unsigned)(hi + r) < (unsigned)p.H && (unsigned)(wi + s2) < (unsigned)p.W) t |= 1u << (r * p.S + s2);
       a_taps[rh] = t;
     }
+  }
+#pragma unroll
+  for (int rh = 0; rh < NB; ++rh) {
     const int nn = n0 + rh * 64 + lane;
     b_off[rh] = nn < p.Cout ? (uint32_t)((nn * p.K + 4 * wave) * 4) : OOB_OFF;
   }
   int ld_r = 0, ld_s = 0, ld_c0 = 0, ld_k = 0;
   auto load_step = [&](int buf) {
-    char* base = smem + buf * G_STAGE;
+    char* base = smem + buf * STAGE;
     const int tap = ld_r * p.S + ld_s;
     const int delta = ((ld_r * p.W + ld_s) * p.C + ld_c0) * 4;
 #pragma unroll
     for (int rh = 0; rh < 2; ++rh) {
       const uint32_t off = ((a_taps[rh] >> tap) & 1u) ? a_off[rh] + (uint32_t)delta : OOB_OFF;
-      buf_lds16(ra, LDS_PTR(base + wave * 2048 + rh * 1024), off, 0);
+      buf_lds16(ra, LDS_PTR(base + wave * A_CH + rh * 1024), off, 0);
     }
 #pragma unroll
-    for (int rh = 0; rh < 2; ++rh) buf_lds16(rb, LDS_PTR(base + 8192 + wave * 2048 + rh * 1024), b_off[rh], ld_k * 4);
+    for (int rh = 0; rh < NB; ++rh) buf_lds16(rb, LDS_PTR(base + B_BASE + wave * B_CH + rh * 1024), b_off[rh], ld_k * 4);
     ld_k += 16;
     ld_c0 += 16;
     if (ld_c0 == p.C) {
@@ -409,38 +429,49 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
       if (++ld_s == p.S) { ld_s = 0; ++ld_r; }
     }
   };
-  v4f acc[4][4];
+  v4f acc[4][TJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   const int KT = p.K / 16;
   load_step(0);
   if (KT > 1) load_step(1);
   const int fr = lane & 15, g = lane >> 4;
-  const int a_rd = g * 2048 + (wm * 64 + fr) * 16, b_rd = 8192 + g * 2048 + (wn * 64 + fr) * 16;
+  const int a_rd = g * A_CH + (wm * 64 + fr) * 16, b_rd = B_BASE + g * B_CH + (wn * (BN / 2) + fr) * 16;
   for (int t = 0; t < KT; ++t) {
     // step t landed (step t+1 stays in flight across the raw barrier), and every wave finished
     // step t-1, whose buffer takes step t+2
-    if (t + 1 < KT) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 1 < KT) {
+      if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
     const int cur = t % 3;
     if (t + 2 < KT) load_step((t + 2) % 3);
-    const char* st = smem + cur * G_STAGE;
-    float4 af[4], bf[4];
+    const char* st = smem + cur * STAGE;
+    float4 af[4], bf[TJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const float4*>(st + a_rd + i * 256);
+    for (int i = 0; i < 4; ++i) af[i] = f32_read16(st + a_rd + i * 256);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const float4*>(st + b_rd + j * 256);
+    for (int j = 0; j < TJ; ++j) bf[j] = f32_read16(st + b_rd + j * 256);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma4v(af[i], bf[j], acc[i][j]);
+      for (int j = 0; j < TJ; ++j) acc[i][j] = mfma4v(af[i], bf[j], acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every fragment read done: the epilogue reuses the pipeline's LDS
 
+  // epilogue: thread -> one 4-column group (CG groups across the tile) and every RPI-th row
+  constexpr int CG = BN / 4, RPI = 256 / CG;
   float* Cs = reinterpret_cast<float*>(smem);
-  const int c4 = (tid & 31) * 4, col = n0 + c4;
+  const int c4 = (tid % CG) * 4, col = n0 + c4;
   const bool vec = col + 3 < p.Cout;
   float sc[4] = {1.f, 1.f, 1.f, 1.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -455,17 +486,17 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TJ; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) Cs[(i * 16 + 4 * g + e) * G_CLD + wn * 64 + j * 16 + fr] = acc[i][j][e];
+          for (int e = 0; e < 4; ++e) Cs[(i * 16 + 4 * g + e) * CLD + wn * (BN / 2) + j * 16 + fr] = acc[i][j][e];
     }
     __syncthreads();
     float cs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int rl = (tid >> 5) + 8 * it, row = m0 + h * 64 + rl;
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int rl = tid / CG + RPI * it, row = m0 + h * 64 + rl;
       if (row >= p.M || col >= p.Cout) continue;
-      const float4 q = *reinterpret_cast<const float4*>(&Cs[rl * G_CLD + c4]);
+      const float4 q = *reinterpret_cast<const float4*>(&Cs[rl * CLD + c4]);
       float v[4] = {q.x, q.y, q.z, q.w};
       long orow = row;
       if (p.epi == F32_EPI_DGRAD && p.up2) {
@@ -518,19 +549,22 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
       }
     }
     if (p.epi == F32_EPI_DGRAD && p.colsum) {
-      // fold the 8 row groups of each 4-column group: lanes l, l + 32 of a wave, then the 4 waves
+      // fold the row groups of each 4-column group: lanes l, l + CG, ... of a wave, then the 4 waves
 #pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
-      __syncthreads();
-      if (lane < 32) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Cs[wave * G_CLD + c4 + e] = cs[e];
+      for (int e = 0; e < 4; ++e) {
+        cs[e] += __shfl_xor(cs[e], 32, 64);
+        if (CG == 16) cs[e] += __shfl_xor(cs[e], 16, 64);
       }
       __syncthreads();
-      if (tid < 32 && m0 + h * 64 < p.M) {
+      if (lane < CG) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Cs[wave * CLD + c4 + e] = cs[e];
+      }
+      __syncthreads();
+      if (tid < CG && m0 + h * 64 < p.M) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float t = Cs[c4 + e] + Cs[G_CLD + c4 + e] + Cs[2 * G_CLD + c4 + e] + Cs[3 * G_CLD + c4 + e];
+          const float t = Cs[c4 + e] + Cs[CLD + c4 + e] + Cs[2 * CLD + c4 + e] + Cs[3 * CLD + c4 + e];
           if (col + e < p.Cout) p.colsum[(long)(tm * 2 + h) * p.Cout + col + e] = t;
         }
       }
@@ -538,10 +572,10 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
     __syncthreads();   // (the next half overwrites Cs)
   }
 }
-int g_conv_f32_variant = 1;   // 1: 128 x 128 LDS-DMA kernels where they apply (C % 16 == 0) and, for the
-                              // forward / dgrad, where the problem has >= 4 tiles per CU (fewer: the
-                              // 2-per-CU 128 x 128 tiles leave a half-empty last round -- b256 stage
-                              // 4/5: 784 / 392 tiles on 512 slots); 2: wherever they apply; 0: 64 x 64 only
+int g_conv_f32_variant = 1;   // 0: 64 x 64 register-staged kernels only; 1: the LDS-DMA kernels where they
+                              // apply (C % 16 == 0: 128 x 64 conv tiles; the 128 x 128 weight-gradient
+                              // tiles where both GEMM sides are >= 128 wide); 2: 128 x 128 conv tiles and
+                              // the 128 x 128 weight gradient wherever they apply
 
 // Weight gradient on 128 (Cout) x 128 (K) tiles, reduction over m in steps of 16 rows, the same
 // 3-stage LDS-DMA pipeline.  Both operands arrive row-major ([m][n] / [m][k] rows of 128 floats,
@@ -672,11 +706,18 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (const char* e = check_f32(p)) return e;
   p.mg_howo = fdiv_magic(p.Ho * p.Wo);
   p.mg_wo = fdiv_magic(p.Wo);
-  const int big_grid = ((p.M + G_BM - 1) / G_BM) * ((p.Cout + G_BN - 1) / G_BN);
-  if (g_conv_f32_variant >= 1 && p.C % 16 == 0 && p.R * p.S <= 32 &&
-      (g_conv_f32_variant == 2 || big_grid >= 4 * num_cus())) {
-    const int grid = big_grid;
-    hipLaunchKernelGGL(conv_f32_big_kernel, dim3(grid), dim3(256), 0, stream, p);
+  if (g_conv_f32_variant >= 1 && p.C % 16 == 0 && p.R * p.S <= 32) {
+    const int mt = (p.M + G_BM - 1) / G_BM;
+    // 128 x 64 tiles unless forced: 4 workgroups per CU (36 KB of LDS, 76 VGPRs) against the wide
+    // tile's 3, equal or faster on every ResNet-50 layer (bench/f32.py, profiles/r4_fp32.txt)
+    const bool wide = g_conv_f32_variant == 2;
+    if (wide) {
+      const int grid = mt * ((p.Cout + 127) / 128);
+      hipLaunchKernelGGL(conv_f32_big_kernel<128>, dim3(grid), dim3(256), 0, stream, p);
+    } else {
+      const int grid = mt * ((p.Cout + 63) / 64);
+      hipLaunchKernelGGL(conv_f32_big_kernel<64>, dim3(grid), dim3(256), 0, stream, p);
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? nullptr : hipGetErrorString(e);
   }
@@ -699,7 +740,10 @@ const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (splits < 1) splits = 1;
   int mps = ((p.M + splits - 1) / splits + F_BK - 1) / F_BK * F_BK;
   splits = (p.M + mps - 1) / mps;
-  if (g_conv_f32_variant >= 1 && p.C % 4 == 0 && p.Cout % 4 == 0) {
+  // the 128 x 128 weight-gradient tiles run half empty on 64-wide sides (Cout or K = 64, or
+  // K = 576 = 4.5 tiles): those layers keep the 64 x 64 kernel unless forced
+  const bool big_fits = p.Cout >= 128 && p.K >= 128 && (p.K % 128 == 0 || p.K >= 1024);
+  if (g_conv_f32_variant >= 1 && p.C % 4 == 0 && p.Cout % 4 == 0 && (big_fits || g_conv_f32_variant >= 2)) {
     const int bt = ((p.Cout + 127) / 128) * ((p.K + 127) / 128);
     int bs = (3 * num_cus() + bt - 1) / bt;                  // ~3 workgroups per CU
     const int bcap = (p.M + 511) / 512;                      // each reducing >= 512 rows of m

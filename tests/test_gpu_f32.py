@@ -324,11 +324,11 @@ def test_f32_pool_gap_softmax_kernels():
 @pytest.mark.parametrize("case", [(4, 28, 64, 128, 3, 1, 1), (2, 30, 16, 64, 4, 1, 0), (2, 14, 256, 1024, 1, 1, 0),
                                   (8, 7, 512, 512, 3, 1, 1), (3, 15, 128, 200, 1, 2, 0)])
 def test_conv_f32_128_tile_kernels_match_64_and_fp64(case):
-    """The 128 x 128 LDS-DMA fp32 kernels (conv_f32_big_kernel / wgrad_f32_big_kernel, knob
-    conv_f32 = 1, the default for C % 16 == 0 and >= 4 tiles per CU; forced here with 2) against float64 and against the 64 x 64 kernels
-    (knob 0): forward with the fused frozen-BN epilogue, data-gradient epilogue with column sums,
-    and the weight gradient, over multi-tile shapes incl. the stem's 4x4 window (C = 16) and a
-    ragged Cout."""
+    """The LDS-DMA fp32 kernels (conv_f32_big_kernel<128> / <64> and wgrad_f32_big_kernel; knob
+    conv_f32 = 1 runs 128 x 64 conv tiles for C % 16 == 0; forced here: 2 = 128 x 128 conv tiles,
+    3 = 128 x 64; both force the 128 x 128 weight-gradient tiles on any shape) against float64 and against the 64 x 64 kernels (knob 0): forward with the fused
+    frozen-BN epilogue, data-gradient epilogue with column sums, and the weight gradient, over
+    multi-tile shapes incl. the stem's 4x4 window (C = 16) and a ragged Cout."""
     torch.manual_seed(1)
     n, h, c, co, r, st, pad = case
     ho = (h + 2 * pad - r) // st + 1
@@ -338,7 +338,7 @@ def test_conv_f32_128_tile_kernels_match_64_and_fp64(case):
     res = torch.randn(n, ho, ho, co, device=dev)
     g = torch.randn(n, ho, ho, co, device=dev)
     outs = []
-    for v in (2, 0):   # (2: the 128 x 128 kernels wherever they apply, whatever the tile count)
+    for v in (2, 3, 0):   # (the LDS-DMA kernels wherever they apply, whatever the tile count)
         N().set_variant("conv_f32", v)
         try:
             y = torch.empty(n, ho, ho, co, device=dev)
@@ -358,7 +358,8 @@ def test_conv_f32_128_tile_kernels_match_64_and_fp64(case):
     ref_yd = torch.where(g > 0, conv + res.double(), torch.zeros_like(conv))
     ref_dw = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (co, c, r, r), g.double().permute(0, 3, 1, 2),
                                          stride=st, padding=pad).permute(0, 2, 3, 1).reshape(co, -1)
-    (y1, yd1, cs1, dw1), (y0, yd0, cs0, dw0) = outs
-    assert rel(y1, ref_y) < 1e-5 and rel(yd1, ref_yd) < 1e-5 and rel(dw1, ref_dw) < 1e-5
-    assert rel(cs1, ref_yd.reshape(-1, co).sum(0)) < 1e-5
-    assert rel(y1, y0) < 1e-5 and rel(dw1, dw0) < 1e-5
+    y0, yd0, cs0, dw0 = outs[-1]
+    for y1, yd1, cs1, dw1 in outs[:-1]:
+        assert rel(y1, ref_y) < 1e-5 and rel(yd1, ref_yd) < 1e-5 and rel(dw1, ref_dw) < 1e-5
+        assert rel(cs1, ref_yd.reshape(-1, co).sum(0)) < 1e-5
+        assert rel(y1, y0) < 1e-5 and rel(dw1, dw0) < 1e-5
