@@ -126,7 +126,15 @@ void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, 
              "dgrad out2 is the compact [N*Ho*Wo][Nn] copy of an up2 scatter");
   }
   p.relu2 = (int)relu2; p.n_split = (int)n_split;
-  PCHECK(up2 >= 0 && up2 <= 2, "up2: 0 none, 1 scatter + zero fill, 2 grid positions only");
+  PCHECK(up2 >= 0 && up2 <= 3, "up2: 0 none, 1 scatter + zero fill, 2 grid positions only, 3 as 2 + compact mask");
+  if (mode == pddl::EPI_FWD && up2) {
+    // forward: a residual on the 2x finer grid, read at the output's stride-2 positions
+    PCHECK(res.has_value() && (Hf - 1) / 2 + 1 == Ho && (Wf - 1) / 2 + 1 == Wo &&
+               res->numel() >= (int64_t)p.N * Hf * Wf * p.Nn && !out2.has_value() && !stats.has_value(),
+           "forward up2: residual [N][Hf][Wf][Nn] with Ho = ceil(Hf / 2), no second output / stats");
+  } else {
+    PCHECK(mode == pddl::EPI_DGRAD || !up2, "up2 is a dgrad scatter or a forward stride-2 residual");
+  }
   p.up2 = (int)up2; p.Hf = (int)Hf; p.Wf = (int)Wf;
   p.colsum = colsum.has_value() ? f32p(*colsum) : nullptr;
   if (p.colsum)
@@ -146,7 +154,7 @@ void igemm_impl(Tensor a1, OptT a2, int64_t H, int64_t W, int64_t R, int64_t S, 
     PCHECK(stats->numel() >= (int64_t)pddl::igemm_partial_rows(p.M, p.Nn, p.K, p.bn_z != nullptr) * 2 * p.Nn,
            "stats partial buffer too short");
   }
-  const int64_t rows_out = up2 ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
+  const int64_t rows_out = (up2 && mode == pddl::EPI_DGRAD) ? (int64_t)p.N * Hf * Wf : (int64_t)p.M;
   PCHECK(out.numel() / std::max<int64_t>(1, out.size(-1)) >= (out2.has_value() ? p.M : rows_out) ||
              out.dim() >= 2,
          "output too small");

@@ -112,7 +112,12 @@ __device__ __forceinline__ void igemm_epi_load(const IgemmParams& p, int mb, int
       const int gm = mb + (pass0 + q) * 32 + it * RPI + rr;
       const bool ok = gm < p.M && col_ok;
       const long gr = gm < p.M ? gm : p.M - 1;
-      const uint4 v = *reinterpret_cast<const uint4*>(psrc + gr * pld + pcol);
+      long rr_res = gr;
+      if (p.mode == EPI_FWD && p.up2) {   // residual on the 2x finer grid, read at the stride-2 positions
+        const int n = fdiv((int)gr, p.mg_howo), rem = (int)gr - n * p.Ho * p.Wo, i = fdiv(rem, p.mg_wo);
+        rr_res = ((long)n * p.Hf + 2 * i) * p.Wf + 2 * (rem - i * p.Wo);
+      }
+      const uint4 v = *reinterpret_cast<const uint4*>(psrc + rr_res * pld + pcol);
       const uint32_t b = bsrc[gr * bld + bcol];
       dst[q * NIT + it] = (ok && pre_on) ? v : make_uint4(0, 0, 0, 0);
       bits[q * NIT + it] = (ok && pf_bits) ? b : 0u;
@@ -242,15 +247,16 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] += av[e];
             }
+            const long rm = p.up2 == 3 ? (long)gm : rq;   // (up2 3: the mask is on the compact grid)
             if (p.mask) {
               float mv[8];
-              unpack8(*reinterpret_cast<const uint4*>(p.mask + rq * p.ld_mask + gn), mv);
+              unpack8(*reinterpret_cast<const uint4*>(p.mask + rm * p.ld_mask + gn), mv);
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = (mv[e] > 0.f) ? w[e] : 0.f;
             } else if (p.bits_mask) {
               uint32_t byte;
               if (pf_bits) byte = pbits[it];
-              else byte = p.bits_mask[rq * p.ld_bits_mask + (gn >> 3)];
+              else byte = p.bits_mask[rm * p.ld_bits_mask + (gn >> 3)];
 #pragma unroll
               for (int e = 0; e < 8; ++e) w[e] = ((byte >> e) & 1u) ? w[e] : 0.f;
             }
@@ -1376,7 +1382,7 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
     return e == hipSuccess ? nullptr : hipGetErrorString(e);
   }
   const bool window = (p.C1 * p.S == 64) && p.C1 < 64;
-  if (pl.ks > 1 && !p.a2 && !window && p.C1 % 64 == 0 && p.slab &&
+  if (pl.ks > 1 && !p.a2 && !window && p.C1 % 64 == 0 && p.slab && !(p.mode == EPI_FWD && p.up2) &&
       p.slab_floats >= igemm_splitk_floats(p.M, p.Nn, p.K)) {
     // slices -> workspace, then the combine + fused epilogue (without a workspace the same
     // tile config runs unsplit, so the partial-row layout does not change)

@@ -29,7 +29,10 @@ struct IgemmParams {
   void* out; int ldo; int relu;
   void* out2; int ldo2; int relu2; int n_split;     // FWD: columns >= n_split -> out2
   int up2; int Hf, Wf;                              // DGRAD: scatter to a 2x finer grid (1: zero-fill the
-                                                    //   off-grid positions; 2: write grid positions only)
+                                                    //   off-grid positions; 2: write grid positions only;
+                                                    //   3: as 2, the ReLU mask on the compact grid)
+                                                    // FWD (up2 != 0): the residual is the Hf x Wf finer
+                                                    //   grid, read at the output rows' stride-2 positions
   float* colsum;                                    // DGRAD: per-wave partial column sums [rows][Nn]
   // ReLU masks as bitmasks (bit e of byte [row][c/8] = value[row][8*(c/8)+e] > 0):
   uint8_t* bits_out; int ld_bits_out;               // FWD: write the mask of the (segment-0) output

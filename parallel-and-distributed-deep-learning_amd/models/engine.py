@@ -52,6 +52,7 @@ class HipEngine:
     C64_OK = True           # stage-2 3x3 convs on the persistent pixel-ring kernel (conv3x3c64.hip)
     C64_MIN_M = 262144      # ... from 4 x 256 CUs x 256-pixel tiles up (b >= 84 at 56 x 56)
     C3C1_OK = True          # stage-2 boundaries: conv3 + next conv1 fused (c3c1.hip)
+    S2C_OK = True           # blocks feeding a downsampling block store only their stride-2 grid
     TWO_STREAM_MAX_BATCH = 1024
     GRAD_RING = 5           # two-stream: gradient buffers per kind, so the data-gradient chain can run
                             # up to four blocks ahead of the weight gradients still reading older ones
@@ -110,6 +111,11 @@ class HipEngine:
         # stage-2 backward boundaries: the next block's conv1 data gradient computed inside this
         # block's fused conv3 backward (bwd1x1 pre form), its 256-channel result never re-read
         self.c1pre = self.C3C1_OK and os.environ.get("PDDL_C1PRE", "1") != "0"
+        # blocks whose output feeds a downsampling block (conv2_block3, conv3_block4, conv4_block6):
+        # every consumer of that output (the next block's stride-2 conv1 and shortcut, forward and
+        # weight gradient, and its ReLU mask) reads only the even rows / columns, so conv3 runs on
+        # the compact quarter and stores only it (3/4 fewer conv3 rows and output bytes)
+        self.s2c = self.S2C_OK and self.bitmask and os.environ.get("PDDL_S2C", "1") != "0"
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -272,15 +278,16 @@ class HipEngine:
         for b in L.blocks:
             f = b.filters
             Ho = (H - 1) // b.stride + 1
+            Hq = self._out_dim(L.blocks.index(b), Ho)
             a = {"y1": torch.empty(B, Ho, Ho, f, **bf), "y2": torch.empty(B, Ho, Ho, f, **bf),
-                 "out": torch.empty(B, Ho, Ho, 4 * f, **bf)}
+                 "out": torch.empty(B, Hq, Hq, 4 * f, **bf)}
             if b.proj and not self.fuse_proj:
                 a["sc"] = torch.empty(B, Ho, Ho, 4 * f, **bf)
             self.acts[b.name] = a
             if self.bitmask:
                 self.bits[b.name] = {"y1": torch.empty(B, Ho, Ho, f // 8, **u8),
                                      "y2": torch.empty(B, Ho, Ho, f // 8, **u8),
-                                     "out": torch.empty(B, Ho, Ho, f // 2, **u8)}
+                                     "out": torch.empty(B, Hq, Hq, f // 2, **u8)}
             self.geo[b.name] = (H, Ho)
             inner = max(inner, B * Ho * Ho * f)
             outer = max(outer, B * H * H * b.cin, B * Ho * Ho * 4 * f)
@@ -319,6 +326,18 @@ class HipEngine:
         self.cap = B
         self._cred = {}
         self.colpart = torch.empty(self._colred(B)[2], dtype=torch.float32, device=dev)
+
+    def _out_dim(self, bi, Ho) -> int:
+        """Spatial size of block bi's stored output: its stride-2 grid when it feeds a
+        downsampling block and the compact form is on (see s2c), else Ho."""
+        return (Ho + 1) // 2 if self.s2c and bi in self._s2_fed() else Ho
+
+    def _x_geom(self, bi, H, stride):
+        """(stored size, stride to apply) of block bi's input: the previous block's output is
+        already the stride-2 grid when it was stored compact."""
+        if bi > 0 and self.s2c and bi - 1 in self._s2_fed():
+            return (H + 1) // 2, 1
+        return H, stride
 
     def _s2_fed(self):
         """Blocks whose output feeds a stride-2 projection block (ResNet v1 downsamples in the
@@ -479,18 +498,19 @@ class HipEngine:
             y1, y2, out = a["y1"][:B], a["y2"][:B], a["out"][:B]
             c1n = b.convs["1"].name
             ch1 = self.ch[c1n]
+            Hx, sx = self._x_geom(bi, H, b.stride)
             if c1_done:
                 res = x
             elif b.proj and self.fuse_proj:
                 # conv1 alone; the shortcut conv runs inside conv3's GEMM (second A source = the block
                 # input at the block's stride, K = f + cin, both BN scales folded into the weights), so
                 # the shortcut activation is never written and re-read as a residual
-                N.igemm(x, None, H, H, 1, 1, b.stride, 0, Ho, Ho, self._wf(c1n, f, cin), 0,
+                N.igemm(x, None, Hx, Hx, 1, 1, sx, 0, Ho, Ho, self._wf(c1n, f, cin), 0,
                         self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, None, 0, 0, 0, 0, 0, None,
                         bt.get("y1"))
                 res = None
             elif b.proj:
-                N.igemm(x, None, H, H, 1, 1, b.stride, 0, Ho, Ho, self._wf(c1n, 5 * f, cin), 0,
+                N.igemm(x, None, Hx, Hx, 1, 1, sx, 0, Ho, Ho, self._wf(c1n, 5 * f, cin), 0,
                         self.scale[ch1:], self.shift[ch1:], None, None, None, y1, 1, a["sc"][:B], 0, f, 0, 0, 0,
                         None, bt.get("y1"))
                 res = a["sc"][:B]
@@ -530,6 +550,13 @@ class HipEngine:
                 N.igemm(y2, x, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(fz, 4 * f, f + cin), 0,
                         self.scale[self.ch[fz]:], self.shift[self.ch[fz]:], None, None, None, out, 1, None, 0, 0, 0,
                         0, 0, None, bt.get("out"))
+            elif self._out_dim(bi, Ho) != Ho:
+                # feeds a downsampling block: conv3 on the stride-2 grid only (1x1 stride-2 gather
+                # of y2, residual read at the grid positions of the full-resolution block input)
+                Hq = self._out_dim(bi, Ho)
+                N.igemm(y2, None, Ho, Ho, 1, 1, 2, 0, Hq, Hq, self._wf(c3, 4 * f, f), 0,
+                        self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 1,
+                        Ho, Ho, None, bt.get("out"))
             else:
                 N.igemm(y2, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wf(c3, 4 * f, f), 0,
                         self.scale[self.ch[c3]:], self.shift[self.ch[c3]:], res, None, None, out, 1, None, 0, 0, 0,
@@ -736,7 +763,8 @@ class HipEngine:
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
             gx_n = [f"gbuf{nxt}"]
             if b.proj:
-                W(N.wgrad, x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0,
+                Hx, sx = self._x_geom(bi, H, b.stride)
+                W(N.wgrad, x_in, Hx, Hx, 1, 1, sx, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0,
                   reads=(f"g1_{rk}", gout_n))
                 W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
                 gxc, up2 = None, 1 if b.stride == 2 else 0
@@ -746,7 +774,7 @@ class HipEngine:
                     # 3/4 zero-fill writes: conv3_block1 c1 dgrad 942 -> 681 us at b1024)
                     gx = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin)
                     gx_n = [f"s2f{bi - 1}", "gc"]
-                    up2 = 2
+                    up2 = 3 if Hx != H else 2   # (3: the stored block input and its mask are compact)
                 self._before_write(*gx_n)
                 N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1n, cin, 5 * f), 1, None, None, None,
                         mask_in, None, gx, 0, gxc, 0, 0, up2, H, H, cs_in, None)

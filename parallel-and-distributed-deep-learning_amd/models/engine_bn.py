@@ -41,6 +41,7 @@ class HipEngineBNTrain(HipEngine):
     TWO_STREAM_OK = False  # (its own backward schedule runs on one stream)
     C64_OK = False         # (train-mode BN needs the batch statistics from the conv epilogue)
     C3C1_OK = False
+    S2C_OK = False
 
     def __init__(self, layout: ParamLayout, batch: int, **kw):
         kw.setdefault("bn_mode", "train")

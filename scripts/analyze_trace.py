@@ -29,6 +29,7 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
     H = H2
     geo = []
     c3c1_on = int(os.environ.get("PDDL_C3C1", "1"))
+    s2c = os.environ.get("PDDL_S2C", "1") != "0"
     blocks = list(L.blocks)
 
     def c3c1(b, nb):   # engine._c3c1_ok
@@ -56,6 +57,10 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         elif b.proj and fuse:   # conv3 + the shortcut conv as one dual-source GEMM (K = f + cin)
             ev.append(("igemm", f"{b.name} c3+c0 fwd", 2 * M * (f + cin) * 4 * f, (M * f + M * cin + M * 4 * f) * 2,
                        (M, 4 * f, f + cin), "dual"))
+        elif s2c and nb is not None and nb.proj and nb.stride == 2:   # engine s2c: conv3 on the stride-2 grid
+            Mq = B * ((Ho + 1) // 2) ** 2
+            ev.append(("igemm", f"{b.name} c3 fwd (s2 grid)", 2 * Mq * f * 4 * f, (Mq * f + 2 * Mq * 4 * f) * 2,
+                       (Mq, 4 * f, f)))
         else:
             ev.append(("igemm", f"{b.name} c3 fwd", 2 * M * f * 4 * f, (M * f + 2 * M * 4 * f) * 2, (M, 4 * f, f)))
         geo.append((b, H, Ho))

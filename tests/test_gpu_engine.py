@@ -378,6 +378,34 @@ def test_c1_dgrad_fused_into_conv3_backward(monkeypatch):
     test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
 
 
+def test_s2_fed_blocks_store_compact_outputs(monkeypatch):
+    """Blocks feeding a downsampling block store only their stride-2 grid (PDDL_S2C=1, the
+    default: conv3 on the compact quarter, the next block's conv1 / shortcut / weight gradient
+    and ReLU mask read it as a stride-1 input) against full-resolution storage: same loss, flat
+    gradients to fp32 order; and within the fp32 reference's noise floor."""
+    from pddl.models.engine import HipEngine
+    from pddl.models.resnet50 import ParamLayout
+    L = ParamLayout()
+    B = 8
+    res = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("PDDL_S2C", on)
+        he = HipEngine(L, B, crop=224, image_size=224)
+        assert he.s2c == (on == "1")
+        he.init(seed=7)
+        img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(1)).cuda()
+        lab = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(2)).cuda()
+        st = he.forward_backward(img, lab, 1.0 / B)
+        torch.cuda.synchronize()
+        res.append((st[0].item() / B, he.grads.clone()))
+    (l1, g1), (l0, g0) = res
+    print(f"s2c: loss rel {abs(l1 - l0) / abs(l0):.2e}, grad rel {((g1 - g0).norm() / g0.norm()).item():.3e}")
+    assert abs(l1 - l0) < 1e-4 * abs(l0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
+    monkeypatch.setenv("PDDL_S2C", "1")
+    test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
+
+
 @pytest.mark.parametrize("variant", ["1", "2"])
 def test_c64_engine_within_noise_floor(monkeypatch, variant):
     """The engine with the stage-2 3x3 convs forced onto conv3x3c64.hip is as close to the fp32

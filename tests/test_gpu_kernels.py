@@ -737,6 +737,61 @@ def test_dgrad_up2_grid_only_scatter(hc, cin, co):
     assert torch.all(f2[:, off] == 7.0)        # up2 = 2 leaves them alone
 
 
+@pytest.mark.parametrize("hc,cin,co", [(7, 256, 128), (4, 512, 256), (8, 128, 64)])
+def test_dgrad_up2_compact_mask(hc, cin, co):
+    """up2 = 3: the grid-only scatter of up2 = 2 with the ReLU bitmask stored on the compact grid
+    (a block input kept only at its stride-2 positions) -- bitwise the up2 = 2 result with the
+    full-resolution mask whose grid positions hold the same bits."""
+    torch.manual_seed(22)
+    n, H = 3, 2 * hc
+    g1 = rnd(n, hc, hc, co)
+    wt = rnd(cin, co, scale=0.05)
+    mask = torch.randint(0, 256, (n, H, H, cin // 8), dtype=torch.uint8, device=dev)
+    mc = mask[:, ::2, ::2].contiguous()
+    rows = N().igemm_partial_rows(n * hc * hc, cin, co)
+    res = []
+    for up2, m in ((2, mask), (3, mc)):
+        full = torch.zeros((n, H, H, cin), dtype=torch.bfloat16, device=dev)
+        comp = torch.empty(n, hc, hc, cin, dtype=torch.bfloat16, device=dev)
+        part = torch.zeros(rows * cin, device=dev)
+        N().igemm(g1, None, hc, hc, 1, 1, 1, 0, hc, hc, wt, 1, None, None, None, m, None, full, 0, comp, 0, 0,
+                  up2, H, H, part, None)
+        res.append((full, comp, _fold(part, rows, cin)))
+    (f2, c2, s2), (f3, c3, s3) = res
+    assert torch.equal(f2, f3) and torch.equal(c2, c3) and torch.equal(s2, s3)
+
+
+@pytest.mark.parametrize("ho,c,co", [(56, 64, 256), (28, 128, 512), (14, 256, 1024), (7, 512, 2048)])
+def test_igemm_forward_stride2_residual(ho, c, co):
+    """Forward with up2 != 0: a stride-2 1x1 conv whose residual is the full-resolution tensor read
+    at the output rows' grid positions (conv3 of a block feeding a downsampling block, stored
+    compact) -- bitwise the full-resolution conv3 + residual + ReLU at the even rows / columns,
+    ReLU bits included."""
+    torch.manual_seed(23)
+    n = 2
+    hq = (ho + 1) // 2
+    y2 = rnd(n, ho, ho, c)
+    w = rnd(co, c, scale=0.05)
+    res = rnd(n, ho, ho, co)
+    sc, sh = torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev) * 0.1
+    full = torch.empty(n, ho, ho, co, dtype=torch.bfloat16, device=dev)
+    bfull = torch.empty(n, ho, ho, co // 8, dtype=torch.uint8, device=dev)
+    N().igemm(y2, None, ho, ho, 1, 1, 1, 0, ho, ho, w, 0, sc, sh, res, None, None, full, 1, None, 0, 0, 0, 0, 0,
+              None, bfull)
+    comp = torch.empty(n, hq, hq, co, dtype=torch.bfloat16, device=dev)
+    bcomp = torch.empty(n, hq, hq, co // 8, dtype=torch.uint8, device=dev)
+    N().igemm(y2, None, ho, ho, 1, 1, 2, 0, hq, hq, w, 0, sc, sh, res, None, None, comp, 1, None, 0, 0, 1, ho, ho,
+              None, bcomp)
+    torch.cuda.synchronize()
+    ref = full[:, ::2, ::2]
+    assert (comp.float() - ref.float()).abs().max().item() <= 1e-2 * ref.float().abs().max().item()
+    assert rel(comp, ref) < 1e-3
+    # (the ReLU bits agree except where a different tile config's fp32 order flips a value at 0)
+    diff = torch.bitwise_xor(bcomp, bfull[:, ::2, ::2].contiguous())
+    flipped = sum(((diff >> k) & 1).sum().item() for k in range(8))
+    assert flipped <= 1e-4 * comp.numel()
+
+
 SPLITK_CASES = [
     # kind, N, H, Cin, Cout, R, pad   (stage-5 3x3 at a small batch, a long-K 1x1, odd widths)
     ("fwd", 2, 7, 512, 512, 3, 1),
