@@ -39,6 +39,18 @@ static_assert(C64_LDS <= 163840, "LDS budget");
 static_assert(C64_RING >= 2 * C64_BM + 2 * C64_AHEAD, "ring too small");
 }  // namespace
 
+// LDS staging of the epilogue as inline asm: a compiler-visible LDS access after an LDS-DMA makes
+// the compiler drain every DMA in flight first (s_waitcnt vmcnt(0)), which would stall each
+// tile's epilogue on the next tile's window load.  Callers wait on lgkmcnt themselves.
+__device__ __forceinline__ void c64_wr8(char* p, uint2 v) {
+  asm volatile("ds_write_b64 %0, %1" : : "v"((uint32_t)(uintptr_t)LDS_PTR(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint4 c64_rd16(const char* p) {
+  uint4 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)LDS_PTR(p)) : "memory");
+  return r;
+}
+
 // Logical 16-byte chunk `c` of LDS row `row` ([rows][128 B] images) sits at chunk c ^ f(row):
 // 16 consecutive rows at one logical chunk hit 16 distinct 16-B slots (igemm.hip sw_chunk).
 __device__ __forceinline__ int c64_sw(int row) { return (row >> 1) & 7; }
@@ -447,14 +459,21 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
           v[e] = x;
         }
         const int chunk = 2 * jb + (kq >> 1);
-        *reinterpret_cast<uint2*>(stage + r16 * 128 + ((chunk ^ c64_sw(r16)) << 4) + 8 * (kq & 1)) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        c64_wr8(stage + r16 * 128 + ((chunk ^ c64_sw(r16)) << 4) + 8 * (kq & 1),
+                make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3])));
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint4 pkr[2];
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int rr = (lane >> 3) + 8 * hh, c = lane & 7;
-        const uint4 pk = *reinterpret_cast<const uint4*>(stage + rr * 128 + ((c ^ c64_sw(rr)) << 4));
+        pkr[hh] = c64_rd16(stage + rr * 128 + ((c ^ c64_sw(rr)) << 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (also orders the next i's writes after these reads)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int rr = (lane >> 3) + 8 * hh, c = lane & 7;
+        const uint4 pk = pkr[hh];
         const int wpx = 16 * i + rr;
         if (row_ok && wpx < p.W) {
           const long mo = mrow + wpx;
@@ -462,7 +481,6 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
           if (bits_st) p.bits_out[mo * 8 + c] = (uint8_t)pos_bits8(pk);
         }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
