@@ -1,4 +1,4 @@
-"""A/B of the stage-2 3x3 conv kernels (conv3x3c64.hip persistent ring vs the generic implicit
+"""A/B of the stage-2 3x3 conv kernels (conv3x3c64.hip row tiles vs the generic implicit
 GEMM / wgrad) on the ResNet-50 conv2_block*_2 shape: N x 56 x 56 x 64 -> 64.
 
     python bench/c64.py [--batch 2560] [--iters 20]
@@ -47,13 +47,13 @@ def main():
     dw = torch.zeros(64, 576, device="cuda")
     flop = 2.0 * M * 576 * 64
     res = {}
-    res["fwd_ring"] = timeit(lambda: N.conv3x3c64(x, w, 0, out, scale=sc, shift=sh, bits=bits), a.iters)
+    res["fwd_row"] = timeit(lambda: N.conv3x3c64(x, w, 0, out, scale=sc, shift=sh, bits=bits), a.iters)
     res["fwd_igemm"] = timeit(lambda: N.igemm(x, None, h, h, 3, 3, 1, 1, h, h, w, 0, sc, sh, None, None, None, out, 1,
                                               None, 0, 0, 0, 0, 0, None, bits), a.iters)
-    res["dgrad_ring"] = timeit(lambda: N.conv3x3c64(g, w, 1, out, bits=mb, colsum=part), a.iters)
+    res["dgrad_row"] = timeit(lambda: N.conv3x3c64(g, w, 1, out, bits=mb, colsum=part), a.iters)
     res["dgrad_igemm"] = timeit(lambda: N.igemm(g, None, h, h, 3, 3, 1, 1, h, h, w, 1, None, None, None, mb, None, out,
                                                 0, None, 0, 0, 0, 0, 0, part, None), a.iters)
-    res["wgrad_ring"] = timeit(lambda: N.conv3x3c64_wgrad(x, g, dw), a.iters)
+    res["wgrad_row"] = timeit(lambda: N.conv3x3c64_wgrad(x, g, dw), a.iters)
     res["wgrad_generic"] = timeit(lambda: N.wgrad(x, h, h, 3, 3, 1, 1, h, h, g, None, 0, dw, 576, 0), a.iters)
     for k, v in res.items():
         print(f"{k:14s} {v:8.1f} us  {flop / v / 1e6:7.1f} TF/s  {2 * M * 128 / v / 1e3:6.0f} GB/s (2 tensors)")

@@ -532,7 +532,7 @@ void stem_pool_bwd(Tensor x2, Tensor gpool, Tensor idx, Tensor dw, Tensor colsum
   p.colsum = f32p(colsum);
   ok(pddl::stem_pool_bwd_launch(p, cur_stream()), "stem_pool_bwd");
 }
-// 3x3 / pad 1 / stride 1 convolution 64 -> 64 on the persistent pixel-ring kernel.
+// 3x3 / pad 1 / stride 1 convolution 64 -> 64 on the persistent row-tile kernel.
 // mode 0 (forward): out = relu(conv(x, w) * scale + shift), bits = its ReLU bits (optional);
 // mode 1 (data gradient): out = conv(x, w) masked by `bits` (input ReLU bits, required),
 // colsum = partial rows [conv3x3c64_partial_rows(M), 64] of out's column sums (optional).
@@ -844,7 +844,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "c64_grid") pddl::g_c64_grid = v;
     else if (which == "c64w_grid") pddl::g_c64w_grid = v;
     else if (which == "stem_pool") pddl::g_stem_pool_variant = v;
-    else if (which == "c64") pddl::g_c64_variant = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;

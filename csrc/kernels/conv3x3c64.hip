@@ -1,24 +1,19 @@
-// Persistent pixel-ring 3x3 convolution for the 64-channel stage (ResNet-50 conv2_block*_2:
-// 56x56x64 -> 64, pad 1, stride 1), forward and data gradient (gfx950).
+// 64-channel 3x3 convolution for the stage-2 bottlenecks (ResNet-50 conv2_block*_2: 56x56x64 -> 64,
+// pad 1, stride 1), forward and data gradient, plus its weight gradient (gfx950).
 //
 // The generic implicit GEMM (igemm.hip) gathers every one of the nine taps of a 256-row tile
 // from L2: 9 x 32 KiB of A per tile for 2 x 256 x 64 x 576 FLOP, plus the 72 KiB weight matrix
 // per tile, and runs these layers at 620-690 TF/s (0.87 / 0.95 ms at b2560, forward / dgrad)
-// while their HBM floor -- read 1 GB, write 1 GB -- is ~0.4 ms.  Here:
-//   * one workgroup per CU owns a contiguous range of 256-pixel tiles; the whole 64 x 576
-//     weight matrix stays resident in LDS (72 KiB, loaded once per workgroup);
-//   * the input pixels stream through a 640-pixel LDS ring (80 KiB): a tile at m0 reads pixels
-//     [m0 - W - 1, m0 + 256 + W + 1) -- every tap of every row is a shifted view of the ring, so
-//     each input pixel crosses L2 -> LDS once instead of nine times; the next tile's 256 new
-//     pixels are LDS-DMA'd while this tile computes (ring slots [m0 + 320, m0 + 576));
-//   * taps that fall outside the image (padding) are zeroed by a per-row 9-bit tap mask on the
-//     fragment, the ring read itself is always in range;
-//   * the MFMAs run with the weights as the A operand, so a lane ends with 4 consecutive output
-//     channels of one pixel: the epilogue (BN scale/shift + ReLU + ReLU bits forward; ReLU-bit
-//     mask + per-channel column sums for the data gradient) runs in fp32 registers and is staged
-//     as bf16 through a 2 KiB per-wave LDS slice into 1 KiB fully contiguous row stores.
-// LDS: 73,728 (weights) + 81,920 (ring) + 8,192 (epilogue slices) = 163,840 B, one 256-thread
-// workgroup per CU (one wave per SIMD).
+// while their HBM floor -- read 1 GB, write 1 GB -- is ~0.4 ms.  Here a tile is 4 output rows of
+// one image, computed from the zero-padded 6-row x 64-slot input window of rows h0 - 1 .. h0 + 4
+// (48 KiB, LDS-DMA'd straight from HBM; padding taps read the zeros the out-of-range DMA wrote, so
+// no tap masks): every tap is a shifted read of that window, so each input row crosses L2 -> LDS
+// 1.5 times instead of nine.  One workgroup per CU walks a contiguous range of tiles with the
+// windows double-buffered (tile t + 1 loads while tile t computes).  The MFMAs run with the
+// weights as the A operand, so a lane ends with 4 consecutive output channels of one pixel: the
+// epilogue (BN scale/shift + ReLU + ReLU bits forward; ReLU-bit mask + per-channel column sums
+// for the data gradient) runs in fp32 registers and is staged as bf16 through a per-wave LDS
+// slice into contiguous row stores.
 // Reference: the Keras Conv2D(64, 3, padding='same') of every conv2 bottleneck block behind
 // keras.applications.ResNet50 (imagenet-resnet50.py:56).
 #include "common.h"
@@ -27,16 +22,7 @@
 namespace pddl {
 
 namespace {
-constexpr int C64_BM = 256;                 // output pixels per tile (4 waves x 64)
-constexpr int C64_RING = 640;               // ring slots (pixels); 128 B each
-constexpr int C64_AHEAD = 64;               // >= W + 1, multiple of 8
-constexpr int C64_W_BYTES = 9 * 64 * 128;   // 73,728
-constexpr int C64_RING_BYTES = C64_RING * 128;
-constexpr int C64_STAGE_BYTES = 2048;       // per wave
-constexpr int C64_LDS = C64_W_BYTES + C64_RING_BYTES + 4 * C64_STAGE_BYTES;
-static_assert(C64_LDS <= 163840, "LDS budget");
-// the current window [m0 - AHEAD, m0 + BM + AHEAD) plus the next tile's new pixels
-static_assert(C64_RING >= 2 * C64_BM + 2 * C64_AHEAD, "ring too small");
+constexpr int CR_WIN = 6 * 64 * 128;                // 49,152 B per input window
 }  // namespace
 
 // LDS staging of the epilogue as inline asm: a compiler-visible LDS access after an LDS-DMA makes
@@ -55,245 +41,33 @@ __device__ __forceinline__ uint4 c64_rd16(const char* p) {
 // 16 consecutive rows at one logical chunk hit 16 distinct 16-B slots (igemm.hip sw_chunk).
 __device__ __forceinline__ int c64_sw(int row) { return (row >> 1) & 7; }
 
-template <int MODE>
-__global__ void __launch_bounds__(256, 1) conv3x3c64_kernel(C64Params p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* wl = smem;
-  char* ring = smem + C64_W_BYTES;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  char* stage = smem + C64_W_BYTES + C64_RING_BYTES + wave * C64_STAGE_BYTES;
-  const int T = (p.M + C64_BM - 1) / C64_BM;
-  const int G = gridDim.x, g = blockIdx.x;
-  const int t_begin = (int)((long)g * T / G), t_end = (int)((long)(g + 1) * T / G);
-  if (t_begin >= t_end) return;   // (whole workgroup; the host sizes G <= T)
-  const int m_start = t_begin * C64_BM;
-  const int rb = m_start - C64_AHEAD;   // pixel held by ring slot 0
-  const long pbase = rb > 0 ? rb : 0;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, pbase * 64, (long)p.M * 64);
-  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, 64 * 576 * 2);
-  const int HW = p.H * p.W;
-
-  // ---- weights -> LDS, tap-major images [tap][n][128 B] (72 pieces of 8 rows, 18 per wave)
-#pragma unroll
-  for (int q = 0; q < 18; ++q) {
-    const int pc = wave * 18 + q;              // piece: tap = pc / 8, rows n = 8 (pc % 8) + lane / 8
-    const int tap = pc >> 3, n = (pc & 7) * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ c64_sw(n);     // logical chunk carried by this lane-linear slot
-    buf_lds16(rw, LDS_PTR(wl + pc * 1024), (uint32_t)((n * 576 + tap * 64 + ch * 8) * 2), 0);
-  }
-  // ring piece: 8 pixels [p0, p0 + 8) (p0 - rb a multiple of 8) into their ring slots
-  auto ring_piece = [&](int p0) {
-    int slot0 = (p0 - rb) % C64_RING;
-    const int pix = p0 + (lane >> 3);
-    const int slot = slot0 + (lane >> 3);
-    const int ch = (lane & 7) ^ c64_sw(slot);
-    const uint32_t off = (pix >= 0 && pix < p.M) ? (uint32_t)(((long)(pix - pbase) * 64 + ch * 8) * 2) : OOB_OFF;
-    buf_lds16(rx, LDS_PTR(ring + slot0 * 128), off, 0);
-  };
-  // first window: pixels [m_start - 64, m_start + 320): 48 pieces, 12 per wave
-#pragma unroll
-  for (int q = 0; q < 12; ++q) ring_piece(rb + (wave * 12 + q) * 8);
-
-  // epilogue constants: this lane's 4 channels in each 16-channel block jb: 16 jb + 4 (lane>>4) + e
-  const int cq = 4 * (lane >> 4);
-  float sc[4][4], sh[4][4];
-  if (MODE == C64_FWD) {
-#pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
-      const float4 a = *reinterpret_cast<const float4*>(p.scale + 16 * jb + cq);
-      const float4 b = *reinterpret_cast<const float4*>(p.shift + 16 * jb + cq);
-      sc[jb][0] = a.x; sc[jb][1] = a.y; sc[jb][2] = a.z; sc[jb][3] = a.w;
-      sh[jb][0] = b.x; sh[jb][1] = b.y; sh[jb][2] = b.z; sh[jb][3] = b.w;
-    }
-  }
-  float csum[4][4];
-#pragma unroll
-  for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) csum[jb][e] = 0.f;
-
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int r16 = lane & 15;
-  const int kq = lane >> 4;
-  // tap offsets (pixels) of (r, s): (r - 1) W + (s - 1)
-  const int dW = p.W;
-  // vmcnt younger than a tile's ring pieces when the next tile starts: the previous tile's
-  // stores, 2 row stores (+ 2 ReLU-bit stores) per 16-row block
-  const bool bits_st = MODE == C64_FWD && p.bits_out != nullptr;
-  int slot_m0 = C64_AHEAD;   // ring slot of this tile's pixel m0
-  for (int t = t_begin; t < t_end; ++t) {
-    const int m0 = t * C64_BM;
-    if (t > t_begin) {
-      // this tile's ring pieces landed (only the previous tile's stores may be outstanding),
-      // and every wave finished the previous tile, whose slots the next DMA overwrites
-      if (bits_st) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    // DGRAD: this tile's ReLU-bit rows (pixel 16 i + r16 of the wave, 8 bytes = 64 channels)
-    uint2 mbits[4];
-    if (MODE == C64_DGRAD) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wave * 64 + 16 * i + r16;
-        const int mc = m < p.M ? m : p.M - 1;
-        mbits[i] = *reinterpret_cast<const uint2*>(p.bits_mask + (long)mc * 8);
-      }
-    }
-    // next tile's new pixels [m0 + 320, m0 + 576): 8 pieces per wave, always issued (past the
-    // range they load zeros into slots nobody reads) so the vmcnt counts stay constant
-#pragma unroll
-    for (int q = 0; q < 8; ++q) ring_piece(m0 + C64_BM + C64_AHEAD + (wave * 8 + q) * 8);
-
-    // per-row ring slot and tap mask
-    int rslot[4];
-    uint32_t taps[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int s = slot_m0 + wave * 64 + 16 * i + r16;
-      if (s >= C64_RING) s -= C64_RING;
-      rslot[i] = s;
-      const int m = m0 + wave * 64 + 16 * i + r16;
-      const int n = fdiv(m, p.mg_hw), rem = m - n * HW;
-      const int h = fdiv(rem, p.mg_w), w = rem - h * p.W;
-      const uint32_t cols = (w > 0 ? 1u : 0u) | 2u | (w + 1 < p.W ? 4u : 0u);
-      taps[i] = (h > 0 ? cols : 0u) | (cols << 3) | (h + 1 < p.H ? cols << 6 : 0u);
-    }
-
-    v4f acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb) acc[i][jb] = v4f{0.f, 0.f, 0.f, 0.f};
-    // 18 steps (tap, 32-channel half kh) of 16 MFMAs, software-pipelined over two fragment sets:
-    // step st + 1's LDS reads are issued before step st's MFMAs (one wave per SIMD: nothing else
-    // hides the LDS latency); the padding-tap zeroing is applied at the MFMA phase so no VALU op
-    // waits on a read in flight.
-    v8bf ra[2][4], rw[2][4];
-    auto load_step = [&](int st, int set) {
-      const int tap = st >> 1, kh = st & 1;
-      const int delta = (tap / 3 - 1) * dW + (tap % 3 - 1);
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb) {
-        const int n = 16 * jb + r16;
-        rw[set][jb] = *reinterpret_cast<const v8bf*>(wl + tap * 8192 + n * 128 + (((kh * 4 + kq) ^ c64_sw(n)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int sl = rslot[i] + delta;
-        sl = sl < 0 ? sl + C64_RING : (sl >= C64_RING ? sl - C64_RING : sl);
-        ra[set][i] = *reinterpret_cast<const v8bf*>(ring + sl * 128 + (((kh * 4 + kq) ^ c64_sw(sl)) << 4));
-      }
-    };
-    auto mfma_step = [&](int st, int set) {
-      const int tap = st >> 1;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = (taps[i] >> tap) & 1u;
-        const v8bf a = ok ? ra[set][i] : v8bf{};
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-          acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rw[set][jb], a, acc[i][jb], 0, 0, 0);
-      }
-    };
-    load_step(0, 0);
-#pragma unroll
-    for (int st = 0; st < 18; st += 2) {
-      load_step(st + 1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_step(st, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (st + 2 < 18) load_step(st + 2, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_step(st + 1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-
-    // ---- epilogue: acc[i][jb][e] = out[pixel 16 i + r16][channel 16 jb + cq + e]
-    if (MODE == C64_DGRAD) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // mbits (ring DMA may fly)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wave * 64 + 16 * i + r16;
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = acc[i][jb][e];
-          if (MODE == C64_FWD) {
-            x = fmaxf(x * sc[jb][e] + sh[jb][e], 0.f);
-          } else {
-            const int c = 16 * jb + cq + e;
-            const uint32_t word = c < 32 ? mbits[i].x : mbits[i].y;
-            x = ((word >> (c & 31)) & 1u) ? x : 0.f;
-            if (m < p.M) csum[jb][e] += x;
-          }
-          v[e] = x;
-        }
-        const int chunk = 2 * jb + (kq >> 1);
-        *reinterpret_cast<uint2*>(stage + r16 * 128 + ((chunk ^ c64_sw(r16)) << 4) + 8 * (kq & 1)) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int r = (lane >> 3) + 8 * hh, c = lane & 7;
-        const uint4 pk = *reinterpret_cast<const uint4*>(stage + r * 128 + ((c ^ c64_sw(r)) << 4));
-        const int mo = m0 + wave * 64 + 16 * i + r;
-        if (mo < p.M) {
-          *reinterpret_cast<uint4*>(p.out + (long)mo * 64 + c * 8) = pk;
-          if (bits_st) p.bits_out[(long)mo * 8 + c] = (uint8_t)pos_bits8(pk);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slice reads done before the next i rewrites it
-    }
-    slot_m0 += C64_BM;
-    if (slot_m0 >= C64_RING) slot_m0 -= C64_RING;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (MODE == C64_DGRAD && p.colsum) {
-    // one partial row per wave: fold the 16 lanes (r16) sharing this lane's channels
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) csum[jb][e] += __shfl_xor(csum[jb][e], o, 64);
-    if (r16 == 0) {
-      float* row = p.colsum + (long)(g * 4 + wave) * 64;
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
-        *reinterpret_cast<float4*>(row + 16 * jb + cq) = make_float4(csum[jb][0], csum[jb][1], csum[jb][2], csum[jb][3]);
-    }
-  }
-}
-
-// Row-tile form of the same forward / data-gradient conv (knob c64 = 2, default): a tile is 4 output
-// rows of one image, wave w computing row h0 + w as 64 pixel slots (slots >= W are padding and are
-// not stored); its input is the zero-padded 6 x 64-slot window of rows h0 - 1 .. h0 + 4 (48 KiB,
-// the wgrad kernel's x image: padding taps read zeros the LDS-DMA wrote, so no tap masks and no
-// ring wrap), double-buffered so tile t + 1 loads while tile t computes.  The whole 64 x 576 weight
-// matrix lives in registers as MFMA A fragments (288 VGPRs, one wave per SIMD), so the k loop reads
-// only the pixel fragments, at addresses precomputed per lane (the window row of tap r is an
-// immediate offset).  (All nine taps in registers -- 288 VGPRs -- spill: the last four taps' weights
-// sit in LDS, read like the igemm B images.)
+// Forward / data gradient: 8 waves in two channel halves -- wave w computes output row h0 + (w & 3)
+// as 64 pixel slots (slots >= W are padding, not stored), channels 32 (w >> 2) .. + 31.  The
+// wave's half of the weight matrix for taps < R8_TR lives in registers as MFMA A fragments (80
+// VGPRs), taps >= R8_TR in LDS (read like the igemm B images), so two waves fit per SIMD: one
+// wave's epilogue, window-DMA issue and fragment-read latency overlap the other's MFMAs.  (The
+// round-4 first form ran 4 waves with the whole weight matrix per wave, one wave per SIMD, MFMA
+// busy 39 %: 767 / 739 us forward / dgrad at b2560 against 695 / 679 us here,
+// profiles/r4_c64_row8.txt; a 12-slot row ring that DMAs only the 4 new rows per tile measured
+// no gain and was dropped.)  The pixel fragments are read by both halves, per lane at
+// precomputed offsets (the window row of tap r is an immediate offset).
 namespace {
-constexpr int CR_WIN = 6 * 64 * 128;                // 49,152 B per window
-constexpr int CR_TR = 5;                            // taps 0..4: weights in registers; 5..8: in LDS
-constexpr int CR_WL = (9 - CR_TR) * 8192;           // LDS weight images [tap - TR][n][128 B]
-constexpr int CR_LDS = 2 * CR_WIN + CR_WL + 4 * C64_STAGE_BYTES;
-static_assert(CR_LDS <= 163840, "LDS budget");
+constexpr int R8_TR = 5;                             // taps 0..4 in registers, 5..8 in LDS
+constexpr int R8_WL = (9 - R8_TR) * 8192;
+constexpr int R8_STAGE = 1024;                       // per wave: 16 pixels x 64 B
+constexpr int R8_LDS = 2 * CR_WIN + R8_WL + 8 * R8_STAGE;
+static_assert(R8_LDS <= 163840, "LDS budget");
+__device__ __forceinline__ int r8_sw(int row) { return (row >> 2) & 3; }   // 64-B rows: 16 rows, 4 chunks
 }  // namespace
 
 template <int MODE>
-__global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
+__global__ void __launch_bounds__(512, 1) conv3x3c64_row8_kernel(C64Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rw = wave & 3, hf = wave >> 2;
   char* wl = smem + 2 * CR_WIN;
-  char* stage = smem + 2 * CR_WIN + CR_WL + wave * C64_STAGE_BYTES;
+  char* stage = smem + 2 * CR_WIN + R8_WL + wave * R8_STAGE;
   const int RT = (p.H + 3) / 4;
   const int T = p.N * RT;
   const int G = gridDim.x, gb = blockIdx.x;
@@ -302,7 +76,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
   const long img = (long)p.H * p.W * 64;
   const int r16 = lane & 15, kq = lane >> 4, cq = 4 * kq;
 
-  // window DMA of tile t into buffer b: 6 rows x 8 pieces, 12 per wave
+  // window DMA of tile t into buffer b: 6 rows x 8 pieces, 6 per wave
   auto load_tile = [&](int t, int b) {
     const bool live = t < t_end;
     const int tt = live ? t : t_begin;
@@ -310,8 +84,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
     const __amdgpu_buffer_rsrc_t rx = make_rsrc_at(p.x, n * img, (n + 1) * img);
     char* base = smem + b * CR_WIN;
 #pragma unroll
-    for (int q = 0; q < 12; ++q) {
-      const int pc = wave * 12 + q;
+    for (int q = 0; q < 6; ++q) {
+      const int pc = wave * 6 + q;
       const int slot = pc * 8 + (lane >> 3);
       const int rr = slot >> 6, j = slot & 63;
       const int h = h0 - 1 + rr, w = j - 1;
@@ -321,28 +95,26 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
     }
   };
 
-  // weights of taps >= TR -> LDS ([tap - TR][n][128 B], chunk swizzled by n): 32 pieces, 8 per wave
+  // weights of taps >= TR -> LDS ([tap - TR][n][128 B], chunk swizzled by n): 32 pieces, 4 per wave
   {
-    const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, 64 * 576 * 2);
+    const __amdgpu_buffer_rsrc_t rw_ = make_rsrc(p.w, 64 * 576 * 2);
 #pragma unroll
-    for (int q = 0; q < (9 - CR_TR) * 2; ++q) {
-      const int pc = wave * ((9 - CR_TR) * 2) + q;
+    for (int q = 0; q < (9 - R8_TR); ++q) {
+      const int pc = wave * (9 - R8_TR) + q;
       const int tl = pc >> 3, nn = (pc & 7) * 8 + (lane >> 3);
       const int ch = (lane & 7) ^ c64_sw(nn);
-      buf_lds16(rw, LDS_PTR(wl + pc * 1024), (uint32_t)((nn * 576 + (CR_TR + tl) * 64 + ch * 8) * 2), 0);
+      buf_lds16(rw_, LDS_PTR(wl + pc * 1024), (uint32_t)((nn * 576 + (R8_TR + tl) * 64 + ch * 8) * 2), 0);
     }
   }
-  // weights of taps < TR as A fragments: wf[tap][kh][jb] = W[16 jb + r16][tap * 64 + kh * 32 + 8 kq .. + 7]
-  v8bf wf[CR_TR][2][4];
+  // this half's weights of taps < TR as A fragments: wf[tap][kh][jl] = W[16 (2 hf + jl) + r16][tap * 64 + kh * 32 + 8 kq ..]
+  v8bf wf[R8_TR][2][2];
 #pragma unroll
-  for (int tap = 0; tap < CR_TR; ++tap)
+  for (int tap = 0; tap < R8_TR; ++tap)
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
-        wf[tap][kh][jb] = *reinterpret_cast<const v8bf*>(p.w + (16 * jb + r16) * 576 + tap * 64 + kh * 32 + 8 * kq);
-  // per-lane fragment offsets within a window row: pixel slot 16 i + r16 + s, chunk kh * 4 + kq
-  // (the swizzle depends on the slot only through (slot >> 1) & 7, which a row offset of 64 keeps)
+      for (int jl = 0; jl < 2; ++jl)
+        wf[tap][kh][jl] = *reinterpret_cast<const v8bf*>(p.w + (16 * (2 * hf + jl) + r16) * 576 + tap * 64 + kh * 32 + 8 * kq);
   int aoff[4][3][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -353,21 +125,21 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
         const int sl = 16 * i + r16 + sx;
         aoff[i][sx][kh] = sl * 128 + (((kh * 4 + kq) ^ c64_sw(sl)) << 4);
       }
-  float sc[4][4], sh[4][4];
+  float sc[2][4], sh[2][4];
   if (MODE == C64_FWD) {
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
-      const float4 a = *reinterpret_cast<const float4*>(p.scale + 16 * jb + cq);
-      const float4 b = *reinterpret_cast<const float4*>(p.shift + 16 * jb + cq);
-      sc[jb][0] = a.x; sc[jb][1] = a.y; sc[jb][2] = a.z; sc[jb][3] = a.w;
-      sh[jb][0] = b.x; sh[jb][1] = b.y; sh[jb][2] = b.z; sh[jb][3] = b.w;
+    for (int jl = 0; jl < 2; ++jl) {
+      const float4 a = *reinterpret_cast<const float4*>(p.scale + 16 * (2 * hf + jl) + cq);
+      const float4 b = *reinterpret_cast<const float4*>(p.shift + 16 * (2 * hf + jl) + cq);
+      sc[jl][0] = a.x; sc[jl][1] = a.y; sc[jl][2] = a.z; sc[jl][3] = a.w;
+      sh[jl][0] = b.x; sh[jl][1] = b.y; sh[jl][2] = b.z; sh[jl][3] = b.w;
     }
   }
-  float csum[4][4];
+  float csum[2][4];
 #pragma unroll
-  for (int jb = 0; jb < 4; ++jb)
+  for (int jl = 0; jl < 2; ++jl)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) csum[jb][e] = 0.f;
+    for (int e = 0; e < 4; ++e) csum[jl][e] = 0.f;
   const bool bits_st = MODE == C64_FWD && p.bits_out != nullptr;
 
   load_tile(t_begin, 0);
@@ -376,41 +148,41 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
   for (int t = t_begin; t < t_end; ++t) {
     const int b = (t - t_begin) & 1;
     if (t > t_begin) {
-      // this tile's window landed (only the previous tile's stores may be outstanding), and every
-      // wave finished the previous tile (its window buffer takes tile t + 1)
-      if (bits_st) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // this tile's window landed (only the previous tile's 4 / 8 stores may be outstanding), and
+      // every wave finished the previous tile (its window buffer takes tile t + 1)
+      if (bits_st) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    const int n = t / RT, h = (t - n * RT) * 4 + wave;   // this wave's output row
+    const int n = t / RT, h = (t - n * RT) * 4 + rw;   // this wave's output row
     const bool row_ok = h < p.H;
-    const long mrow = ((long)n * p.H + (row_ok ? h : 0)) * p.W;   // pixel index of (n, h, 0)
-    uint2 mbits[4];
+    const long mrow = ((long)n * p.H + (row_ok ? h : 0)) * p.W;
+    uint32_t mbits[4];
     if (MODE == C64_DGRAD) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int wpx = 16 * i + r16;
         const long m = mrow + (wpx < p.W ? wpx : p.W - 1);
-        mbits[i] = *reinterpret_cast<const uint2*>(p.bits_mask + m * 8);
+        mbits[i] = *reinterpret_cast<const uint32_t*>(p.bits_mask + m * 8 + 4 * hf);
       }
     }
     load_tile(t + 1, b ^ 1);                     // (past the range: zeros into the idle buffer)
-    const char* xw = smem + b * CR_WIN + wave * 8192;   // window row of tap r = 0 for this wave
+    const char* xw = smem + b * CR_WIN + rw * 8192;
 
-    v4f acc[4][4];
+    v4f acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb) acc[i][jb] = v4f{0.f, 0.f, 0.f, 0.f};
-    v8bf ra[2][4], rwt[2][4];
+      for (int jl = 0; jl < 2; ++jl) acc[i][jl] = v4f{0.f, 0.f, 0.f, 0.f};
+    v8bf ra[2][4], rwt[2][2];
     auto load_step = [&](int st, int set) {
       const int tap = st >> 1, kh = st & 1, r = tap / 3, sx = tap % 3;
 #pragma unroll
       for (int i = 0; i < 4; ++i) ra[set][i] = *reinterpret_cast<const v8bf*>(xw + r * 8192 + aoff[i][sx][kh]);
-      if (tap >= CR_TR) {
+      if (tap >= R8_TR) {
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) {
-          const int nn = 16 * jb + r16;
-          rwt[set][jb] = *reinterpret_cast<const v8bf*>(wl + (tap - CR_TR) * 8192 + nn * 128 +
+        for (int jl = 0; jl < 2; ++jl) {
+          const int nn = 16 * (2 * hf + jl) + r16;
+          rwt[set][jl] = *reinterpret_cast<const v8bf*>(wl + (tap - R8_TR) * 8192 + nn * 128 +
                                                          (((kh * 4 + kq) ^ c64_sw(nn)) << 4));
         }
       }
@@ -420,9 +192,9 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-          acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tap < CR_TR ? wf[tap < CR_TR ? tap : 0][kh][jb] : rwt[set][jb],
-                                                               ra[set][i], acc[i][jb], 0, 0, 0);
+        for (int jl = 0; jl < 2; ++jl)
+          acc[i][jl] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tap < R8_TR ? wf[tap < R8_TR ? tap : 0][kh][jl] : rwt[set][jl],
+                                                               ra[set][i], acc[i][jl], 0, 0, 0);
     };
     load_step(0, 0);
 #pragma unroll
@@ -437,49 +209,38 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- epilogue: acc[i][jb][e] = out[pixel slot 16 i + r16 of row h][channel 16 jb + cq + e]
-    if (MODE == C64_DGRAD) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // mbits (the window DMA may fly)
+    // ---- epilogue: acc[i][jl][e] = out[pixel slot 16 i + r16][channel 32 hf + 16 jl + cq + e]
+    if (MODE == C64_DGRAD) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // mbits (the window DMA may fly)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool px_ok = row_ok && 16 * i + r16 < p.W;
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb) {
+      for (int jl = 0; jl < 2; ++jl) {
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float x = acc[i][jb][e];
+          float x = acc[i][jl][e];
           if (MODE == C64_FWD) {
-            x = fmaxf(x * sc[jb][e] + sh[jb][e], 0.f);
+            x = fmaxf(x * sc[jl][e] + sh[jl][e], 0.f);
           } else {
-            const int c = 16 * jb + cq + e;
-            const uint32_t word = c < 32 ? mbits[i].x : mbits[i].y;
-            x = ((word >> (c & 31)) & 1u) ? x : 0.f;
-            if (px_ok) csum[jb][e] += x;
+            x = ((mbits[i] >> (16 * jl + cq + e)) & 1u) ? x : 0.f;
+            if (px_ok) csum[jl][e] += x;
           }
           v[e] = x;
         }
-        const int chunk = 2 * jb + (kq >> 1);
-        c64_wr8(stage + r16 * 128 + ((chunk ^ c64_sw(r16)) << 4) + 8 * (kq & 1),
+        const int chunk = 2 * jl + (kq >> 1);
+        c64_wr8(stage + r16 * 64 + ((chunk ^ r8_sw(r16)) << 4) + 8 * (kq & 1),
                 make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3])));
       }
-      uint4 pkr[2];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int rr = (lane >> 3) + 8 * hh, c = lane & 7;
-        pkr[hh] = c64_rd16(stage + rr * 128 + ((c ^ c64_sw(rr)) << 4));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (also orders the next i's writes after these reads)
+      const int rr = lane >> 2, c = lane & 3;
+      const uint4 pk = c64_rd16(stage + rr * 64 + ((c ^ r8_sw(rr)) << 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (also orders the next i's writes after this read)
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int rr = (lane >> 3) + 8 * hh, c = lane & 7;
-        const uint4 pk = pkr[hh];
-        const int wpx = 16 * i + rr;
-        if (row_ok && wpx < p.W) {
-          const long mo = mrow + wpx;
-          *reinterpret_cast<uint4*>(p.out + mo * 64 + c * 8) = pk;
-          if (bits_st) p.bits_out[mo * 8 + c] = (uint8_t)pos_bits8(pk);
-        }
+      const int wpx = 16 * i + rr;
+      if (row_ok && wpx < p.W) {
+        const long mo = mrow + wpx;
+        *reinterpret_cast<uint4*>(p.out + mo * 64 + 32 * hf + c * 8) = pk;
+        if (bits_st) p.bits_out[mo * 8 + 4 * hf + c] = (uint8_t)pos_bits8(pk);
       }
     }
   }
@@ -488,35 +249,28 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_row_kernel(C64Params p) {
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1)
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
+      for (int jl = 0; jl < 2; ++jl)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) csum[jb][e] += __shfl_xor(csum[jb][e], o, 64);
+        for (int e = 0; e < 4; ++e) csum[jl][e] += __shfl_xor(csum[jl][e], o, 64);
     if (r16 == 0) {
-      float* rowp = p.colsum + (long)(gb * 4 + wave) * 64;
+      float* rowp = p.colsum + (long)(gb * 4 + rw) * 64 + 32 * hf;
 #pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
-        *reinterpret_cast<float4*>(rowp + 16 * jb + cq) = make_float4(csum[jb][0], csum[jb][1], csum[jb][2], csum[jb][3]);
+      for (int jl = 0; jl < 2; ++jl)
+        *reinterpret_cast<float4*>(rowp + 16 * jl + cq) = make_float4(csum[jl][0], csum[jl][1], csum[jl][2], csum[jl][3]);
     }
   }
 }
 
-int g_c64_variant = 2;   // 2: row-tile kernel (weights in registers); 1: pixel-ring kernel
 int g_c64_grid = 0;   // test knob: cap on the workgroup count (0: one per CU), so that small
-                      // problems still run many tiles per workgroup through the ring
-// workgroups: one per CU (capped by the tile count); the partial column-sum rows are 4 per
-// workgroup for either form, so a caller sizes them from the pixel count alone
-int conv3x3c64_grid(int M) {
-  const int T = (M + C64_BM - 1) / C64_BM;
-  int C = num_cus();
-  if (g_c64_grid > 0 && g_c64_grid < C) C = g_c64_grid;
-  return T < C ? T : C;
-}
+                      // problems still run many tiles per workgroup
+// the partial column-sum rows are 4 per workgroup (one per output row of a tile), so a caller
+// sizes them from the CU count alone
 int conv3x3c64_partial_rows(int M) { return num_cus() * 4; }
 
 const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
   C64Params p = p_in;
   if (p.M <= 0 || p.M != p.N * p.H * p.W) return "conv3x3c64: M must be N * H * W";
-  if (p.W + 1 > C64_AHEAD) return "conv3x3c64: image rows wider than 63 pixels";
+  if (p.W + 2 > 64) return "conv3x3c64: image rows wider than 62 pixels";
   if ((long)p.M * 64 >= (1L << 40)) return "conv3x3c64: too many pixels";
   if (mode == C64_FWD && (!p.scale || !p.shift)) return "conv3x3c64: forward needs scale / shift";
   if (mode == C64_DGRAD && !p.bits_mask) return "conv3x3c64: data gradient needs the ReLU bits";
@@ -524,29 +278,18 @@ const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
   p.mg_w = fdiv_magic(p.W);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv3x3c64_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, C64_LDS);
-    (void)hipFuncSetAttribute((const void*)conv3x3c64_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, C64_LDS);
-    (void)hipFuncSetAttribute((const void*)conv3x3c64_row_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, CR_LDS);
-    (void)hipFuncSetAttribute((const void*)conv3x3c64_row_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, CR_LDS);
+    (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
+    (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
     attr = true;
   }
-  if (g_c64_variant == 2 && p.W + 2 <= 64) {
-    const int T = p.N * ((p.H + 3) / 4);
-    int G = num_cus();
-    if (g_c64_grid > 0 && g_c64_grid < G) G = g_c64_grid;
-    if (G > T) G = T;
-    if (p.colsum)   // (rows of workgroups the grid leaves out stay zero for the reduction)
-      (void)hipMemsetAsync(p.colsum + (long)G * 4 * 64, 0, (size_t)(num_cus() - G) * 4 * 64 * sizeof(float), s);
-    if (mode == C64_FWD) hipLaunchKernelGGL(conv3x3c64_row_kernel<C64_FWD>, dim3(G), dim3(256), CR_LDS, s, p);
-    else hipLaunchKernelGGL(conv3x3c64_row_kernel<C64_DGRAD>, dim3(G), dim3(256), CR_LDS, s, p);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? nullptr : hipGetErrorString(e);
-  }
-  const int G = conv3x3c64_grid(p.M);
-  if (p.colsum && G < num_cus())
+  const int T = p.N * ((p.H + 3) / 4);
+  int G = num_cus();
+  if (g_c64_grid > 0 && g_c64_grid < G) G = g_c64_grid;
+  if (G > T) G = T;
+  if (p.colsum)   // (rows of workgroups the grid leaves out stay zero for the reduction)
     (void)hipMemsetAsync(p.colsum + (long)G * 4 * 64, 0, (size_t)(num_cus() - G) * 4 * 64 * sizeof(float), s);
-  if (mode == C64_FWD) hipLaunchKernelGGL(conv3x3c64_kernel<C64_FWD>, dim3(G), dim3(256), C64_LDS, s, p);
-  else hipLaunchKernelGGL(conv3x3c64_kernel<C64_DGRAD>, dim3(G), dim3(256), C64_LDS, s, p);
+  if (mode == C64_FWD) hipLaunchKernelGGL(conv3x3c64_row8_kernel<C64_FWD>, dim3(G), dim3(512), R8_LDS, s, p);
+  else hipLaunchKernelGGL(conv3x3c64_row8_kernel<C64_DGRAD>, dim3(G), dim3(512), R8_LDS, s, p);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -183,7 +183,7 @@ struct StemPoolBwdParams {
   int B, Hs, Ws, H1, W1, H2, W2;
   int PB, nblk;
 };
-// Persistent pixel-ring 3x3 / pad 1 / stride 1 convolution, 64 -> 64 channels (conv3x3c64.hip).
+// Persistent row-tile 3x3 / pad 1 / stride 1 convolution, 64 -> 64 channels (conv3x3c64.hip).
 enum { C64_FWD = 0, C64_DGRAD = 1 };
 struct C64Params {
   const uint16_t* x;          // [M][64] NHWC input (forward) / output gradient (dgrad)
@@ -199,7 +199,7 @@ struct C64Params {
 };
 const char* conv3x3c64_launch(const C64Params& p, int mode, hipStream_t s);
 int conv3x3c64_partial_rows(int M);
-extern int g_c64_grid, g_c64w_grid, g_stem_pool_variant, g_c64_variant;
+extern int g_c64_grid, g_c64w_grid, g_stem_pool_variant;
 struct C64WgradParams {
   const uint16_t* x;          // [N][H][W][64] conv input
   const uint16_t* g;          // [N][H][W][64] output gradient

@@ -49,7 +49,7 @@ class HipEngine:
     FUSE_BWD_OK = True      # stage-2/3 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
     FUSE_STEM_OK = True     # stem conv + BN + ReLU + max-pool forward in one launch (stem.hip)
     TWO_STREAM_OK = True
-    C64_OK = True           # stage-2 3x3 convs on the persistent pixel-ring kernel (conv3x3c64.hip)
+    C64_OK = True           # stage-2 3x3 convs on the row-tile kernels (conv3x3c64.hip)
     C64_MIN_M = 262144      # ... from 4 x 256 CUs x 256-pixel tiles up (b >= 84 at 56 x 56)
     C3C1_OK = True          # stage-2 boundaries: conv3 + next conv1 fused (c3c1.hip)
     S2C_OK = True           # blocks feeding a downsampling block store only their stride-2 grid
@@ -101,8 +101,8 @@ class HipEngine:
         self._fuse_bwd_s2 = os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0"
         # stem conv + max-pool forward as one launch (stem.hip): conv1's output never reaches HBM
         self.fuse_stem = self.FUSE_STEM_OK and os.environ.get("PDDL_FUSE_STEM", "1") != "0" and crop <= 250
-        # stage-2 3x3 convs (64 -> 64) on the persistent pixel-ring kernel (conv3x3c64.hip) at
-        # batches where every CU streams several tiles through its ring
+        # stage-2 3x3 convs (64 -> 64) on the persistent row-tile kernels (conv3x3c64.hip) at
+        # batches where every CU streams several row tiles through its windows
         self.c64 = self.C64_OK and os.environ.get("PDDL_C64", "1") != "0"
         self.c64w = self.c64 and os.environ.get("PDDL_C64W", "1") != "0"
         self.c64_min_m = int(os.environ.get("PDDL_C64_MIN_M", self.C64_MIN_M))
@@ -429,7 +429,7 @@ class HipEngine:
         return self.fuse_bwd and bi not in s2 and (b.filters == 64 or (b.filters == 128 and self._fuse_bwd3))
 
     def _use_c64(self, f, M, W, bits=True) -> bool:
-        return self.c64 and f == 64 and W + 1 <= 64 and M >= self.c64_min_m and bits
+        return self.c64 and f == 64 and W + 2 <= 64 and M >= self.c64_min_m and bits
 
     def _c3c1_ok(self, b, nb) -> bool:
         """Fuse block b's conv3 with block nb's conv1 (c3c1.hip): 64-channel stride-1 boundaries

@@ -46,7 +46,7 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         if not c1_done:
             ev.append(("igemm", f"{b.name} c1{'+c0' if n1 > f else ''} fwd", 2 * M * cin * n1,
                        (B * H * H * cin + M * n1) * 2, (M, n1, cin)))
-        c64 = f == 64 and M >= 262144 and Ho + 1 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
+        c64 = f == 64 and M >= 262144 and Ho + 2 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
         ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2,
                    (M, f, 9 * f)))
         c1_done = c3c1(b, nb)
@@ -101,7 +101,7 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         c64w = f == 64 and M >= 262144 and Ho + 2 <= 64 and Mc == M and os.environ.get("PDDL_C64", "1") != "0" \
             and os.environ.get("PDDL_C64W", "1") != "0"
         ev.append(("conv3x3c64" if c64w else "wgrad", f"{b.name} c2 wgrad", 2 * Mc * 9 * f * f, (Mc + M) * f * 2))
-        c64 = f == 64 and M >= 262144 and Ho + 1 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
+        c64 = f == 64 and M >= 262144 and Ho + 2 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
         ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2,
                    (M, f, 9 * f)))
         n1 = 5 * f if b.proj else f

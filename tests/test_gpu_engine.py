@@ -286,38 +286,31 @@ def test_fused_conv3_backward_matches_unfused(monkeypatch):
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
 
 
-@pytest.mark.parametrize("variant", ["1", "2"])
-def test_c64_kernels_in_engine_match_generic(monkeypatch, variant):
-    """The stage-2 3x3 convs on conv3x3c64.hip (forward, data gradient -- 1: pixel ring, 2: row
-    tiles -- and the row-tile weight gradient; the engine enables them from b >= 84 at 224, here
-    forced on with PDDL_C64_MIN_M) against the generic implicit GEMM / wgrad kernels: same loss,
-    flat gradients to fp32 accumulation order."""
+def test_c64_kernels_in_engine_match_generic(monkeypatch):
+    """The stage-2 3x3 convs on conv3x3c64.hip (forward, data gradient and weight gradient; the
+    engine enables them from b >= 84 at 224, here forced on with PDDL_C64_MIN_M) against the
+    generic implicit GEMM / wgrad kernels: same loss, flat gradients to fp32 accumulation order."""
     from pddl.models.engine import HipEngine
     from pddl.models.resnet50 import ParamLayout
     L = ParamLayout()
     B = 8
     res = []
     monkeypatch.setenv("PDDL_C64_MIN_M", "1")
-    from pddl.ops.native import require_native
-    require_native().set_variant("c64", int(variant))
-    try:
-        for on in ("1", "0"):
-            monkeypatch.setenv("PDDL_C64", on)
-            he = HipEngine(L, B, crop=224, image_size=224)
-            he.init(seed=7)
-            assert he.c64 == (on == "1") and he._use_c64(64, B * 56 * 56, 56) == (on == "1")
-            img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8,
-                                generator=torch.Generator().manual_seed(1)).cuda()
-            lab = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(2)).cuda()
-            st = he.forward_backward(img, lab, 1.0 / B)
-            torch.cuda.synchronize()
-            res.append((st[0].item() / B, he.grads.clone()))
-    finally:
-        require_native().set_variant("c64", 2)
+    for on in ("1", "0"):
+        monkeypatch.setenv("PDDL_C64", on)
+        he = HipEngine(L, B, crop=224, image_size=224)
+        he.init(seed=7)
+        assert he.c64 == (on == "1") and he._use_c64(64, B * 56 * 56, 56) == (on == "1")
+        img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8,
+                            generator=torch.Generator().manual_seed(1)).cuda()
+        lab = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(2)).cuda()
+        st = he.forward_backward(img, lab, 1.0 / B)
+        torch.cuda.synchronize()
+        res.append((st[0].item() / B, he.grads.clone()))
     (l1, g1), (l0, g0) = res
-    print(f"c64 variant {variant}: loss rel {abs(l1 - l0) / abs(l0):.2e}, grad rel {((g1 - g0).norm() / g0.norm()).item():.3e}")
+    print(f"c64: loss rel {abs(l1 - l0) / abs(l0):.2e}, grad rel {((g1 - g0).norm() / g0.norm()).item():.3e}")
     assert abs(l1 - l0) < 1e-4 * abs(l0)
-    # (both variants land at 1.5e-2 -- identical, so not a variant defect: the swapped-operand
+    # (every c64 kernel form measured lands at 1.5e-2 -- not a kernel defect: the swapped-operand
     # MFMAs round a few bf16 activations the other way and the flat gradient, dominated by
     # cancellation-heavy BN-gamma terms, moves by that much; the numeric check of the c64 path
     # against the fp32 reference is test_c64_engine_within_noise_floor)
@@ -406,18 +399,12 @@ def test_s2_fed_blocks_store_compact_outputs(monkeypatch):
     test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
 
 
-@pytest.mark.parametrize("variant", ["1", "2"])
-def test_c64_engine_within_noise_floor(monkeypatch, variant):
+def test_c64_engine_within_noise_floor(monkeypatch):
     """The engine with the stage-2 3x3 convs forced onto conv3x3c64.hip is as close to the fp32
     reference as the reference's own bf16-point floor (same criteria as the generic path:
-    measured ratios 0.92-1.13 ring, 0.99-1.13 row tiles vs 0.98-1.15 generic, crops 224/160/244)."""
-    from pddl.ops.native import require_native
+    measured ratios 0.92-1.00 on the 8-wave row tiles vs 0.98-1.15 generic, crops 224/160/244)."""
     monkeypatch.setenv("PDDL_C64_MIN_M", "1")
-    require_native().set_variant("c64", int(variant))
-    try:
-        test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
-    finally:
-        require_native().set_variant("c64", 2)
+    test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
 
 
 @pytest.mark.parametrize("graphed", [False, True])
