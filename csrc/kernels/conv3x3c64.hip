@@ -300,9 +300,9 @@ const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
 // w >= W zero): 256 slots of g (32 KiB) and the 6 x 64 zero-padded input rows h0 - 1 .. h0 + 4
 // (slot j <-> w = j - 1; padding rows / columns are zeros straight from the LDS-DMA's out-of-range
 // loads), so every tap of every slot is a plain shifted read -- no tap masks.  Two such buffers
-// (2 x 80 KiB) alternate: tile t + 1 is DMA'd while tile t computes.  Wave w owns input channels
-// 16 w .. 16 w + 15 for all 9 taps x 64 output channels (acc[9][4]: 144 accumulators) for the
-// workgroup's whole range and adds them once at the end (row-contiguous fp32 atomics).  The
+// (2 x 80 KiB) alternate: tile t + 1 is DMA'd while tile t computes.  A wave owns 16 input channels
+// x 32 output channels for all 9 taps (acc[9][2]) for the workgroup's whole range and adds them
+// once at the end (row-contiguous fp32 atomics).  The
 // reduction runs over pixels, so both operands are read with ds_read_b64_tr_b16.
 // Reference: the Conv2D kernel gradient of conv2_block*_2 (tf.GradientTape in model.fit,
 // imagenet-resnet50.py:67).
@@ -326,10 +326,16 @@ __device__ __forceinline__ v4bf cw_tr(const char* p) {
   return r;
 }
 
-__global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams p) {
+// 8 waves: wave w owns input-channel block w & 3 for output channels 32 (w >> 2) .. + 31
+// (acc[9][2]), so two waves fit per SIMD and one wave's fragment reads overlap the other's MFMAs;
+// the x fragments are read by both halves.  (The first form, 4 waves with all 64 output channels
+// each and one wave per SIMD, ran 680-700 us at b2560 against 654 us: profiles/r4_c64_row8.txt.)
+__global__ void __launch_bounds__(512, 1) conv3x3c64_wgrad_kernel(C64WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PPW = 10, NI = 2;   // DMA pieces per wave (80 / 8 waves), output-channel blocks per wave
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cb = wave & 3, i0 = (wave >> 2) * NI;   // ci block, first co block
   const int RT = (p.H + 3) / 4;                 // row tiles per image
   const int T = p.N * RT;
   const int G = gridDim.x, gb = blockIdx.x;
@@ -337,7 +343,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams
   if (t_begin >= t_end) return;
   const long img = (long)p.H * p.W * 64;        // elements per image
 
-  // DMA of tile t into buffer b: 48 x-window pieces then 32 g pieces (8 slots each), 20 per wave
+  // DMA of tile t into buffer b: 48 x-window pieces then 32 g pieces (8 slots each), 10 per wave
   auto load_tile = [&](int t, int b) {
     const bool live = t < t_end;
     const int tt = live ? t : t_begin;
@@ -346,8 +352,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams
     const __amdgpu_buffer_rsrc_t rg = make_rsrc_at(p.g, n * img, (n + 1) * img);
     char* base = smem + b * CW_BUF;
 #pragma unroll
-    for (int q = 0; q < 20; ++q) {
-      const int pc = wave * 20 + q;             // 0..79
+    for (int q = 0; q < PPW; ++q) {
+      const int pc = wave * PPW + q;            // 0..79
       const bool isx = pc < 48;
       const int sp0 = (isx ? pc : pc - 48) * 8;                 // first slot of the piece
       const int slot = sp0 + (lane >> 3);
@@ -362,11 +368,11 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams
     }
   };
 
-  v4f acc[9][4];
+  v4f acc[9][NI];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[t][i] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NI; ++i) acc[t][i] = v4f{0.f, 0.f, 0.f, 0.f};
 
   // ds_read_b64_tr_b16: lane 4 q + pp of each 16-lane group addresses slot row q, channels 4 pp .. +3
   // of a 16-channel block; lane i of the group then holds channel i for the 4 slots
@@ -382,15 +388,15 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams
     // 8 k-steps of 32 slots; each step's 26 transposed reads (4 g + 9 x fragments, two halves)
     // are issued during the previous step's MFMAs, in two batches of 13 (the LDS counter tracks
     // at most 15 reads in flight), behind explicit waits and scheduling barriers (asm reads)
-    v8bf af[2][4], bfr[2][9];
+    v8bf af[2][NI], bfr[2][9];
     auto rd_a = [&](int ks, int set) {
       const int rl = ks >> 1, w0 = (ks & 1) * 32;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int sg = rl * 64 + w0 + 8 * gq + 4 * hh + q;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const v4bf r = cw_tr(gt + sg * 128 + (((2 * i + (pp >> 1)) ^ cw_sw(sg)) << 4) + (pp & 1) * 8);
+        for (int i = 0; i < NI; ++i) {
+          const v4bf r = cw_tr(gt + sg * 128 + (((2 * (i0 + i) + (pp >> 1)) ^ cw_sw(sg)) << 4) + (pp & 1) * 8);
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[set][i][4 * hh + e] = r[e];
         }
@@ -404,7 +410,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams
 #pragma unroll
         for (int tap = t0; tap < t1; ++tap) {
           const int sx = (rl + tap / 3) * 64 + ws + tap % 3;
-          const v4bf r = cw_tr(xw + sx * 128 + (((2 * wave + (pp >> 1)) ^ cw_sw(sx)) << 4) + (pp & 1) * 8);
+          const v4bf r = cw_tr(xw + sx * 128 + (((2 * cb + (pp >> 1)) ^ cw_sw(sx)) << 4) + (pp & 1) * 8);
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfr[set][tap][4 * hh + e] = r[e];
         }
@@ -414,7 +420,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams
 #pragma unroll
       for (int tap = t0; tap < t1; ++tap)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NI; ++i)
           acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[set][i], bfr[set][tap], acc[tap][i], 0, 0, 0);
     };
     rd_a(0, 0);
@@ -436,14 +442,14 @@ __global__ void __launch_bounds__(256, 1) conv3x3c64_wgrad_kernel(C64WgradParams
     // tile t + 1 landed; every wave is done with buffer b (tile t + 2 goes there next)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  // D[co][ci] of tap: co = 16 i + 4 (lane >> 4) + e, ci = 16 wave + (lane & 15)
+  // D[co][ci] of tap: co = 16 (i0 + i) + 4 (lane >> 4) + e, ci = 16 cb + (lane & 15)
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = 16 * i + 4 * gq + e, ci = 16 * wave + (lane & 15);
+        const int co = 16 * (i0 + i) + 4 * gq + e, ci = 16 * cb + (lane & 15);
         atomicAdd(p.dw + (long)co * p.ld_dw + tap * 64 + ci, acc[tap][i][e]);
       }
 }
@@ -463,7 +469,7 @@ const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CW_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL(conv3x3c64_wgrad_kernel, dim3(G), dim3(256), CW_LDS, s, p);
+  hipLaunchKernelGGL(conv3x3c64_wgrad_kernel, dim3(G), dim3(512), CW_LDS, s, p);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -1161,9 +1161,9 @@ def _c64_case(mode, n, h, grid):
 
 @pytest.mark.parametrize("n,h,grid", [(24, 56, 0), (5, 56, 3), (7, 13, 2), (3, 61, 0)])
 def test_conv3x3c64_wgrad_matches_reference(n, h, grid):
-    """Row-tile weight gradient of the 64 -> 64 3x3 conv (conv3x3c64.hip) against the fp32
-    PyTorch weight gradient of the same bf16 operands and against the generic wgrad kernel;
-    accumulates into dw (atomics) like the engine's zeroed gradient buffer."""
+    """Row-tile weight gradient of the 64 -> 64 3x3 conv (conv3x3c64.hip, 8 waves) against the fp32 PyTorch weight gradient of the same bf16
+    operands and against the generic wgrad kernel; accumulates into dw (atomics) like the
+    engine's zeroed gradient buffer."""
     torch.manual_seed(44)
     x = rnd(n, h, h, 64)
     g = rnd(n, h, h, 64)
