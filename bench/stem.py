@@ -1,4 +1,5 @@
-"""A/B of the fused stem forward (stem.hip, knob `stem_pool`) on the ResNet-50 stem shape."""
+"""Fused stem forward (stem.hip: conv1 + BN + ReLU + max-pool in one launch) against the unfused
+igemm conv1 + max-pool pair on the ResNet-50 stem shape: time and bitwise equality."""
 import argparse
 import os
 import sys
@@ -21,13 +22,7 @@ def main():
     x2 = torch.randn(B, Hs, Hs, 16, device="cuda").to(torch.bfloat16)
     w = (torch.randn(64, 256, device="cuda") * 0.05).to(torch.bfloat16)
     sc, sh = torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * 0.1
-    outs = {}
-    for v in (0, 1):
-        N.set_variant("stem_pool", v)
-        pool = torch.empty(B, H2, H2, 64, dtype=torch.bfloat16, device="cuda")
-        idx = torch.empty(B, H2, H2, 64, dtype=torch.uint8, device="cuda")
-        bits = torch.empty(B, H2, H2, 8, dtype=torch.uint8, device="cuda")
-        fn = lambda: N.stem_pool_fwd(x2, w, sc, sh, pool, idx, bits)  # noqa: E731
+    def timed(fn):
         for _ in range(2):
             fn()
         torch.cuda.synchronize()
@@ -37,13 +32,24 @@ def main():
             fn()
         e1.record()
         torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / a.iters * 1e3
-        flop = 2.0 * B * H1 * H1 * 64 * 256
-        print(f"stem_pool variant {v}: {us:8.1f} us  {flop / us / 1e6:6.1f} TF/s")
-        outs[v] = (pool.clone(), idx.clone(), bits.clone())
-    N.set_variant("stem_pool", 1)
-    print("variant outputs equal:", all(torch.equal(a_, b_) for a_, b_ in zip(outs[0], outs[1])))
+        return e0.elapsed_time(e1) / a.iters * 1e3
+    flop = 2.0 * B * H1 * H1 * 64 * 256
+    pool = torch.empty(B, H2, H2, 64, dtype=torch.bfloat16, device="cuda")
+    idx = torch.empty(B, H2, H2, 64, dtype=torch.uint8, device="cuda")
+    bits = torch.empty(B, H2, H2, 8, dtype=torch.uint8, device="cuda")
+    us = timed(lambda: N.stem_pool_fwd(x2, w, sc, sh, pool, idx, bits))
+    print(f"fused stem conv + pool: {us:8.1f} us  {flop / us / 1e6:6.1f} TF/s")
+    # the unfused pair: conv1 (igemm, 4x4 window over the s2d input) + max-pool
+    c1 = torch.empty(B, H1, H1, 64, dtype=torch.bfloat16, device="cuda")
+    pool2, idx2, bits2 = torch.empty_like(pool), torch.empty_like(idx), torch.empty_like(bits)
 
+    def unfused():
+        N.igemm(x2, None, Hs, Hs, 4, 4, 1, 0, H1, H1, w, 0, sc, sh, None, None, None, c1, 1, None, 0, 0, 0, 0, 0,
+                None, None)
+        N.maxpool_fwd(c1, pool2, idx2, bits2)
+    us2 = timed(unfused)
+    print(f"igemm conv1 + maxpool:  {us2:8.1f} us  {flop / us2 / 1e6:6.1f} TF/s")
+    print("outputs equal:", torch.equal(pool, pool2) and torch.equal(idx, idx2) and torch.equal(bits, bits2))
 
 if __name__ == "__main__":
     main()

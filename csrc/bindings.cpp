@@ -584,15 +584,12 @@ void conv3x3c64_wgrad(Tensor x, Tensor g, Tensor dw) {
 }
 // Fused 64-channel bottleneck boundary: out = relu(a . w3^T * scale3 + shift3 (+ res)), bits3;
 // y1 = relu(out . w1^T * scale1 + shift1), bits1 (a2: second K source of the fused projection).
-void c3c1(Tensor a, OptT a2, Tensor w3, Tensor scale3, Tensor shift3, OptT res, Tensor out, OptT bits3, Tensor w1,
+void c3c1(Tensor a, Tensor w3, Tensor scale3, Tensor shift3, OptT res, Tensor out, OptT bits3, Tensor w1,
           Tensor scale1, Tensor shift1, Tensor y1, OptT bits1) {
   PCHECK(a.size(-1) == 64 && a.is_contiguous() && a.scalar_type() == torch::kBFloat16, "c3c1: a [..,64] bf16");
   const int64_t M = a.numel() / 64;
   PCHECK(M < (1LL << 30), "c3c1: too many rows");
-  const int K1 = a2.has_value() ? 128 : 64;
-  if (a2.has_value())
-    PCHECK(a2->numel() == a.numel() && a2->is_contiguous() && a2->scalar_type() == torch::kBFloat16, "c3c1: a2 like a");
-  PCHECK(w3.dim() == 2 && w3.size(0) == 256 && w3.size(1) == K1 && w3.is_contiguous(), "c3c1: w3 [256, 64 | 128]");
+  PCHECK(w3.dim() == 2 && w3.size(0) == 256 && w3.size(1) == 64 && w3.is_contiguous(), "c3c1: w3 [256, 64]");
   PCHECK(w1.dim() == 2 && w1.size(0) == 64 && w1.size(1) == 256 && w1.is_contiguous(), "c3c1: w1 [64, 256]");
   PCHECK(scale3.numel() >= 256 && shift3.numel() >= 256 && scale1.numel() >= 64 && shift1.numel() >= 64,
          "c3c1: scale / shift sizes");
@@ -600,11 +597,11 @@ void c3c1(Tensor a, OptT a2, Tensor w3, Tensor scale3, Tensor shift3, OptT res, 
     PCHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "c3c1: 16-byte aligned scale / shift");
   PCHECK(out.numel() == M * 256 && out.is_contiguous() && out.scalar_type() == torch::kBFloat16, "c3c1: out [M,256]");
   PCHECK(y1.numel() == M * 64 && y1.is_contiguous() && y1.scalar_type() == torch::kBFloat16, "c3c1: y1 [M,64]");
-  if (res.has_value()) PCHECK(!a2.has_value() && res->numel() == M * 256 && res->is_contiguous(), "c3c1: res [M,256]");
+  if (res.has_value()) PCHECK(res->numel() == M * 256 && res->is_contiguous(), "c3c1: res [M,256]");
   if (bits3.has_value()) PCHECK(bits3->numel() == M * 32 && bits3->scalar_type() == torch::kUInt8, "c3c1: bits3 [M,32]");
   if (bits1.has_value()) PCHECK(bits1->numel() == M * 8 && bits1->scalar_type() == torch::kUInt8, "c3c1: bits1 [M,8]");
   pddl::C3C1Params p{};
-  p.a = bfp(a); p.a2 = a2.has_value() ? bfp(*a2) : nullptr; p.w3 = bfp(w3);
+  p.a = bfp(a); p.w3 = bfp(w3);
   p.scale3 = f32p(scale3); p.shift3 = f32p(shift3); p.res = obfp(res); p.out = bfpm(out);
   p.bits3 = bits3.has_value() ? bits3->data_ptr<uint8_t>() : nullptr;
   p.w1 = bfp(w1); p.scale1 = f32p(scale1); p.shift1 = f32p(shift1); p.y1 = bfpm(y1);
@@ -814,7 +811,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("bits") = py::none(),
         py::arg("colsum") = py::none());
   m.def("conv3x3c64_wgrad", &conv3x3c64_wgrad, REL, py::arg("x"), py::arg("g"), py::arg("dw"));
-  m.def("c3c1", &c3c1, REL, py::arg("a"), py::arg("a2"), py::arg("w3"), py::arg("scale3"), py::arg("shift3"),
+  m.def("c3c1", &c3c1, REL, py::arg("a"), py::arg("w3"), py::arg("scale3"), py::arg("shift3"),
         py::arg("res"), py::arg("out"), py::arg("bits3"), py::arg("w1"), py::arg("scale1"), py::arg("shift1"),
         py::arg("y1"), py::arg("bits1"));
   m.def("conv3x3c64_partial_rows", [](int64_t M) { return pddl::conv3x3c64_partial_rows((int)M); });
@@ -833,7 +830,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm_ns1_kt") pddl::g_igemm_ns1_kt = v;
     else if (which == "igemm8_min_n") pddl::g_igemm8_min_n = v;
     else if (which == "wgrad1") pddl::g_wgrad1 = v;
-    else if (which == "wgrad") pddl::g_wgrad_variant = v;
     else if (which == "igemm_n64") pddl::g_igemm_n64 = v;
     else if (which == "igemm_splitk") pddl::g_igemm_splitk = v;
     else if (which == "igemm_pk_all") pddl::g_igemm_pk_all = v;
@@ -843,7 +839,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "conv_f32") pddl::g_conv_f32_variant = v;
     else if (which == "c64_grid") pddl::g_c64_grid = v;
     else if (which == "c64w_grid") pddl::g_c64w_grid = v;
-    else if (which == "stem_pool") pddl::g_stem_pool_variant = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;
     else if (which == "bn_apply_blocks") pddl::g_bn_apply_blocks = v;
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;

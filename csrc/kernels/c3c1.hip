@@ -6,9 +6,7 @@
 // stride-2 projection block and keeps the separate launches).
 //
 // A workgroup owns 64 rows (pixels), 4 waves:
-//   phase 1  out[64][256] = A1[64][K1] . W3^T  -- wave w: output channels [64 w, 64 w + 64), K1 = 64
-//            (y2) or 128 (DUAL: y2 | block input, the fused projection of block b = 1: its shortcut
-//            conv rides along K and both BN shifts are in `shift3`, no residual)
+//   phase 1  out[64][256] = y2[64][64] . W3^T  -- wave w: output channels [64 w, 64 w + 64)
 //   epilogue relu(acc * scale3 + shift3 (+ res)) -> bf16 into an LDS tile [64][256], then row stores
 //            of that tile (+ the ReLU bits of the block output)
 //   phase 2  y1[64][64] = out[64][256] . W1^T -- wave w: channels [16 w, 16 w + 16), K = 256 from LDS
@@ -16,11 +14,13 @@
 // Both MFMA phases run with the weights as the A operand (fragments loaded once per workgroup from
 // L2 into registers), so a lane's accumulator holds 4 consecutive channels of one pixel and the
 // epilogues write 8-byte chunks; the residual tile is DMA'd into the output tile's LDS at the start
-// and each lane reads its 8 bytes of it where it then writes its 8 bytes of output.  LDS: 8 KiB A tile (DUAL 16) + 32 KiB
-// output tile.  Same arithmetic as the unfused igemm epilogues (fp32 scale / shift / residual, one
+// and each lane reads its 8 bytes of it where it then writes its 8 bytes of output.  LDS: 8 KiB A
+// tile + 32 KiB output tile.  Same arithmetic as the unfused igemm epilogues (fp32 scale / shift / residual, one
 // bf16 rounding), so the outputs match the two-launch form bitwise up to MFMA operand order.
 // Reference: the conv*_block*_3_conv -> add -> relu -> conv*_block*_1_conv chain of the Keras
-// ResNet50 (imagenet-resnet50.py:56).
+// ResNet50 (imagenet-resnet50.py:56).  (A dual-source form for the projection
+// boundary conv2_block1 -> 2, K = 128 with the shortcut conv, measured no gain -- 2.77 ms fused vs
+// 1.87 + 0.90 ms separate at b2560, profiles/r4_c3c1.txt -- and was removed.)
 #include "common.h"
 #include "kernels.h"
 
@@ -34,19 +34,18 @@ constexpr int CC_BM = 64;
 __device__ __forceinline__ int cc_sw(int row) { return (row >> 1) & 7; }
 }  // namespace
 
-template <bool DUAL>
 __global__ void __launch_bounds__(256, 2) c3c1_kernel(C3C1Params p) {
-  constexpr int K1 = DUAL ? 128 : 64;
-  constexpr int A_BYTES = CC_BM * 128;                 // one 64-channel source tile
-  __shared__ __attribute__((aligned(16))) char smem[(DUAL ? 2 : 1) * A_BYTES + CC_BM * 512];
-  char* at = smem;                                     // A1 tile(s); later the y1 staging tile
-  char* ot = smem + (DUAL ? 2 : 1) * A_BYTES;          // block-b output tile [64][512 B]
+  constexpr int K1 = 64;
+  constexpr int A_BYTES = CC_BM * 128;                 // the 64-channel source tile
+  __shared__ __attribute__((aligned(16))) char smem[A_BYTES + CC_BM * 512];
+  char* at = smem;                                     // A1 tile; later the y1 staging tile
+  char* ot = smem + A_BYTES;                           // block-b output tile [64][512 B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, kq = lane >> 4;
   const int m0 = blockIdx.x * CC_BM;
 
-  // ---- A tile(s) by LDS-DMA: 8 pieces of 8 rows per source, 2 (DUAL 4) per wave
+  // ---- A tile by LDS-DMA: 8 pieces of 8 rows, 2 per wave
   {
     const __amdgpu_buffer_rsrc_t ra = make_rsrc_at(p.a, (long)m0 * 64, (long)p.M * 64);
 #pragma unroll
@@ -55,21 +54,11 @@ __global__ void __launch_bounds__(256, 2) c3c1_kernel(C3C1Params p) {
       const int ch = (lane & 7) ^ cc_sw(row);
       buf_lds16(ra, LDS_PTR(at + pc * 1024), m0 + row < p.M ? (uint32_t)((row * 64 + ch * 8) * 2) : OOB_OFF, 0);
     }
-    if (DUAL) {
-      const __amdgpu_buffer_rsrc_t rb = make_rsrc_at(p.a2, (long)m0 * 64, (long)p.M * 64);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int pc = wave * 2 + q, row = pc * 8 + (lane >> 3);
-        const int ch = (lane & 7) ^ cc_sw(row);
-        buf_lds16(rb, LDS_PTR(at + A_BYTES + pc * 1024), m0 + row < p.M ? (uint32_t)((row * 64 + ch * 8) * 2) : OOB_OFF,
-                  0);
-      }
-    }
   }
   // ---- residual tile by LDS-DMA straight into the output tile (same swizzled image): the epilogue
   //      reads each lane's 8 bytes of residual where it then writes its 8 bytes of output.
   //      32 pieces of 2 rows x 512 B, 8 per wave.
-  const bool has_res = !DUAL && p.res != nullptr;
+  const bool has_res = p.res != nullptr;
   if (has_res) {
     const __amdgpu_buffer_rsrc_t rr = make_rsrc_at(p.res, (long)m0 * 256, (long)p.M * 256);
 #pragma unroll
@@ -200,8 +189,7 @@ const char* c3c1_launch(const C3C1Params& p, hipStream_t s) {
   if (!p.a || !p.w3 || !p.scale3 || !p.shift3 || !p.out || !p.w1 || !p.scale1 || !p.shift1 || !p.y1)
     return "c3c1: missing operand";
   const dim3 grid((unsigned)((p.M + CC_BM - 1) / CC_BM));
-  if (p.a2) hipLaunchKernelGGL(c3c1_kernel<true>, grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(c3c1_kernel<false>, grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL(c3c1_kernel, grid, dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

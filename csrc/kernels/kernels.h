@@ -57,7 +57,7 @@ long igemm_splitk_floats(int M, int Nn, int K);     // split-K workspace a probl
 extern int g_igemm8, g_igemm8_min_tiles, g_igemm8_min_n, g_igemm_ns1_kt, g_wgrad8, g_wgrad1;
 int num_cus();   // compute units of the current device (cached)
 extern int g_igemm_splitk, g_wgrad8_min_rows, g_igemm_pk, g_igemm_pk_all;   // split-K: 0 off, 1 heuristic (default), >= 2 forced slices (where legal)
-extern int g_stem_variant, g_igemm_n64, g_igemm_variant, g_igemm_deep, g_igemm_pf, g_wgrad_variant, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
+extern int g_stem_variant, g_igemm_n64, g_igemm_variant, g_igemm_deep, g_igemm_pf, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
 
 struct WgradParams {
   const uint16_t* x; int N, H, W, C;   // conv input, NHWC (or [M][ldx] rows for 1x1/s1)
@@ -199,7 +199,7 @@ struct C64Params {
 };
 const char* conv3x3c64_launch(const C64Params& p, int mode, hipStream_t s);
 int conv3x3c64_partial_rows(int M);
-extern int g_c64_grid, g_c64w_grid, g_stem_pool_variant;
+extern int g_c64_grid, g_c64w_grid;
 struct C64WgradParams {
   const uint16_t* x;          // [N][H][W][64] conv input
   const uint16_t* g;          // [N][H][W][64] output gradient
@@ -212,8 +212,7 @@ const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s);
 // projection with a second A source) and block b + 1's conv1, one launch.
 struct C3C1Params {
   const uint16_t* a;           // [M][64] conv3 input (block b's conv2 output)
-  const uint16_t* a2;          // optional [M][64] second K source (fused projection: block input)
-  const uint16_t* w3;          // [256][64 or 128] conv3 (+ shortcut) weights, BN scale folded or not
+  const uint16_t* w3;          // [256][64] conv3 weights
   const float* scale3; const float* shift3;   // [256]
   const uint16_t* res;         // optional [M][256] residual (plain blocks)
   uint16_t* out;               // [M][256] block-b output

@@ -31,7 +31,7 @@ __device__ __forceinline__ uint32_t swz_chunk(int chunk, int x) { return (uint32
 
 }  // namespace
 
-template <bool BITS, int V>
+template <bool BITS>
 __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int SLOT = p.Ws * 32;
@@ -46,11 +46,11 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
   const int lr = lane & 15, lg = lane >> 4;
 
   // ---- weights as A fragments: co = 16 nt + lr, k = 32 t + 8 lg + j (held for the whole launch)
-  // V = 1: wave w owns output channels [32 (w & 1), + 32) of every tile and tiles w >> 1, +2, ...:
-  // 7 tiles per wave per pool row (V = 0: whole tiles, 4 / 4 / 3 / 3 waves) with half the weight
-  // registers
-  constexpr int NTW = V == 1 ? 2 : 4;
-  const int nt0 = V == 1 ? 2 * (wave & 1) : 0;
+  // wave w owns output channels [32 (w & 1), + 32) of every tile and tiles w >> 1, +2, ...: 7 tiles
+  // per wave per pool row with half the weight registers (the round-4 first form, whole tiles per
+  // wave, ran 2.14 ms against 1.88 ms at b2560: profiles/r4_fused_stem_ab.txt)
+  constexpr int NTW = 2;
+  const int nt0 = 2 * (wave & 1);
   v8bf wa[NTW][8];
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt)
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
     const int ylo = (pr == P0 && pr > 0) ? 2 * pr - 1 : 2 * pr;
     const int nrows = 2 * pr + 2 - ylo;
     const int ntiles = nrows * nct;
-    for (int ti = V == 1 ? (wave >> 1) : wave; ti < ntiles; ti += V == 1 ? 2 : SP_THREADS / 64) {
+    for (int ti = wave >> 1; ti < ntiles; ti += 2) {
       const int y = ylo + ti / nct, x0 = (ti % nct) * 16;
       v4f acc[NTW];
 #pragma unroll
@@ -136,80 +136,43 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
     __syncthreads();
     // ---- pool row pr: window rows 2pr-1 .. 2pr+1, columns 2q-1 .. 2q+1; item = (q, 8-channel group)
     const long orow = ((long)b * p.H2 + pr) * p.W2;
-    if (V == 1) {
-      // branch-free: the conv rows are ReLU outputs (>= 0), so bf16 bit patterns (sign cleared:
-      // a -0 counts as 0) order like unsigned integers; key = bits << 16 | (15 - tap) and one
-      // unsigned max per tap per channel keeps the largest value and, among equal values, the
-      // first tap in scan order -- the same winner as the float compare.  Padding taps are 0.
-      for (int it = tid; it < p.W2 * 8; it += SP_THREADS) {
-        const int q = it >> 3, cg = it & 7;
-        uint32_t key[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) key[e] = 15u;   // (tap 0 of a zero: the padding corner)
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const int y = 2 * pr - 1 + r;
-#pragma unroll
-          for (int sx = 0; sx < 3; ++sx) {
-            const int x = 2 * q - 1 + sx;
-            const uint32_t c = 15u - (uint32_t)(r * 3 + sx);
-            const bool ok = y >= 0 && x >= 0;
-            const uint4 u = *reinterpret_cast<const uint4*>(cbuf + ((ok ? y : 0) % 3) * CROW + (ok ? x : 0) * 128 +
-                                                            swz_chunk(2 * cg, ok ? x : 0) * 8);
-            const uint32_t d[4] = {ok ? u.x : 0u, ok ? u.y : 0u, ok ? u.z : 0u, ok ? u.w : 0u};
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              key[2 * h] = max(key[2 * h], ((d[h] << 16) & 0x7fff0000u) | c);
-              key[2 * h + 1] = max(key[2 * h + 1], (d[h] & 0x7fff0000u) | c);
-            }
-          }
-        }
-        const long o = (orow + q) * 64 + cg * 8;
-        const uint4 yv = make_uint4((key[0] >> 16) | (key[1] & 0xffff0000u), (key[2] >> 16) | (key[3] & 0xffff0000u),
-                                    (key[4] >> 16) | (key[5] & 0xffff0000u), (key[6] >> 16) | (key[7] & 0xffff0000u));
-        *reinterpret_cast<uint4*>(p.pool + o) = yv;
-        if (BITS) p.bits[o >> 3] = (uint8_t)pos_bits8(yv);
-        uint32_t cd[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) cd[e] = 15u - (key[e] & 15u);
-        *reinterpret_cast<uint2*>(p.idx + o) =
-            make_uint2(cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24), cd[4] | (cd[5] << 8) | (cd[6] << 16) | (cd[7] << 24));
-      }
-    } else {
+    // branch-free: the conv rows are ReLU outputs (>= 0), so bf16 bit patterns (sign cleared:
+    // a -0 counts as 0) order like unsigned integers; key = bits << 16 | (15 - tap) and one
+    // unsigned max per tap per channel keeps the largest value and, among equal values, the
+    // first tap in scan order -- the same winner as the float compare.  Padding taps are 0.
     for (int it = tid; it < p.W2 * 8; it += SP_THREADS) {
-        const int q = it >> 3, cg = it & 7;
-        float best[8];
-        uint32_t code[8];
+      const int q = it >> 3, cg = it & 7;
+      uint32_t key[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; code[e] = 0; }
+      for (int e = 0; e < 8; ++e) key[e] = 15u;   // (tap 0 of a zero: the padding corner)
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const int y = 2 * pr - 1 + r;
+      for (int r = 0; r < 3; ++r) {
+        const int y = 2 * pr - 1 + r;
 #pragma unroll
-          for (int s = 0; s < 3; ++s) {
-            const int x = 2 * q - 1 + s;
-            float v[8];
-            if (y >= 0 && x >= 0) {
-              const uint4 u = *reinterpret_cast<const uint4*>(cbuf + (y % 3) * CROW + x * 128 +
-                                                              swz_chunk(2 * cg, x) * 8);
-              unpack8(u, v);
-            } else {
+        for (int sx = 0; sx < 3; ++sx) {
+          const int x = 2 * q - 1 + sx;
+          const uint32_t c = 15u - (uint32_t)(r * 3 + sx);
+          const bool ok = y >= 0 && x >= 0;
+          const uint4 u = *reinterpret_cast<const uint4*>(cbuf + ((ok ? y : 0) % 3) * CROW + (ok ? x : 0) * 128 +
+                                                          swz_chunk(2 * cg, ok ? x : 0) * 8);
+          const uint32_t d[4] = {ok ? u.x : 0u, ok ? u.y : 0u, ok ? u.z : 0u, ok ? u.w : 0u};
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] = 0.f;
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (v[e] > best[e]) { best[e] = v[e]; code[e] = (uint32_t)(r * 3 + s); }
+          for (int h = 0; h < 4; ++h) {
+            key[2 * h] = max(key[2 * h], ((d[h] << 16) & 0x7fff0000u) | c);
+            key[2 * h + 1] = max(key[2 * h + 1], (d[h] & 0x7fff0000u) | c);
           }
         }
-        const long o = (orow + q) * 64 + cg * 8;
-        const uint4 yv = pack8(best);
-        *reinterpret_cast<uint4*>(p.pool + o) = yv;
-        if (BITS) p.bits[o >> 3] = (uint8_t)pos_bits8(yv);
-        *reinterpret_cast<uint2*>(p.idx + o) =
-            make_uint2(code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24),
-                       code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24));
       }
+      const long o = (orow + q) * 64 + cg * 8;
+      const uint4 yv = make_uint4((key[0] >> 16) | (key[1] & 0xffff0000u), (key[2] >> 16) | (key[3] & 0xffff0000u),
+                                  (key[4] >> 16) | (key[5] & 0xffff0000u), (key[6] >> 16) | (key[7] & 0xffff0000u));
+      *reinterpret_cast<uint4*>(p.pool + o) = yv;
+      if (BITS) p.bits[o >> 3] = (uint8_t)pos_bits8(yv);
+      uint32_t cd[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cd[e] = 15u - (key[e] & 15u);
+      *reinterpret_cast<uint2*>(p.idx + o) =
+          make_uint2(cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24), cd[4] | (cd[5] << 8) | (cd[6] << 16) | (cd[7] << 24));
     }
     __syncthreads();   // the next rows' epilogue overwrites conv rows 2pr-1 / 2pr
   }
@@ -440,7 +403,6 @@ const char* stem_pool_bwd_launch(StemPoolBwdParams p, hipStream_t s) {
 
 int stem_pool_lds_bytes(int Ws, int W1) { return 8 * Ws * 32 + 3 * W1 * 128 + 512; }
 
-int g_stem_pool_variant = 1;   // 1: channel-half waves + branch-free key max pool; 0: round-4 first form
 const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s) {
   if (p.H1 != p.Hs - 3 || p.W1 != p.Ws - 3) return "stem_pool: conv1 output must be the s2d input minus 3";
   if (p.H1 % 2 || p.W1 % 2) return "stem_pool: even conv1 output (even crop) expected";
@@ -458,24 +420,15 @@ const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s) {
   p.nblk = (p.H2 + p.PB - 1) / p.PB;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<true, 0>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<false, 0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<true, 1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<false, 1>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     attr = true;
   }
   const dim3 grid((unsigned)((long)p.B * p.nblk));
-  if (g_stem_pool_variant == 1) {
-    if (p.bits) hipLaunchKernelGGL((stem_pool_fwd_kernel<true, 1>), grid, dim3(SP_THREADS), lds, s, p);
-    else hipLaunchKernelGGL((stem_pool_fwd_kernel<false, 1>), grid, dim3(SP_THREADS), lds, s, p);
-  } else {
-    if (p.bits) hipLaunchKernelGGL((stem_pool_fwd_kernel<true, 0>), grid, dim3(SP_THREADS), lds, s, p);
-    else hipLaunchKernelGGL((stem_pool_fwd_kernel<false, 0>), grid, dim3(SP_THREADS), lds, s, p);
-  }
+  if (p.bits) hipLaunchKernelGGL((stem_pool_fwd_kernel<true>), grid, dim3(SP_THREADS), lds, s, p);
+  else hipLaunchKernelGGL((stem_pool_fwd_kernel<false>), grid, dim3(SP_THREADS), lds, s, p);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

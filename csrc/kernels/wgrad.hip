@@ -548,7 +548,6 @@ static const int2* rowinfo_for(const WgradParams& p, hipStream_t stream, const c
   return buf;
 }
 
-int g_wgrad_variant = 0;   // A/B knob (unused: one pipeline depth remains)
 int g_wgrad1 = 1;          // LDS stages of the 128/64-wide wgrad kernel: 1 = single stage except the
                            // long-reduction direct layers (1x1 / stem window, M >= 2M rows: stage-2
                            // 1x1s -4..-12 %, stem -8 %, 3x3 and stage 3+ +8..+13 % with 2 stages;

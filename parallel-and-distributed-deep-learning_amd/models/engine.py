@@ -432,14 +432,12 @@ class HipEngine:
         return self.c64 and f == 64 and W + 2 <= 64 and M >= self.c64_min_m and bits
 
     def _c3c1_ok(self, b, nb) -> bool:
-        """Fuse block b's conv3 with block nb's conv1 (c3c1.hip): 64-channel stride-1 boundaries
-        (stage 2: conv2_block1 -> 2 with the fused projection, 2 -> 3), not into a projection block."""
-        if not self.c3c1 or nb is None or b.filters != 64 or nb.filters != 64 or nb.proj or nb.stride != 1:
-            return False
-        if b.proj:   # the fused-projection form (K = 128, two A tiles) measured no gain: 2.77 ms fused vs
-            # 1.87 + 0.90 ms separate at b2560 (profiles/r4_c3c1.txt); opt in with PDDL_C3C1=2
-            return self.c3c1 == 2 and self.fuse_proj and b.stride == 1 and b.cin == 64
-        return True
+        """Fuse block b's conv3 with block nb's conv1 (c3c1.hip): 64-channel stride-1 boundaries out of
+        a plain block (stage 2: conv2_block2 -> 3), not into a projection block.  (Out of the fused
+        projection block conv2_block1, K = 128, it measured no gain: 2.77 ms fused vs 1.87 + 0.90 ms
+        separate at b2560, profiles/r4_c3c1.txt.)"""
+        return (bool(self.c3c1) and nb is not None and b.filters == 64 and nb.filters == 64 and not b.proj
+                and not nb.proj and nb.stride == 1)
 
     def _c2_wgrad(self, W, y1, g2, c2n, f, B, Ho, g2_n):
         """Weight gradient of a bottleneck's stride-1 3x3 conv (on the side stream when two-stream)."""
@@ -536,12 +534,8 @@ class HipEngine:
                 an = self.acts[nb.name]
                 btn = {k: v[:B] for k, v in self.bits[nb.name].items()} if use_bits else {}
                 c1x = nb.convs["1"].name
-                if b.proj:
-                    fz = "fuse:" + b.name
-                    w3, k3, a2, rs = self._wf(fz, 4 * f, f + cin), self.ch[fz], x, None
-                else:
-                    w3, k3, a2, rs = self._wf(c3, 4 * f, f), self.ch[c3], None, res
-                N.c3c1(y2, a2, w3, self.scale[k3:], self.shift[k3:], rs, out, bt.get("out"),
+                k3 = self.ch[c3]
+                N.c3c1(y2, self._wf(c3, 4 * f, f), self.scale[k3:], self.shift[k3:], res, out, bt.get("out"),
                        self._wf(c1x, nb.filters, nb.cin), self.scale[self.ch[c1x]:], self.shift[self.ch[c1x]:],
                        an["y1"][:B], btn.get("y1"))
                 c1_done = True

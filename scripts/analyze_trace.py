@@ -33,9 +33,8 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
     blocks = list(L.blocks)
 
     def c3c1(b, nb):   # engine._c3c1_ok
-        if not c3c1_on or nb is None or b.filters != 64 or nb.filters != 64 or nb.proj or nb.stride != 1:
-            return False
-        return not b.proj or (c3c1_on == 2 and fuse and b.stride == 1 and b.cin == 64)
+        return bool(c3c1_on) and nb is not None and b.filters == 64 and nb.filters == 64 and not b.proj \
+            and not nb.proj and nb.stride == 1
     c1_done = False
     for bi, b in enumerate(blocks):
         f, cin = b.filters, b.cin

@@ -326,7 +326,7 @@ def test_c3c1_boundary_fusion_in_engine(monkeypatch):
     L = ParamLayout()
     B = 8
     res = []
-    for on in ("2", "0"):   # (2: also the fused-projection boundary conv2_block1 -> 2)
+    for on in ("1", "0"):
         monkeypatch.setenv("PDDL_C3C1", on)
         he = HipEngine(L, B, crop=224, image_size=224)
         assert he.c3c1 == int(on)

@@ -1181,39 +1181,36 @@ def test_conv3x3c64_wgrad_matches_reference(n, h, grid):
     assert rel(dw - 0.5, dw2) < 1e-3
 
 
-@pytest.mark.parametrize("dual", [False, True])
+@pytest.mark.parametrize("with_res", [True, False])
 @pytest.mark.parametrize("m", [4096, 3 * 56 * 56 + 17])
-def test_c3c1_boundary_fusion_matches_two_launches(dual, m):
-    """conv3 of a 64-channel block (+ residual, or the fused projection's second K source) and the
-    next block's conv1 in one launch (c3c1.hip) against the two igemm launches: block output, its
-    ReLU bits, the next conv1 output and its bits; rows not a multiple of the 64-row tile."""
-    torch.manual_seed(50 + dual)
+def test_c3c1_boundary_fusion_matches_two_launches(with_res, m):
+    """conv3 of a 64-channel block (+ residual) and the next block's conv1 in one launch (c3c1.hip)
+    against the two igemm launches: block output, its ReLU bits, the next conv1 output and its
+    bits; rows not a multiple of the 64-row tile."""
+    torch.manual_seed(50 + with_res)
     a = torch.relu(rnd(m, 64)).to(torch.bfloat16)
-    a2 = torch.relu(rnd(m, 64)).to(torch.bfloat16) if dual else None
-    k1 = 128 if dual else 64
-    w3 = rnd(256, k1, scale=0.05)
+    w3 = rnd(256, 64, scale=0.05)
     sc3, sh3 = torch.rand(256, device=dev) + 0.5, torch.randn(256, device=dev) * 0.1
-    res = None if dual else torch.relu(rnd(m, 256)).to(torch.bfloat16)
+    res = torch.relu(rnd(m, 256)).to(torch.bfloat16) if with_res else None
     w1 = rnd(64, 256, scale=0.05)
     sc1, sh1 = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.1
     out = torch.empty(m, 256, dtype=torch.bfloat16, device=dev)
     y1 = torch.empty(m, 64, dtype=torch.bfloat16, device=dev)
     b3 = torch.zeros(m, 32, dtype=torch.uint8, device=dev)
     b1 = torch.zeros(m, 8, dtype=torch.uint8, device=dev)
-    N().c3c1(a, a2, w3, sc3, sh3, res, out, b3, w1, sc1, sh1, y1, b1)
+    N().c3c1(a, w3, sc3, sh3, res, out, b3, w1, sc1, sh1, y1, b1)
     # two launches: igemm forward with the 1x1 geometry (M rows as a 1 x M image)
     out_r = torch.empty_like(out)
     y1_r = torch.empty_like(y1)
     b3_r, b1_r = torch.zeros_like(b3), torch.zeros_like(b1)
     av = a.view(1, 1, m, 64)
-    N().igemm(av, a2.view(1, 1, m, 64) if dual else None, 1, m, 1, 1, 1, 0, 1, m, w3, 0, sc3, sh3,
+    N().igemm(av, None, 1, m, 1, 1, 1, 0, 1, m, w3, 0, sc3, sh3,
               res.view(1, 1, m, 256) if res is not None else None, None, None, out_r.view(1, 1, m, 256), 1, None, 0,
               0, 0, 0, 0, None, b3_r.view(1, 1, m, 32))
     N().igemm(out_r.view(1, 1, m, 256), None, 1, m, 1, 1, 1, 0, 1, m, w1, 0, sc1, sh1, None, None, None,
               y1_r.view(1, 1, m, 64), 1, None, 0, 0, 0, 0, 0, None, b1_r.view(1, 1, m, 8))
     torch.cuda.synchronize()
-    ref = torch.relu(a.float() @ w3[:, :64].float().t() * sc3 + sh3 +
-                     (a2.float() @ w3[:, 64:].float().t() * sc3 if dual else res.float()))
+    ref = torch.relu(a.float() @ w3.float().t() * sc3 + sh3 + (res.float() if with_res else 0.0))
     assert rel(out, ref) < 1e-2
     assert rel(out, out_r) < 2e-3
     assert (b3 != b3_r).float().mean().item() < 1e-3
