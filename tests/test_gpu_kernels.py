@@ -351,6 +351,42 @@ def test_bitmask_forward_and_dgrad():
     assert torch.equal(pb, pack_bits(yp))
 
 
+@pytest.mark.parametrize("ring", [False, True])
+@pytest.mark.parametrize("aligned", [True, False])
+def test_bits_out_packed_and_unaligned(ring, aligned):
+    """The forward epilogues' ReLU-bit side output (one byte per lane) equals the bf16 output's
+    signs and writes nothing outside the mask, at an aligned and an odd byte offset, on the
+    per-tile kernel (with an M tail and a split second output) and on the ring kernel (residual
+    forward, K = 128).  (A packed 4-byte store of four lanes' bytes measured slower and was
+    removed, profiles/r4_bits_pkdual.txt.)"""
+    torch.manual_seed(19)
+    n, h = 3, 37                                   # M = 4107 rows: a partial last row tile
+    K, Nn = (128, 256) if ring else (64, 320)
+    x = rnd(n, h, h, K)
+    w = rnd(Nn, K, scale=0.1)
+    sc, sh = torch.rand(Nn, device=dev) + 0.5, torch.randn(Nn, device=dev)
+    f = 64 if not ring else Nn                     # (per-tile: y1 = first 64 columns, the rest to out2)
+    nb = n * h * h * f // 8
+    raw = torch.full((nb + 4,), 0x5A, dtype=torch.uint8, device=dev)
+    bits = (raw[:nb] if aligned else raw[1:nb + 1]).view(n, h, h, f // 8)
+    y = torch.empty(n, h, h, f, dtype=torch.bfloat16, device=dev)
+    if ring:
+        res = rnd(n, h, h, Nn)
+        N().igemm(x, None, h, h, 1, 1, 1, 0, h, h, w, 0, sc, sh, res, None, None, y, 1, None, 0, 0, 0, 0, 0, None,
+                  bits)
+    else:
+        y2 = torch.empty(n, h, h, Nn - f, dtype=torch.bfloat16, device=dev)
+        N().igemm(x, None, h, h, 1, 1, 1, 0, h, h, w, 0, sc, sh, None, None, None, y, 1, y2, 0, f, 0, 0, 0, None,
+                  bits)
+    torch.cuda.synchronize()
+    assert torch.equal(bits, pack_bits(y))
+    # nothing outside the mask was written
+    if aligned:
+        assert torch.equal(raw[nb:], torch.full((4,), 0x5A, dtype=torch.uint8, device=dev))
+    else:
+        assert raw[0].item() == 0x5A and torch.equal(raw[nb + 1:], torch.full((3,), 0x5A, dtype=torch.uint8, device=dev))
+
+
 WG_CASES = [
     (2, 14, 64, 256, 1, 1, 0),
     (3, 9, 64, 64, 3, 1, 1),
