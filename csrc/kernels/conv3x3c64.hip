@@ -280,13 +280,17 @@ const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
     (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
+    (void)hipGetLastError();   // (a refused attribute call must not read as the launch's error)
     attr = true;
   }
   const int T = p.N * ((p.H + 3) / 4);
   int G = num_cus();
   if (g_c64_grid > 0 && g_c64_grid < G) G = g_c64_grid;
   if (G > T) G = T;
-  if (p.colsum)   // (rows of workgroups the grid leaves out stay zero for the reduction)
+  // (rows of workgroups the grid leaves out stay zero for the reduction; no zero-byte memset: a
+  // HIP graph capture rejects it as an invalid argument -- the Mirrored entry script's first,
+  // captured step with the full 256-workgroup grid)
+  if (p.colsum && G < num_cus())
     (void)hipMemsetAsync(p.colsum + (long)G * 4 * 64, 0, (size_t)(num_cus() - G) * 4 * 64 * sizeof(float), s);
   if (mode == C64_FWD) hipLaunchKernelGGL(conv3x3c64_row8_kernel<C64_FWD>, dim3(G), dim3(512), R8_LDS, s, p);
   else hipLaunchKernelGGL(conv3x3c64_row8_kernel<C64_DGRAD>, dim3(G), dim3(512), R8_LDS, s, p);
@@ -467,6 +471,7 @@ const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CW_LDS);
+    (void)hipGetLastError();
     attr = true;
   }
   hipLaunchKernelGGL(conv3x3c64_wgrad_kernel, dim3(G), dim3(512), CW_LDS, s, p);

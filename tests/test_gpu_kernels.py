@@ -1195,6 +1195,43 @@ def _c64_case(mode, n, h, grid):
     assert rel(out, ref_ig) < 2e-3
 
 
+def test_conv3x3c64_kernels_capture_in_a_hip_graph():
+    """The 64-channel 3x3 kernels inside a HIP-graph capture (the Mirrored strategy captures its
+    first step): the data gradient with column sums on the full 256-workgroup grid once added a
+    zero-byte memset node, which the capture rejects as an invalid argument.  Forward, data
+    gradient and weight gradient are captured, replayed, and match eager runs bitwise."""
+    torch.manual_seed(44)
+    n, h = 24, 56                                  # N * 14 row tiles >= #CUs: the full grid
+    x = rnd(n, h, h, 64)
+    w = rnd(64, 576, scale=0.05)
+    sc, sh = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.1
+    mbits = pack_bits(rnd(n, h, h, 64))
+    rows = N().conv3x3c64_partial_rows(n * h * h)
+    outs = [dict(y=torch.empty_like(x), bits=torch.zeros(n, h, h, 8, dtype=torch.uint8, device=dev),
+                 g=torch.empty_like(x), part=torch.zeros(rows * 64, device=dev),
+                 dw=torch.zeros(64, 576, device=dev)) for _ in range(2)]
+
+    def run(o):
+        N().conv3x3c64(x, w, 0, o["y"], scale=sc, shift=sh, bits=o["bits"])
+        N().conv3x3c64(x, w, 1, o["g"], bits=mbits, colsum=o["part"])
+        o["dw"].zero_()
+        N().conv3x3c64_wgrad(x, x, o["dw"])
+
+    run(outs[0])
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            run(outs[1])
+    g.replay()
+    torch.cuda.synchronize()
+    for k in ("y", "bits", "g", "part"):
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    assert rel(outs[1]["dw"], outs[0]["dw"]) < 1e-5   # (fp32 atomics: order may differ)
+
+
 @pytest.mark.parametrize("n,h,grid", [(24, 56, 0), (5, 56, 3), (7, 13, 2), (3, 61, 0)])
 def test_conv3x3c64_wgrad_matches_reference(n, h, grid):
     """Row-tile weight gradient of the 64 -> 64 3x3 conv (conv3x3c64.hip, 8 waves) against the fp32 PyTorch weight gradient of the same bf16
