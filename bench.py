@@ -97,6 +97,9 @@ def parse(argv=None):
     ap.add_argument("--comm-proxy", default=None, metavar="SPEC",
                     help="1 GPU: run a paced, CU-holding stand-in for each bucket's RCCL all-reduce on a side "
                          "stream (e.g. 'world=8,busbw=350,nch=32'), to measure the backward under comm contention")
+    ap.add_argument("--baseline-ips", type=float, default=None, metavar="IPS",
+                    help="1-GPU images/sec of the same config (the reference publishes none): fills vs_baseline "
+                         "(value / IPS) and scaling_efficiency (value / (n_gpus * IPS))")
     ap.add_argument("--timeout", type=float, default=None,
                     help="job deadline in seconds (default: derived from steps + warmup); on expiry every "
                          "rank dumps its stacks and the job exits non-zero")
@@ -374,6 +377,7 @@ def run(args):
             "per_gpu_images_per_sec": round(ips / args.gpus, 2),
             "final_loss": round(loss, 4),
         }
+        add_scaling(out, args)
         if not cpu:   # HBM footprint of the step (torch caching allocator, device of rank 0)
             out["peak_mem_gb"] = round(torch.cuda.max_memory_allocated(local_devs[0]) / 1e9, 2)
         out["comm"] = comm
@@ -392,6 +396,15 @@ def run(args):
         dist.destroy_process_group()
     faulthandler.cancel_dump_traceback_later()
     return 0
+
+
+def add_scaling(out, args):
+    """--baseline-ips: vs_baseline and scaling_efficiency against a measured 1-GPU rate."""
+    from pddl.utils.scaling import efficiency
+    if args.baseline_ips:
+        out["vs_baseline"] = round(out["value"] / args.baseline_ips, 4)
+        out["scaling_efficiency"] = round(efficiency(out["value"], args.gpus, args.baseline_ips), 4)
+        out["baseline_ips"] = args.baseline_ips
 
 
 def comm_report(st, world, rank, local_devs, cpu):
@@ -482,7 +495,7 @@ def run_ps(args):
         fail("parameter-server job returned no timed epoch")
     ep = hist[0][1]
     ips = ep["images_per_sec"]
-    print(json.dumps({
+    out = {
         "metric": METRIC, "value": round(ips, 2), "unit": "images/sec", "n_gpus": args.gpus, "steps": args.steps,
         "warmup": args.steps, "ms_per_step": round(args.batch * n_w / ips * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if args.device == "cpu" else "bf16",
@@ -498,7 +511,9 @@ def run_ps(args):
         "per_gpu_images_per_sec": round(ips / n_w, 2), "steps_timed_epoch": ep.get("steps"),
         "job_wall_s": round(wall, 1), **({"rehearsal": True} if rehearsing() else {}),
         **({"ps_service": svc} if svc else {}),
-    }), flush=True)
+    }
+    add_scaling(out, args)
+    print(json.dumps(out), flush=True)
     return 0
 
 

@@ -708,6 +708,7 @@ void register_rccl(pybind11::module& m);
 void register_fusion(pybind11::module& m);
 void register_loader(pybind11::module& m);
 void register_ps(pybind11::module& m);
+void register_crash_trace(pybind11::module& m);
 
 // Kernel launches release the GIL: replica threads (Mirrored / multi-GPU workers) then enqueue
 // their launch streams concurrently instead of serializing on the interpreter lock.
@@ -719,6 +720,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_fusion(m);
   register_loader(m);
   register_ps(m);
+  register_crash_trace(m);
   // rows: host int64 [n, 3] of (flat offset, packed offset, length), bounds-checked here
   m.def("range_copy", [](Tensor src, Tensor dst, Tensor rows, bool scatter) {
     PCHECK(!rows.is_cuda() && rows.scalar_type() == torch::kInt64 && rows.dim() == 2 && rows.size(1) == 3,

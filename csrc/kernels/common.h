@@ -4,6 +4,7 @@
 // bit pattern); every kernel computes in fp32 and rounds once on store.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 
 namespace pddl {
@@ -109,6 +110,16 @@ __device__ __forceinline__ float warp_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// True the first time it is called on the current device for this `done` mask (one bit per
+// device): per-device one-time launch setup (hipFuncSetAttribute is per device, so a
+// process-wide flag would leave devices >= 1 unconfigured).
+inline bool first_on_device(std::atomic<unsigned long long>& done) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 63;
+  const unsigned long long bit = 1ull << dev;
+  return !(done.fetch_or(bit) & bit);
 }
 
 }  // namespace pddl

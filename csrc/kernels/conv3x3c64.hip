@@ -276,12 +276,11 @@ const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
   if (mode == C64_DGRAD && !p.bits_mask) return "conv3x3c64: data gradient needs the ReLU bits";
   p.mg_hw = fdiv_magic(p.H * p.W);
   p.mg_w = fdiv_magic(p.W);
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<unsigned long long> attr{0};
+  if (first_on_device(attr)) {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
     (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
     (void)hipGetLastError();   // (a refused attribute call must not read as the launch's error)
-    attr = true;
   }
   const int T = p.N * ((p.H + 3) / 4);
   int G = num_cus();
@@ -468,11 +467,10 @@ const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s) {
   int G = num_cus();
   if (g_c64w_grid > 0 && g_c64w_grid < G) G = g_c64w_grid;
   if (G > T) G = T;
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<unsigned long long> attr{0};
+  if (first_on_device(attr)) {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CW_LDS);
     (void)hipGetLastError();
-    attr = true;
   }
   hipLaunchKernelGGL(conv3x3c64_wgrad_kernel, dim3(G), dim3(512), CW_LDS, s, p);
   hipError_t e = hipGetLastError();

@@ -390,11 +390,10 @@ const char* stem_pool_bwd_launch(StemPoolBwdParams p, hipStream_t s) {
   if (lds > 80 * 1024) return "stem_pool_bwd: LDS per workgroup above the two-per-CU budget";
   p.PB = stem_pool_rows(p.B, p.H2, p.PB);
   p.nblk = (p.H2 + p.PB - 1) / p.PB;
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<unsigned long long> attr{0};
+  if (first_on_device(attr)) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_bwd_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    attr = true;
   }
   hipLaunchKernelGGL(stem_pool_bwd_kernel, dim3((unsigned)((long)p.B * p.nblk)), dim3(SP_THREADS), lds, s, p);
   hipError_t e = hipGetLastError();
@@ -418,13 +417,12 @@ const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s) {
     p.PB = pb;
   }
   p.nblk = (p.H2 + p.PB - 1) / p.PB;
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<unsigned long long> attr{0};
+  if (first_on_device(attr)) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    attr = true;
   }
   const dim3 grid((unsigned)((long)p.B * p.nblk));
   if (p.bits) hipLaunchKernelGGL((stem_pool_fwd_kernel<true>), grid, dim3(SP_THREADS), lds, s, p);

@@ -244,12 +244,28 @@ class RcclComm {
     check();
     std::lock_guard<std::mutex> lk(issue_mu_);
     check_local(ts);
+    // The handles are read once, before the group opens: an abort() that gave up waiting for
+    // this lock nulls them concurrently, and a null read between ncclGroupStart and
+    // ncclGroupEnd would throw with the group left open.  ncclGroupEnd also runs on an error
+    // path (an aborted communicator makes the op itself fail), so the group depth stays balanced.
+    std::vector<ncclComm_t> cs(ts.size());
+    for (size_t i = 0; i < ts.size(); ++i) cs[i] = comm(i);
     nck(ncclGroupStart(), "group start");
-    for (size_t i = 0; i < ts.size(); ++i) {
-      c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
-      nck(op(i, comm(i)), tag.c_str());
+    ncclResult_t first = ncclSuccess;
+    size_t bad = 0;
+    try {
+      for (size_t i = 0; i < ts.size() && first == ncclSuccess; ++i) {
+        c10::hip::HIPGuardMasqueradingAsCUDA g(devs_[i]);
+        first = op(i, cs[i]);
+        bad = i;
+      }
+    } catch (...) {
+      (void)ncclGroupEnd();
+      throw;
     }
-    nck(ncclGroupEnd(), "group end");
+    const ncclResult_t end = ncclGroupEnd();
+    TORCH_CHECK(first == ncclSuccess, "pddl rccl: ", tag, " (local rank ", bad, "): ", ncclGetErrorString(first));
+    nck(end, "group end");
     if (!watch_) return;
     auto evs = std::make_shared<std::vector<hipEvent_t>>();
     for (size_t i = 0; i < ts.size(); ++i) {

@@ -73,6 +73,7 @@ class TrainConfig:
     checkpoint_every: int = 0                      # additive: periodic checkpoints (0 = off)
     resume: Optional[str] = None
     metrics_jsonl: Optional[str] = None
+    baseline_ips: Optional[float] = None           # 1-GPU images/sec: the JSONL log adds scaling efficiency
     timeline: Optional[str] = None                 # chrome-trace JSON of the fusion engine
     graphs: Optional[bool] = None                  # HIP graphs: None = auto (on for Mirrored / local replicas)
     roctx: bool = False                            # roctx ranges per step phase (utils/profiling.py)
@@ -152,6 +153,7 @@ def add_cli_args(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--resume", type=str)
     a("--checkpoint-every", type=int, dest="checkpoint_every")
     a("--metrics-jsonl", type=str, dest="metrics_jsonl")
+    a("--baseline-ips", type=float, dest="baseline_ips")
     a("--timeline", type=str)
     a("--graphs", action="store_true", default=None)
     a("--no-graphs", action="store_false", dest="graphs", default=None)

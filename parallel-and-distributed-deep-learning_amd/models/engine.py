@@ -145,6 +145,7 @@ class HipEngine:
         self.two_stream = self._two_stream_wanted(batch)
         self.side = torch.cuda.Stream(dev) if self.two_stream and dev.type == "cuda" else None
         self._pending, self._last_side = {}, None
+        self._evpool, self._evi = [], 0   # fork/join events (see _event)
 
     # ------------------------------------------------------------------ tables
     def _build_weight_tables(self):
@@ -574,6 +575,17 @@ class HipEngine:
         ts = os.environ.get("PDDL_TWO_STREAM", "auto")
         return self.TWO_STREAM_OK and ((batch <= self.TWO_STREAM_MAX_BATCH) if ts == "auto" else ts == "1")
 
+    def _event(self):
+        """The next fork/join event of this step, from a pool the engine owns for its whole
+        life: the i-th record of every step reuses the i-th event (a wait binds to the record
+        made before it, so reuse after the wait is safe), so a step -- eager or captured --
+        creates and destroys no HIP events."""
+        i = self._evi
+        self._evi += 1
+        if i == len(self._evpool):
+            self._evpool.append(torch.cuda.Event())
+        return self._evpool[i]
+
     def _side_run(self, fn, *args, reads=()):
         """Launch a weight-gradient kernel on the side stream, ordered after everything enqueued
         on the compute stream so far; `reads` names the gradient buffers it reads, which the
@@ -582,12 +594,12 @@ class HipEngine:
             fn(*args)
             return
         main = torch.cuda.current_stream(self.device)
-        ev = torch.cuda.Event()
+        ev = self._event()
         ev.record(main)
         self.side.wait_event(ev)
         with torch.cuda.stream(self.side):
             fn(*args)
-        done = torch.cuda.Event()
+        done = self._event()
         done.record(self.side)
         for r in reads:
             self._pending[r] = done
@@ -616,12 +628,12 @@ class HipEngine:
             self._join_side()
             cb(i)
             return
-        ev = torch.cuda.Event()
+        ev = self._event()
         ev.record(torch.cuda.current_stream(self.device))
         self.side.wait_event(ev)
         with torch.cuda.stream(self.side):
             cb(i)
-        done = torch.cuda.Event()
+        done = self._event()
         done.record(self.side)
         self._last_side = done
 
@@ -652,6 +664,7 @@ class HipEngine:
         bks = buckets if buckets is not None else []
         nb = [0]
         self._pending, self._last_side = {}, None
+        self._evi = 0
         W = self._side_run
 
         def done_upto(off):

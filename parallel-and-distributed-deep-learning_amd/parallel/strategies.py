@@ -66,34 +66,6 @@ def collective_timeout():
     return datetime.timedelta(seconds=float(os.environ.get("PDDL_COLLECTIVE_TIMEOUT", "600")))
 
 
-def overlap_buckets(engine):
-    """Gradient slices whose optimizer update can start as soon as backward completes them
-    (8 MiB: fine enough that only the last stage-2 / stem slice and the per-channel tail wait
-    for the end of backward)."""
-    if not hasattr(engine, "_ov_buckets"):
-        engine._ov_buckets = engine.L.buckets(8.0)
-    return engine._ov_buckets
-
-
-def overlap_opt_wanted() -> bool:
-    """Optimizer bucket updates overlapped with backward: opt-in (PDDL_OVERLAP_OPT=1).  Measured
-    no gain on one GPU -- the fused Adam is 0.11 ms of a 92 ms b2560 step, and at b32 the side-
-    stream updates cost 2.7 % (4.36 vs 4.24 ms, profiles/r4_ovopt_ab.txt) -- and inside a HIP
-    graph capture together with the two-stream backward the replayed updates diverge from the
-    eager ones, so GraphedTrainStep never overlaps."""
-    return os.environ.get("PDDL_OVERLAP_OPT", "0") == "1"
-
-
-def overlap_stream(engine):
-    """The stream the overlapped optimizer updates run on: the engine's weight-gradient side
-    stream when it has one, else a stream of their own."""
-    if getattr(engine, "side", None) is not None:
-        return engine.side
-    if not hasattr(engine, "_opt_stream"):
-        engine._opt_stream = torch.cuda.Stream(engine.params.device)
-    return engine._opt_stream
-
-
 def gpu_available() -> bool:
     return torch.cuda.is_available() and torch.cuda.device_count() > 0
 
@@ -291,15 +263,8 @@ class SingleStrategy(Strategy):
             return self.graphed(images.to(self.device, non_blocking=True), labels.to(self.device, non_blocking=True),
                                 flip, off).clone()
         eng = self.engine
-        if eng.params.is_cuda and hasattr(eng, "wbf") and overlap_opt_wanted():
-            bks = overlap_buckets(eng)       # optimizer bucket updates under the rest of backward
-            self.opt.overlap_begin(bks, overlap_stream(eng))
-            s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off,
-                                     bucket_cb=self.opt.overlap_bucket, buckets=bks).clone()
-            self.opt.overlap_finish()
-        else:
-            s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off).clone()
-            self.opt.step()
+        s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off).clone()
+        self.opt.step()
         eng.after_update()
         return s
 
@@ -345,13 +310,43 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
         super().__init__(cfg)
         self.comm = os.environ.get("PDDL_COMM", comm)
 
+    def _graphed_ranks(self) -> bool:
+        """GPU ranks of a multi-process job replay their step from HIP graphs segmented at the
+        gradient buckets, with the bucket all-reduces on a native RCCL communicator between the
+        segment replays (the Mirrored replica design, _LocalReplicas with one local replica).
+        Eager FusionEngine / bucket reducer only with --no-graphs (cfg.graphs False),
+        PDDL_COMM=fusion|bucket, the fp32 engine, or a rehearsal (ranks sharing one GPU: RCCL
+        refuses that)."""
+        if not (self.device.type == "cuda" and self.cfg.precision == "bf16" and self.cfg.graphs is not False
+                and not rehearsing()):
+            return False
+        comm = os.environ.get("PDDL_COMM")
+        # one rank: no collective is needed (the whole-step graph below with --graphs);
+        # PDDL_COMM=graphs still runs the multi-rank design over a 1-rank communicator
+        return comm == "graphs" if self.world == 1 else comm in (None, "graphs")
+
     def _build(self, trainer):
         info = resolve_cluster(port_base=self.cfg.port_base)
         self.device = self._pick_device(info.local_rank if gpu_available() else 0)
         self._init_process_group(info)
+        if self._graphed_ranks():
+            # one local replica on this rank's GPU, one RCCL communicator over every rank
+            # (ncclCommInitRank; the unique id travels over the c10d group)
+            self.mirror = _LocalReplicas(self.cfg, [self.device], global_rank_base=self.rank,
+                                         world_ranks=self.world)
+            self.engine, self.opt = self.mirror.replicas[0]
+            self.fusion, self.reducer, self._tune = None, None, None
+            self.buckets = self.engine.L.buckets(self.cfg.bucket_mb if self.cfg.bucket_mb > 0 else 32.0)
+            return
         cap = max(self.cfg.batch_size, self.cfg.val_batch_size or 0)
         self.engine, self.opt = self._make_engine_and_opt(self.device, cap)
         self.aug = Augment(self.cfg, self.device, self.cfg.seed + 1000 * self.rank)
+        self.graphed = None
+        if self.world == 1 and self.cfg.graphs and self.device.type == "cuda" and hasattr(self.engine, "wbf"):
+            from ..train.graph import GraphedTrainStep   # one rank: the whole step as one HIP graph
+            B = self.cfg.batch_size
+            self.graphed = GraphedTrainStep(self.engine, self.opt, B, (self.cfg.image_size, self.cfg.image_size),
+                                            1.0 / B)
         # bucket_mb <= 0: autotune (Horovod's HOROVOD_AUTOTUNE analogue for the fusion threshold)
         self._tune = None
         mb = self.cfg.bucket_mb
@@ -415,33 +410,42 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
 
     def train_step(self, images, labels):
         self._fault_tick()
+        if getattr(self, "mirror", None) is not None:
+            return self.mirror.step(images, labels, self.global_batch)
         if self._tune is not None:
             return self._autotune_step(images, labels)
         return self._step(images, labels)
 
-    def _overlap_opt(self) -> bool:
-        """One replica on the GPU: the optimizer's bucket updates run under the rest of backward
-        (PDDL_OVERLAP_OPT=1 turns it on).  With collectives the update waits for the all-reduce."""
-        return (self.world == 1 and self.fusion is None and self.reducer is None and self.device.type == "cuda"
-                and hasattr(self.engine, "wbf") and overlap_opt_wanted())
+    def _replicas(self):
+        m = getattr(self, "mirror", None)
+        return m.replicas if m is not None else super()._replicas()
+
+    def broadcast_state(self, trainer, root=0):
+        if getattr(self, "mirror", None) is not None:
+            self.mirror.broadcast()      # (RCCL broadcast of parameters + optimizer slots from rank 0)
+        else:
+            super().broadcast_state(trainer, root)
 
     def _step(self, images, labels):
-        ov = self._overlap_opt()
-        s = self.compute_gradients(images, labels, overlap_opt=ov)
+        g = getattr(self, "graphed", None)
+        if g is not None and images.shape[0] == g.B and tuple(images.shape[1:3]) == tuple(g.images.shape[1:3]):
+            flip, off = self.aug(images.shape[0])
+            return g(images.to(self.device, non_blocking=True), labels.to(self.device, non_blocking=True),
+                     flip, off).clone()
+        s = self.compute_gradients(images, labels)
         prof.push("step/optimizer")
-        if ov:
-            self.opt.overlap_finish()
-        else:
-            self.opt.step()
+        self.opt.step()
         self.engine.after_update()
         prof.pop()
         return s
 
-    def compute_gradients(self, images, labels, overlap_opt: bool = False):
+    def compute_gradients(self, images, labels):
         """Forward + backward + the bucketed all-reduce, without applying the update
         (Optimizer.compute_gradients of the reference's DistributedOptimizer,
         imagenet-resnet50-hvd.py:101): afterwards `engine.grads` holds the global-batch mean
         gradient on every rank.  Returns the step's (loss sum, correct) stats."""
+        if getattr(self, "mirror", None) is not None:
+            return self.mirror.compute_gradients(images, labels, self.global_batch)
         B = images.shape[0]
         flip, off = self.aug(B)
         gscale = 1.0 / (B * self.world)
@@ -453,10 +457,6 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
         elif self.reducer is not None:
             self.reducer.begin()
             cb = self.reducer.on_bucket_ready
-        elif overlap_opt:   # (the caller finishes the step with opt.overlap_finish())
-            bks = overlap_buckets(self.engine)
-            self.opt.overlap_begin(bks, overlap_stream(self.engine))
-            cb = self.opt.overlap_bucket
         s = self.engine.forward_backward(images, labels, gscale, flip=flip, crop_offset=off, bucket_cb=cb,
                                          buckets=bks).clone()
         prof.push("step/allreduce")
@@ -468,9 +468,14 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
         return s
 
     def write_timeline(self, path: str):
+        js = None
         if self.fusion is not None:
+            js = self.fusion.timeline_json()
+        elif getattr(self, "mirror", None) is not None:
+            js = self.mirror.timeline_json(self.rank)
+        if js is not None:
             with open(f"{path}.rank{self.rank}.json", "w") as f:
-                f.write(self.fusion.timeline_json())
+                f.write(js)
 
 
 class MultiWorkerStrategy(HorovodStrategy):
@@ -524,8 +529,8 @@ class MultiWorkerStrategy(HorovodStrategy):
         return self.mirror.replicas if hasattr(self, "mirror") else super()._replicas()
 
     def reduce_metrics(self, t):
-        if hasattr(self, "mirror") and self.world > 1:
-            x = t.to("cpu", torch.float64)       # (the control group is gloo)
+        if self.req_local > 1 and hasattr(self, "mirror") and self.world > 1:
+            x = t.to("cpu", torch.float64)       # (the P x R layout's control group is gloo)
             dist.all_reduce(x)
             return x
         return super().reduce_metrics(t)
@@ -641,10 +646,13 @@ class _LocalReplicas:
         return out
 
     # ------------------------------------------------------------------ graphed step
+    def _bucket_mb(self) -> float:
+        return self.cfg.bucket_mb if self.cfg.bucket_mb > 0 else 32.0
+
     def _capture(self, parts, global_batch: int):
         from ..train.graph import SegmentedStepGraphs
         eng0 = self.replicas[0][0]
-        self.buckets = eng0.L.buckets(self.cfg.bucket_mb)
+        self.buckets = eng0.L.buckets(self._bucket_mb())
         B = parts[0][0].shape[0]
         H, W = parts[0][0].shape[1:3]
         self.graphs = []
@@ -656,6 +664,19 @@ class _LocalReplicas:
                 self.graphs.append(g)
         self.comm_streams = [torch.cuda.Stream(device=d) for d in self.devices]
         self.evs = [[torch.cuda.Event() for _ in self.devices] for _ in self.buckets]
+        # bf16 wire (cfg.grad_dtype, Horovod's fp16 compression analogue): each bucket is rounded
+        # into a bf16 copy on the comm stream, all-reduced, and widened back into the fp32 grads
+        self.lowp = None
+        if self.cfg.grad_dtype == "bf16":
+            self.lowp = [torch.empty(e.grads.numel(), dtype=torch.bfloat16, device=d)
+                         for (e, _), d in zip(self.replicas, self.devices)]
+        # timeline (cfg.timeline): READY / ALLREDUCE per bucket from GPU events of device 0
+        self.tl = None
+        if self.cfg.timeline:
+            d0 = self.devices[0]
+            mk = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
+            with torch.cuda.device(d0):
+                self.tl = {"t0": mk(), "b": [(mk(), mk(), mk()) for _ in self.buckets], "steps": 0}
         self._gb = global_batch
 
     def _graphed_step(self, parts, global_batch: int):
@@ -664,25 +685,74 @@ class _LocalReplicas:
             out = self._eager_step(parts, global_batch)   # first step eager (lazy tables), then capture
             self._capture(parts, global_batch)
             return out
+        from ..ops.native import native
         grads = [e.grads for e, _ in self.replicas]
-        cur = [torch.cuda.current_stream(d) for d in self.devices]
+        # Graphs are launched on a stream of their own, never on the legacy default stream: a
+        # multi-branch graph (the two-stream backward) launched there segfaulted inside
+        # hipGraphLaunch (its parallel-stream table read as garbage) once the process had run
+        # other graphs -- train/graph.py replay_stream
+        from ..train.graph import replay_stream
+        amb = [torch.cuda.current_stream(d) for d in self.devices]
+        cur = [replay_stream(d) for d in self.devices]
+        for r in range(self.R):
+            cur[r].wait_stream(amb[r])
         for r, (g, d) in enumerate(zip(self.graphs, self.devices)):
-            with torch.cuda.device(d):
+            with torch.cuda.device(d), torch.cuda.stream(cur[r]):
                 flip, off = self.augs[r](B)
                 g.load(parts[r][0], parts[r][1], flip, off)
         streams = [cs.cuda_stream for cs in self.comm_streams]
+        tl = self.tl
+        if tl is not None:
+            tl["t0"].record(cur[0])
         for k, (s, e) in enumerate(self.buckets):
             for r, d in enumerate(self.devices):
-                with torch.cuda.device(d):
+                with torch.cuda.device(d), torch.cuda.stream(cur[r]):
                     self.graphs[r].replay_segment(k)
                     self.evs[k][r].record(cur[r])
                     self.comm_streams[r].wait_event(self.evs[k][r])
-            self.comm.all_reduce_on([gr[s:e] for gr in grads], "sum", streams, f"bucket {k} all_reduce")
+            if tl is not None:
+                tl["b"][k][0].record(cur[0])
+                tl["b"][k][1].record(self.comm_streams[0])
+            if self.lowp is None:
+                self.comm.all_reduce_on([gr[s:e] for gr in grads], "sum", streams, f"bucket {k} all_reduce")
+            else:
+                for r, d in enumerate(self.devices):
+                    with torch.cuda.device(d), torch.cuda.stream(self.comm_streams[r]):
+                        native.cast_bf16(grads[r][s:e], self.lowp[r][s:e])
+                self.comm.all_reduce_on([lp[s:e] for lp in self.lowp], "sum", streams, f"bucket {k} all_reduce (bf16)")
+                for r, d in enumerate(self.devices):
+                    with torch.cuda.device(d), torch.cuda.stream(self.comm_streams[r]):
+                        native.cast_f32(self.lowp[r][s:e], grads[r][s:e])
+            if tl is not None:
+                tl["b"][k][2].record(self.comm_streams[0])
         for r, d in enumerate(self.devices):
-            with torch.cuda.device(d):
+            with torch.cuda.device(d), torch.cuda.stream(cur[r]):
                 cur[r].wait_stream(self.comm_streams[r])
                 self.graphs[r].replay_optimizer()
+            amb[r].wait_stream(cur[r])
+        if tl is not None:
+            tl["steps"] += 1
         return self._sum_stats([g.stats for g in self.graphs])
+
+    def timeline_json(self, rank: int = 0) -> Optional[str]:
+        """Chrome-trace JSON of the last graphed step (device 0): per bucket READY (its segment
+        replayed) and ALLREDUCE (the grouped RCCL call on the comm stream), microseconds from
+        the step start -- the FusionEngine timeline's phases for the graphed replicas."""
+        import json
+        tl = getattr(self, "tl", None)
+        if tl is None or not tl["steps"]:
+            return None
+        torch.cuda.synchronize(self.devices[0])
+        ev = []
+        for k, (ready, start, end) in enumerate(tl["b"]):
+            s, e = self.buckets[k]
+            args = {"bytes": (e - s) * (2 if self.lowp is not None else 4), "step": tl["steps"], "clock": "gpu"}
+            ev.append({"name": "READY", "cat": f"bucket{k}", "ph": "i", "s": "t", "pid": rank, "tid": k,
+                       "ts": round(tl["t0"].elapsed_time(ready) * 1e3, 1), "args": args})
+            t0 = tl["t0"].elapsed_time(start) * 1e3
+            ev.append({"name": "ALLREDUCE", "cat": f"bucket{k}", "ph": "X", "pid": rank, "tid": k, "ts": round(t0, 1),
+                       "dur": round(start.elapsed_time(end) * 1e3, 1), "args": args})
+        return json.dumps(ev)
 
     # ------------------------------------------------------------------ eager step
     def _overlap_setup(self):
@@ -694,7 +764,7 @@ class _LocalReplicas:
         the whole backward, imagenet-resnet50-mirror.py:21 [lib].)"""
         import queue
         eng0 = self.replicas[0][0]
-        self.buckets = eng0.L.buckets(self.cfg.bucket_mb)
+        self.buckets = eng0.L.buckets(self._bucket_mb())
         self.comm_streams = [torch.cuda.Stream(device=d) for d in self.devices]
         self._q = queue.Queue()
         self._lock = threading.Lock()

@@ -209,13 +209,27 @@ class TimeHistory(Callback):
 
 
 class JsonlLogger(Callback):
-    def __init__(self, path):
+    """One JSON line per epoch (chief only): the epoch's logs -- loss / accuracy / val_*, lr,
+    images_per_sec (ThroughputMeter, runs before this) -- plus the replica count and, with a
+    configured 1-GPU rate (`baseline_ips`), the weak-scaling efficiency
+    images_per_sec / (replicas * baseline_ips) (utils/scaling.py)."""
+
+    def __init__(self, path, baseline_ips=None):
         self.path = path
+        self.baseline_ips = baseline_ips
 
     def on_epoch_end(self, epoch, logs=None):
-        if self.trainer.strategy.is_chief:
-            with open(self.path, "a") as f:
-                f.write(json.dumps({"epoch": epoch + 1, **{k: float(v) for k, v in (logs or {}).items()}}) + "\n")
+        if not self.trainer.strategy.is_chief:
+            return
+        from ..utils.scaling import efficiency
+        rec = {"epoch": epoch + 1, **{k: float(v) for k, v in (logs or {}).items()}}
+        n = self.trainer.strategy.num_replicas_in_sync
+        rec["replicas"] = n
+        if "images_per_sec" in rec and self.baseline_ips:
+            rec["baseline_ips"] = float(self.baseline_ips)
+            rec["scaling_efficiency"] = efficiency(rec["images_per_sec"], n, self.baseline_ips)
+        with open(self.path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
 
 
 class ModelCheckpoint(Callback):

@@ -30,6 +30,55 @@ import torch
 # hipErrorStreamCaptureUnsupported on the Mirrored entry script's first (captured) step.
 CAPTURE_MODE = "thread_local"
 
+import os as _os
+
+
+def _exec_layout(g):
+    """(diagnostics, PDDL_GRAPH_DEBUG=1) the HIP runtime's view of a graph executable of this
+    image's libamdhip64: parallel branch count and the size of its parallel-stream table."""
+    import ctypes
+    ex = g.raw_cuda_graph_exec()
+    if not ex:
+        return None
+    n = ctypes.c_int.from_address(ex + 0x48).value
+    b0 = ctypes.c_uint64.from_address(ex + 0x1b8).value
+    b1 = ctypes.c_uint64.from_address(ex + 0x1c0).value
+    ents = [hex(ctypes.c_uint64.from_address(b0 + 8 * i).value) for i in range((b1 - b0) // 8)] if b0 else []
+    return n, (b1 - b0) // 8, hex(b0), ents
+
+
+def _glog(msg):
+    path = _os.environ.get("PDDL_CRASH_TRACE")
+    if _os.environ.get("PDDL_GRAPH_DEBUG") == "1" and path:
+        with open(path, "a") as f:
+            f.write(msg + "\n")
+
+
+_REPLAY = {}
+
+
+def replay_stream(device) -> torch.cuda.Stream:
+    """The stream HIP graphs of `device` are launched on (one per device, made once).
+
+    Never the legacy default stream: launched there, a graph with parallel branches (the
+    two-stream backward forks a side stream into every captured step) segfaulted inside
+    hipGraphLaunch -- the runtime's per-launch stream assignment read its parallel-stream table
+    as garbage (faulting address 0x1d8 = 0x30 + 0x1a8; native stack from
+    csrc/runtime/crash_trace.cpp) -- once the process had created and run other graphs
+    (deterministic after tests/test_gpu_{bn_train,capture,engine}.py, then the Mirrored
+    graphed step; alone it passed).  The same graphs launched on a created stream ran clean in
+    the same sequence (scripts/crash_bisect.sh, profiles/r5_graph_crash.txt)."""
+    d = torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    s = _REPLAY.get(idx)
+    if s is None:
+        s = _REPLAY[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def _new_graph(**kw):
+    return torch.cuda.CUDAGraph(**kw)
+
 class GraphedTrainStep:
     """with_optimizer=False records forward + backward only (Mirrored: the cross-device
     all-reduce runs between the replay and an eager optimizer step)."""
@@ -81,11 +130,13 @@ class GraphedTrainStep:
             self.opt.sync_hparams()
         torch.cuda.synchronize()
         it = self.opt._iterations
-        g = torch.cuda.CUDAGraph()
+        g = _new_graph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             self.stats = self._body()
         self.opt._iterations = it    # the capture pass did not step (no setter: hs is current)
         self.graph = g
+        if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
+            _glog(f"whole-step graph captured: {_exec_layout(g)}")
 
     def __call__(self, images, labels, flip=None, crop_offset=(0, 0)):
         self._load(images, labels, flip, crop_offset)
@@ -95,7 +146,7 @@ class GraphedTrainStep:
             return out
         if self.with_optimizer:
             self.opt.sync_hparams()
-        self.graph.replay()
+        _launch(self.graph)
         if self.with_optimizer:
             self.opt._iterations += 1
         return self.stats
@@ -114,11 +165,15 @@ class SegmentedStepGraphs(GraphedTrainStep):
     MirroredStrategy (imagenet-resnet50-mirror.py:21,54) with its NCCL all-reduce."""
 
     def __init__(self, engine, optimizer, batch: int, image_hw: Tuple[int, int], gscale: float, buckets,
-                 image_dtype=torch.uint8):
+                 image_dtype=torch.uint8, two_stream: Optional[bool] = None, keep_graph: bool = False,
+                 probe=None):
         super().__init__(engine, optimizer, batch, image_hw, gscale, image_dtype, with_optimizer=False)
         self.buckets = list(buckets)
         self.segments = []
         self.opt_graph: Optional[torch.cuda.CUDAGraph] = None
+        self.two_stream = two_stream
+        self.keep_graph = keep_graph     # (diagnostics: keep the hipGraph_t for node queries)
+        self.probe = probe               # (diagnostics: probe(segment_index, graph) after each cut)
 
     @property
     def captured(self) -> bool:
@@ -128,26 +183,43 @@ class SegmentedStepGraphs(GraphedTrainStep):
         eng, opt = self.engine, self.opt
         dev = eng.params.device
         nb = len(self.buckets)
-        # one stream: the two-stream backward's side stream forked across the segment cuts
-        # captured fine but its replay segfaulted inside hipGraphLaunch in a long-lived process
-        # (tests/test_gpu_runtime.py::test_mirrored_graphed_step_matches_eager after the rest of
-        # the GPU suite; alone it passed), so segmented replicas run the single-stream schedule
-        if getattr(eng, "side", None) is not None:
+        # The engine's two-stream backward (weight gradients on its side stream) is captured as
+        # is: every cut first joins the side stream into the capture stream (cut.needs_join), so
+        # each segment is a closed fork/join graph.  Checked node by node on the GPU
+        # (scripts/graph_diag.py, profiles/r5_graph_diag.txt): after every cut neither stream is
+        # left capturing, the segments hold exactly the single-stream schedule's kernels (234 at
+        # b8, 213 at b32) and one replay reproduces the eager gradient to 5e-8.
+        # two_stream=False forces the single-stream schedule.
+        if getattr(eng, "side", None) is not None and self.two_stream is False:
             eng.side = None
         opt.sync_hparams()
         torch.cuda.synchronize(dev)
+        # as torch.cuda.graph does: collect garbage now, and none while capturing
+        import gc
+        gc.collect()
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            self._capture_segments(eng, opt, dev, nb)
+        finally:
+            if gc_was:
+                gc.enable()
+
+    def _capture_segments(self, eng, opt, dev, nb):
         it = opt._iterations
         segs = []
         mark = self._mark = torch.zeros(1, device=dev)   # (kept alive: the graphs write it)
 
         def begin():
-            g = torch.cuda.CUDAGraph()
+            g = _new_graph(keep_graph=self.keep_graph)
             g.capture_begin(pool=segs[0].pool() if segs else None, capture_error_mode=CAPTURE_MODE)
             mark.zero_()     # never an empty graph (two buckets can complete at the same layer)
             segs.append(g)
 
         def cut(i):
             segs[-1].capture_end()
+            if self.probe is not None:
+                self.probe(len(segs) - 1, segs[-1])
             if i < nb - 1:
                 begin()
         cut.needs_join = True   # (a two-stream engine joins its side stream before each cut)
@@ -159,7 +231,7 @@ class SegmentedStepGraphs(GraphedTrainStep):
                 begin()
                 self.stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip,
                                                   crop_offset=self.crop, bucket_cb=cut, buckets=self.buckets)
-                og = torch.cuda.CUDAGraph()
+                og = _new_graph(keep_graph=self.keep_graph)
                 og.capture_begin(pool=segs[0].pool(), capture_error_mode=CAPTURE_MODE)
                 opt.step()
                 eng.after_update()
@@ -170,14 +242,32 @@ class SegmentedStepGraphs(GraphedTrainStep):
         opt._iterations = it        # capture ran no kernels: training state did not advance
         self.segments = segs
         self.opt_graph = og
+        if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
+            _glog(f"captured {id(self):x}: " + ", ".join(str(_exec_layout(g)) for g in segs))
 
     def load(self, images, labels, flip=None, crop_offset=(0, 0)):
         self._load(images, labels, flip, crop_offset)
 
     def replay_segment(self, k: int):
-        self.segments[k].replay()
+        if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
+            _glog(f"replay segment {k} of {id(self):x}: exec (branches, streams, table) {_exec_layout(self.segments[k])}")
+        _launch(self.segments[k])
 
     def replay_optimizer(self):
         self.opt.sync_hparams()
-        self.opt_graph.replay()
+        _launch(self.opt_graph)
         self.opt._iterations += 1
+
+
+def _launch(g):
+    """Replay on the current stream, or through replay_stream() when that is the legacy
+    default stream (ordered after and before the default stream's work)."""
+    amb = torch.cuda.current_stream()
+    if amb.cuda_stream != 0:
+        g.replay()
+        return
+    rs = replay_stream(amb.device)
+    rs.wait_stream(amb)
+    with torch.cuda.stream(rs):
+        g.replay()
+    amb.wait_stream(rs)

@@ -65,39 +65,6 @@ class FlatOptimizer:
     def state_tensors(self):
         return {}
 
-    # ---- optimizer step overlapped with backward (one replica, GPU): the update of a gradient
-    # bucket is launched on a side stream as soon as the engine reports the bucket complete, so
-    # it runs under the rest of backward; only the per-channel tail is left for the end.
-    def overlap_begin(self, buckets, stream):
-        """Before forward_backward: advance the device step counter (the bucket updates read
-        the step size from it) and remember where updates may be issued."""
-        self._device_step(*self._hparam_args())
-        self._iterations += 1
-        self._ov = {"buckets": list(buckets), "stream": stream, "upto": 0}
-
-    def overlap_bucket(self, i: int):
-        """Bucket i's gradient is final (called on the compute stream after its producers)."""
-        ov = self._ov
-        s, e = ov["buckets"][i]
-        if s != ov["upto"] or s % 4 or (e - s) % 4 or e > self.n:
-            return                       # (not contiguous / not 16-byte aligned: left for the end)
-        main = torch.cuda.current_stream(self.params.device)
-        if main != ov["stream"]:   # (a two-stream engine runs the callback on the update stream
-            ev = torch.cuda.Event()  # itself; a self-wait inside a graph capture crashes capture_end)
-            ev.record(main)
-            ov["stream"].wait_event(ev)
-        with torch.cuda.stream(ov["stream"]):
-            self._update_range(s, e)
-        ov["upto"] = e
-
-    def overlap_finish(self):
-        """After forward_backward: join the bucket updates and update the rest (the per-channel
-        tail, whose BN / bias gradients are produced last)."""
-        ov, self._ov = self._ov, None
-        torch.cuda.current_stream(self.params.device).wait_stream(ov["stream"])
-        if ov["upto"] < self.n:
-            self._update_range(ov["upto"], self.n)
-
 
 class Adam(FlatOptimizer):
     def __init__(self, engine, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-7):
@@ -120,14 +87,6 @@ class Adam(FlatOptimizer):
             self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
             self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
             self.params.sub_(lr_t * self.m / (self.v.sqrt() + self.eps))
-
-    def _hparam_args(self):
-        return (True, self.b1, self.b2)
-
-    def _update_range(self, s, e):
-        from ..ops.native import native
-        native.adam(self.params[s:e], self.grads[s:e], self.m[s:e], self.v[s:e], 0.0, self.b1, self.b2, self.eps,
-                    self.gscale, self.hs)
 
     def state_tensors(self):
         return {"m": self.m, "v": self.v}
@@ -153,14 +112,6 @@ class SGD(FlatOptimizer):
                 self.params.add_(self.mu * self.mom - self.lr * g)
             else:
                 self.params.add_(self.mom)
-
-    def _hparam_args(self):
-        return (False,)
-
-    def _update_range(self, s, e):
-        from ..ops.native import native
-        native.sgd(self.params[s:e], self.grads[s:e], self.mom[s:e], 0.0, self.mu, self.wd, self.nesterov, self.gscale,
-                   self.hs)
 
     def state_tensors(self):
         return {"momentum": self.mom}

@@ -181,7 +181,7 @@ def default_callbacks(cfg, strategy, extra: Optional[List[Callback]] = None) -> 
     cbs.append(ThroughputMeter())
     cbs.append(TimeHistory())
     if cfg.metrics_jsonl:
-        cbs.append(JsonlLogger(cfg.metrics_jsonl))
+        cbs.append(JsonlLogger(cfg.metrics_jsonl, cfg.baseline_ips))
     if cfg.checkpoint_every:
         cbs.append(ModelCheckpoint(f"{cfg.save_dir}/ckpt-{{epoch:03d}}.h5", cfg.checkpoint_every))
     cbs += list(extra or [])

@@ -22,3 +22,14 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords and not has_gpu:
             it.add_marker(pytest.mark.skip(reason="no GPU"))
+
+
+def pytest_sessionstart(session):
+    # GPU runs: a fatal signal writes the native stack (HIP runtime / RCCL / extension frames) to
+    # $PDDL_CRASH_TRACE (a file: pytest captures fd 2) before pytest's faulthandler prints the
+    # Python ones (csrc/runtime/crash_trace.cpp)
+    import torch
+    if torch.cuda.is_available():
+        from pddl.ops.native import native_available, require_native
+        if native_available():
+            require_native().install_crash_trace(os.environ.get("PDDL_CRASH_TRACE", ""))

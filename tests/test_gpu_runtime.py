@@ -312,3 +312,47 @@ def test_comm_proxy_holds_its_duration_and_leaves_the_gradient():
     dt = time.perf_counter() - t0
     assert 0.019 < dt < 0.2, dt
     assert torch.equal(g, ref) and torch.equal(scratch, g)
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_horovod_rank_graphs_over_one_rank_communicator(monkeypatch, tmp_path, wire):
+    """Horovod (and 1-GPU-per-process MWMS) ranks replay their step from HIP graphs segmented at
+    the gradient buckets, with each bucket's all-reduce on a native RCCL communicator between
+    the segment replays (the Mirrored replica design).  PDDL_COMM=graphs forces it on a 1-rank
+    job (nranks = 1 communicator): 4 steps of the Horovod preset's crop 160 at the reference's
+    batch 32 follow the eager rank step, and the timeline has a READY and an ALLREDUCE per
+    bucket (imagenet-resnet50-hvd.py:25,89,101)."""
+    import json
+    from pddl.parallel.strategies import make_strategy
+    from pddl.train.trainer import Trainer
+    res = []
+    for comm in ("graphs", "eager"):
+        if comm == "graphs":
+            monkeypatch.setenv("PDDL_COMM", "graphs")
+        else:
+            monkeypatch.delenv("PDDL_COMM", raising=False)
+        tl = str(tmp_path / "tl")
+        cfg = _cfg("horovod", flip=False, max_steps=4, batch_size=32, crop=160, lr=1e-3, lr_scale_by_size=False,
+                   warmup_epochs=0, grad_dtype=wire, timeline=tl if comm == "graphs" else None)
+        st = make_strategy(cfg)
+        tr = Trainer(cfg, st)
+        h = tr.fit(1, [], validation=False)
+        res.append((h.history["loss"][0], st.engine.params.clone(), st.opt.iterations))
+        if comm == "graphs":
+            m = st.mirror
+            assert m.graph_mode and m.graphs is not None and m.comm.nranks == 1
+            assert (m.lowp is not None) == (wire == "bf16")
+            st.write_timeline(tl)
+            ev = json.loads(open(f"{tl}.rank0.json").read())
+            nb = len(m.buckets)
+            assert sum(e["name"] == "READY" for e in ev) == nb and sum(e["name"] == "ALLREDUCE" for e in ev) == nb
+            assert all(e["dur"] >= 0 for e in ev if e["name"] == "ALLREDUCE")
+        else:
+            assert getattr(st, "mirror", None) is None and st.fusion is None
+    (l0, p0, i0), (l1, p1, i1) = res
+    assert i0 == i1 == 4
+    if wire == "fp32":
+        assert abs(l0 - l1) <= 1e-3 * abs(l1)
+        assert ((p0 - p1).norm() / p1.norm()).item() < 2e-3
+    else:   # (the bf16 round trip of the gradient is the one difference on one rank)
+        assert l0 == l0 and abs(l0 - l1) <= 2e-2 * abs(l1)
