@@ -350,9 +350,12 @@ def run(args):
     desc = {
         "horovod": "horovod-style 1 proc/GPU, native FusionEngine: RCCL bucketed all-reduce overlapped with backward",
         "single": "single process, whole step replayed as one HIP graph",
-        "mirrored": f"mirrored: 1 process x {args.gpus} GPUs, ncclCommInitAll, grouped bucket all-reduce"
-                    + (" between per-device HIP-graph segments" if getattr(st, "mirror", None) is not None
-                       and st.mirror.graph_mode else ""),
+        "mirrored": (f"mirrored: 1 process x {args.gpus} GPUs, ncclCommInitAll, grouped bucket all-reduce"
+                     + (" between per-device HIP-graph segments" if getattr(st, "mirror", None) is not None
+                        and st.mirror.graph_mode else "")
+                     if not (getattr(st, "mirror", None) is not None and st.mirror.graph_mode
+                             and st.mirror._single_replica_job())
+                     else "mirrored: 1 replica, whole step as one HIP graph (no collective to run)"),
         "multiworker": f"multiworker: {world} process(es) x {args.local_gpus if args.strategy == 'multiworker' else 1}"
                        " GPU(s), one RCCL communicator",
     }[cfg.strategy]

@@ -570,6 +570,7 @@ class _LocalReplicas:
         self.devices = [torch.device(d) if not isinstance(d, int) else torch.device("cuda", d) for d in devices]
         self.R = len(self.devices)
         world_ranks = world_ranks or self.R
+        self.world_ranks = world_ranks
         self.cross = world_ranks > self.R           # replicas of the job in other processes
         cap = max(cfg.batch_size, cfg.val_batch_size or 0)
         self.replicas = []
@@ -862,9 +863,32 @@ class _LocalReplicas:
         if self.comm is not None:
             self.comm.check()      # a stall verdict of the previous step's collectives raises here
         parts = self._split(images, labels)
+        if self.graph_mode and self._single_replica_job():
+            return self._whole_step(parts, global_batch)
         if self.graph_mode:
             return self._graphed_step(parts, global_batch)
         return self._eager_step(parts, global_batch)
+
+    def _single_replica_job(self) -> bool:
+        """One replica in the whole job: the gradient needs no reduction (a 1-rank all-reduce is
+        the identity), so the step is one whole-step HIP graph with the optimizer inside, like
+        TF's MirroredStrategy on one device (no cross-device ops).  PDDL_MIRROR_SEGMENTED=1 (and
+        PDDL_COMM=graphs) keep the segmented multi-replica schedule and its collectives."""
+        return (self.world_ranks == 1 and os.environ.get("PDDL_MIRROR_SEGMENTED", "0") != "1"
+                and os.environ.get("PDDL_COMM") != "graphs")
+
+    def _whole_step(self, parts, global_batch: int):
+        from ..train.graph import GraphedTrainStep
+        (eng, opt), d = self.replicas[0], self.devices[0]
+        im, lb = parts[0]
+        B = im.shape[0]
+        g = getattr(self, "_whole", None)
+        if g is None or g.B != B or g.gscale != 1.0 / global_batch or tuple(g.images.shape[1:3]) != tuple(im.shape[1:3]):
+            g = self._whole = GraphedTrainStep(eng, opt, B, tuple(im.shape[1:3]), 1.0 / global_batch,
+                                               image_dtype=im.dtype)
+        with torch.cuda.device(d):
+            flip, off = self.augs[0](B)
+            return g(im, lb, flip, off).clone()
 
 
 class MirroredStrategy(Strategy):

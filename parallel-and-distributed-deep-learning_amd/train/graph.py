@@ -207,17 +207,25 @@ class SegmentedStepGraphs(GraphedTrainStep):
 
     def _capture_segments(self, eng, opt, dev, nb):
         it = opt._iterations
-        segs = []
-        mark = self._mark = torch.zeros(1, device=dev)   # (kept alive: the graphs write it)
+        segs = []         # segs[i]: the graph ending with bucket i, None when bucket i completed
+        live = []         # at the same point as bucket i-1 (nothing captured in between)
+        pool = []
 
         def begin():
             g = _new_graph(keep_graph=self.keep_graph)
-            g.capture_begin(pool=segs[0].pool() if segs else None, capture_error_mode=CAPTURE_MODE)
-            mark.zero_()     # never an empty graph (two buckets can complete at the same layer)
-            segs.append(g)
+            g.capture_begin(pool=pool[0] if pool else None, capture_error_mode=CAPTURE_MODE)
+            live.append(g)
 
         def cut(i):
-            segs[-1].capture_end()
+            if _capture_is_empty():
+                segs.append(None)          # (an empty capture cannot end: it stays open for i+1)
+                if i == nb - 1:
+                    raise RuntimeError("segmented capture: the last bucket captured no work")
+                return
+            live[-1].capture_end()
+            if not pool:                   # (pool() exists once a capture has ended)
+                pool.append(live[-1].pool())
+            segs.append(live[-1])
             if self.probe is not None:
                 self.probe(len(segs) - 1, segs[-1])
             if i < nb - 1:
@@ -229,13 +237,23 @@ class SegmentedStepGraphs(GraphedTrainStep):
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
                 begin()
-                self.stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip,
-                                                  crop_offset=self.crop, bucket_cb=cut, buckets=self.buckets)
-                og = _new_graph(keep_graph=self.keep_graph)
-                og.capture_begin(pool=segs[0].pool(), capture_error_mode=CAPTURE_MODE)
-                opt.step()
-                eng.after_update()
-                og.capture_end()
+                try:
+                    self.stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip,
+                                                      crop_offset=self.crop, bucket_cb=cut, buckets=self.buckets)
+                    og = _new_graph(keep_graph=self.keep_graph)
+                    live.append(og)
+                    og.capture_begin(pool=pool[0], capture_error_mode=CAPTURE_MODE)
+                    opt.step()
+                    eng.after_update()
+                    og.capture_end()
+                except BaseException:
+                    # leave no stream capturing (a dangling capture aborts the process at exit)
+                    if torch.cuda.is_current_stream_capturing():
+                        try:
+                            live[-1].capture_end()
+                        except Exception:
+                            pass
+                    raise
             torch.cuda.current_stream(dev).wait_stream(s)
         if len(segs) != nb:
             raise RuntimeError(f"segmented capture produced {len(segs)} segments for {nb} buckets")
@@ -243,20 +261,43 @@ class SegmentedStepGraphs(GraphedTrainStep):
         self.segments = segs
         self.opt_graph = og
         if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
-            _glog(f"captured {id(self):x}: " + ", ".join(str(_exec_layout(g)) for g in segs))
+            _glog(f"captured {id(self):x}: " + ", ".join(str(_exec_layout(g) if g else None) for g in segs))
 
     def load(self, images, labels, flip=None, crop_offset=(0, 0)):
         self._load(images, labels, flip, crop_offset)
 
     def replay_segment(self, k: int):
         if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
-            _glog(f"replay segment {k} of {id(self):x}: exec (branches, streams, table) {_exec_layout(self.segments[k])}")
-        _launch(self.segments[k])
+            _glog(f"replay segment {k} of {id(self):x}: exec (branches, streams, table) {_exec_layout(self.segments[k]) if self.segments[k] else None}")
+        if self.segments[k] is not None:
+            _launch(self.segments[k])
 
     def replay_optimizer(self):
         self.opt.sync_hparams()
         _launch(self.opt_graph)
         self.opt._iterations += 1
+
+
+def _capture_is_empty() -> bool:
+    """True while the current stream's capture has recorded nothing since it began (no
+    dependency nodes): hipStreamGetCaptureInfo_v2 of the HIP runtime torch loaded."""
+    import ctypes
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_int(0)
+    cid = ctypes.c_ulonglong(0)
+    graph = ctypes.c_void_p()
+    deps = ctypes.c_void_p()
+    n = ctypes.c_size_t(0)
+    rc = _HIP.hipStreamGetCaptureInfo_v2(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), ctypes.byref(st),
+                                        ctypes.byref(cid), ctypes.byref(graph), ctypes.byref(deps), ctypes.byref(n))
+    if rc != 0 or st.value != 1:
+        raise RuntimeError(f"segmented capture: stream not capturing (hip error {rc}, status {st.value})")
+    return n.value == 0
+
+
+_HIP = None
 
 
 def _launch(g):

@@ -11,7 +11,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-me
 rc=$?; tail -4 $OUT/gputests.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
 rc=$?; tail -1 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
-j() { python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[1], d['value'], d['ms_per_step'])" $1; }
+j() { python -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]);print(sys.argv[1], d['value'], d['ms_per_step'])" $1; }
 b() { local tag=$1; shift; timeout -k 10 240 python bench.py "$@" > $OUT/$tag.json 2> $OUT/$tag.err || { echo "$tag failed"; tail -3 $OUT/$tag.err; return 1; }; j $OUT/$tag.json; }
 b b2560 --steps 20 --warmup 5 || exit 1
 [ "$MODE" = quick ] && exit 0

@@ -81,13 +81,17 @@ def run(B, two_stream, report):
     tot = {}
     per = []
     for k, g in enumerate(sg.segments):
+        if g is None:      # (bucket k completed with bucket k-1: no segment of its own)
+            per.append(0)
+            continue
         t = node_types(g)
         per.append(t.get(KERNEL, 0))
         for a, b in t.items():
             tot[a] = tot.get(a, 0) + b
     report(f"  kernel nodes per segment: {per} total {sum(per)}; all node types {tot}")
     for g in sg.segments:
-        g.instantiate()
+        if g is not None:
+            g.instantiate()
     sg.opt_graph.instantiate()
     sg.load(img, lab, None, (0, 0))
     eng.grads.fill_(12345.0)     # (segment 0 zeroes the workspace: the sentinel only checks that)

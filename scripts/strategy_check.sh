@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 bash scripts/strategy_bench.sh 1 30 256 || exit $?
 cp gpurun_out/strategy_bench.txt $OUT/
-j() { python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[1], d['value'], d['ms_per_step'])" $1; }
+j() { python -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]);print(sys.argv[1], d['value'], d['ms_per_step'])" $1; }
 b() { local tag=$1; shift; timeout -k 10 240 python bench.py "$@" > $OUT/$tag.json 2> $OUT/$tag.err || { echo "$tag failed"; tail -3 $OUT/$tag.err; return 1; }; j $OUT/$tag.json; }
 b mirrored_b32 --strategy mirrored --batch 32 --steps 60 --warmup 10 && \
 b mirrored_b32c244 --strategy mirrored --batch 32 --crop 244 --steps 60 --warmup 10 && \

@@ -103,9 +103,10 @@ def test_single_strategy_fit_with_hip_graph():
     assert all(map(lambda v: v == v, h.history["loss"]))
 
 
-def test_mirrored_strategy_one_gpu_uses_rccl():
+def test_mirrored_strategy_one_gpu_uses_rccl(monkeypatch):
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
+    monkeypatch.setenv("PDDL_MIRROR_SEGMENTED", "1")   # (the multi-replica schedule on 1 GPU)
     cfg = _cfg("mirrored")
     st = make_strategy(cfg)
     tr = Trainer(cfg, st)
@@ -127,12 +128,17 @@ def test_single_strategy_train_mode_bn_on_hip():
     assert h.history["loss"][0] == h.history["loss"][0]
 
 
-def test_mirrored_graphed_step_matches_eager():
-    """Mirrored with HIP graphs (default: per-device step segments split at the gradient
-    buckets, grouped all-reduce of bucket k between segment k and k+1, captured optimizer)
-    follows the eager Mirrored trajectory."""
+@pytest.mark.parametrize("segmented", [True, False])
+def test_mirrored_graphed_step_matches_eager(monkeypatch, segmented):
+    """Mirrored with HIP graphs follows the eager Mirrored trajectory.  segmented: the
+    multi-replica schedule (per-device step segments split at the gradient buckets, with the
+    two-stream backward, grouped all-reduce of bucket k between segment k and k+1, captured
+    optimizer), forced on this 1-replica job with PDDL_MIRROR_SEGMENTED=1; otherwise the
+    1-replica job's whole-step graph (no collective to run)."""
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
+    if segmented:
+        monkeypatch.setenv("PDDL_MIRROR_SEGMENTED", "1")
     res = []
     for graphs in (False, True):
         cfg = _cfg("mirrored", graphs=graphs, flip=False, max_steps=3, batch_size=8)
@@ -141,9 +147,12 @@ def test_mirrored_graphed_step_matches_eager():
         h = tr.fit(1, [], validation=False)
         res.append((h.history["loss"][0], st.engine.params.clone(), st.opt.iterations))
         assert st.mirror.graph_mode == graphs
-        if graphs:
+        if graphs and segmented:
             g = st.mirror.graphs[0]
-            assert g.captured and len(g.segments) == len(st.mirror.buckets) >= 2
+            assert g.captured and len(g.segments) == len(st.mirror.buckets) >= 2 and st.engine.side is not None
+            assert st.mirror.comm.watchdog_state()["issued"] >= 2 * len(st.mirror.buckets)
+        elif graphs:
+            assert st.mirror.graphs is None and st.mirror._whole.graph is not None
     (l0, p0, i0), (l1, p1, i1) = res
     assert i0 == i1 == 3
     assert abs(l0 - l1) <= 1e-3 * abs(l0)
@@ -222,6 +231,7 @@ def test_mirrored_on_init_rank_communicator(monkeypatch):
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
     monkeypatch.setenv("PDDL_RCCL_INIT", "rank")
+    monkeypatch.setenv("PDDL_MIRROR_SEGMENTED", "1")
     cfg = _cfg("mirrored", max_steps=4, batch_size=8)
     st = make_strategy(cfg)
     tr = Trainer(cfg, st)
