@@ -122,8 +122,8 @@ __global__ void __launch_bounds__(256, 2) c3c1_kernel(C3C1Params p) {
                            __uint_as_float(rv.y << 16), __uint_as_float(rv.y & 0xffff0000u)};
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc[i][jb][e] * sc[e] + sh[e] + r4[e], 0.f);
-      *slot = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][jb][e] * sc[e] + sh[e] + r4[e];
+      *slot = make_uint2(relu_pk2(pack2(v[0], v[1])), relu_pk2(pack2(v[2], v[3])));
     }
   }
   __syncthreads();
@@ -166,10 +166,10 @@ __global__ void __launch_bounds__(256, 2) c3c1_kernel(C3C1Params p) {
       const int row = 16 * i + r16;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc2[i][e] * sc[e] + sh[e], 0.f);
+      for (int e = 0; e < 4; ++e) v[e] = acc2[i][e] * sc[e] + sh[e];
       const int chunk = n >> 3;
       *reinterpret_cast<uint2*>(at + row * 128 + ((chunk ^ cc_sw(row)) << 4) + 8 * (kq & 1)) =
-          make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          make_uint2(relu_pk2(pack2(v[0], v[1])), relu_pk2(pack2(v[2], v[3])));
     }
   }
   __syncthreads();

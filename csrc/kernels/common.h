@@ -41,16 +41,39 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 
 // ReLU bitmask of 8 packed bf16 values: bit e = (value e > 0), i.e. nonzero with a clear
 // sign bit.  Derived from the stored (rounded) values so it matches a bf16 mask exactly.
+// Branch- and compare-free (19 VALU, was 31 with per-half compares and selects): per word,
+// t = ((w & 0x7fff7fff) + 0x7fff7fff) & ~w has bit 15 / 31 set exactly when the low / high
+// half is positive (magnitude nonzero, sign clear; no carry crosses the halves); v_perm's
+// sign-replicate selectors 8-11 turn those bits of two words into 0x00 / 0xff bytes, and a
+// dot4 against 1,1,1,1 of the bytes masked with 1,2,4,8 packs each group into a nibble.
 __device__ __forceinline__ uint32_t pos_bits8(const uint4& u) {
-  const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
-  uint32_t byte = 0;
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  uint32_t t[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const uint32_t lo = w4[e] & 0xffffu, hi = w4[e] >> 16;
-    byte |= (uint32_t)(lo != 0 && !(lo & 0x8000u)) << (2 * e);
-    byte |= (uint32_t)(hi != 0 && !(hi & 0x8000u)) << (2 * e + 1);
-  }
-  return byte;
+  for (int e = 0; e < 4; ++e) t[e] = ((w[e] & 0x7fff7fffu) + 0x7fff7fffu) & ~w[e];
+  const uint32_t s01 = __builtin_amdgcn_perm(t[1], t[0], 0x0b0a0908u);
+  const uint32_t s23 = __builtin_amdgcn_perm(t[3], t[2], 0x0b0a0908u);
+  const uint32_t n01 = __builtin_amdgcn_udot4(s01 & 0x08040201u, 0x01010101u, 0u, false);
+  const uint32_t n23 = __builtin_amdgcn_udot4(s23 & 0x08040201u, 0x01010101u, 0u, false);
+  return n01 | (n23 << 4);
+}
+
+// ReLU of 8 packed bf16 values in the integer domain: a bf16 orders like a sign-magnitude
+// int16, so max_i16(x, 0) zeroes exactly the negatives (and -0): 4 v_pk_max_i16 instead of 8
+// v_max_f32 before the pack.  Rounding is monotonic, so relu(round(v)) == round(relu(v)).
+__device__ __forceinline__ uint32_t relu_pk2(uint32_t u) {
+  typedef short v2s __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(v2s, u), v2s{0, 0}));
+}
+__device__ __forceinline__ uint4 relu_pk8(uint4 u) {
+  typedef short v2s __attribute__((ext_vector_type(2)));
+  const v2s z = {0, 0};
+  const v2s a = __builtin_elementwise_max(__builtin_bit_cast(v2s, u.x), z);
+  const v2s b = __builtin_elementwise_max(__builtin_bit_cast(v2s, u.y), z);
+  const v2s c = __builtin_elementwise_max(__builtin_bit_cast(v2s, u.z), z);
+  const v2s d = __builtin_elementwise_max(__builtin_bit_cast(v2s, u.w), z);
+  return make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c),
+                    __builtin_bit_cast(uint32_t, d));
 }
 
 // Buffer offset past every descriptor's range (record counts are clamped below 2 GiB; large

@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3c64_row8_kernel(C64Params p) {
         for (int e = 0; e < 4; ++e) {
           float x = acc[i][jl][e];
           if (MODE == C64_FWD) {
-            x = fmaxf(x * sc[jl][e] + sh[jl][e], 0.f);
+            x = x * sc[jl][e] + sh[jl][e];   // (ReLU on the packed pairs below)
           } else {
             x = ((mbits[i] >> (16 * jl + cq + e)) & 1u) ? x : 0.f;
             if (px_ok) csum[jl][e] += x;
@@ -229,8 +229,9 @@ __global__ void __launch_bounds__(512, 1) conv3x3c64_row8_kernel(C64Params p) {
           v[e] = x;
         }
         const int chunk = 2 * jl + (kq >> 1);
-        c64_wr8(stage + r16 * 64 + ((chunk ^ r8_sw(r16)) << 4) + 8 * (kq & 1),
-                make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3])));
+        uint2 pv = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if (MODE == C64_FWD) pv = make_uint2(relu_pk2(pv.x), relu_pk2(pv.y));
+        c64_wr8(stage + r16 * 64 + ((chunk ^ r8_sw(r16)) << 4) + 8 * (kq & 1), pv);
       }
       const int rr = lane >> 2, c = lane & 3;
       const uint4 pk = c64_rd16(stage + rr * 64 + ((c ^ r8_sw(rr)) << 4));

@@ -198,11 +198,8 @@ __device__ __forceinline__ void igemm_epilogue(const IgemmParams& p, v4f (&acc)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += rv[e];
           }
-          if (relu) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
-          const uint4 pk = pack8(v);
+          uint4 pk = pack8(v);
+          if (relu) pk = relu_pk8(pk);
           *reinterpret_cast<uint4*>(out + (long)gm * ldo + col) = pk;
           if (p.bits_out && seg0) {
             p.bits_out[(long)gm * p.ld_bits_out + (col >> 3)] = (uint8_t)pos_bits8(pk);
@@ -556,7 +553,7 @@ __device__ __forceinline__ int cdiv_signed(int a, int b) { return a >= 0 ? (a + 
 // (row & 3) | (row & 4) << 1 keeps those 16 positions distinct (conflict-free).
 __device__ __forceinline__ int pk_sw(int row) { return (row & 3) | ((row & 4) << 1); }
 
-template <int KT, int NB, bool OPS>
+template <int KT, int NB, bool OPS, bool FWD>
 __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmParams p) {
   constexpr int BM = 128, BN = 128, NW = 4, TM = 4, TN = 4, WAVES_N = 2;
   constexpr int A_BYTES = BM * 128, STAGE = A_BYTES + BN * 128;   // 32 KiB: A | B, or the operand tile
@@ -583,7 +580,8 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
 
   // launch-uniform epilogue configuration and the vector-memory op counts it implies
-  const bool is_fwd = p.mode == EPI_FWD;
+  // (FWD: one instantiation per epilogue mode, so neither carries the other's code)
+  constexpr bool is_fwd = FWD;
   const uint16_t* opnd = is_fwd ? p.res : p.add;
   const int ld_op = is_fwd ? p.ld_res : p.ld_add;
   const bool res_on = OPS && opnd != nullptr;
@@ -827,14 +825,11 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
         float ov[8];
         unpack8(make_uint4(ov4[k].x, ov4[k].y, ov4[k].z, ov4[k].w), ov);
         uint4 pk;
-        if (is_fwd) {
+        if constexpr (is_fwd) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e] + ov[e];
-          if (p.relu) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
           pk = pack8(v);
+          if (p.relu) pk = relu_pk8(pk);
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += ov[e];
@@ -1354,7 +1349,11 @@ static bool igemm_pk_launch(const IgemmParams& p, hipStream_t stream) {
   const int nb = g_igemm_pk;
   long G = (long)num_cus() * (nb == 2 ? 2 : 1);
   if (G > T) G = T;
-#define PK_GO(KT_, NB_) hipLaunchKernelGGL((igemm_pk_kernel<KT_, NB_, true>), dim3((unsigned)G), dim3(256), 0, stream, p);
+#define PK_GO(KT_, NB_)                                                                                      \
+  {                                                                                                          \
+    if (p.mode == EPI_FWD) hipLaunchKernelGGL((igemm_pk_kernel<KT_, NB_, true, true>), dim3((unsigned)G), dim3(256), 0, stream, p); \
+    else hipLaunchKernelGGL((igemm_pk_kernel<KT_, NB_, true, false>), dim3((unsigned)G), dim3(256), 0, stream, p); \
+  }
 #define PK_NB(KT_)                          \
   {                                         \
     if (nb == 2) PK_GO(KT_, 2)              \

@@ -116,8 +116,8 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
           const float sc[4] = {a.x, a.y, a.z, a.w}, sh[4] = {c.x, c.y, c.z, c.w};
           float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = fmaxf(acc[ntl][i] * sc[i] + sh[i], 0.f);
-          const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          for (int i = 0; i < 4; ++i) v[i] = acc[ntl][i] * sc[i] + sh[i];
+          const uint2 pk = make_uint2(relu_pk2(pack2(v[0], v[1])), relu_pk2(pack2(v[2], v[3])));
           *reinterpret_cast<uint2*>(crow + swz_chunk(4 * nt + lg, xl) * 8) = pk;
         }
       }
