@@ -86,8 +86,9 @@ def parse(argv=None):
                     help="frozen = the reference's training=False BN (folded); train = batch statistics")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--ps-wire", default="fp32", choices=["fp32", "bf16"],
-                    help="ps: element type of the gradient push / parameter pull over xGMI")
+    ap.add_argument("--ps-wire", default="bf16", choices=["fp32", "bf16"],
+                    help="ps: element type of the gradient push / parameter pull over xGMI (fp32 master weights and "
+                         "Adam on the PS either way)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="fp32: the reference's precision on the fp32-MFMA HIP convolutions (models/engine_f32.py)")
     ap.add_argument("--graph", type=int, default=None,
@@ -488,7 +489,7 @@ def run_ps(args):
                       optimizer="adam", lr=1e-3, bn_mode=args.bn_mode, device=args.device, data="synthetic",
                       steps_per_epoch=args.steps, validation_steps=0, epochs=2, save=False, verbose=0,
                       train_images=max(1_281_167, args.steps * args.batch), num_ps=n_ps, num_workers=n_w,
-                      ps_wire=args.ps_wire)
+                      ps_wire=args.ps_wire, graphs=None if args.graph is None else bool(args.graph))
     t0 = time.perf_counter()
     res = run_ps_job(cfg, num_ps=n_ps, num_workers=n_w, return_results=True)
     wall = time.perf_counter() - t0
@@ -507,7 +508,7 @@ def run_ps(args):
                    "per_gpu_batch": args.batch, "seq_len": None, "image_size": args.crop,
                    "parallelism": f"ps{n_ps}+w{n_w}", "strategy":
                    f"async parameter server: {n_ps} PS + {n_w} workers, native HIP-IPC push/pull, PS-side fused Adam",
-                   "replicas": n_w, "optimizer": "adam", "bn": args.bn_mode, "hip_graph": False,
+                   "replicas": n_w, "optimizer": "adam", "bn": args.bn_mode, "hip_graph": args.device == "cuda" and args.graph != 0,
                    "ps_wire": args.ps_wire,
                    "device": "cpu" if args.device == "cpu" else "MI355X",
                    "note": "ms_per_step = one synchronous-equivalent step of all workers; warmup = one untimed epoch"},

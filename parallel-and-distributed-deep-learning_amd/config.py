@@ -65,7 +65,8 @@ class TrainConfig:
     min_shard_bytes: int = 256 << 10               # MinSizePartitioner (ps.py:77)
     shard_by: str = "batch"                        # hvd: batch-then-shard (hvd.py:77-78); mwms: element DATA
     ps_overlap: bool = True                        # PS: a worker's push/pull round trip overlaps its next step
-    ps_wire: str = "fp32"                          # PS: gradient push / parameter pull element type (bf16 halves xGMI bytes)
+    ps_wire: str = "bf16"                          # PS: gradient push / parameter pull element type on GPU roles
+                                                   # (bf16 halves the xGMI bytes; fp32 master + Adam on the PS; CPU: fp32)
     # device / output
     device: str = "auto"                           # auto | cpu | cuda
     save: bool = True
@@ -73,6 +74,7 @@ class TrainConfig:
     checkpoint_every: int = 0                      # additive: periodic checkpoints (0 = off)
     resume: Optional[str] = None
     metrics_jsonl: Optional[str] = None
+    data_cache: Optional[str] = None               # tfds / folder data: decoded-image cache directory (--cache)
     baseline_ips: Optional[float] = None           # 1-GPU images/sec: the JSONL log adds scaling efficiency
     timeline: Optional[str] = None                 # chrome-trace JSON of the fusion engine
     graphs: Optional[bool] = None                  # HIP graphs: None = auto (on for Mirrored / local replicas)
@@ -140,6 +142,7 @@ def add_cli_args(ap: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--lr", type=float)
     a("--momentum", type=float)
     a("--data", type=str)
+    a("--cache", type=str, dest="data_cache")
     a("--steps-per-epoch", type=int, dest="steps_per_epoch")
     a("--validation-steps", type=int, dest="validation_steps")
     a("--max-steps", type=int, dest="max_steps")

@@ -12,7 +12,8 @@ Sources (no network on the target machines, so no tfds download):
     `<split>_labels.i64`), memory-mapped and gathered by the native loader thread pool
     (csrc/runtime/loader.cpp) into pinned buffers, then copied asynchronously to the GPU.
   * TFDSImageNet / JpegFolderImageNet (data/imagenet.py) — the reference's tfds TFRecord
-    shards or the untarred ILSVRC folders, decoded by the native reader (csrc/io).
+    shards or the untarred ILSVRC folders, decoded by the native reader (csrc/io); with
+    --cache <dir> behind a DecodedCache (decode once, then mmap gathers).
 """
 from __future__ import annotations
 
@@ -132,6 +133,102 @@ class RecordsImageNet(ImageSource):
         if torch.cuda.is_available():
             lab = lab.pin_memory()
         return buf.view(len(idx), S, S, 3), lab
+
+
+class DecodedCache(ImageSource):
+    """Decoded-image cache in front of a decoding source (tfds / folder): the reference's C6 map
+    (imagenet-resnet50.py:36-41: cast + resize_with_crop_or_pad to 224, all augmentation is
+    in-model) is deterministic per image, so its uint8 output can be kept.  The first time an
+    example is fetched it is decoded by the wrapped source and written into a memory-mapped
+    cache file (`<dir>/<split>-<S>.u8`, one S*S*3 row per example, plus `.i64` labels and a
+    `.ok` byte per example, set after the row is written); afterwards it is gathered from the
+    cache by the native loader thread pool into pinned memory, and the pipeline's prefetch
+    stage copies it to the device asynchronously, like raw records.  Example order stays the
+    pipeline's (a fresh permutation per epoch: the reference's shuffle_files=True).  Files are
+    sized once (sparse) and may be shared by every rank of a job: ranks write disjoint
+    examples, and a row is only read after its `.ok` byte."""
+    host = True
+
+    def __init__(self, inner: ImageSource, cache_dir: str, split: str, threads: int = 8):
+        import json
+        self.inner = inner
+        self.num_examples = inner.num_examples
+        self.image_size = inner.image_size
+        self.num_classes = inner.num_classes
+        S, N = self.image_size, self.num_examples
+        self.row = S * S * 3
+        os.makedirs(cache_dir, exist_ok=True)
+        stem = os.path.join(cache_dir, f"{split}-{S}")
+        meta = {"examples": N, "image_size": S, "source": type(inner).__name__,
+                "files": len(getattr(inner, "files", []) or [])}
+        mpath = stem + ".json"
+        if os.path.exists(mpath):
+            old = json.load(open(mpath))
+            if old != meta:
+                raise ValueError(f"decoded cache {stem}: made for {old}, not {meta} (use another --cache dir)")
+        else:
+            tmp = f"{mpath}.{os.getpid()}"
+            with open(tmp, "w") as f:
+                json.dump(meta, f)
+            os.replace(tmp, mpath)
+        self.paths = (stem + ".u8", stem + ".i64", stem + ".ok")
+        for path, nbytes in zip(self.paths, (N * self.row, N * 8, N)):
+            fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)
+            try:
+                if os.fstat(fd).st_size != nbytes:
+                    os.ftruncate(fd, nbytes)       # (sparse; same size again keeps the contents)
+            finally:
+                os.close(fd)
+        self.img = np.memmap(self.paths[0], dtype=np.uint8, mode="r+", shape=(N, self.row))
+        self.labels = np.memmap(self.paths[1], dtype=np.int64, mode="r+", shape=(N,))
+        self.ok = np.memmap(self.paths[2], dtype=np.uint8, mode="r+", shape=(N,))
+        self.threads = threads
+        self._loader = None
+        self.hits = 0
+        self.misses = 0
+
+    def _gather(self, idx: np.ndarray, out: torch.Tensor):
+        if self._loader is None:
+            from ..ops.native import native_available, require_native
+            self._loader = (require_native().Loader(self.paths[0], self.row, self.threads)
+                            if native_available() and hasattr(require_native(), "Loader") else False)
+        if self._loader:
+            self._loader.gather(torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)), out)
+        else:
+            out.copy_(torch.from_numpy(np.ascontiguousarray(self.img[idx])))
+
+    def fetch_host(self, idx: np.ndarray):
+        idx = np.asarray(idx, dtype=np.int64)
+        n, S = len(idx), self.image_size
+        hit = self.ok[idx] == 1
+        buf = torch.empty((n, self.row), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+        lab = torch.from_numpy(np.asarray(self.labels[idx]).copy())
+        if not hit.all():
+            miss = np.nonzero(~hit)[0]
+            im_m, lab_m = self.inner.fetch_host(idx[miss])
+            rows = im_m.reshape(len(miss), self.row)
+            buf[torch.from_numpy(miss)] = rows
+            lab[torch.from_numpy(miss)] = lab_m.to(torch.int64)
+            self.img[idx[miss]] = rows.numpy()
+            self.labels[idx[miss]] = lab_m.numpy().astype(np.int64)
+            self.ok[idx[miss]] = 1               # (after the row: a reader never sees half a row)
+            self.misses += len(miss)
+        if hit.any():
+            h = np.nonzero(hit)[0]
+            if len(h) == n:
+                self._gather(idx, buf)
+            else:
+                part = torch.empty((len(h), self.row), dtype=torch.uint8)
+                self._gather(idx[h], part)
+                buf[torch.from_numpy(h)] = part
+            self.hits += len(h)
+        if torch.cuda.is_available():
+            lab = lab.pin_memory()
+        return buf.view(n, S, S, 3), lab
+
+    def flush(self):
+        for m in (self.img, self.labels, self.ok):
+            m.flush()
 
 
 def write_records(root: str, split: str, images: np.ndarray, labels: np.ndarray) -> None:
@@ -298,10 +395,13 @@ def make_source(spec: str, split: str, cfg) -> ImageSource:
                                  fixed=spec == "synthetic_fixed")
     if spec.startswith("records:"):
         return RecordsImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+    cache = getattr(cfg, "data_cache", None)
     if spec.startswith("tfds:"):
         from .imagenet import TFDSImageNet
-        return TFDSImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+        src = TFDSImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+        return DecodedCache(src, cache, split) if cache else src
     if spec.startswith("folder:"):
         from .imagenet import JpegFolderImageNet
-        return JpegFolderImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+        src = JpegFolderImageNet(spec.split(":", 1)[1], split, cfg.image_size, cfg.num_classes)
+        return DecodedCache(src, cache, split) if cache else src
     raise ValueError(f"unknown data spec {spec!r} (synthetic | records:<dir> | tfds:<dir> | folder:<dir>)")

@@ -185,6 +185,10 @@ class _LockedStore:
         with self._lock:
             return self._s.compare_set(k, expected, desired)
 
+    def multi_set(self, keys, values):
+        with self._lock:
+            return self._s.multi_set(keys, values)
+
 
 class _Heartbeat:
     """A worker's liveness beacon (the coordinator's worker-failure watch): a daemon thread
@@ -195,8 +199,13 @@ class _Heartbeat:
     declared dead and its ticket re-queued exactly like a crashed one.  `stall_s` is its own
     threshold (PDDL_PS_STEP_STALL), separate from and larger than the coordinator's liveness
     timeout `hb_timeout`: a slow but healthy step (a cold first batch from real data, a PS slowed
-    by many workers) keeps beating.  A worker still stuck `stall_s + 2 * hb_timeout` into a step
-    -- its ticket re-queued by then -- ends itself."""
+    by many workers) keeps beating.  A worker still stuck `stall_s + hb_timeout / 2` into a step
+    ends itself: the coordinator declares it dead (and re-queues its tickets) no earlier than
+    `stall_s + hb_timeout` (the last stamp is at most one period older than `stall_s`), so a
+    stalled worker is gone before its tickets can run twice -- a worker that exited only after
+    the re-queue could wake up in between and push a gradient for a re-queued ticket, or count
+    its steps into done/<epoch> a second time.  (The worker also checks dead/<rank> before it
+    publishes a finished block of tickets.)"""
 
     def __init__(self, store, rank: int, period: float, stall_s: float, hb_timeout: Optional[float] = None):
         self.store, self.rank, self.period, self.stall_s = store, rank, period, stall_s
@@ -226,12 +235,11 @@ class _Heartbeat:
     def _run(self):
         while not self._stop.wait(self.period):
             if not self.healthy():
-                # stalled inside a step: let the coordinator's watch expire; past twice the
-                # timeout the ticket has been re-queued, and a worker that may still wake up and
-                # push a stale gradient is worse than a dead one -- end the process (fail fast)
+                # stalled inside a step: the stamps stop; end the process before the
+                # coordinator's watch expires (see the class docstring)
                 with self._lock:
                     stuck = time.time() - self._since
-                if stuck > self.stall_s + 2 * self.hb_timeout:
+                if stuck > self.stall_s + 0.5 * self.hb_timeout:
                     sys.stderr.write(f"[ps worker rank {self.rank}] stuck in a step for {stuck:.0f} s "
                                      f"(step stall {self.stall_s:g} s, heartbeat timeout {self.hb_timeout:g} s): "
                                      "exiting\n")
@@ -291,9 +299,11 @@ def requeue_orphans(store, epoch: int, live_workers: List[int]) -> List[int]:
     held = set()
     for r in live_workers:
         if store.check([f"cur/{r}"]):
-            ep, t = (int(x) for x in store.get(f"cur/{r}").decode().split(":"))
-            if ep == epoch and t >= 0:
-                held.add(t)
+            f = [int(x) for x in store.get(f"cur/{r}").decode().split(":")]
+            ep, lo = f[0], f[1]
+            hi = f[2] if len(f) > 2 else lo + 1     # "<epoch>:<lo>:<hi>": a claimed block of tickets
+            if ep == epoch and lo >= 0:
+                held.update(range(lo, hi))
     out = []
     for t in _missing_tickets(store, epoch, 0, _claimed(store, epoch)):
         if t in held:
@@ -519,6 +529,27 @@ class _PSControl:
         print(msg, flush=True)
 
 
+def claim_block(store, spe: int, epoch: int, rank: int, block: int, workers: int) -> Tuple[int, int]:
+    """Claim up to `block` consecutive step tickets of `epoch` with one compare-and-set
+    ([lo, hi), or (-1, -1) while the epoch's tickets are exhausted): a worker pays the control
+    plane's round trips once per block instead of once per step.  Near the end of the epoch the
+    block shrinks to an even share of what is left (no worker sits on a long tail while the
+    others idle).  Same counter and re-queue budget as _claim."""
+    key = f"claim/{epoch}"
+    raw = store.compare_set(key, "", "0/-1").decode()
+    while True:
+        cur = int(raw.split("/")[0])
+        budget = spe + store.add(f"requeue/{epoch}", 0)
+        if cur >= budget:
+            return -1, -1
+        n = max(1, min(block, (budget - cur) // max(1, 2 * workers)))
+        want = f"{cur + n}/{rank}"
+        got = store.compare_set(key, raw, want).decode()
+        if got == want:
+            return cur, cur + n
+        raw = got
+
+
 def _claim(store, spe: int, epoch: int, rank: int) -> int:
     """Claim the next step ticket of `epoch`; -1 while the epoch's tickets are exhausted
     (re-queued tickets of dead workers extend the budget, so callers poll).  A claim is one
@@ -586,17 +617,12 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         dist.destroy_process_group()
         return
     # ---------------------------------------------------------------- worker
-    eng = build_engine(cfg, device, max(cfg.batch_size, cfg.val_batch_size or 0))
-    eng.init(seed=cfg.seed)
-    if cfg.weights and cfg.weights != "none":
-        from ..utils.checkpoint import load_pretrained
-        load_pretrained(cfg.weights, eng)
-        eng.after_update()
+    st = ParameterServerStrategy(cfg, cluster=cl)
+    st.setup(None)
+    eng, worker, widx = st.engine, st.worker, st.widx
     from ..data.datasets import Pipeline, make_source
-    widx = rank - num_ps
     src = make_source(cfg.data, "train", cfg)
     pipe = Pipeline(src, cfg.batch_size, repeat=True, shuffle=cfg.data != "synthetic", seed=cfg.seed + 17 * widx)
-    worker = PSWorker(cl, eng, None)
     dist.barrier()
     lr = cfg.lr
     worker._exchange(OP_PULL, lr)                     # initial pull (variables live on the PS)
@@ -609,9 +635,8 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     step_stall = float(os.environ.get("PDDL_PS_STEP_STALL", str(max(300.0, 10 * hb_timeout))))
     hb = _Heartbeat(store, rank, max(0.05, hb_timeout / 6), step_stall, hb_timeout)
     epoch_timeout = float(os.environ.get("PDDL_PS_EPOCH_TIMEOUT", str(max(600.0, 10 * hb_timeout))))
+    block = max(1, int(os.environ.get("PDDL_PS_TICKET_BLOCK", "16")))
     it = pipe.iterate(device)
-    from .strategies import Augment
-    aug = Augment(cfg, device, cfg.seed + 7919 * widx)
     history = []
     steps_done = 0
     ctl = _PSControl(lr)
@@ -632,12 +657,14 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             break
         if store.check(["lr"]):
             lr = float(store.get("lr").decode())
-        acc = torch.zeros(3, dtype=torch.float64)
+        st.begin_epoch()
         t_epoch = time.perf_counter()
         t_drained = None
         while True:
-            t = _claim(store, spe, epoch, rank)
-            if t < 0:
+            # tickets are claimed in blocks: the control plane costs a few round trips per
+            # block, none per step (no host / device synchronisation inside a block either)
+            lo, hi = claim_block(store, spe, epoch, rank, block, cl.num_workers)
+            if lo < 0:
                 # out of tickets: the epoch ends when every ticket is DONE; until then a ticket
                 # of a worker that died holding it may be re-queued by the coordinator
                 hb.wait()
@@ -654,35 +681,35 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
                 continue
             t_drained = None
             hb.step()
-            store.set(f"cur/{rank}", f"{epoch}:{t}")
-            if fault_at is not None and steps_done == fault_at[1]:
-                print(f"[worker {widx}] injected {fault_at[0]} at step {steps_done}", flush=True)
-                if fault_at[0] == "kill_worker":
-                    os._exit(17)
-                while True:                       # hang_worker: stuck inside the step
-                    time.sleep(3600)
-            images, labels = next(it)
-            B = images.shape[0]
-            flip, off = aug(B)
-            s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off)
-            acc[:2] += s.detach().double().cpu()
-            acc[2] += B
-            if cfg.ps_overlap:
-                worker.exchange_end()            # the previous push's fresh parameters
-                worker.exchange_begin(lr)        # this push flies while the next step computes
-            else:
-                worker._exchange(OP_PUSH, lr)
-            store.set(f"tdone/{epoch}/{t}", "1")
+            store.set(f"cur/{rank}", f"{epoch}:{lo}:{hi}")
+            for _t in range(lo, hi):
+                hb.step()
+                if fault_at is not None and steps_done == fault_at[1]:
+                    print(f"[worker {widx}] injected {fault_at[0]} at step {steps_done}", flush=True)
+                    if fault_at[0] == "kill_worker":
+                        os._exit(17)
+                    while True:                       # hang_worker: stuck inside the step
+                        time.sleep(3600)
+                images, labels = next(it)
+                st.train_step(images, labels, lr)
+                steps_done += 1
+            if store.check([f"dead/{rank}"]):
+                # declared dead while running this block (its tickets are re-queued): publishing
+                # them now would count them twice
+                sys.stderr.write(f"[ps worker rank {rank}] declared dead by the coordinator: exiting\n")
+                sys.stderr.flush()
+                os._exit(18)
+            store.multi_set([f"tdone/{epoch}/{t}" for t in range(lo, hi)], ["1"] * (hi - lo))
             store.set(f"cur/{rank}", f"{epoch}:-1")
-            store.add(f"done/{epoch}", 1)
-            steps_done += 1
+            store.add(f"done/{epoch}", hi - lo)
         hb.step()
         worker.exchange_end()                    # drain the last overlapped push of the epoch
         hb.wait()
         # epoch end: worker 0 (coordinator-side logic) validates and runs the callbacks
-        store.add(f"acc/{epoch}/loss", int(acc[0].item() * 1e6))
-        store.add(f"acc/{epoch}/correct", int(acc[1].item()))
-        store.add(f"acc/{epoch}/n", int(acc[2].item()))
+        loss_sum, correct, n_img = st.end_epoch()       # (the epoch's one device -> host read)
+        store.add(f"acc/{epoch}/loss", int(loss_sum * 1e6))
+        store.add(f"acc/{epoch}/correct", int(correct))
+        store.add(f"acc/{epoch}/n", int(n_img))
         store.add(f"epoch_end/{epoch}", 1)
         if widx == 0:
             _wait_count(store, f"epoch_end/{epoch}", lambda: cl.num_workers - store.add("dead_workers", 0))
@@ -816,8 +843,79 @@ def run_ps_job(cfg, num_ps: Optional[int] = None, num_workers: Optional[int] = N
 
 
 class ParameterServerStrategy:
-    """Marker so `make_strategy(cfg)` can name the PS strategy; training runs through
-    `run_ps_job` (roles are processes, not a single fit loop)."""
+    """ParameterServerStrategy + ClusterCoordinator (imagenet-resnet50-ps.py:75-84) behind the
+    strategy interface.  The job's roles are processes (run_job / run_ps_job spawns the
+    in-process cluster); in a WORKER role this object is the worker's strategy: setup builds
+    the engine, the native push/pull client and -- on the GPU -- the forward + backward as one
+    HIP graph; train_step runs one step (graph replay, device-side loss / accuracy sums, the
+    overlapped gradient push + parameter pull); end_epoch reads the epoch's sums once."""
+    name = "ps"
 
-    def __init__(self, cfg):
+    def __init__(self, cfg, cluster: Optional[_Cluster] = None):
         self.cfg = cfg
+        self.cl = cluster
+        self.engine = None
+
+    @property
+    def num_replicas_in_sync(self) -> int:
+        return self.cfg.num_workers
+
+    @property
+    def is_chief(self) -> bool:
+        return self.cl is None or self.cl.rank == self.cl.num_ps
+
+    def run_job(self):
+        return run_ps_job(self.cfg)
+
+    # ------------------------------------------------------------------ worker role
+    def setup(self, trainer=None):
+        from .strategies import Augment, build_engine
+        cfg, cl = self.cfg, self.cl
+        if cl is None or cl.is_ps:
+            raise RuntimeError("ParameterServerStrategy.setup runs in a worker role of run_ps_job")
+        self.device = cl.device
+        eng = build_engine(cfg, cl.device, max(cfg.batch_size, cfg.val_batch_size or 0))
+        eng.init(seed=cfg.seed)
+        if cfg.weights and cfg.weights != "none":
+            from ..utils.checkpoint import load_pretrained
+            load_pretrained(cfg.weights, eng)
+            eng.after_update()
+        self.engine = eng
+        self.worker = PSWorker(cl, eng, None)
+        self.widx = cl.rank - cl.num_ps
+        self.aug = Augment(cfg, cl.device, cfg.seed + 7919 * self.widx)
+        self.graphed = None
+        if cl.device.type == "cuda" and hasattr(eng, "wbf") and cfg.graphs is not False:
+            from ..train.graph import GraphedTrainStep   # forward + backward as one HIP graph
+            self.graphed = GraphedTrainStep(eng, None, cfg.batch_size, (cfg.image_size, cfg.image_size),
+                                            1.0 / cfg.batch_size, with_optimizer=False)
+        self.acc = torch.zeros(2, dtype=torch.float64, device=cl.device)
+        self.n_img = 0
+
+    def begin_epoch(self):
+        self.acc.zero_()
+        self.n_img = 0
+
+    def train_step(self, images, labels, lr: float):
+        eng, B = self.engine, images.shape[0]
+        flip, off = self.aug(B)
+        g = self.graphed
+        if g is not None and B == g.B and tuple(images.shape[1:3]) == tuple(g.images.shape[1:3]):
+            s = g(images, labels, flip, off)
+        else:
+            s = eng.forward_backward(images, labels, 1.0 / B, flip=flip, crop_offset=off)
+        self.acc.add_(s[:2])            # (device-side: no per-step device -> host read)
+        self.n_img += B
+        if self.cfg.ps_overlap:
+            self.worker.exchange_end()            # the previous push's fresh parameters
+            self.worker.exchange_begin(lr)        # this push flies while the next step computes
+        else:
+            self.worker._exchange(OP_PUSH, lr)
+        return s
+
+    def end_epoch(self):
+        a = self.acc.cpu()
+        return float(a[0]), float(a[1]), self.n_img
+
+    def set_lr(self, lr: float):
+        self.cfg = self.cfg.replace(lr=lr)

@@ -80,8 +80,8 @@ def _new_graph(**kw):
     return torch.cuda.CUDAGraph(**kw)
 
 class GraphedTrainStep:
-    """with_optimizer=False records forward + backward only (Mirrored: the cross-device
-    all-reduce runs between the replay and an eager optimizer step)."""
+    """with_optimizer=False records forward + backward only (optimizer may then be None: the
+    parameter-server worker, whose update runs on the PS)."""
 
     def __init__(self, engine, optimizer, batch: int, image_hw: Tuple[int, int], gscale: float,
                  image_dtype=torch.uint8, with_optimizer: bool = True):
@@ -129,11 +129,12 @@ class GraphedTrainStep:
         if self.with_optimizer:
             self.opt.sync_hparams()
         torch.cuda.synchronize()
-        it = self.opt._iterations
+        it = self.opt._iterations if self.opt is not None else 0
         g = _new_graph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             self.stats = self._body()
-        self.opt._iterations = it    # the capture pass did not step (no setter: hs is current)
+        if self.opt is not None:
+            self.opt._iterations = it    # the capture pass did not step (no setter: hs is current)
         self.graph = g
         if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
             _glog(f"whole-step graph captured: {_exec_layout(g)}")

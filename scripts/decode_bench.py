@@ -5,6 +5,8 @@ imagenet-resnet50.py:44-49).
 
     python scripts/decode_bench.py --images 2048 --threads 1,2,4,8,16 --json gpurun_out/decode.json
     python scripts/decode_bench.py --train-steps 20 --batch 256          # + the GPU step comparison
+    python scripts/decode_bench.py --train-steps 30 --batch 256 --crop 244 --cache-threads 8
+        # + a decoded-image cache (data/datasets.py DecodedCache) warmed once, then fed to the step
 
 Data: photo-like synthetic JPEGs (smooth gradients + noise, ImageNet-typical 500x375, quality 90)
 written as tfds-style TFRecord shards into a temp dir (no dataset download is possible), then
@@ -46,6 +48,9 @@ def main():
     ap.add_argument("--threads", default="1,2,4,8,16")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--train-steps", type=int, default=0, help="GPU: also compare step time vs synthetic")
+    ap.add_argument("--crop", type=int, default=224, help="network input of the step comparison (244: the presets)")
+    ap.add_argument("--cache-threads", type=int, default=0,
+                    help="also feed the step from a warm decoded-image cache gathered by this many threads")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     import torch
@@ -101,7 +106,7 @@ def main():
         from pddl.config import make_config
         from pddl.parallel.strategies import make_strategy
         from pddl.train.trainer import Trainer
-        cfg = make_config("single", device="cuda", batch_size=B, crop=224, image_size=224, save=False, verbose=0,
+        cfg = make_config("single", device="cuda", batch_size=B, crop=a.crop, image_size=224, save=False, verbose=0,
                           data=f"records:{recdir}", train_images=a.images)
         st = make_strategy(cfg)
         Trainer(cfg, st)
@@ -130,8 +135,27 @@ def main():
                 ep += 1
         ms_syn = run(synthetic())
         ms_rec = run(records())
-        emit({"kind": "train_step", "batch": B, "synthetic_ms": round(ms_syn, 2), "records_ms": round(ms_rec, 2),
-              "ratio": round(ms_rec / ms_syn, 3)})
+        row = {"kind": "train_step", "batch": B, "crop": a.crop, "synthetic_ms": round(ms_syn, 2),
+               "records_ms": round(ms_rec, 2), "ratio": round(ms_rec / ms_syn, 3)}
+        if a.cache_threads:
+            from pddl.data.datasets import DecodedCache
+            cache = DecodedCache(TFDSImageNet(tmp, "train", 224, threads=a.cache_threads),
+                                 os.path.join(tmp, "cache"), "train", threads=a.cache_threads)
+            t0 = time.perf_counter()
+            for i in range(n_b):                          # first epoch: decode + write the cache
+                cache.fetch_host(np.arange(i * B, (i + 1) * B))
+            row["cache_fill_images_per_sec"] = round(n_b * B / (time.perf_counter() - t0), 1)
+
+            def cached():
+                ep = 0
+                while True:
+                    for b in Pipeline(cache, B, shuffle=True, seed=5).iterate(st.device, epoch=ep):
+                        yield b
+                    ep += 1
+            ms_c = run(cached())
+            row.update(cache_ms=round(ms_c, 2), cache_ratio=round(ms_c / ms_syn, 3), cache_threads=a.cache_threads,
+                       cache_hits=cache.hits, cache_misses=cache.misses)
+        emit(row)
     if a.json:
         json.dump(rows, open(a.json, "w"), indent=1)
 

@@ -98,3 +98,44 @@ def test_folder_reader_and_pipeline(tmp_path):
     assert lab.tolist() == [0, 1]
     want = resize_with_crop_or_pad(_pil_rgb(jpegs[1]), 96).astype(np.int16)
     assert np.abs(img[0].numpy().astype(np.int16) - want).mean() < 1.5
+
+
+def test_decoded_cache_is_bitwise_the_decoded_batches(tmp_path):
+    """--cache <dir>: the first fetch of an example decodes it (native reader + C6 crop-or-pad)
+    and writes it to the memory-mapped cache; later fetches gather it from the cache.  Cached,
+    half-cached and decoded batches are bitwise equal, labels included, and a second cache object
+    on the same directory (another rank / a later run) starts warm."""
+    from pddl.config import make_config
+    from pddl.data.datasets import DecodedCache, Pipeline, make_source
+    from pddl.data.imagenet import TFDSImageNet, write_tfrecord_imagenet
+    rng = np.random.default_rng(1)
+    jpegs = _images(rng) * 2
+    labels = list(range(100, 100 + len(jpegs)))
+    d = tmp_path / "tfds"
+    d.mkdir()
+    write_tfrecord_imagenet(str(d / "imagenet2012-train.tfrecord-00000-of-00001"), jpegs, labels)
+    ref = TFDSImageNet(str(d), "train", image_size=224, threads=2)
+    cfg = make_config("single", data=f"tfds:{d}", image_size=224, crop=224, device="cpu")
+    cfg = cfg.replace(data_cache=str(tmp_path / "cache"))
+    src = make_source(cfg.data, "train", cfg)
+    assert isinstance(src, DecodedCache) and src.num_examples == len(jpegs)
+    want_i, want_l = ref.fetch_host(np.arange(len(jpegs)))
+    a = np.array([3, 1, 7])
+    i1, l1 = src.fetch_host(a)                         # all misses: decode + write
+    assert src.misses == 3 and src.hits == 0
+    assert torch.equal(i1, want_i[a]) and torch.equal(l1, want_l[a])
+    b = np.array([7, 0, 3, 11])                        # mixed: 2 hits, 2 misses
+    i2, l2 = src.fetch_host(b)
+    assert src.hits == 2 and src.misses == 5
+    assert torch.equal(i2, want_i[b]) and torch.equal(l2, want_l[b])
+    src.flush()
+    warm = DecodedCache(TFDSImageNet(str(d), "train", image_size=224, threads=2), str(tmp_path / "cache"), "train")
+    i3, l3 = warm.fetch_host(b)                        # all hits, gathered by the native loader
+    assert warm.hits == 4 and warm.misses == 0
+    assert torch.equal(i3, want_i[b]) and torch.equal(l3, want_l[b])
+    # through the prefetching pipeline: two epochs, identical batches whatever the cache state
+    p = Pipeline(src, 4, shuffle=True, seed=3)
+    for ep in range(2):
+        for (im, lb), idx in zip(p.iterate("cpu", epoch=ep), p.batches(ep)):
+            assert torch.equal(im, want_i[idx]) and torch.equal(lb, want_l[idx])
+    assert src.ok.all()

@@ -203,8 +203,8 @@ def test_resume_continues_epochs_lr_and_callbacks(tmp_path):
 def test_ps_stalled_worker_declared_dead_and_requeued(monkeypatch):
     """A LIVE worker stuck inside a step (hang_worker) stops heartbeating (the beacon stamps
     only while the main loop makes progress), is declared dead, its ticket is re-queued and
-    the epoch completes; the stuck process ends itself after the step-stall threshold plus twice
-    the heartbeat timeout."""
+    the epoch completes; the stuck process ends itself after the step-stall threshold plus half
+    the heartbeat timeout (before the coordinator can declare it dead)."""
     from pddl.parallel.parameter_server import run_ps_job
     monkeypatch.setenv("PDDL_FAULT", "hang_worker:1@1")
     monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
@@ -270,3 +270,30 @@ def test_ps_resume_rejected(tmp_path):
                         "--resume", str(tmp_path / "x.h5"), "--device", "cpu"], cwd=ROOT, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 2 and "--resume is not supported for --strategy ps" in r.stderr, r.stderr[-2000:]
+
+
+def test_claim_block_shares_the_tail_and_requeue_sees_held_blocks():
+    """Step tickets are claimed in blocks (one compare-and-set per block); near the end of the
+    epoch the block shrinks to an even share of what is left; a live worker's claimed block
+    (cur = <epoch>:<lo>:<hi>) is never re-queued, an unpublished block of a dead worker is."""
+    import torch.distributed as dist
+    from pddl.parallel.parameter_server import claim_block, requeue_orphans
+    st = dist.HashStore()
+    assert claim_block(st, 100, 0, 3, 16, 2) == (0, 16)
+    assert claim_block(st, 100, 0, 4, 16, 2) == (16, 32)
+    lo, hi = 32, 32
+    while True:                                   # drain: blocks shrink to (left) // (2 * workers)
+        a, b = claim_block(st, 100, 0, 3, 16, 2)
+        if a < 0:
+            break
+        assert a == hi and b - a == max(1, min(16, (100 - a) // 4))
+        lo, hi = a, b
+    assert hi == 100
+    for t in range(0, 16):
+        st.set(f"tdone/0/{t}", "1")               # worker 3's first block published
+    st.set("cur/4", "0:16:32")                    # live worker 4 still holds [16, 32)
+    for t in range(32, 100):
+        st.set(f"tdone/0/{t}", "1")
+    assert requeue_orphans(st, 0, [4]) == []      # nothing orphaned while worker 4 lives
+    assert requeue_orphans(st, 0, []) == list(range(16, 32))   # worker 4 died: its block comes back
+    assert claim_block(st, 100, 0, 3, 16, 2)[0] == 100          # the re-queue extends the budget
