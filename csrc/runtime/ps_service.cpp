@@ -10,9 +10,12 @@
 //   * Data plane over xGMI with HIP IPC (dmabuf): a worker's pack kernel gathers its gradient
 //     ranges and writes them STRAIGHT into its mailbox slot on the PS GPU (peer writes), then
 //     bumps its request sequence number.  The PS service thread sees the request, ENQUEUES the
-//     fused Adam kernel (optim.hip, TF epsilon-hat form) on the mailbox and the copy of the
-//     fresh shard into the worker's receive buffer on the worker GPU (peer copy) on the PS
-//     stream, records the worker's completion event and moves on to the next request; `done`
+//     fused Adam kernel (optim.hip, TF epsilon-hat form) on the mailbox, which also writes the
+//     requester's own snapshot buffer of the fresh shard, on the PS stream; the copy of that
+//     snapshot into the worker's receive buffer on the worker GPU (peer copy over the worker's
+//     xGMI link) runs on the worker's own copy stream, so the PS stream serialises only the
+//     updates while the copies to different workers proceed in parallel over their links.  It
+//     records the worker's completion event and moves on to the next request; `done`
 //     is published when that event has completed (the service thread never blocks on the
 //     device, so the Adam / copy work of several workers' requests queues back to back on the
 //     PS GPU).  Updates are applied one at a time in arrival order on the PS stream, so every
@@ -145,10 +148,13 @@ class PSServer {
       hck(hipMemcpy(params_, host.data_ptr<float>(), n_real_ * sizeof(float), hipMemcpyHostToDevice), "init copy");
       hck(hipMalloc(&mailbox_, (size_t)W_ * n_ * esz), "malloc mailbox");
       hck(hipMemset(mailbox_, 0, (size_t)W_ * n_ * esz), "memset mailbox");
-      if (wire_) {   // the bf16 snapshot the pulls copy, kept current by every update
-        hck(hipMalloc(&snap_, n_ * sizeof(uint16_t)), "malloc snapshot");
-        kck(pddl::cast_bf16_launch(params_, snap_, n_, nullptr), "snapshot cast");
-      }
+      // per-worker snapshot buffers: request r of worker w writes ITS snapshot into snap_[w]
+      // on the PS stream, then the copy to w's receive buffer runs on w's own copy stream over
+      // w's xGMI link while the PS stream goes on with the next request (w's next request --
+      // the only writer of snap_[w] -- comes after w saw this one done)
+      hck(hipMalloc(&snap_, (size_t)W_ * n_ * esz), "malloc snapshots");
+      cstream_.assign(W_, nullptr);
+      for (auto& cs : cstream_) hck(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "copy stream");
       hipIpcMemHandle_t mh;
       hck(hipIpcGetMemHandle(&mh, mailbox_), "ipc handle");
       std::memcpy(ctrl_->mailbox_handle, &mh, sizeof(mh));
@@ -156,8 +162,10 @@ class PSServer {
       rx_ptr_.assign(W_, nullptr);
       done_ev_.assign(W_, nullptr);
       start_ev_.assign(W_, nullptr);
+      snap_ev_.assign(W_, nullptr);
       for (auto& e : done_ev_) hck(hipEventCreate(&e), "event");   // (timed: per-request service time)
       for (auto& e : start_ev_) hck(hipEventCreate(&e), "event");
+      for (auto& e : snap_ev_) hck(hipEventCreate(&e), "event");
     } else {
       host_.assign(3 * n_, 0.f);
       std::memcpy(host_.data(), host.data_ptr<float>(), n_real_ * sizeof(float));
@@ -176,6 +184,8 @@ class PSServer {
       for (void* r : rx_ptr_) if (r) hipIpcCloseMemHandle(r);
       for (auto e : done_ev_) if (e) hipEventDestroy(e);
       for (auto e : start_ev_) if (e) hipEventDestroy(e);
+      for (auto e : snap_ev_) if (e) hipEventDestroy(e);
+      for (auto cs : cstream_) if (cs) hipStreamDestroy(cs);
       if (mailbox_) hipFree(mailbox_);
       if (snap_) hipFree(snap_);
       if (params_) hipFree(params_);
@@ -194,9 +204,11 @@ class PSServer {
   py::dict service_stats() const {
     py::dict d;
     d["requests"] = svc_n_;
-    d["mean_ms"] = svc_n_ ? svc_sum_ms_ / svc_n_ : 0.0;
+    d["mean_ms"] = svc_n_ ? svc_sum_ms_ / svc_n_ : 0.0;          // start of Adam -> copy landed
     d["max_ms"] = svc_max_ms_;
     d["total_ms"] = svc_sum_ms_;
+    d["busy_mean_ms"] = svc_n_ ? busy_sum_ms_ / svc_n_ : 0.0;     // the PS stream's share (serialised)
+    d["busy_total_ms"] = busy_sum_ms_;
     d["shard_elems"] = n_real_;
     return d;
   }
@@ -223,7 +235,8 @@ class PSServer {
       started_[w] = true;
       if (wire_)
         kck(pddl::adam_bf16_wire_launch(params_, static_cast<const uint16_t*>(mailbox_) + (size_t)w * n_, m_, v_,
-                                        snap_, n_, (float)lr_t, (float)b1_, (float)b2_, (float)eps_, stream_),
+                                        static_cast<uint16_t*>(snap_) + (size_t)w * n_, n_, (float)lr_t, (float)b1_,
+                                        (float)b2_, (float)eps_, stream_),
             "adam (bf16 wire)");
       else
         kck(pddl::adam_launch(params_, g, m_, v_, n_, (float)lr_t, (float)b1_, (float)b2_, (float)eps_, 1.f, nullptr,
@@ -249,13 +262,25 @@ class PSServer {
         hck(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "open rx handle");
         rx_ptr_[w] = ptr;
       }
-      if (!started_[w]) hck(hipEventRecord(start_ev_[w], stream_), "record start");   // (pull: copy only)
+      const bool pushed = started_[w];
+      if (!started_[w]) hck(hipEventRecord(start_ev_[w], stream_), "record start");   // (pull: snapshot only)
       started_[w] = false;
-      if (wire_)
-        hck(hipMemcpyAsync(rx_ptr_[w], snap_, n_ * sizeof(uint16_t), hipMemcpyDeviceToDevice, stream_), "snapshot");
-      else
-        hck(hipMemcpyAsync(rx_ptr_[w], params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
-      hck(hipEventRecord(done_ev_[w], stream_), "record done");
+      // w's snapshot of the shard as of this point of the PS stream (bf16 push: written by the
+      // fused Adam already), then the cross-link copy on w's copy stream
+      if (wire_) {
+        uint16_t* sw = static_cast<uint16_t*>(snap_) + (size_t)w * n_;
+        if (!pushed) kck(pddl::cast_bf16_launch(params_, sw, n_, stream_), "snapshot cast");
+        hck(hipEventRecord(snap_ev_[w], stream_), "record snapshot");
+        hck(hipStreamWaitEvent(cstream_[w], snap_ev_[w], 0), "copy stream wait");
+        hck(hipMemcpyAsync(rx_ptr_[w], sw, n_ * sizeof(uint16_t), hipMemcpyDeviceToDevice, cstream_[w]), "snapshot");
+      } else {
+        float* sw = static_cast<float*>(snap_) + (size_t)w * n_;
+        hck(hipMemcpyAsync(sw, params_, n_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "snapshot");
+        hck(hipEventRecord(snap_ev_[w], stream_), "record snapshot");
+        hck(hipStreamWaitEvent(cstream_[w], snap_ev_[w], 0), "copy stream wait");
+        hck(hipMemcpyAsync(rx_ptr_[w], sw, n_ * sizeof(float), hipMemcpyDeviceToDevice, cstream_[w]), "snapshot");
+      }
+      hck(hipEventRecord(done_ev_[w], cstream_[w]), "record done");
     } else {
       std::memcpy(static_cast<float*>(rx_shm_.ptr) + (size_t)w * n_, params_, n_ * sizeof(float));
     }
@@ -270,10 +295,12 @@ class PSServer {
             const hipError_t q = hipEventQuery(done_ev_[w]);
             if (q == hipErrorNotReady) return false;
             hck(q, "completion event");
-            float ms = 0.f;   // GPU time of this request's Adam + snapshot copy (both events are in-stream)
-            if (hipEventElapsedTime(&ms, start_ev_[w], done_ev_[w]) == hipSuccess) {
+            float ms = 0.f, busy = 0.f;   // request: Adam start -> copy landed; busy: the PS stream's part
+            if (hipEventElapsedTime(&ms, start_ev_[w], done_ev_[w]) == hipSuccess &&
+                hipEventElapsedTime(&busy, start_ev_[w], snap_ev_[w]) == hipSuccess) {
               svc_n_++;
               svc_sum_ms_ += ms;
+              busy_sum_ms_ += busy;
               svc_max_ms_ = std::max(svc_max_ms_, (double)ms);
             }
             return true;
@@ -289,7 +316,10 @@ class PSServer {
             }
           },
           [](int pid) { return !(kill(pid, 0) != 0 && errno == ESRCH); }, &dead_);
-      if (dev_ >= 0) hipStreamSynchronize(stream_);
+      if (dev_ >= 0) {
+        hipStreamSynchronize(stream_);
+        for (auto cs : cstream_) hipStreamSynchronize(cs);
+      }
     } catch (const std::exception& e) {
       err_ = e.what();
     }
@@ -304,14 +334,16 @@ class PSServer {
   float* m_ = nullptr;
   float* v_ = nullptr;
   void* mailbox_ = nullptr;            // [W][n] fp32 or (bf16 wire) bf16
-  uint16_t* snap_ = nullptr;           // bf16 wire: bf16 copy of params_
+  void* snap_ = nullptr;               // [W][n] per-worker snapshots (bf16 or fp32 wire)
+  std::vector<hipStream_t> cstream_;   // per worker: its snapshot's copy over its link
   std::vector<float> host_;
   std::vector<void*> rx_ptr_;
   std::vector<hipEvent_t> done_ev_;   // per worker: its request's Adam + snapshot copy finished
   std::vector<hipEvent_t> start_ev_;  // per worker: its request's work started (timing)
+  std::vector<hipEvent_t> snap_ev_;   // per worker: its snapshot is written (end of the PS stream's part)
   std::vector<char> started_ = std::vector<char>(pddl::ps::kMaxWorkers, 0);
   int64_t svc_n_ = 0;
-  double svc_sum_ms_ = 0, svc_max_ms_ = 0;
+  double svc_sum_ms_ = 0, svc_max_ms_ = 0, busy_sum_ms_ = 0;
   hipStream_t stream_ = nullptr;
   std::thread thr_;
   std::atomic<bool> stop_{false};

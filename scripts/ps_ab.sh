@@ -7,5 +7,5 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 for g in 1 0; do for blk in 16 1; do
   PDDL_PS_TICKET_BLOCK=$blk PDDL_REHEARSE=1 timeout -k 10 300 python bench.py --gpus 3 --strategy ps --ps 1 --batch 32 --steps 300 --graph $g > $OUT/g${g}_b${blk}.json 2> $OUT/g${g}_b${blk}.err || { tail -5 $OUT/g${g}_b${blk}.err; exit 1; }
-  python -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]);print('graph',sys.argv[2],'block',sys.argv[3], d['value'], round(d['ps_service'][0]['mean_ms'],3))" $OUT/g${g}_b${blk}.json $g $blk
+  python -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]);print('graph',sys.argv[2],'block',sys.argv[3], d['value'], {k: round(v,3) for k,v in d['ps_service'][0].items()})" $OUT/g${g}_b${blk}.json $g $blk
 done; done
