@@ -11,5 +11,5 @@ if [ $# -gt 0 ]; then
   timeout -k 10 600 python -u -m pytest "$@" -v -x --timeout 200 --timeout-method thread > $OUT/focused.log 2>&1
   rc=$?; grep -E "PASS|FAIL|^E |passed|failed|crash trace" $OUT/focused.log | tail -30; [ $rc -eq 0 ] || exit $rc
 fi
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $OUT/gputests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 200 --timeout-method thread > $OUT/gputests.log 2>&1
 rc=$?; tail -4 $OUT/gputests.log; exit $rc
