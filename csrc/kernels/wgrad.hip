@@ -549,11 +549,12 @@ static const int2* rowinfo_for(const WgradParams& p, hipStream_t stream, const c
 }
 
 int g_wgrad1 = 1;          // LDS stages of the 128/64-wide wgrad kernel: 1 = single stage except the
-                           // long-reduction direct layers (1x1 / stem window, M >= 2M rows: stage-2
+                           // long-reduction direct layers and grids of at most one block per CU (1x1 / stem window, M >= 2M rows: stage-2
                            // 1x1s -4..-12 %, stem -8 %, 3x3 and stage 3+ +8..+13 % with 2 stages;
                            // per-layer A/B at b1024), 0 = 2 stages everywhere, 2 = single everywhere
-int g_wgrad8 = 1;          // 8-phase 256x256 wgrad8_kernel for Cout >= 256, K >= 256: 0 off, 1 on, 2 with the
-                           // wave-row stagger (measured slower here); +8 (probe): skip the atomic epilogue
+int g_wgrad8 = 1;          // 8-phase 256x256 wgrad8_kernel for Cout >= 256, K >= 256: 0 off, 1 on where its grid
+                           // fills >= half the CUs, 2 with the wave-row stagger (measured slower here);
+                           // +8 (probe): skip the atomic epilogue; +16: whatever the grid
 
 int g_wgrad8_min_rows = 512;    // wgrad8 m-reduction split: at least this many rows per split (knob;
                                 // b32: 1024 -> 512 rows 5.32 -> 5.06 ms/step, 256: 5.26)
@@ -604,8 +605,14 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
   if (sp > cap) sp = cap;
   if (sp < 1) sp = 1;
   int mps8 = ((p.M + sp - 1) / sp + 63) / 64 * 64;
+  // The one-block-per-CU 256x256 tiles need at least half the chip's CUs in the grid: a small
+  // reduction (batch 32: stage 4/5 give 52-144 blocks) leaves most CUs idle for the whole
+  // launch, and each block's 128 KiB of LDS shuts the concurrent data-gradient chain out of
+  // its CU; the 128-wide tiles spread the same layer over >= 256 smaller blocks there
+  // (b32 graphed step 3.95 -> 3.89 ms with the 2-stage 128-wide tiles, profiles/r5_b32_wgrad_ab.txt).
+  const bool fills8 = (long)nt8 * ((p.M + mps8 - 1) / mps8) * 2 >= num_cus() || (g_wgrad8 & 16);
   // (the generic gather steps pixel indices through 24-bit multiplies: < 2^22 pixels per split)
-  if (g_wgrad8 && p.Cout >= 256 && p.K >= 256 && !window && p.splits <= 0 && span_ok(mps8) &&
+  if (g_wgrad8 && fills8 && p.Cout >= 256 && p.K >= 256 && !window && p.splits <= 0 && span_ok(mps8) &&
       (fast || (span_pix(mps8) < (1L << 22) && 2L * p.C < (1L << 23)))) {
     const int mps = mps8;
     sp = (p.M + mps - 1) / mps;
@@ -661,7 +668,9 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
     if (!ri) return why;
   }
 #define WG_LAUNCH(F_, BM_, NS_) hipLaunchKernelGGL((wgrad_kernel<F_, BM_, NS_>), dim3(nwg), dim3(256), 0, stream, p, mps, ri);
-  const bool one_stage = g_wgrad1 == 2 || (g_wgrad1 == 1 && !((fast || window) && p.M >= (1 << 21)));
+  // (a grid of at most one block per CU has no co-resident block to overlap a single stage's
+  // load and MFMA phases: small batches take the 2-stage pipeline)
+  const bool one_stage = g_wgrad1 == 2 || (g_wgrad1 == 1 && nwg > num_cus() && !((fast || window) && p.M >= (1 << 21)));
   if (one_stage) {
     if (BM == 64) {
       if (fast) WG_LAUNCH(true, 64, 1) else WG_LAUNCH(false, 64, 1)
