@@ -544,6 +544,14 @@ static const int2* rowinfo_for(const WgradParams& p, hipStream_t stream, const c
   if (hipMalloc(&buf, sizeof(int2) * (size_t)p.M) != hipSuccess) { *why = "wgrad: rowinfo allocation failed"; return nullptr; }
   hipLaunchKernelGGL(rowinfo_kernel, dim3((p.M + 255) / 256 < 8192 ? (p.M + 255) / 256 : 8192), dim3(256), 0, stream,
                      buf, p.M, p.Ho, p.Wo, p.H, p.W, p.stride, p.pad, p.R, p.S);
+  // The table is shared by every stream of the device (engines of several replicas, side
+  // streams), so it must be complete before any other caller gets the pointer: finish the
+  // build here, under the lock.  (Without this a second engine on another stream read a table
+  // still being written -- a 1-GPU Mirrored rehearsal with two replicas in threads.)
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    if (hipStreamSynchronize(stream) != hipSuccess) { *why = "wgrad: rowinfo build failed"; return nullptr; }
+  }
   cache[key] = buf;
   return buf;
 }

@@ -567,7 +567,8 @@ class HipEngine:
 
     def _labels(self, labels, B):
         lab = self.labels_dev[:B]
-        lab.copy_(labels, non_blocking=True)
+        if labels.data_ptr() != lab.data_ptr():   # (a graphed step loads straight into labels_dev)
+            lab.copy_(labels, non_blocking=True)
         return lab
 
     # ------------------------------------------------------------------ two-stream backward
@@ -650,6 +651,8 @@ class HipEngine:
         N, L = self.N, self.L
         B = images.shape[0]
         assert B <= self.cap, "batch larger than the engine's buffers"
+        self._pending, self._last_side = {}, None
+        self._evi = 0
         self.ws.zero_()
         lab = self._labels(labels, B)
         prof.push("step/forward")
@@ -663,8 +666,6 @@ class HipEngine:
         # bucket readiness tracking (kernels region is filled in layout order)
         bks = buckets if buckets is not None else []
         nb = [0]
-        self._pending, self._last_side = {}, None
-        self._evi = 0
         W = self._side_run
 
         def done_upto(off):

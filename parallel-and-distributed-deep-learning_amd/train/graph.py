@@ -92,9 +92,15 @@ class GraphedTrainStep:
         dev = engine.params.device
         H, W = image_hw
         self.images = torch.zeros(batch, H, W, 3, dtype=image_dtype, device=dev)
-        self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
+        lab = getattr(engine, "labels_dev", None)
+        if lab is not None and lab.dtype == torch.int64 and lab.device == dev and lab.shape[0] >= batch:
+            self.labels = lab[:batch]   # the engine reads its labels here: no copy inside the step
+        else:
+            self.labels = torch.zeros(batch, dtype=torch.int64, device=dev)
         self.flip = torch.zeros(batch, dtype=torch.uint8, device=dev)
         self.crop = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._flip_zero = True        # (flip holds zeros: a flip-less load needs no memset)
+        self._crop_host = (0, 0)      # (the tuple crop currently in `crop`: unchanged -> no copy)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.stats = None
 
@@ -110,18 +116,24 @@ class GraphedTrainStep:
         self.images.copy_(images, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
         if flip is None:
-            self.flip.zero_()
+            if not self._flip_zero:
+                self.flip.zero_()
+                self._flip_zero = True
         else:
             self.flip.copy_(flip, non_blocking=True)
+            self._flip_zero = False
         if isinstance(crop_offset, torch.Tensor):
             self.crop.copy_(crop_offset, non_blocking=True)
+            self._crop_host = None
         else:
-            oy, ox = crop_offset
+            oy, ox = (int(v) for v in crop_offset)
             H, W = self.images.shape[1:3]
             c = self.engine.crop
             if not (0 <= oy <= H - c and 0 <= ox <= W - c) and c < H:
                 raise ValueError("crop offset out of range")
-            self.crop.copy_(torch.tensor([oy, ox], dtype=torch.int32), non_blocking=True)
+            if self._crop_host != (oy, ox):
+                self.crop.copy_(torch.tensor([oy, ox], dtype=torch.int32), non_blocking=True)
+                self._crop_host = (oy, ox)
 
     def capture(self):
         """Record the step.  Call after one eager step of the engine (its lazily built tables
