@@ -311,19 +311,28 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
         self.comm = os.environ.get("PDDL_COMM", comm)
 
     def _graphed_ranks(self) -> bool:
-        """GPU ranks of a multi-process job replay their step from HIP graphs segmented at the
-        gradient buckets, with the bucket all-reduces on a native RCCL communicator between the
-        segment replays (the Mirrored replica design, _LocalReplicas with one local replica).
-        Eager FusionEngine / bucket reducer only with --no-graphs (cfg.graphs False),
-        PDDL_COMM=fusion|bucket, the fp32 engine, or a rehearsal (ranks sharing one GPU: RCCL
-        refuses that)."""
+        """Graphed ranks: each GPU rank replays its step from HIP graphs segmented at the
+        gradient buckets, with the bucket all-reduces on a native RCCL communicator
+        (ncclCommInitRank) between the segment replays (the Mirrored replica design,
+        _LocalReplicas with one local replica).  Selected by --graphs (cfg.graphs True) with
+        world > 1, or PDDL_COMM=graphs (also on a 1-rank communicator).
+
+        The default is the eager step with the FusionEngine (buckets all-reduced over the c10d
+        RCCL group by its worker thread while the backward runs): measured on one MI355X through
+        the Trainer at the Horovod preset (b32, crop 160) the eager rank runs 10,059 img/s, the
+        whole-step graph 9,261 and the segmented graphs 8,137 (seven graph launches plus the
+        host-ordered all-reduces per step); at b2560 the segmented path costs 86.2 vs 85.8 ms
+        (profiles/r5_strategy_bench_1gpu.txt).  Never in a rehearsal (ranks sharing one GPU:
+        RCCL refuses that) or on the fp32 engine."""
         if not (self.device.type == "cuda" and self.cfg.precision == "bf16" and self.cfg.graphs is not False
                 and not rehearsing()):
             return False
         comm = os.environ.get("PDDL_COMM")
         # one rank: no collective is needed (the whole-step graph below with --graphs);
         # PDDL_COMM=graphs still runs the multi-rank design over a 1-rank communicator
-        return comm == "graphs" if self.world == 1 else comm in (None, "graphs")
+        if comm == "graphs":
+            return True
+        return self.world > 1 and comm is None and self.cfg.graphs is True
 
     def _build(self, trainer):
         info = resolve_cluster(port_base=self.cfg.port_base)
