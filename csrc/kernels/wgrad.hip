@@ -561,7 +561,7 @@ int g_wgrad1 = 1;          // LDS stages of the 128/64-wide wgrad kernel: 1 = si
                            // 1x1s -4..-12 %, stem -8 %, 3x3 and stage 3+ +8..+13 % with 2 stages;
                            // per-layer A/B at b1024), 0 = 2 stages everywhere, 2 = single everywhere
 int g_wgrad8 = 1;          // 8-phase 256x256 wgrad8_kernel for Cout >= 256, K >= 256: 0 off, 1 on where its grid
-                           // fills >= half the CUs, 2 with the wave-row stagger (measured slower here);
+                           // each block's reduction amortises its atomic burst (wgrad_launch_one), 2 with the wave-row stagger (slower here);
                            // +8 (probe): skip the atomic epilogue; +16: whatever the grid
 
 int g_wgrad8_min_rows = 512;    // wgrad8 m-reduction split: at least this many rows per split (knob;
@@ -605,25 +605,58 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
     const long xs = fast ? rows * p.ldx : span_pix(mps) * p.C;
     return xs * 2 < (1L << 31) - (1L << 24) && rows * p.ldg * 2 < (1L << 31) - (1L << 24);
   };
-  // one 256x256 block per CU: split the m reduction so tiles x splits ~ one round of CUs,
-  // each split at least g_wgrad8_min_rows rows
+  // 128-wide tiles (4 waves, 2 blocks per CU): the m-split plan.
+  const int BM = p.Cout <= 64 ? 64 : 128;
+  const int ntiles = ((p.Cout + BM - 1) / BM) * ((p.K + 127) / 128);
+  int splits = p.splits;
+  if (splits <= 0) {
+    // Every split adds one 64 KiB fp32 atomic tile (~1.3 TB/s chip-wide), so a workgroup
+    // should own >= ~48 m-iterations (3072 rows); but keep >= 256 workgroups when the
+    // tile count alone cannot fill the 256 CUs.
+    const int fill = (1536 + ntiles - 1) / ntiles;
+    const int work = (p.M + 3071) / 3072;
+    splits = fill < work ? fill : work;
+    if ((long)ntiles * splits < 256) {
+      const int f2 = (256 + ntiles - 1) / ntiles, w2 = (p.M + 511) / 512;
+      splits = f2 < w2 ? f2 : w2;
+    }
+    if (splits < 1) splits = 1;
+  }
+  int mps = (p.M + splits - 1) / splits;
+  mps = (mps + 63) / 64 * 64;
+  while (!span_ok(mps) && mps > 64) mps = (mps / 2 + 63) / 64 * 64;   // (batches beyond ~1.5k)
+  const bool plan1_ok = span_ok(mps);
+  splits = (p.M + mps - 1) / mps;
+  const int nwg = ntiles * splits;
+
+  // 8-phase 256x256 tiles (one block per CU): split the m reduction so tiles x splits ~ one
+  // round of CUs, each split at least g_wgrad8_min_rows rows.
   const int nt8 = ((p.Cout + 255) / 256) * ((p.K + 255) / 256);
   int sp = (num_cus() + nt8 / 2) / nt8;
   const int cap = (p.M + g_wgrad8_min_rows - 1) / g_wgrad8_min_rows;
   if (sp > cap) sp = cap;
   if (sp < 1) sp = 1;
-  int mps8 = ((p.M + sp - 1) / sp + 63) / 64 * 64;
-  // The one-block-per-CU 256x256 tiles need at least half the chip's CUs in the grid: a small
-  // reduction (batch 32: stage 4/5 give 52-144 blocks) leaves most CUs idle for the whole
-  // launch, and each block's 128 KiB of LDS shuts the concurrent data-gradient chain out of
-  // its CU; the 128-wide tiles spread the same layer over >= 256 smaller blocks there
-  // (b32 graphed step 3.95 -> 3.89 ms with the 2-stage 128-wide tiles, profiles/r5_b32_wgrad_ab.txt).
-  const bool fills8 = (long)nt8 * ((p.M + mps8 - 1) / mps8) * 2 >= num_cus() || (g_wgrad8 & 16);
+  const int mps8 = ((p.M + sp - 1) / sp + 63) / 64 * 64;
+  sp = (p.M + mps8 - 1) / mps8;
   // (the generic gather steps pixel indices through 24-bit multiplies: < 2^22 pixels per split)
-  if (g_wgrad8 && fills8 && p.Cout >= 256 && p.K >= 256 && !window && p.splits <= 0 && span_ok(mps8) &&
-      (fast || (span_pix(mps8) < (1L << 22) && 2L * p.C < (1L << 23)))) {
+  const bool elig8 = g_wgrad8 && p.Cout >= 256 && p.K >= 256 && !window && p.splits <= 0 && span_ok(mps8) &&
+                     (fast || (span_pix(mps8) < (1L << 22) && 2L * p.C < (1L << 23)));
+  // Which tiling.  Every 8-phase block ends with a burst of fp32 atomics of its 256 KiB partial
+  // tile, and one round of blocks (one per CU) is ~64 MiB of atomics at the chip's ~1.3 TB/s
+  // atomic rate (MI355X_MICROARCH.md "Global float atomics"): ~50 us that no block's MFMA work
+  // overlaps, since the blocks finish together (wgrad8=9 probe: 48-51 us of a 84-124 us layer at
+  // b256, 17-26 us of 340-740 at b2560; scripts/wgrad_probe.sh).  The 8-phase tiles pay off when
+  // each block's reduction is long enough to amortise that burst -- >= 0.4 GFLOP per block
+  // (~47 us of MFMA work) -- and the grid covers at least half the CUs; otherwise the 128-wide
+  // tiles (64 KiB partials, 2 blocks per CU) win: b256 whole step 11.72 -> 11.03 ms, b32 3.95 ->
+  // 3.85 ms, b1024 / b2560 unchanged (profiles/r5_b32_wgrad_ab.txt, profiles/r5_b256_wgrad_ab.txt).
+  bool use8 = false;
+  if (elig8) {
+    const double F = 2.0 * p.M * (double)p.Cout * p.K, w8 = (double)nt8 * sp;
+    use8 = (g_wgrad8 & 16) || !plan1_ok || (F >= 4e8 * w8 && 2 * w8 >= num_cus());
+  }
+  if (use8) {
     const int mps = mps8;
-    sp = (p.M + mps - 1) / mps;
     Wg8Geom geo{};
     geo.mg_howo = fdiv_magic(p.Ho * p.Wo);
     geo.mg_wo = fdiv_magic(p.Wo);
@@ -646,28 +679,7 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? nullptr : hipGetErrorString(e);
   }
-  const int BM = p.Cout <= 64 ? 64 : 128;
-  const int ntiles = ((p.Cout + BM - 1) / BM) * ((p.K + 127) / 128);
-  int splits = p.splits;
-  if (splits <= 0) {
-    // Every split adds one 64 KiB fp32 atomic tile (~1.3 TB/s chip-wide), so a workgroup
-    // should own >= ~48 m-iterations (3072 rows); but keep >= 256 workgroups when the
-    // tile count alone cannot fill the 256 CUs.
-    const int fill = (1536 + ntiles - 1) / ntiles;
-    const int work = (p.M + 3071) / 3072;
-    splits = fill < work ? fill : work;
-    if ((long)ntiles * splits < 256) {
-      const int f2 = (256 + ntiles - 1) / ntiles, w2 = (p.M + 511) / 512;
-      splits = f2 < w2 ? f2 : w2;
-    }
-    if (splits < 1) splits = 1;
-  }
-  int mps = (p.M + splits - 1) / splits;
-  mps = (mps + 63) / 64 * 64;
-  while (!span_ok(mps) && mps > 64) mps = (mps / 2 + 63) / 64 * 64;   // (batches beyond ~1.5k)
-  if (!span_ok(mps)) return "wgrad: one 64-row tile spans more than 2 GiB";
-  splits = (p.M + mps - 1) / mps;
-  const int nwg = ntiles * splits;
+  if (!plan1_ok) return "wgrad: one 64-row tile spans more than 2 GiB";
   // 2 LDS stages + 2 blocks/CU (a 3-stage ring at 1 block/CU measured slower and was removed)
   const int2* ri = nullptr;
   if (!fast) {
