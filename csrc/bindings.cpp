@@ -829,7 +829,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm8") pddl::g_igemm8 = v;
     else if (which == "igemm8_min_tiles") pddl::g_igemm8_min_tiles = v;
     else if (which == "wgrad8") pddl::g_wgrad8 = v;
-    else if (which == "wgrad8_rounds") { TORCH_CHECK(v >= 1 && v <= 8, "wgrad8_rounds"); pddl::g_wgrad8_rounds = v; }
     else if (which == "igemm_ns1_kt") pddl::g_igemm_ns1_kt = v;
     else if (which == "igemm8_min_n") pddl::g_igemm8_min_n = v;
     else if (which == "wgrad1") pddl::g_wgrad1 = v;

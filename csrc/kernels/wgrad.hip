@@ -564,8 +564,6 @@ int g_wgrad8 = 1;          // 8-phase 256x256 wgrad8_kernel for Cout >= 256, K >
                            // each block's reduction amortises its atomic burst (wgrad_launch_one), 2 with the wave-row stagger (slower here);
                            // +8 (probe): skip the atomic epilogue; +16: whatever the grid
 
-int g_wgrad8_rounds = 1;        // blocks per CU over the launch (A/B knob: 2 = two rounds, so one
-                                // round's atomic burst can overlap the other's MFMA work)
 int g_wgrad8_min_rows = 512;    // wgrad8 m-reduction split: at least this many rows per split (knob;
                                 // b32: 1024 -> 512 rows 5.32 -> 5.06 ms/step, 256: 5.26)
 
@@ -634,7 +632,7 @@ static const char* wgrad_launch_one(const WgradParams& pin, hipStream_t stream) 
   // 8-phase 256x256 tiles (one block per CU): split the m reduction so tiles x splits ~ one
   // round of CUs, each split at least g_wgrad8_min_rows rows.
   const int nt8 = ((p.Cout + 255) / 256) * ((p.K + 255) / 256);
-  int sp = (g_wgrad8_rounds * num_cus() + nt8 / 2) / nt8;
+  int sp = (num_cus() + nt8 / 2) / nt8;
   const int cap = (p.M + g_wgrad8_min_rows - 1) / g_wgrad8_min_rows;
   if (sp > cap) sp = cap;
   if (sp < 1) sp = 1;
