@@ -15,7 +15,8 @@ j() { python -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l
 b() { local tag=$1; shift; timeout -k 10 240 python bench.py "$@" > $OUT/$tag.json 2> $OUT/$tag.err || { echo "$tag failed"; tail -3 $OUT/$tag.err; return 1; }; j $OUT/$tag.json; }
 b b2560 --steps 20 --warmup 5 || exit 1
 [ "$MODE" = quick ] && exit 0
-b b1024 --batch 1024 --steps 20 --warmup 5 && \
+b b1024 --batch 1024 --steps 20 --warmup 5 && b b256 --batch 256 --steps 30 --warmup 5 && \
+b b256c160 --batch 256 --crop 160 --steps 30 --warmup 5 && \
 b b32 --batch 32 --steps 40 --warmup 10 && b b32g --batch 32 --steps 40 --warmup 10 --graph 1 && \
 b b32c160g --batch 32 --crop 160 --steps 40 --warmup 10 --graph 1 && \
 b fp32 --precision fp32 --steps 10 --warmup 3 || exit 1
