@@ -57,6 +57,10 @@ class HipEngine:
     GRAD_RING = 5           # two-stream: gradient buffers per kind, so the data-gradient chain can run
                             # up to four blocks ahead of the weight gradients still reading older ones
                             # (b32: 3 -> 5 buffers 4.21 -> 4.17 ms eager, 4.17 -> 4.05 ms graphed)
+    GRAD_RING_SMALL = 16    # ... and at batches <= 64, where a whole stage's data gradients outrun
+                            # its weight gradients: b32 eager 3.90 (5) -> 3.82 (8) -> 3.77 (12) ->
+                            # 3.75 ms (16), 24 / 32 no better; b256 within noise from 5 to 24
+                            # (round 5, gpurun_out/gr_*); 16 x 51 MB of ring at b32
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
@@ -295,7 +299,8 @@ class HipEngine:
             H = Ho
         self.H5 = H
         # (set before _alloc_acts runs; the subclasses' engines keep one stream)
-        ring = int(os.environ.get("PDDL_GRAD_RING", self.GRAD_RING)) if self._two_stream_wanted(B) else 1
+        ring0 = self.GRAD_RING_SMALL if B <= 64 else self.GRAD_RING
+        ring = int(os.environ.get("PDDL_GRAD_RING", ring0)) if self._two_stream_wanted(B) else 1
         self.gbuf = [torch.empty(outer, **bf) for _ in range(max(2, ring))]
         self.g1bufs = [torch.empty(inner, **bf) for _ in range(ring)]
         self.g2bufs = [torch.empty(inner, **bf) for _ in range(ring)]

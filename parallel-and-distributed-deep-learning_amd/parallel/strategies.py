@@ -873,18 +873,34 @@ class _LocalReplicas:
             self.comm.check()      # a stall verdict of the previous step's collectives raises here
         parts = self._split(images, labels)
         if self.graph_mode and self._single_replica_job():
-            return self._whole_step(parts, global_batch)
+            if self.cfg.graphs:            # (--graphs: the whole step as one HIP graph)
+                return self._whole_step(parts, global_batch)
+            return self._single_step(parts, global_batch)
         if self.graph_mode:
             return self._graphed_step(parts, global_batch)
         return self._eager_step(parts, global_batch)
 
     def _single_replica_job(self) -> bool:
         """One replica in the whole job: the gradient needs no reduction (a 1-rank all-reduce is
-        the identity), so the step is one whole-step HIP graph with the optimizer inside, like
-        TF's MirroredStrategy on one device (no cross-device ops).  PDDL_MIRROR_SEGMENTED=1 (and
-        PDDL_COMM=graphs) keep the segmented multi-replica schedule and its collectives."""
+        the identity), so the step runs without collectives, like TF's MirroredStrategy on one
+        device (no cross-device ops): eager by default, one whole-step HIP graph with --graphs.
+        PDDL_MIRROR_SEGMENTED=1 (and PDDL_COMM=graphs) keep the segmented multi-replica schedule
+        and its collectives."""
         return (self.world_ranks == 1 and os.environ.get("PDDL_MIRROR_SEGMENTED", "0") != "1"
                 and os.environ.get("PDDL_COMM") != "graphs")
+
+    def _single_step(self, parts, global_batch: int):
+        """One replica in the whole job, default: the eager two-stream step (no collective to
+        run).  Measured faster than its whole-step graph replay once the host enqueue hides
+        behind the GPU step (b32: 3.77 vs 4.08 ms, profiles/r5_strategy_bench_1gpu.txt)."""
+        (eng, opt), d = self.replicas[0], self.devices[0]
+        im, lb = parts[0]
+        with torch.cuda.device(d):
+            flip, off = self.augs[0](im.shape[0])
+            s = eng.forward_backward(im, lb, 1.0 / global_batch, flip=flip, crop_offset=off).clone()
+            opt.step()
+            eng.after_update()
+        return s
 
     def _whole_step(self, parts, global_batch: int):
         from ..train.graph import GraphedTrainStep
