@@ -60,10 +60,14 @@ class HipEngine:
     GRAD_RING_SMALL = 16    # ... and at batches <= 64, where a whole stage's data gradients outrun
                             # its weight gradients: b32 eager 3.90 (5) -> 3.82 (8) -> 3.77 (12) ->
                             # 3.75 ms (16), 24 / 32 no better; b256 within noise from 5 to 24
-                            # (round 5, gpurun_out/gr_*); 16 x 51 MB of ring at b32
+                            # (round 5, gpurun_out/gr_*); 16 x 51 MB of ring at b32.  Engines whose
+                            # step replays from HIP graphs keep GRAD_RING (build_engine graphed=True):
+                            # b32 graph 3.90 -> 4.08 ms, PS workers 6.72k -> 6.50k img/s with 16
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
-                 device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None):
+                 device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None,
+                 grad_ring: Optional[int] = None):
+        self._grad_ring = grad_ring   # None: GRAD_RING_SMALL at batches <= 64, else GRAD_RING
         if bn_mode not in self.BN_MODES:
             raise ValueError(f"{type(self).__name__} runs bn_mode in {self.BN_MODES}, not {bn_mode!r} "
                              "(use make_hip_engine)")
@@ -299,7 +303,7 @@ class HipEngine:
             H = Ho
         self.H5 = H
         # (set before _alloc_acts runs; the subclasses' engines keep one stream)
-        ring0 = self.GRAD_RING_SMALL if B <= 64 else self.GRAD_RING
+        ring0 = self._grad_ring or (self.GRAD_RING_SMALL if B <= 64 else self.GRAD_RING)
         ring = int(os.environ.get("PDDL_GRAD_RING", ring0)) if self._two_stream_wanted(B) else 1
         self.gbuf = [torch.empty(outer, **bf) for _ in range(max(2, ring))]
         self.g1bufs = [torch.empty(inner, **bf) for _ in range(ring)]

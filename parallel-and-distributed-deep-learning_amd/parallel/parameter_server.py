@@ -874,7 +874,8 @@ class ParameterServerStrategy:
         if cl is None or cl.is_ps:
             raise RuntimeError("ParameterServerStrategy.setup runs in a worker role of run_ps_job")
         self.device = cl.device
-        eng = build_engine(cfg, cl.device, max(cfg.batch_size, cfg.val_batch_size or 0))
+        eng = build_engine(cfg, cl.device, max(cfg.batch_size, cfg.val_batch_size or 0),
+                           graphed=cfg.graphs is not False)
         eng.init(seed=cfg.seed)
         if cfg.weights and cfg.weights != "none":
             from ..utils.checkpoint import load_pretrained

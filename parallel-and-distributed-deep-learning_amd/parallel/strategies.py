@@ -70,16 +70,20 @@ def gpu_available() -> bool:
     return torch.cuda.is_available() and torch.cuda.device_count() > 0
 
 
-def build_engine(cfg, device: torch.device, cap: int):
+def build_engine(cfg, device: torch.device, cap: int, graphed: Optional[bool] = None):
     """On a GPU: the bf16 HIP engine (bf16 MFMA kernels; frozen or train-mode BN), or for
     precision=fp32 the reference-precision engine on the fp32-MFMA HIP convolutions
     (models/engine_f32.py).  On CPU: the fp32 PyTorch reference engine (config 1 of
-    BASELINE.json: CPU plumbing)."""
+    BASELINE.json: CPU plumbing).  graphed (default: cfg.graphs is True): the step will replay
+    from HIP graphs, which keep the shallower gradient rings (HipEngine.GRAD_RING_SMALL)."""
     L = ParamLayout(cfg.num_classes)
     if device.type == "cuda" and cfg.precision == "bf16":
-        from ..models.engine import make_hip_engine
+        from ..models.engine import HipEngine, make_hip_engine
+        if graphed is None:
+            graphed = cfg.graphs is True
         return make_hip_engine(L, cap, bn_mode=cfg.bn_mode, crop=cfg.crop, image_size=cfg.image_size,
-                               device=device, num_classes=cfg.num_classes)
+                               device=device, num_classes=cfg.num_classes,
+                               grad_ring=HipEngine.GRAD_RING if graphed else None)
     if device.type == "cuda":
         from ..models.engine_f32 import HipF32AutogradEngine, HipF32Engine
         if cfg.bn_mode == "frozen":   # the reference's configuration: explicit fused fp32 schedule
@@ -584,10 +588,14 @@ class _LocalReplicas:
         cap = max(cfg.batch_size, cfg.val_batch_size or 0)
         self.replicas = []
         self.augs = []
+        # (several replicas / ranks replay graphed segments unless --no-graphs; one replica in the
+        # whole job runs eager unless --graphs)
+        ws = world_ranks or len(self.devices)
+        graphed = cfg.graphs is True or (cfg.graphs is None and ws > 1)
         for i, d in enumerate(self.devices):
             if d.type == "cuda":
                 torch.cuda.set_device(d)
-            eng = build_engine(cfg, d, cap)
+            eng = build_engine(cfg, d, cap, graphed=graphed)
             eng.init(seed=cfg.seed)
             opt = make_optimizer(cfg.optimizer, eng, lr=cfg.lr, momentum=cfg.momentum, nesterov=cfg.nesterov,
                                  weight_decay=cfg.weight_decay, beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.adam_eps)
