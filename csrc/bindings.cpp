@@ -660,10 +660,11 @@ void prep_fuse(Tensor params, Tensor table, int64_t nlayers, int64_t max_elems, 
                             (int)max_elems, bfpm(wbf), f32p(scale), f32p(shift), (float)eps, cur_stream()),
      "prep_fuse");
 }
-void wgrad_finalize(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor scale, Tensor dgamma_raw) {
+void wgrad_finalize(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor scale, Tensor dgamma_raw,
+                    int64_t max_cout) {
   PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::FinLayer), "finalize table size");
   ok(pddl::wgrad_finalize_launch(f32p(params), f32p(grads), reinterpret_cast<const pddl::FinLayer*>(table.data_ptr()),
-                                 (int)nlayers, f32p(scale), f32p(dgamma_raw), cur_stream()),
+                                 (int)nlayers, f32p(scale), f32p(dgamma_raw), cur_stream(), (int)max_cout),
      "wgrad_finalize");
 }
 void bn_grad(Tensor params, Tensor grads, Tensor table, int64_t nlayers, Tensor colsum, Tensor dgamma_raw,
@@ -861,7 +862,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);
   m.def("prep", &prep, REL);
   m.def("prep_fuse", &prep_fuse, REL);
-  m.def("wgrad_finalize", &wgrad_finalize, REL);
+  m.def("wgrad_finalize", &wgrad_finalize, REL, py::arg("params"), py::arg("grads"), py::arg("table"),
+        py::arg("nlayers"), py::arg("scale"), py::arg("dgamma_raw"), py::arg("max_cout") = 2048);
   m.def("bn_grad", &bn_grad, REL);
   m.def("synth", &synth, REL);
   m.def("opt_hparams", &opt_hparams, REL);

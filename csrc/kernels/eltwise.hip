@@ -967,8 +967,11 @@ __global__ void wgrad_finalize_kernel(const float* __restrict__ prm, float* __re
   if (threadIdx.x == 0 && l.dg_off >= 0) dgamma_raw[l.dg_off + co] = red[0] + red[1] + red[2] + red[3];
 }
 const char* wgrad_finalize_launch(const float* params, float* grads, const FinLayer* layers_dev, int nlayers,
-                                  const float* scale, float* dgamma_raw, hipStream_t s) {
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(2048, nlayers), dim3(256), 0, s, params, grads, layers_dev, scale,
+                                  const float* scale, float* dgamma_raw, hipStream_t s, int max_cout) {
+  // one workgroup per output row of the widest layer in the table (the table's other layers'
+  // surplus rows exit at once): a stage-2 block's table is 256 rows wide, not 2048
+  if (max_cout < 1 || max_cout > 65535) return "wgrad_finalize: max_cout out of range";
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(max_cout, nlayers), dim3(256), 0, s, params, grads, layers_dev, scale,
                      dgamma_raw);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);

@@ -283,7 +283,7 @@ struct FinLayer {
   int dg_off;                   // output offset for dgamma_raw (per channel, -1: none)
 };
 const char* wgrad_finalize_launch(const float* params, float* grads, const FinLayer* layers_dev, int nlayers,
-                                  const float* scale, float* dgamma_raw, hipStream_t s);
+                                  const float* scale, float* dgamma_raw, hipStream_t s, int max_cout = 2048);
 
 // Per-channel BN/bias grads from column sums and dgamma_raw.
 struct BnGradLayer {

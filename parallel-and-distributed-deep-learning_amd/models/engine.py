@@ -231,10 +231,13 @@ class HipEngine:
             self._fin_rows[c.name] = struct.pack(_FIN_FMT, L.off(c.name, "kernel"), c.cout, c.k * c.k * c.cin,
                                                  self.ch[c.name], self.ch[c.name])
         self._fin_tabs: Dict[str, torch.Tensor] = {}
+        self._fin_rows_n: Dict[str, int] = {}   # widest layer of each table (finalize grid rows)
         for b in L.blocks:
             keys = ["3", "2", "1", "0"] if b.proj else ["3", "2", "1"]
             self._fin_tabs[b.name] = self._dev_table([self._fin_rows[b.convs[k].name] for k in keys])
+            self._fin_rows_n[b.name] = max(b.convs[k].cout for k in keys)
         self._fin_tabs["stem"] = self._dev_table([self._fin_rows[L.stem.name]])
+        self._fin_rows_n["stem"] = L.stem.cout
         bg = []
         for c in L.convs:
             cs = self.ch[c.name]
@@ -783,7 +786,8 @@ class HipEngine:
                 Hx, sx = self._x_geom(bi, H, b.stride)
                 W(N.wgrad, x_in, Hx, Hx, 1, 1, sx, 0, Ho, Ho, g1, gout, f, self._gview(c1n, 5 * f, cin), cin, 0,
                   reads=(f"g1_{rk}", gout_n))
-                W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr)
+                W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 4, self.scale, self.dgr,
+                  self._fin_rows_n[b.name])
                 gxc, up2 = None, 1 if b.stride == 2 else 0
                 if bi - 1 in s2:   # compact copy for the previous block's stride-2-grid passes
                     gxc = self.gcbuf[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
@@ -799,7 +803,8 @@ class HipEngine:
             else:
                 W(N.wgrad, x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1n, f, cin), cin, 0,
                   reads=(f"g1_{rk}",))
-                W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr)
+                W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs[b.name], 3, self.scale, self.dgr,
+                  self._fin_rows_n[b.name])
                 self._before_write(*gx_n)
                 if self._pre_fused(bi, s2):   # deferred into block bi-1's fused conv3 backward
                     pre_next = {"add": gout, "g1": g1, "w1d": self._wdv(c1n, cin, f), "gmask": mask_in, "cs": cs_in}
@@ -825,7 +830,8 @@ class HipEngine:
             N.maxpool_bwd(gpool, self.pidx[:B], None, gc1, part(s.name))
             W(N.wgrad, self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
             W(N.stem_wgrad_fold, self.stem_dw2, self._gview(s.name, 64, 147), 64)
-        W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr)
+        W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr,
+          self._fin_rows_n["stem"])
         self._join_side()
         done_upto(L.kernels_end)
         N.colsum_reduce(cp, ctab, cn, self.colsum)
