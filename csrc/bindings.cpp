@@ -840,6 +840,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
     else if (which == "conv_f32") pddl::g_conv_f32_variant = v;
+    else if (which == "wgrad_f32_wpc64") { TORCH_CHECK(v >= 1 && v <= 32, "wgrad_f32_wpc64"); pddl::g_wgrad_f32_wpc[0] = v; }
+    else if (which == "wgrad_f32_wpc128") { TORCH_CHECK(v >= 1 && v <= 32, "wgrad_f32_wpc128"); pddl::g_wgrad_f32_wpc[1] = v; }
     else if (which == "c64_grid") pddl::g_c64_grid = v;
     else if (which == "c64w_grid") pddl::g_c64w_grid = v;
     else if (which == "bn_red_blocks") pddl::g_bn_red_blocks = v;

@@ -728,13 +728,19 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
+// Workgroups per CU of the 64- / 128-wide fp32 weight gradients (knobs wgrad_f32_wpc64 / _wpc128).
+// Measured whole fp32 step at b256 (round 5, gpurun_out/ks45-ks47): {4, 3} 64.18 ms; fewer splits
+// (the atomic epilogue shrinks) lose -- {4, 2} 65.11, {4, 1} 69.63, {2, 3} 65.73; more win:
+// {8, 3} 63.27, {16, 3} 63.02, {4, 6} 63.14, {16, 6} 62.09, {24, 8} 62.24, {32, 12} 62.20.  The
+// kernels are MFMA-bound and the surplus workgroups keep every CU fed to the end of the launch.
+int g_wgrad_f32_wpc[2] = {16, 6};
 const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (const char* e = check_f32(p)) return e;
   p.mg_howo = fdiv_magic(p.Ho * p.Wo);
   p.mg_wo = fdiv_magic(p.Wo);
   const int ntiles = ((p.Cout + F_BM - 1) / F_BM) * ((p.K + F_BN - 1) / F_BN);
-  // ~4 workgroups per CU, each reducing at least 256 rows of m
-  int splits = (4 * num_cus() + ntiles - 1) / ntiles;
+  // ~16 workgroups per CU, each reducing at least 256 rows of m
+  int splits = (g_wgrad_f32_wpc[0] * num_cus() + ntiles - 1) / ntiles;
   const int cap = (p.M + 255) / 256;
   if (splits > cap) splits = cap;
   if (splits < 1) splits = 1;
@@ -745,7 +751,7 @@ const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
   const bool big_fits = p.Cout >= 128 && p.K >= 128 && (p.K % 128 == 0 || p.K >= 1024);
   if (g_conv_f32_variant >= 1 && p.C % 4 == 0 && p.Cout % 4 == 0 && (big_fits || g_conv_f32_variant >= 2)) {
     const int bt = ((p.Cout + 127) / 128) * ((p.K + 127) / 128);
-    int bs = (3 * num_cus() + bt - 1) / bt;                  // ~3 workgroups per CU
+    int bs = (g_wgrad_f32_wpc[1] * num_cus() + bt - 1) / bt;   // ~6 workgroups per CU
     const int bcap = (p.M + 511) / 512;                      // each reducing >= 512 rows of m
     bs = bs > bcap ? bcap : (bs < 1 ? 1 : bs);
     const int bmps = ((p.M + bs - 1) / bs + 15) / 16 * 16;
