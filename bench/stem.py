@@ -15,6 +15,7 @@ def main():
     ap.add_argument("--batch", type=int, default=2560)
     ap.add_argument("--crop", type=int, default=224)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--fwd-only", action="store_true")
     a = ap.parse_args()
     N = require_native()
     B, H1 = a.batch, a.crop // 2
@@ -50,6 +51,13 @@ def main():
     us2 = timed(unfused)
     print(f"igemm conv1 + maxpool:  {us2:8.1f} us  {flop / us2 / 1e6:6.1f} TF/s")
     print("outputs equal:", torch.equal(pool, pool2) and torch.equal(idx, idx2) and torch.equal(bits, bits2))
+    # fused backward: max-pool routing + conv1 weight gradient (+ per-channel sums)
+    gpool = torch.randn(B, H2, H2, 64, device="cuda").to(torch.bfloat16)
+    dw = torch.zeros(64, 256, device="cuda")
+    rows = N.stem_pool_bwd_partial_rows(B, H2)
+    cs = torch.empty(rows * 64, device="cuda")
+    us3 = timed(lambda: N.stem_pool_bwd(x2, gpool, idx, dw, cs))
+    print(f"fused stem pool bwd + conv1 wgrad: {us3:8.1f} us  {flop / us3 / 1e6:6.1f} TF/s")
 
 if __name__ == "__main__":
     main()

@@ -836,6 +836,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "igemm_n64") pddl::g_igemm_n64 = v;
     else if (which == "igemm_splitk") pddl::g_igemm_splitk = v;
     else if (which == "igemm_pk_all") pddl::g_igemm_pk_all = v;
+    else if (which == "igemm_pk_dual") pddl::g_igemm_pk_dual = v;
     else if (which == "igemm_pk") { TORCH_CHECK(v == 0 || (v >= 2 && v <= 4), "igemm_pk: 0 or ring depth 2-4"); pddl::g_igemm_pk = v; }
     else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
@@ -849,6 +850,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "pool_blocks") pddl::g_pool_blocks = v;
     else if (which == "colred_chunks") { TORCH_CHECK(v >= 1 && v <= 65535, "colred_chunks"); pddl::g_colred_chunks = v; }
     else TORCH_CHECK(false, "unknown kernel knob ", which);
+  });
+  // (train/graph.py: is the stream's current capture still empty?) (hip error, capture status, #deps)
+  m.def("stream_capture_deps", [](int64_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t n = 0;
+    const hipError_t e = hipStreamGetCaptureInfo_v2(reinterpret_cast<hipStream_t>(stream), &st, &id, &g, &deps, &n);
+    return std::make_tuple((int)e, (int)st, (int64_t)n);
   });
   m.def("igemm_partial_rows", [](int M, int Nn, int K, bool bnz) { return pddl::igemm_partial_rows(M, Nn, K, bnz); },
         py::arg("M"), py::arg("Nn"), py::arg("K"), py::arg("bnz") = false);

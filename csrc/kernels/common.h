@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <atomic>
+#include <mutex>
 #include <stdint.h>
 
 namespace pddl {
@@ -135,14 +136,22 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
-// True the first time it is called on the current device for this `done` mask (one bit per
-// device): per-device one-time launch setup (hipFuncSetAttribute is per device, so a
-// process-wide flag would leave devices >= 1 unconfigured).
-inline bool first_on_device(std::atomic<unsigned long long>& done) {
+// Per-device one-time launch setup (hipFuncSetAttribute is per device, so a process-wide flag
+// would leave devices >= 1 unconfigured): runs `setup` the first time it is reached on the
+// current device for this `done` mask (one bit per device).  The bit is published only after
+// `setup` has returned, under a lock, so a second thread launching on the same device (replica
+// threads of a 1-GPU Mirrored rehearsal) waits for the attributes instead of racing past them.
+template <class F>
+inline void once_per_device(std::atomic<unsigned long long>& done, F&& setup) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 63;
   const unsigned long long bit = 1ull << dev;
-  return !(done.fetch_or(bit) & bit);
+  if (done.load(std::memory_order_acquire) & bit) return;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.load(std::memory_order_relaxed) & bit) return;
+  setup();
+  done.fetch_or(bit, std::memory_order_release);
 }
 
 }  // namespace pddl

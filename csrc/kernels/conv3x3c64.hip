@@ -278,11 +278,11 @@ const char* conv3x3c64_launch(const C64Params& p_in, int mode, hipStream_t s) {
   p.mg_hw = fdiv_magic(p.H * p.W);
   p.mg_w = fdiv_magic(p.W);
   static std::atomic<unsigned long long> attr{0};
-  if (first_on_device(attr)) {
+  once_per_device(attr, [&] {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_FWD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
     (void)hipFuncSetAttribute((const void*)conv3x3c64_row8_kernel<C64_DGRAD>, hipFuncAttributeMaxDynamicSharedMemorySize, R8_LDS);
     (void)hipGetLastError();   // (a refused attribute call must not read as the launch's error)
-  }
+  });
   const int T = p.N * ((p.H + 3) / 4);
   int G = num_cus();
   if (g_c64_grid > 0 && g_c64_grid < G) G = g_c64_grid;
@@ -469,10 +469,10 @@ const char* conv3x3c64_wgrad_launch(const C64WgradParams& p, hipStream_t s) {
   if (g_c64w_grid > 0 && g_c64w_grid < G) G = g_c64w_grid;
   if (G > T) G = T;
   static std::atomic<unsigned long long> attr{0};
-  if (first_on_device(attr)) {
+  once_per_device(attr, [&] {
     (void)hipFuncSetAttribute((const void*)conv3x3c64_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CW_LDS);
     (void)hipGetLastError();
-  }
+  });
   hipLaunchKernelGGL(conv3x3c64_wgrad_kernel, dim3(G), dim3(512), CW_LDS, s, p);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);

@@ -553,7 +553,10 @@ __device__ __forceinline__ int cdiv_signed(int a, int b) { return a >= 0 ? (a + 
 // (row & 3) | (row & 4) << 1 keeps those 16 positions distinct (conflict-free).
 __device__ __forceinline__ int pk_sw(int row) { return (row & 3) | ((row & 4) << 1); }
 
-template <int KT, int NB, bool OPS, bool FWD>
+// DUAL: two A sources concatenated along K (the projection block's conv3 + shortcut conv,
+// K = K1 + K2): k-steps [0, K1 / 64) read the first source, the rest the second at its own
+// geometry (H2 x W2, stride2) -- the same ring, the same B walk over the concatenated weights.
+template <int KT, int NB, bool OPS, bool FWD, bool DUAL = false>
 __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmParams p) {
   constexpr int BM = 128, BN = 128, NW = 4, TM = 4, TN = 4, WAVES_N = 2;
   constexpr int A_BYTES = BM * 128, STAGE = A_BYTES + BN * 128;   // 32 KiB: A | B, or the operand tile
@@ -576,6 +579,8 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
   if (bq >= T) return;   // (whole workgroup)
   const int t_begin = bq, t_end = T;
   const long HW = (long)p.H * p.W, pix_end = p.N * HW;
+  const long HW2 = DUAL ? (long)p.H2 * p.W2 : 0;
+  const int KT1 = DUAL ? p.K1 / 64 : KT;   // k-steps of the first source
   const int HoWo = p.Ho * p.Wo;
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.b, p.Nn * p.ldb * 2);
 
@@ -593,21 +598,27 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
 
   // ---- loader: LDS-DMA of ring step (ld_t, ld_j) ----
   int ld_t = t_begin, ld_j = 0;
-  uint32_t a_o[AI], b_o[BI];
-  __amdgpu_buffer_rsrc_t ra;
+  uint32_t a_o[AI], a_o2[DUAL ? AI : 1], b_o[BI];
+  __amdgpu_buffer_rsrc_t ra, ra2;
   auto set_tile = [&](int t) {
     const int m0 = p.m_begin + (t / nt) * BM, n0 = (t % nt) * BN;
     const int n_first = fdiv(m0, p.mg_howo);
     ra = make_rsrc_at(p.a1, n_first * HW * p.C1, pix_end * p.C1);
+    if (DUAL) ra2 = make_rsrc_at(p.a2, n_first * HW2 * p.C2, p.N * HW2 * p.C2);
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int m = m0 + (wave * AI + i) * 8 + (lane >> 3);
       a_o[i] = OOB_OFF;
+      if (DUAL) a_o2[i] = OOB_OFF;
       if (m < p.M) {
         const int n = fdiv(m, p.mg_howo), rem = m - n * HoWo;
         const int ho = fdiv(rem, p.mg_wo), wo = rem - ho * p.Wo;
         const int pix = ((n - n_first) * p.H + ho * p.stride) * p.W + wo * p.stride;
         a_o[i] = (uint32_t)((pix * p.C1 + sw_chunk(lane, i) * 8) * 2);
+        if (DUAL) {
+          const int pix2 = ((n - n_first) * p.H2 + ho * p.stride2) * p.W2 + wo * p.stride2;
+          a_o2[i] = (uint32_t)((pix2 * p.C2 + sw_chunk(lane, i) * 8) * 2);
+        }
       }
     }
 #pragma unroll
@@ -622,8 +633,14 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
     char* base = smem + buf * STAGE;
     if (!OPS || ld_j < KT) {           // k-step: channels [64 ld_j, 64 ld_j + 64) of the rows
       const int kofs = ld_j * 128;
+      if (DUAL && ld_j >= KT1) {       // (uniform) the second source's channels [64 (ld_j - KT1), +64)
 #pragma unroll
-      for (int i = 0; i < AI; ++i) buf_lds16(ra, LDS_PTR(base + (wave * AI + i) * 1024), live ? a_o[i] : OOB_OFF, kofs);
+        for (int i = 0; i < AI; ++i)
+          buf_lds16(ra2, LDS_PTR(base + (wave * AI + i) * 1024), live ? a_o2[i] : OOB_OFF, kofs - KT1 * 128);
+      } else {
+#pragma unroll
+        for (int i = 0; i < AI; ++i) buf_lds16(ra, LDS_PTR(base + (wave * AI + i) * 1024), live ? a_o[i] : OOB_OFF, kofs);
+      }
 #pragma unroll
       for (int i = 0; i < BI; ++i)
         buf_lds16(rb, LDS_PTR(base + A_BYTES + (wave * BI + i) * 1024), live ? b_o[i] : OOB_OFF, kofs);
@@ -1334,10 +1351,39 @@ int igemm_partial_rows(int M, int Nn, int K, bool bnz) {
 
 static void igemm_launch_cfg(const IgemmParams& p, int cfg, hipStream_t stream);
 
+// The dual-source (projection block conv3 + shortcut) forward on the persistent ring: the
+// fused c3 + c0 launches of the four projection blocks (K = 128 / 384 / 768 / 1536).  The
+// one-block-per-CU 8-phase tiles and the 2-stage 128x128 tiles both serialise each tile's
+// 32-128 KiB output store behind its K loop (35-56 % of the measured-bytes bound,
+// profiles/r6_roofline_b2560.txt); here the next tile's operands stream in during the
+// epilogue.  Ring depth 2 only.
+int g_igemm_pk_dual = 2;    // largest K / 64 run on the ring (0: off): K = 128 (conv2_block1) only --
+                            // the longer-K blocks ran 3-16 % slower there than on their tiles (ring
+                            // fills of 32 KiB per k-step cannot feed the MFMAs from L2: profiles/r6_pk_dual.txt)
+static bool igemm_pk_dual_launch(const IgemmParams& p, hipStream_t stream) {
+  const int KT = p.K / 64;
+  if (!g_igemm_pk_dual || KT > g_igemm_pk_dual || g_igemm_pk != 2) return false;
+  if (p.mode != EPI_FWD || !p.scale || !p.shift || p.res || p.up2 || p.out2 || p.stats || p.bn_z) return false;
+  if (p.R != 1 || p.S != 1 || p.pad != 0 || p.C1 != p.K1 || p.C2 != p.K - p.K1 || !igemm_no_halo(p)) return false;
+  if (p.Nn % 32) return false;
+  const long T = (long)((p.M - p.m_begin + 127) / 128) * ((p.Nn + 127) / 128);
+  long G = (long)num_cus() * 2;
+  if (G > T) G = T;
+#define PKD_GO(KT_) hipLaunchKernelGGL((igemm_pk_kernel<KT_, 2, true, true, true>), dim3((unsigned)G), dim3(256), 0, stream, p)
+  if (KT == 2) PKD_GO(2);
+  else if (KT == 6) PKD_GO(6);
+  else if (KT == 12) PKD_GO(12);
+  else if (KT == 24) PKD_GO(24);
+  else return false;
+#undef PKD_GO
+  return true;
+}
+
 // The persistent ring kernel for a short-K 1x1 problem (false: not eligible, nothing launched).
 static bool igemm_pk_launch(const IgemmParams& p, hipStream_t stream) {
   const int KT = p.K / 64;
-  if (p.a2 || p.R != 1 || p.S != 1 || p.pad != 0 || p.C1 != p.K || !igemm_no_halo(p)) return false;
+  if (p.a2) return igemm_pk_dual_launch(p, stream);
+  if (p.R != 1 || p.S != 1 || p.pad != 0 || p.C1 != p.K || !igemm_no_halo(p)) return false;
   if (KT != 1 && KT != 2 && KT != 4 && KT != 8) return false;
   if (p.mode != EPI_FWD && p.mode != EPI_DGRAD) return false;
   if (p.up2 || p.out2 || p.stats || p.bn_z || p.mask || p.Nn % 32) return false;
@@ -1376,7 +1422,9 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
   p.prow_begin = 0;
   p.ksplit = 1;
   const IgemmPlan pl = igemm_plan(p.M, p.Nn, p.K, p.bn_z != nullptr);
-  if (g_igemm_pk && pl.ks == 1 && pl.split >= p.M && pl.cfg == 1 && igemm_pk_launch(p, stream)) {
+  // (a forward dual-source problem goes to the ring whatever tile the plan picked: it has no
+  // column sums, so the partial-row layout of the plan does not apply)
+  if (g_igemm_pk && pl.ks == 1 && ((pl.split >= p.M && pl.cfg == 1) || p.a2) && igemm_pk_launch(p, stream)) {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? nullptr : hipGetErrorString(e);
   }

@@ -1,10 +1,10 @@
 // Fused stem forward (gfx950): conv1 (7x7/s2 as the 4x4/s1 space-to-depth window GEMM, K = 256)
 // + frozen BN + ReLU + ZeroPadding2D(1) + MaxPooling2D(3, 2), in one launch.  The conv output
 // (N x 112 x 112 x 64 bf16 at crop 224: 1.6 MB per image) never reaches HBM: the workgroup keeps
-// the three conv rows a pool row needs in LDS and writes only the pool output, its argmax taps
-// and its ReLU bits -- what the backward uses (the max-pool backward routes by the argmax tap,
-// and conv2_block1's dgrad masks with the pool output's bits).  Reference: the Keras ResNet50
-// stem behind imagenet-resnet50.py:56.
+// the conv rows a pool row needs in LDS and writes only the pool output, its argmax taps and its
+// ReLU bits -- what the backward uses (the max-pool backward routes by the argmax tap, and
+// conv2_block1's dgrad masks with the pool output's bits).  Reference: the Keras ResNet50 stem
+// behind imagenet-resnet50.py:56.
 //
 // Workgroup = (image, block of PB pool rows), 256 threads (4 waves), two workgroups per CU.
 // Per pool row p: conv rows 2p and 2p+1 (and 2p-1 for the block's first row) are computed as
@@ -14,10 +14,14 @@
 // a 16-pixel tile are consecutive pixels, conflict-free); the epilogue (scale / shift / ReLU /
 // bf16, exactly the igemm forward epilogue's expression) writes 4 channels x 1 pixel per lane
 // into a 3-row conv buffer (8-byte chunks XOR-swizzled by the pixel column so the stores and the
-// 16-byte pool reads are conflict-free).  After a barrier the workgroup pools row p (first
-// maximum in scan order, padding taps are zeros, as maxpool_fwd_kernel) while the next rows'
-// input is already in flight (global loads issued before the MFMA phase, written to the ring
-// after it).
+// 16-byte pool reads are conflict-free; index 0 of a row is a zero pixel).  After a barrier the
+// workgroup pools row p (first maximum in scan order, padding taps are zeros, as
+// maxpool_fwd_kernel) while the next rows' input is already in flight (global loads issued
+// before the MFMA phase, written to the ring after it).
+// (Round 6 also measured a one-workgroup-per-CU form with the roles split over the waves -- four
+// waves computing conv rows beside four pooling the previous row, input rows loaded four rows
+// ahead -- at 1.77 ms against 1.68 ms for this one at b2560: with one wave per SIMD per role both
+// roles were latency-bound.)
 #include "common.h"
 #include "kernels.h"
 
@@ -35,14 +39,17 @@ template <bool BITS>
 __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int SLOT = p.Ws * 32;
-  const int CROW = p.W1 * 128;
+  // conv row buffer: pixel x at index x + 1, index 0 a zero pixel (the pool's left padding tap
+  // reads it like any other: no per-tap bounds selects)
+  const int CROW = (p.W1 + 1) * 128;
   uint8_t* ring = lds;
   uint8_t* cbuf = lds + 8 * SLOT;
   const int b = blockIdx.x / p.nblk;
   const int blk = blockIdx.x - b * p.nblk;
   const int P0 = blk * p.PB;
   const int P1 = min(P0 + p.PB, p.H2);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // (uniform: the tile walk in SGPRs)
   const int lr = lane & 15, lg = lane >> 4;
 
   // ---- weights as A fragments: co = 16 nt + lr, k = 32 t + 8 lg + j (held for the whole launch)
@@ -61,6 +68,7 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
   // weight fragments keep the register file
   float* bn = reinterpret_cast<float*>(cbuf + 3 * CROW);
   if (tid < 128) bn[tid] = tid < 64 ? p.scale[tid] : p.shift[tid - 64];
+  if (tid < 24) *reinterpret_cast<uint4*>(cbuf + (tid >> 3) * CROW + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
 
   const uint4* x2b = reinterpret_cast<const uint4*>(p.x2 + (long)b * p.Hs * p.Ws * 16);
   const int RCH = p.Ws * 2;   // 16-byte chunks per input row
@@ -71,7 +79,21 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
     uint4* dst = reinterpret_cast<uint4*>(ring + (yy & 7) * SLOT);
     for (int c = tid; c < RCH; c += SP_THREADS) dst[c] = x2b[(long)yy * RCH + c];
   }
+  // wait for the weights here (an empty asm reading them): left pending into the row loop, the
+  // compiler's in-order vmcnt waits before their MFMAs also wait for every pool row's prefetch
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(wa[nt][t]));
   __syncthreads();
+  float bsc[NTW][4], bsh[NTW][4];   // this lane's folded BN: channels 16 (nt0 + ntl) + 4 lg + i
+#pragma unroll
+  for (int ntl = 0; ntl < NTW; ++ntl) {
+    const float4 a = *reinterpret_cast<const float4*>(bn + 16 * (nt0 + ntl) + 4 * lg);
+    const float4 c = *reinterpret_cast<const float4*>(bn + 64 + 16 * (nt0 + ntl) + 4 * lg);
+    bsc[ntl][0] = a.x; bsc[ntl][1] = a.y; bsc[ntl][2] = a.z; bsc[ntl][3] = a.w;
+    bsh[ntl][0] = c.x; bsh[ntl][1] = c.y; bsh[ntl][2] = c.z; bsh[ntl][3] = c.w;
+  }
 
   const int nct = (p.W1 + 15) >> 4;
   for (int pr = P0; pr < P1; ++pr) {
@@ -107,18 +129,14 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
       }
       // epilogue: lane holds D[co = 16 nt + 4 lg + i][px = lr]
       if (xl < p.W1) {
-        uint8_t* crow = cbuf + (y % 3) * CROW + xl * 128;
+        uint8_t* crow = cbuf + (y % 3) * CROW + (xl + 1) * 128;
 #pragma unroll
         for (int ntl = 0; ntl < NTW; ++ntl) {
-          const int nt = nt0 + ntl;
-          const float4 a = *reinterpret_cast<const float4*>(bn + 16 * nt + 4 * lg);
-          const float4 c = *reinterpret_cast<const float4*>(bn + 64 + 16 * nt + 4 * lg);
-          const float sc[4] = {a.x, a.y, a.z, a.w}, sh[4] = {c.x, c.y, c.z, c.w};
           float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = acc[ntl][i] * sc[i] + sh[i];
+          for (int i = 0; i < 4; ++i) v[i] = acc[ntl][i] * bsc[ntl][i] + bsh[ntl][i];
           const uint2 pk = make_uint2(relu_pk2(pack2(v[0], v[1])), relu_pk2(pack2(v[2], v[3])));
-          *reinterpret_cast<uint2*>(crow + swz_chunk(4 * nt + lg, xl) * 8) = pk;
+          *reinterpret_cast<uint2*>(crow + swz_chunk(4 * (nt0 + ntl) + lg, xl + 1) * 8) = pk;
         }
       }
     }
@@ -136,33 +154,36 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_fwd_kernel(StemPoolPa
     __syncthreads();
     // ---- pool row pr: window rows 2pr-1 .. 2pr+1, columns 2q-1 .. 2q+1; item = (q, 8-channel group)
     const long orow = ((long)b * p.H2 + pr) * p.W2;
-    // branch-free: the conv rows are ReLU outputs (>= 0), so bf16 bit patterns (sign cleared:
-    // a -0 counts as 0) order like unsigned integers; key = bits << 16 | (15 - tap) and one
-    // unsigned max per tap per channel keeps the largest value and, among equal values, the
-    // first tap in scan order -- the same winner as the float compare.  Padding taps are 0.
+    // branch-free: the conv rows are ReLU outputs (relu_pk2 leaves no sign bit, -0 included),
+    // so bf16 bit patterns order like unsigned integers; key = bits << 16 | (15 - tap), one byte
+    // permute per element, and one unsigned max per tap keeps the largest value and, among equal
+    // values, the first tap in scan order -- the float compare's winner.  Every key starts as a
+    // zero at tap 0 (15): a padding tap (zero) never beats it, so the top padding row is skipped
+    // (uniform branch) and the left one reads the zero pixel at index 0.  (Round 5 built the keys
+    // with shifts / masks and bounds-selected every tap: 280 VALU per item, 150 now.)
+    const int rs0 = pr > 0 ? ((2 * pr - 1) % 3) * CROW : 0, rs1 = ((2 * pr) % 3) * CROW, rs2 = ((2 * pr + 1) % 3) * CROW;
     for (int it = tid; it < p.W2 * 8; it += SP_THREADS) {
       const int q = it >> 3, cg = it & 7;
       uint32_t key[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) key[e] = 15u;   // (tap 0 of a zero: the padding corner)
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int y = 2 * pr - 1 + r;
+      for (int e = 0; e < 8; ++e) key[e] = 15u;   // (tap 0 of a zero)
+      auto tap_row = [&](int roff, uint32_t cbase) __attribute__((always_inline)) {   // window row r: cbase = 15 - 3 r
 #pragma unroll
         for (int sx = 0; sx < 3; ++sx) {
-          const int x = 2 * q - 1 + sx;
-          const uint32_t c = 15u - (uint32_t)(r * 3 + sx);
-          const bool ok = y >= 0 && x >= 0;
-          const uint4 u = *reinterpret_cast<const uint4*>(cbuf + ((ok ? y : 0) % 3) * CROW + (ok ? x : 0) * 128 +
-                                                          swz_chunk(2 * cg, ok ? x : 0) * 8);
-          const uint32_t d[4] = {ok ? u.x : 0u, ok ? u.y : 0u, ok ? u.z : 0u, ok ? u.w : 0u};
+          const int xi = 2 * q + sx;                   // buffer index of conv pixel 2q - 1 + sx
+          const uint4 u = *reinterpret_cast<const uint4*>(cbuf + roff + xi * 128 + swz_chunk(2 * cg, xi) * 8);
+          const uint32_t c = cbase - (uint32_t)sx;
+          const uint32_t d[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            key[2 * h] = max(key[2 * h], ((d[h] << 16) & 0x7fff0000u) | c);
-            key[2 * h + 1] = max(key[2 * h + 1], (d[h] & 0x7fff0000u) | c);
+            key[2 * h] = max(key[2 * h], __builtin_amdgcn_perm(d[h], c, 0x05040100u));       // lo << 16 | c
+            key[2 * h + 1] = max(key[2 * h + 1], __builtin_amdgcn_perm(d[h], c, 0x07060100u));   // hi | c
           }
         }
-      }
+      };
+      if (pr > 0) tap_row(rs0, 15u);
+      tap_row(rs1, 12u);
+      tap_row(rs2, 9u);
       const long o = (orow + q) * 64 + cg * 8;
       const uint4 yv = make_uint4((key[0] >> 16) | (key[1] & 0xffff0000u), (key[2] >> 16) | (key[3] & 0xffff0000u),
                                   (key[4] >> 16) | (key[5] & 0xffff0000u), (key[6] >> 16) | (key[7] & 0xffff0000u));
@@ -238,6 +259,31 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_bwd_kernel(StemPoolBw
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const long gbase = (long)b * p.H2 * p.W2;
   const int Wq = W1 / 2;   // conv column pairs (= W2)
+  // The router's operands (pool gradient + argmax taps of pool rows rp, rp + 1 at the item's two
+  // column pairs) are loaded one row pair AHEAD, during the previous row pair's MFMAs: loaded at
+  // the top of the router, every row pair paid a dependent HBM round trip before any MFMA.
+  // Raw values only (clamped, always-valid addresses); the bounds masks are applied at use, so
+  // no select makes the compiler wait for a load early.  Items it = tid + 256 k, k < RI.
+  constexpr int RI = 2;   // (W2 * 8 <= 512 items: checked by the launcher)
+  uint4 rgv[RI][2][2];
+  uint2 riv[RI][2][2];
+  auto router_load = [&](int rp) {
+#pragma unroll
+    for (int k = 0; k < RI; ++k) {
+      const int it = tid + k * SP_THREADS;
+      const int qq = min(it >> 3, Wq - 1), cg = it & 7;
+#pragma unroll
+      for (int dr = 0; dr < 2; ++dr)
+#pragma unroll
+        for (int dc = 0; dc < 2; ++dc) {
+          const int pr = min(rp + dr, p.H2 - 1), pc = min(qq + dc, p.W2 - 1);
+          const long o = (gbase + (long)pr * p.W2 + pc) * 64 + cg * 8;
+          rgv[k][dr][dc] = *reinterpret_cast<const uint4*>(p.gpool + o);
+          riv[k][dr][dc] = *reinterpret_cast<const uint2*>(p.idx + o);
+        }
+    }
+  };
+  router_load(P0);
   __syncthreads();
 
   for (int rp = P0; rp < P1; ++rp) {
@@ -254,7 +300,10 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_bwd_kernel(StemPoolBw
     }
     // ---- route pool rows rp (taps r = 1, 2) and rp + 1 (tap r = 0) into conv rows 2rp, 2rp+1:
     //      item = (column pair qq, 8-channel group cg), as maxpool_bwd_stream_kernel
-    for (int it = tid; it < Wq * 8; it += SP_THREADS) {
+#pragma unroll
+    for (int k = 0; k < RI; ++k) {
+      const int it = tid + k * SP_THREADS;
+      if (it >= Wq * 8) continue;
       const int qq = it >> 3, cg = it & 7;
       uint4 gv[2][2];
       uint2 iv[2][2];
@@ -262,13 +311,9 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_bwd_kernel(StemPoolBw
       for (int dr = 0; dr < 2; ++dr)
 #pragma unroll
         for (int dc = 0; dc < 2; ++dc) {
-          const int pr = rp + dr, pc = qq + dc;
-          const bool ok = pr < p.H2 && pc < p.W2;
-          const long o = (gbase + (long)(ok ? pr : 0) * p.W2 + (ok ? pc : 0)) * 64 + cg * 8;
-          const uint4 gl = *reinterpret_cast<const uint4*>(p.gpool + o);
-          const uint2 il = *reinterpret_cast<const uint2*>(p.idx + o);
-          gv[dr][dc] = ok ? gl : make_uint4(0, 0, 0, 0);
-          iv[dr][dc] = ok ? il : make_uint2(0xffffffffu, 0xffffffffu);
+          const bool ok = rp + dr < p.H2 && qq + dc < p.W2;
+          gv[dr][dc] = ok ? rgv[k][dr][dc] : make_uint4(0, 0, 0, 0);
+          iv[dr][dc] = ok ? riv[k][dr][dc] : make_uint2(0xffffffffu, 0xffffffffu);
         }
       float ga[8], gb[8], gc[8], gd[8];
       unpack8(gv[0][0], ga); unpack8(gv[0][1], gb); unpack8(gv[1][0], gc); unpack8(gv[1][1], gd);
@@ -303,6 +348,7 @@ __global__ void __launch_bounds__(SP_THREADS, 2) stem_pool_bwd_kernel(StemPoolBw
       }
     }
     __syncthreads();
+    if (more) router_load(rp + 1);   // (lands during this row pair's MFMAs)
     // ---- weight-gradient MFMAs over the row pair: 2 rows x nst steps of 32 pixels
     for (int a = 0; a < 2; ++a) {
       const int y = 2 * rp + a;
@@ -386,21 +432,22 @@ const char* stem_pool_bwd_launch(StemPoolBwdParams p, hipStream_t s) {
   if (p.H1 % 2 || p.W1 % 2) return "stem_pool_bwd: even conv1 output (even crop) expected";
   if (p.H2 != p.H1 / 2 || p.W2 != p.W1 / 2) return "stem_pool_bwd: pool output must be the pad-1 3x3/s2 size";
   if (p.Ws > 128 || p.W1 > 128) return "stem_pool_bwd: rows wider than the image / prefetch cover (crop <= 250)";
+  if (p.W2 * 8 > 2 * SP_THREADS) return "stem_pool_bwd: more router items per row than the prefetch registers cover";
   const int lds = stem_pool_bwd_lds_bytes(p.Ws);
   if (lds > 80 * 1024) return "stem_pool_bwd: LDS per workgroup above the two-per-CU budget";
   p.PB = stem_pool_rows(p.B, p.H2, p.PB);
   p.nblk = (p.H2 + p.PB - 1) / p.PB;
   static std::atomic<unsigned long long> attr{0};
-  if (first_on_device(attr)) {
+  once_per_device(attr, [&] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_bwd_kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-  }
+  });
   hipLaunchKernelGGL(stem_pool_bwd_kernel, dim3((unsigned)((long)p.B * p.nblk)), dim3(SP_THREADS), lds, s, p);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }
 
-int stem_pool_lds_bytes(int Ws, int W1) { return 8 * Ws * 32 + 3 * W1 * 128 + 512; }
+int stem_pool_lds_bytes(int Ws, int W1) { return 8 * Ws * 32 + 3 * (W1 + 1) * 128 + 512; }
 
 const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s) {
   if (p.H1 != p.Hs - 3 || p.W1 != p.Ws - 3) return "stem_pool: conv1 output must be the s2d input minus 3";
@@ -418,12 +465,12 @@ const char* stem_pool_fwd_launch(StemPoolParams p, hipStream_t s) {
   }
   p.nblk = (p.H2 + p.PB - 1) / p.PB;
   static std::atomic<unsigned long long> attr{0};
-  if (first_on_device(attr)) {
+  once_per_device(attr, [&] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_pool_fwd_kernel<false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-  }
+  });
   const dim3 grid((unsigned)((long)p.B * p.nblk));
   if (p.bits) hipLaunchKernelGGL((stem_pool_fwd_kernel<true>), grid, dim3(SP_THREADS), lds, s, p);
   else hipLaunchKernelGGL((stem_pool_fwd_kernel<false>), grid, dim3(SP_THREADS), lds, s, p);

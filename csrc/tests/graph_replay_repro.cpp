@@ -1,0 +1,164 @@
+// Standalone reproducer for the round-5 hipGraphLaunch segfault (profiles/r5_graph_crash.txt):
+// HIP graphs with parallel branches (the engine's two-stream backward forks a side stream into
+// every captured step) launched on the LEGACY DEFAULT STREAM after other graph executables of
+// the process were created, run and destroyed.  No torch, no pddl code: plain HIP runtime calls
+// in the order torch.cuda.CUDAGraph makes them (stream capture in thread-local mode on a created
+// stream, fork / join through events, instantiate, destroy the hipGraph_t, hipGraphLaunch).
+//
+//   hipcc --offload-arch=gfx950 -O2 csrc/tests/graph_replay_repro.cpp -o /tmp/graph_repro
+//   /tmp/graph_repro [rounds=200]
+//
+// Every replay's kernels add to device counters; the program checks the counts after each
+// scenario and prints one line per scenario.  A fault inside hipGraphLaunch kills the process
+// (SIGSEGV, exit 139) at a printed scenario, which then names the runtime as the owner: the
+// program has no other state.  Scenarios (each launches on stream 0 = legacy default and on a
+// created stream, so both paths run in the same process):
+//   A  one 2-branch exec, replayed `rounds` times
+//   B  8 execs of 2..5 branches; execs 0..3 destroyed; 4..7 replayed
+//   C  churn: per round create an exec of (round % 4 + 2) branches, replay it on a created
+//      stream, destroy the previous one, replay the new one on stream 0
+//   D  as C with the capture's side streams destroyed and re-created every round (torch creates
+//      side streams from its pool; an exec keeps a stream pointer only if the runtime copies it)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                   \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      std::fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(2);                                                                             \
+    }                                                                                           \
+  } while (0)
+
+__global__ void bump(unsigned long long* c, int slot) {
+  if (threadIdx.x == 0) atomicAdd(c + slot, 1ull);
+}
+
+// Capture a graph whose work forks into `branches` parallel streams (one kernel each, plus one
+// on the origin before the fork and one after the join), the engine's fork / join pattern.
+static hipGraphExec_t make_exec(hipStream_t origin, std::vector<hipStream_t>& side, int branches,
+                                unsigned long long* ctr, int slot0) {
+  hipGraph_t g = nullptr;
+  std::vector<hipEvent_t> ev(2 * branches + 1);
+  for (auto& e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  CK(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
+  hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, origin, ctr, slot0);
+  CK(hipEventRecord(ev[0], origin));
+  for (int b = 0; b < branches; ++b) {
+    CK(hipStreamWaitEvent(side[b], ev[0], 0));
+    hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, side[b], ctr, slot0 + 1 + b);
+    hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, side[b], ctr, slot0 + 1 + b);
+    CK(hipEventRecord(ev[1 + b], side[b]));
+    CK(hipStreamWaitEvent(origin, ev[1 + b], 0));
+  }
+  hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, origin, ctr, slot0);
+  CK(hipStreamEndCapture(origin, &g));
+  hipGraphExec_t ex = nullptr;
+  CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  CK(hipGraphDestroy(g));   // (torch keeps only the executable unless keep_graph)
+  for (auto& e : ev) CK(hipEventDestroy(e));
+  return ex;
+}
+
+static unsigned long long expect_total(int branches, int replays) { return (unsigned long long)replays * (2 + 2 * branches); }
+
+static bool check(const char* tag, unsigned long long* ctr, unsigned long long want) {
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> h(64);
+  CK(hipMemcpy(h.data(), ctr, 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  unsigned long long got = 0;
+  for (auto v : h) got += v;
+  std::printf("%s: kernel executions %llu, expected %llu -> %s\n", tag, got, want, got == want ? "ok" : "MISMATCH");
+  std::fflush(stdout);
+  CK(hipMemset(ctr, 0, 64 * sizeof(unsigned long long)));
+  CK(hipDeviceSynchronize());
+  return got == want;
+}
+
+int main(int argc, char** argv) {
+  const int rounds = argc > 1 ? std::atoi(argv[1]) : 200;
+  unsigned long long* ctr = nullptr;
+  CK(hipMalloc(&ctr, 64 * sizeof(unsigned long long)));
+  CK(hipMemset(ctr, 0, 64 * sizeof(unsigned long long)));
+  hipStream_t cap, launch;
+  CK(hipStreamCreate(&cap));
+  CK(hipStreamCreate(&launch));
+  std::vector<hipStream_t> side(8);
+  for (auto& s : side) CK(hipStreamCreate(&s));
+  bool ok = true;
+
+  {  // A
+    std::printf("A: one 2-branch exec, %d replays on stream 0\n", rounds);
+    std::fflush(stdout);
+    hipGraphExec_t ex = make_exec(cap, side, 2, ctr, 0);
+    for (int r = 0; r < rounds; ++r) CK(hipGraphLaunch(ex, 0));
+    ok &= check("A", ctr, expect_total(2, rounds));
+    CK(hipGraphExecDestroy(ex));
+  }
+  {  // B
+    std::printf("B: 8 execs (2..5 branches), 0..3 destroyed, 4..7 replayed %d times on stream 0\n", rounds);
+    std::fflush(stdout);
+    std::vector<hipGraphExec_t> ex(8);
+    for (int i = 0; i < 8; ++i) ex[i] = make_exec(cap, side, 2 + i % 4, ctr, 8 * (i % 8));
+    for (int i = 0; i < 8; ++i) CK(hipGraphLaunch(ex[i], launch));   // run every one once
+    CK(hipStreamSynchronize(launch));
+    unsigned long long want = 0;
+    for (int i = 0; i < 8; ++i) want += expect_total(2 + i % 4, 1);
+    for (int i = 0; i < 4; ++i) CK(hipGraphExecDestroy(ex[i]));
+    for (int r = 0; r < rounds; ++r)
+      for (int i = 4; i < 8; ++i) CK(hipGraphLaunch(ex[i], 0));
+    for (int i = 4; i < 8; ++i) want += expect_total(2 + i % 4, rounds);
+    ok &= check("B", ctr, want);
+    for (int i = 4; i < 8; ++i) CK(hipGraphExecDestroy(ex[i]));
+  }
+  {  // C
+    std::printf("C: exec churn, %d rounds (create, run on a created stream, destroy the previous, run on stream 0)\n",
+                rounds);
+    std::fflush(stdout);
+    hipGraphExec_t prev = nullptr;
+    unsigned long long want = 0;
+    for (int r = 0; r < rounds; ++r) {
+      const int nb = 2 + r % 4;
+      hipGraphExec_t ex = make_exec(cap, side, nb, ctr, 8 * (r % 8));
+      CK(hipGraphLaunch(ex, launch));
+      if (prev) CK(hipGraphExecDestroy(prev));
+      CK(hipGraphLaunch(ex, 0));
+      want += expect_total(nb, 2);
+      prev = ex;
+    }
+    CK(hipGraphExecDestroy(prev));
+    ok &= check("C", ctr, want);
+  }
+  {  // D
+    std::printf("D: as C, side streams destroyed and re-created every round, %d rounds\n", rounds);
+    std::fflush(stdout);
+    hipGraphExec_t prev = nullptr;
+    unsigned long long want = 0;
+    for (int r = 0; r < rounds; ++r) {
+      const int nb = 2 + r % 4;
+      hipGraphExec_t ex = make_exec(cap, side, nb, ctr, 8 * (r % 8));
+      CK(hipGraphLaunch(ex, launch));
+      CK(hipStreamSynchronize(launch));
+      for (auto& s : side) {
+        CK(hipStreamDestroy(s));
+        CK(hipStreamCreate(&s));
+      }
+      if (prev) CK(hipGraphExecDestroy(prev));
+      CK(hipGraphLaunch(ex, 0));
+      want += expect_total(nb, 2);
+      prev = ex;
+    }
+    CK(hipGraphExecDestroy(prev));
+    ok &= check("D", ctr, want);
+  }
+  for (auto& s : side) CK(hipStreamDestroy(s));
+  CK(hipStreamDestroy(cap));
+  CK(hipStreamDestroy(launch));
+  CK(hipFree(ctr));
+  std::printf("graph_replay_repro: %s\n", ok ? "all scenarios completed, counts match" : "COUNT MISMATCH");
+  return ok ? 0 : 1;
+}

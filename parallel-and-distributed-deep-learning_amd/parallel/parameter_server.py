@@ -682,7 +682,7 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             t_drained = None
             hb.step()
             store.set(f"cur/{rank}", f"{epoch}:{lo}:{hi}")
-            for _t in range(lo, hi):
+            for t in range(lo, hi):
                 hb.step()
                 if fault_at is not None and steps_done == fault_at[1]:
                     print(f"[worker {widx}] injected {fault_at[0]} at step {steps_done}", flush=True)
@@ -693,15 +693,18 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
                 images, labels = next(it)
                 st.train_step(images, labels, lr)
                 steps_done += 1
-            if store.check([f"dead/{rank}"]):
-                # declared dead while running this block (its tickets are re-queued): publishing
-                # them now would count them twice
-                sys.stderr.write(f"[ps worker rank {rank}] declared dead by the coordinator: exiting\n")
-                sys.stderr.flush()
-                os._exit(18)
-            store.multi_set([f"tdone/{epoch}/{t}" for t in range(lo, hi)], ["1"] * (hi - lo))
-            store.set(f"cur/{rank}", f"{epoch}:-1")
-            store.add(f"done/{epoch}", hi - lo)
+                # progress is published per step, not per block: a worker that dies inside a
+                # block leaves only its unfinished tickets to the re-queue (each finished step
+                # already pushed its gradient; re-running it would apply that update twice)
+                if store.check([f"dead/{rank}"]):
+                    # declared dead while running this block (its open tickets are re-queued):
+                    # publishing this step now would count it twice
+                    sys.stderr.write(f"[ps worker rank {rank}] declared dead by the coordinator: exiting\n")
+                    sys.stderr.flush()
+                    os._exit(18)
+                store.multi_set([f"tdone/{epoch}/{t}", f"cur/{rank}"],
+                                ["1", f"{epoch}:{t + 1}:{hi}" if t + 1 < hi else f"{epoch}:-1"])
+                store.add(f"done/{epoch}", 1)
         hb.step()
         worker.exchange_end()                    # drain the last overlapped push of the epoch
         hb.wait()

@@ -30,30 +30,6 @@ import torch
 # hipErrorStreamCaptureUnsupported on the Mirrored entry script's first (captured) step.
 CAPTURE_MODE = "thread_local"
 
-import os as _os
-
-
-def _exec_layout(g):
-    """(diagnostics, PDDL_GRAPH_DEBUG=1) the HIP runtime's view of a graph executable of this
-    image's libamdhip64: parallel branch count and the size of its parallel-stream table."""
-    import ctypes
-    ex = g.raw_cuda_graph_exec()
-    if not ex:
-        return None
-    n = ctypes.c_int.from_address(ex + 0x48).value
-    b0 = ctypes.c_uint64.from_address(ex + 0x1b8).value
-    b1 = ctypes.c_uint64.from_address(ex + 0x1c0).value
-    ents = [hex(ctypes.c_uint64.from_address(b0 + 8 * i).value) for i in range((b1 - b0) // 8)] if b0 else []
-    return n, (b1 - b0) // 8, hex(b0), ents
-
-
-def _glog(msg):
-    path = _os.environ.get("PDDL_CRASH_TRACE")
-    if _os.environ.get("PDDL_GRAPH_DEBUG") == "1" and path:
-        with open(path, "a") as f:
-            f.write(msg + "\n")
-
-
 _REPLAY = {}
 
 
@@ -67,7 +43,15 @@ def replay_stream(device) -> torch.cuda.Stream:
     csrc/runtime/crash_trace.cpp) -- once the process had created and run other graphs
     (deterministic after tests/test_gpu_{bn_train,capture,engine}.py, then the Mirrored
     graphed step; alone it passed).  The same graphs launched on a created stream ran clean in
-    the same sequence (scripts/crash_bisect.sh, profiles/r5_graph_crash.txt)."""
+    the same sequence (profiles/r5_graph_crash.txt).
+
+    Owner (round 6): not reproduced outside torch.  The standalone HIP program
+    csrc/tests/graph_replay_repro.cpp (no torch: 2-5-branch fork / join captures, executables
+    created, run, destroyed and churned, side streams destroyed and re-created, thousands of
+    replays on the legacy default stream) ran clean against both the ROCm 7.2 runtime and the
+    runtime torch bundles (scripts/graph_repro.sh, profiles/r6_graph_repro.txt).  So the plain
+    runtime API sequence does not fault; the trigger needs torch's graph / allocator / stream
+    pool state in that long-lived process, and the created launch stream stays the fix."""
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
     s = _REPLAY.get(idx)
@@ -148,8 +132,6 @@ class GraphedTrainStep:
         if self.opt is not None:
             self.opt._iterations = it    # the capture pass did not step (no setter: hs is current)
         self.graph = g
-        if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
-            _glog(f"whole-step graph captured: {_exec_layout(g)}")
 
     def __call__(self, images, labels, flip=None, crop_offset=(0, 0)):
         self._load(images, labels, flip, crop_offset)
@@ -273,15 +255,11 @@ class SegmentedStepGraphs(GraphedTrainStep):
         opt._iterations = it        # capture ran no kernels: training state did not advance
         self.segments = segs
         self.opt_graph = og
-        if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
-            _glog(f"captured {id(self):x}: " + ", ".join(str(_exec_layout(g) if g else None) for g in segs))
 
     def load(self, images, labels, flip=None, crop_offset=(0, 0)):
         self._load(images, labels, flip, crop_offset)
 
     def replay_segment(self, k: int):
-        if _os.environ.get("PDDL_GRAPH_DEBUG") == "1":
-            _glog(f"replay segment {k} of {id(self):x}: exec (branches, streams, table) {_exec_layout(self.segments[k]) if self.segments[k] else None}")
         if self.segments[k] is not None:
             _launch(self.segments[k])
 
@@ -293,24 +271,13 @@ class SegmentedStepGraphs(GraphedTrainStep):
 
 def _capture_is_empty() -> bool:
     """True while the current stream's capture has recorded nothing since it began (no
-    dependency nodes): hipStreamGetCaptureInfo_v2 of the HIP runtime torch loaded."""
-    import ctypes
-    global _HIP
-    if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so")
-    st = ctypes.c_int(0)
-    cid = ctypes.c_ulonglong(0)
-    graph = ctypes.c_void_p()
-    deps = ctypes.c_void_p()
-    n = ctypes.c_size_t(0)
-    rc = _HIP.hipStreamGetCaptureInfo_v2(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), ctypes.byref(st),
-                                        ctypes.byref(cid), ctypes.byref(graph), ctypes.byref(deps), ctypes.byref(n))
-    if rc != 0 or st.value != 1:
-        raise RuntimeError(f"segmented capture: stream not capturing (hip error {rc}, status {st.value})")
-    return n.value == 0
-
-
-_HIP = None
+    dependency nodes): hipStreamGetCaptureInfo_v2 through the native extension, i.e. the HIP
+    runtime the kernels and torch use (no second runtime loaded by name)."""
+    from ..ops.native import require_native
+    rc, st, n = require_native().stream_capture_deps(torch.cuda.current_stream().cuda_stream)
+    if rc != 0 or st != 1:
+        raise RuntimeError(f"segmented capture: stream not capturing (hip error {rc}, status {st})")
+    return n == 0
 
 
 def _launch(g):

@@ -130,17 +130,13 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
     return ev
 
 
-def main():
-    path = sys.argv[1]
-    B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
-    crop = int(sys.argv[3]) if len(sys.argv) > 3 else 224
-    knobs = sys.argv[4] if len(sys.argv) > 4 else ""   # the run's PDDL_KNOBS (changes the launch plan)
+def segment(path, B=1024, crop=224, knobs=""):
+    """The last complete training step of a rocprofv3 CSV (kernel trace or one-counter
+    collection), paired with the engine's launch schedule: [(event, [csv rows])]."""
     rows = [r for r in csv.DictReader(open(path))]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
-    proxy = [r for r in rows if "comm_proxy" in r["Kernel_Name"]]   # bench --comm-proxy stand-ins
-    rows = [r for r in rows if "comm_proxy" not in r["Kernel_Name"]]
-    import os
+    rows = [r for r in rows if "comm_proxy" not in r["Kernel_Name"]]   # bench --comm-proxy stand-ins
     ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0", os.environ.get("PDDL_FUSE_BWD", "1") != "0",
                   os.environ.get("PDDL_FUSE_BWD", "1") != "2", os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0",
                   os.environ.get("PDDL_FUSE_STEM", "1") != "0")
@@ -153,10 +149,18 @@ def main():
         plan = require_native().igemm_plan
     except Exception:   # no native module: unsplit schedule
         plan = None
+
     # ... and a split-K launch is the slices + the combine (igemm_splitk_reduce_kernel); the
     # projection blocks' dual-source c1 dgrad is never split
+    pk_dual = 2   # (igemm_pk_dual knob: dual-source forwards with K / 64 <= this run as one ring launch)
+    for knob in filter(None, knobs.split(",")):
+        if knob.startswith("igemm_pk_dual="):
+            pk_dual = int(knob.split("=")[1])
+
     def ndisp(e):
         if e[0] != "igemm" or plan is None:
+            return 1
+        if len(e) > 5 and e[5] == "dual" and "fwd" in e[1] and e[4][2] // 64 <= pk_dual:
             return 1
         cfg, split, ks = plan(*e[4])
         dual = len(e) > 5 and e[5] == "dual"
@@ -170,21 +174,38 @@ def main():
             st = s
             break
     seg = rows[st:st + need]
-    tot = 0
-    agg = {}
-    k = 0
+    out, k = [], 0
     for e, n in zip(ev, nd):
-        kind, name, flops, byts = e[:4]
         rs = seg[k:k + n]
         k += n
-        kn = " + ".join(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("pddl::", "")[:22] for r in rs)
-        assert kind.split("_")[0] in kn, (kind, kn)
+        kn = kernel_names(rs)
+        assert e[0].split("_")[0] in kn, (e[0], kn)
+        out.append((e, rs))
+    return out
+
+
+def kernel_names(rs):
+    return " + ".join(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+                      .replace("pddl::", "")[:22] for r in rs)
+
+
+def main():
+    path = sys.argv[1]
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    crop = int(sys.argv[3]) if len(sys.argv) > 3 else 224
+    knobs = sys.argv[4] if len(sys.argv) > 4 else ""   # the run's PDDL_KNOBS (changes the launch plan)
+    segs = segment(path, B, crop, knobs)
+    tot = 0
+    agg = {}
+    for e, rs in segs:
+        kind, name, flops, byts = e[:4]
+        kn = kernel_names(rs)
         t = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rs)
         tot += t
         k2 = kind + (" fwd" if "fwd" in name and kind == "igemm" else " dgrad" if "dgrad" in name else "")
         agg[k2] = agg.get(k2, 0) + t
         tf = flops / t / 1e12 if flops else 0
-        gb = byts / t / 1e9 if byts else 0
+        gb = byts / t / 1e9 if byts else 0   # MODELLED logical bytes (see scripts/roofline.py for measured)
         grid = "+".join(r.get("Grid_Size_X") or r.get("Grid_Size", "?") for r in rs)
         meas = ""
         if "Counter_Value" in rs[0]:
@@ -193,14 +214,11 @@ def main():
             cn = rs[0]["Counter_Name"]
             mb = sum(float(r["Counter_Value"]) for r in rs) * 1024 * (2 if cn == "FETCH_SIZE" else 1) / 1e6
             meas = f"  {cn[:5]} {mb:8.1f} MB ({mb * 1e6 / t / 1e9:6.0f} GB/s)"
-        print(f"{t*1e6:9.1f} us  {tf:7.1f} TF/s  {gb:7.0f} GB/s  grid={grid:>16}  {kn[:40]:40s} {name}{meas}")
+        print(f"{t*1e6:9.1f} us  {tf:7.1f} TF/s  {gb:7.0f} GB/s(model)  grid={grid:>16}  {kn[:40]:40s} {name}{meas}")
     print(f"step total {tot*1e3:.2f} ms")
-    t_first, t_last = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
+    seg0, seg1 = segs[0][1][0], segs[-1][1][-1]
+    t_first, t_last = int(seg0["Start_Timestamp"]), int(seg1["End_Timestamp"])
     print(f"step span (first start -> last end) {(t_last - t_first) * 1e-6:.2f} ms")
-    px = [r for r in proxy if t_first <= int(r["Start_Timestamp"]) <= t_last]
-    if px:
-        print(f"comm proxy: {len(px)} launches in the step, "
-              f"{sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in px) * 1e-6:.2f} ms busy")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1]):
         print(f"  {k:24s} {v*1e3:8.3f} ms")
 

@@ -30,6 +30,20 @@ hip = ctypes.CDLL("libamdhip64.so")
 KERNEL, EMPTY, WAIT_EV, REC_EV = 0, 5, 6, 7
 
 
+def exec_layout(g):
+    """The HIP runtime's private view of a graph executable (parallel branch count and its
+    parallel-stream table) at the struct offsets of THIS image's libamdhip64 -- a diagnostic of
+    the round-5 hipGraphLaunch fault only; nothing in the package reads runtime internals."""
+    ex = g.raw_cuda_graph_exec()
+    if not ex:
+        return None
+    n = ctypes.c_int.from_address(ex + 0x48).value
+    b0 = ctypes.c_uint64.from_address(ex + 0x1b8).value
+    b1 = ctypes.c_uint64.from_address(ex + 0x1c0).value
+    ents = [hex(ctypes.c_uint64.from_address(b0 + 8 * i).value) for i in range((b1 - b0) // 8)] if b0 else []
+    return n, (b1 - b0) // 8, hex(b0), ents
+
+
 def stream_status(s):
     st = ctypes.c_int(-1)
     rc = hip.hipStreamIsCapturing(ctypes.c_void_p(s.cuda_stream), ctypes.byref(st))

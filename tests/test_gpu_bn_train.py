@@ -176,7 +176,7 @@ def _engines(B, crop, image_size):
         if e.kind == "gamma":
             # Train-mode BN makes a randomly initialised ResNet-50 chaotic: the bf16 rounding of
             # the activations (~0.4% per layer) grows ~7% per conv and reaches ~50% relative
-            # difference at conv5 (scripts/debug_bn_train.py), with every layer individually
+            # difference at conv5 (a round-5 layer-by-layer bisection), with every layer individually
             # exact.  Small residual-branch gammas (as in zero-init-residual training) keep the
             # blocks near identity so the end-to-end comparison stays meaningful.
             lo = 0.1 if e.layer.endswith("_3_bn") else 0.5
@@ -199,7 +199,7 @@ def test_train_bn_engine_matches_reference(crop, image_size):
 
     Train-mode BN makes a randomly initialised ResNet-50 chaotic: bf16 rounding of the
     activations (~0.4% per layer, each layer individually exact) grows ~7% per conv end to end
-    (scripts/debug_bn_train.py).  So the forward is compared end to end with small
+    (a round-5 layer-by-layer bisection).  So the forward is compared end to end with small
     residual-branch gammas, and every backward stage is checked against fp32 autograd /
     torch conv gradients applied to the engine's OWN bf16 inputs of that stage."""
     from torch.nn.grad import conv2d_input, conv2d_weight

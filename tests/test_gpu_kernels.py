@@ -314,6 +314,36 @@ def test_igemm_dgrad_dual_source():
     assert rel(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(64, 64, 1, 11), (128, 256, 2, 9), (256, 512, 2, 7), (512, 1024, 2, 5)])
+@pytest.mark.parametrize("ring", [0, 24])
+def test_igemm_dual_source_forward(shape, ring):
+    """The projection block's fused conv3 + shortcut forward (two A sources along K, the shortcut
+    at its own geometry and stride) against fp32: on the persistent ring (igemm_pk_kernel DUAL,
+    K / 64 = 2, 6, 12, 24) and on the per-tile kernels; odd spatial sizes give partial row tiles,
+    the ReLU bits are checked against the output's signs."""
+    torch.manual_seed(23)
+    f, cin, st, ho = shape
+    n, h = 3, (ho - 1) * st + 1 + (st - 1)
+    y2 = rnd(n, ho, ho, f)
+    x = rnd(n, h, h, cin)
+    w3 = rnd(4 * f, 1, 1, f, scale=0.05)
+    w0 = rnd(4 * f, 1, 1, cin, scale=0.05)
+    wcat = torch.cat([w3.view(4 * f, f), w0.view(4 * f, cin)], 1).contiguous()
+    sc, sh = torch.rand(4 * f, device=dev) + 0.5, torch.randn(4 * f, device=dev)
+    out = torch.empty(n, ho, ho, 4 * f, dtype=torch.bfloat16, device=dev)
+    bits = torch.empty(n, ho, ho, f // 2, dtype=torch.uint8, device=dev)
+    N().set_variant("igemm_pk_dual", ring)
+    try:
+        N().igemm(y2, x, ho, ho, 1, 1, 1, 0, ho, ho, wcat, 0, sc, sh, None, None, None, out, 1, None, 0, 0, 0, 0, 0,
+                  None, bits)
+        torch.cuda.synchronize()
+    finally:
+        N().set_variant("igemm_pk_dual", 2)
+    ref = ((conv_ref(y2, w3, 1, 0) + conv_ref(x, w0, st, 0)) * sc + sh).relu()
+    assert rel(out, ref) < 1e-2
+    assert torch.equal(bits, pack_bits(out))
+
+
 def pack_bits(x):
     """Reference ReLU bitmask: bit e of byte [..., c // 8] is (x[..., 8 * (c // 8) + e] > 0)."""
     b = (x.float() > 0).to(torch.int32).view(*x.shape[:-1], x.shape[-1] // 8, 8)

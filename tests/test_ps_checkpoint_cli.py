@@ -54,6 +54,24 @@ def test_ps_worker_failure_requeues_closure(impl, monkeypatch):
     assert ps[0][2] >= 6                                     # all 6 closures done despite the failure
 
 
+def test_ps_worker_death_inside_a_ticket_block_is_not_replayed(monkeypatch):
+    """A worker killed at its 4th step, in the middle of a claimed block of >= 4 tickets: the
+    three steps it finished were pushed and published, so only the unfinished tickets are
+    re-queued and the PS applies spe updates (spe + 1 if the last push was in flight), not
+    spe + 3 as with per-block publishing."""
+    from pddl.parallel.parameter_server import run_ps_job
+    monkeypatch.setenv("PDDL_PS_IMPL", "c10d")
+    monkeypatch.setenv("PDDL_FAULT", "kill_worker:1@3")
+    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
+    monkeypatch.setenv("PDDL_PS_TICKET_BLOCK", "16")
+    spe = 40
+    cfg = _cfg("ps", steps_per_epoch=spe, batch_size=2, epochs=1, train_images=2 * spe)
+    res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
+    ps = [r for r in res if r[0] == "ps"]
+    assert ps[0][3] == [2]
+    assert spe <= ps[0][2] <= spe + 1, ps[0][2]
+
+
 def test_ps_plateau_lowers_lr_and_early_stop_ends_job(monkeypatch):
     """The coordinator runs ReduceLROnPlateau / EarlyStopping (imagenet-resnet50-ps.py:139-140)
     on worker 0's val_loss and publishes the LR and the stop flag to every worker: a flat
