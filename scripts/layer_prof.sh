@@ -10,4 +10,4 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof -o run -- python bench.py --steps 3 --warmup 2 "$@" > $OUT/prof.log 2>&1 || exit $?
 t=$(find $OUT/prof -name "run_kernel_trace.csv" | head -1)
-python scripts/analyze_trace.py $t ${BATCH:-2560} ${CROP:-224} > $OUT/per_layer.txt 2>&1; tail -12 $OUT/per_layer.txt
+python scripts/analyze_trace.py $t ${BATCH:-2560} ${CROP:-224} "$PDDL_KNOBS" > $OUT/per_layer.txt 2>&1; tail -12 $OUT/per_layer.txt
