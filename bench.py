@@ -356,7 +356,8 @@ def run(args):
                         and st.mirror.graph_mode else "")
                      if not (getattr(st, "mirror", None) is not None and st.mirror.graph_mode
                              and st.mirror._single_replica_job())
-                     else "mirrored: 1 replica, whole step as one HIP graph (no collective to run)"),
+                     else ("mirrored: 1 replica, whole step as one HIP graph (no collective to run)" if cfg.graphs
+                           else "mirrored: 1 replica, eager step (no collective to run)")),
         "multiworker": f"multiworker: {world} process(es) x {args.local_gpus if args.strategy == 'multiworker' else 1}"
                        " GPU(s), one RCCL communicator",
     }[cfg.strategy]
@@ -472,8 +473,10 @@ def run_ps(args):
     untimed warmup epoch, then a timed epoch of `steps` worker steps claimed by the workers
     asynchronously; value = aggregate worker images/sec of the timed epoch (worker 0's clock
     over every worker's training steps, parameter_server.py).  The role processes are bounded
-    by run_ps_job's job deadline (PDDL_PS_JOB_TIMEOUT, set from --timeout)."""
-    os.environ.setdefault("PDDL_PS_JOB_TIMEOUT", str(args.timeout))
+    by run_ps_job's job deadline (PDDL_PS job_timeout, set from --timeout unless given)."""
+    from pddl.utils.envopts import opts, with_opt
+    if "job_timeout" not in opts("PDDL_PS"):
+        os.environ["PDDL_PS"] = with_opt("PDDL_PS", "job_timeout", args.timeout)
     import pddl  # noqa: F401
     from pddl.config import make_config
     from pddl.parallel.parameter_server import run_ps_job

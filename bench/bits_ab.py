@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     N = require_native()
+    N.allow_knob_changes(True)   # (A/B of tile knobs between launches)
     dev = "cuda"
     B = a.batch
     bf = dict(dtype=torch.bfloat16, device=dev)

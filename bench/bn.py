@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     N = require_native()
+    N.allow_knob_changes(True)   # (A/B of tile knobs between launches)
     dev = "cuda"
     res = []
     for name, h, c in SHAPES:

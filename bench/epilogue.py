@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     N = require_native()
+    N.allow_knob_changes(True)   # (A/B of tile knobs between launches)
     B, dev = a.batch, "cuda"
     out = []
     for name, H, f in STAGES:

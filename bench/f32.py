@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
     N = require_native()
+    N.allow_knob_changes(True)   # (A/B of tile knobs between launches)
     B, dev = a.batch, "cuda"
     variants = [int(v) for v in a.variants.split(",")]
     tot = {(v, k): 0.0 for v in variants for k in ("fwd", "dgrad", "wgrad")}

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--set", default="", help="extra knobs for every variant, e.g. igemm8_min_tiles=1")
     a = ap.parse_args()
     N = require_native()
+    N.allow_knob_changes(True)   # (A/B of tile knobs between launches)
     for kv in filter(None, a.set.split(",")):
         k, v = kv.split("=")
         N.set_variant(k, int(v))

@@ -4,6 +4,8 @@
 // launch error; the Python layer (pddl.ops) never silently falls back to eager PyTorch on
 // a GPU tensor.
 #include <torch/extension.h>
+
+#include <atomic>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/util/Optional.h>
@@ -18,7 +20,16 @@ namespace py = pybind11;
 
 namespace {
 
-hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+// Kernel knobs (set_variant) are process-global launch configuration shared by every device and
+// replica thread: they are fixed once the first kernel has been issued (every launching binding
+// takes its stream from cur_stream), so no replica can see a plan change mid-step.  Tuning code
+// (A/B tests, micro-benchmarks) opts in with allow_knob_changes(True).
+std::atomic<bool> g_launched{false};
+std::atomic<bool> g_knob_tuning{false};
+hipStream_t cur_stream() {
+  if (!g_launched.load(std::memory_order_relaxed)) g_launched.store(true, std::memory_order_relaxed);
+  return at::hip::getCurrentHIPStream().stream();
+}
 
 void ok(const char* err, const char* what) { TORCH_CHECK(err == nullptr, "pddl ", what, ": ", err ? err : ""); }
 
@@ -823,7 +834,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum, REL);
   m.def("softmax_xent", &softmax_xent, REL);
   m.def("colsum_reduce", &colsum_reduce, REL);
+  m.def("allow_knob_changes", [](bool on) { g_knob_tuning.store(on); }, py::arg("on") = true);
+  m.def("knobs_frozen", []() { return g_launched.load() && !g_knob_tuning.load(); });
   m.def("set_variant", [](const std::string& which, int v) {
+    TORCH_CHECK(!g_launched.load() || g_knob_tuning.load(), "kernel knob ", which,
+                ": knobs are read-only once a kernel has launched (set them before the first launch, "
+                "e.g. PDDL_KNOBS, or call allow_knob_changes(True) in tuning code)");
     if (which == "igemm") pddl::g_igemm_variant = v;
     else if (which == "igemm_deep") pddl::g_igemm_deep = v;
     else if (which == "igemm_pf") pddl::g_igemm_pf = v;

@@ -29,6 +29,7 @@ import torch
 
 from ..ops.native import require_native
 from ..utils import profiling as prof
+from ..utils.envopts import opt
 from .resnet50 import BN_EPS, ParamLayout
 
 _PREP_FMT = "<6i2q8i"
@@ -37,6 +38,7 @@ _FIN_FMT = "<5i"
 _CRED_FMT = "<q4i"
 _BNG_FMT = "<9i"
 _FUSE_FMT = "<16iq"   # FuseLayer (csrc/kernels/kernels.h)
+E = "PDDL_ENGINE"     # the engine's fusion / schedule switches (utils/envopts.py KEYS)
 
 
 def _ceil(a, b):
@@ -81,7 +83,7 @@ class HipEngine:
         self.num_classes = num_classes
         self.ncls_pad = _ceil(num_classes, 64)
         if bitmask is None:
-            bitmask = os.environ.get("PDDL_BITMASK", "1") != "0"
+            bitmask = opt(E, "bitmask", True)
         self.bitmask = bool(bitmask)
         assert struct.calcsize(_PREP_FMT) == self.N.PREP_LAYER_BYTES
         assert struct.calcsize(_FIN_FMT) == self.N.FIN_LAYER_BYTES
@@ -101,29 +103,30 @@ class HipEngine:
         off += _ceil(num_classes, 8)
         # fused projection blocks (conv3 + shortcut conv as one dual-source GEMM, no shortcut
         # activation in HBM): their own folded affine slots (scale 1, shift b3 + b0)
-        self.fuse_proj = self.FUSE_PROJ_OK and os.environ.get("PDDL_FUSE_PROJ", "1") != "0"
+        self.fuse_proj = self.FUSE_PROJ_OK and opt(E, "fuse_proj", True)
         # stage-2/3 conv3 backward as one launch (bwd1x1.hip: data + weight gradient from one read
         # of the 256 / 512-channel gradient; needs the ReLU bitmasks)
-        self.fuse_bwd = self.FUSE_BWD_OK and self.bitmask and os.environ.get("PDDL_FUSE_BWD", "1") != "0"
-        self._fuse_bwd3 = os.environ.get("PDDL_FUSE_BWD", "1") != "2"
-        self._fuse_bwd_s2 = os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0"
+        fb = opt(E, "fuse_bwd", 1)
+        self.fuse_bwd = self.FUSE_BWD_OK and self.bitmask and fb != 0
+        self._fuse_bwd3 = fb != 2
+        self._fuse_bwd_s2 = opt(E, "fuse_bwd_s2", True)
         # stem conv + max-pool forward as one launch (stem.hip): conv1's output never reaches HBM
-        self.fuse_stem = self.FUSE_STEM_OK and os.environ.get("PDDL_FUSE_STEM", "1") != "0" and crop <= 250
+        self.fuse_stem = self.FUSE_STEM_OK and opt(E, "fuse_stem", True) and crop <= 250
         # stage-2 3x3 convs (64 -> 64) on the persistent row-tile kernels (conv3x3c64.hip) at
         # batches where every CU streams several row tiles through its windows
-        self.c64 = self.C64_OK and os.environ.get("PDDL_C64", "1") != "0"
-        self.c64w = self.c64 and os.environ.get("PDDL_C64W", "1") != "0"
-        self.c64_min_m = int(os.environ.get("PDDL_C64_MIN_M", self.C64_MIN_M))
+        self.c64 = self.C64_OK and opt(E, "c64", True)
+        self.c64w = self.c64 and opt(E, "c64w", True)
+        self.c64_min_m = opt(E, "c64_min_m", self.C64_MIN_M)
         # stage-2 block boundaries: conv3 + the next block's conv1 in one launch (c3c1.hip)
-        self.c3c1 = int(os.environ.get("PDDL_C3C1", "1")) if self.C3C1_OK else 0
+        self.c3c1 = opt(E, "c3c1", 1) if self.C3C1_OK else 0
         # stage-2 backward boundaries: the next block's conv1 data gradient computed inside this
         # block's fused conv3 backward (bwd1x1 pre form), its 256-channel result never re-read
-        self.c1pre = self.C3C1_OK and os.environ.get("PDDL_C1PRE", "1") != "0"
+        self.c1pre = self.C3C1_OK and opt(E, "c1pre", True)
         # blocks whose output feeds a downsampling block (conv2_block3, conv3_block4, conv4_block6):
         # every consumer of that output (the next block's stride-2 conv1 and shortcut, forward and
         # weight gradient, and its ReLU mask) reads only the even rows / columns, so conv3 runs on
         # the compact quarter and stores only it (3/4 fewer conv3 rows and output bytes)
-        self.s2c = self.S2C_OK and self.bitmask and os.environ.get("PDDL_S2C", "1") != "0"
+        self.s2c = self.S2C_OK and self.bitmask and opt(E, "s2c", True)
         for b in L.blocks:
             if b.proj:
                 self.ch["fuse:" + b.name] = off
@@ -149,7 +152,7 @@ class HipEngine:
                                      device=dev)
         # two-stream backward (small batches, where single kernels underfill the chip): the weight
         # gradients run on a side stream concurrently with the data-gradient chain.
-        # PDDL_TWO_STREAM=1 / 0 forces it; default on up to TWO_STREAM_MAX_BATCH images.
+        # PDDL_ENGINE two_stream=1 / 0 forces it; default on up to TWO_STREAM_MAX_BATCH images.
         self.two_stream = self._two_stream_wanted(batch)
         self.side = torch.cuda.Stream(dev) if self.two_stream and dev.type == "cuda" else None
         self._pending, self._last_side = {}, None
@@ -307,7 +310,7 @@ class HipEngine:
         self.H5 = H
         # (set before _alloc_acts runs; the subclasses' engines keep one stream)
         ring0 = self._grad_ring or (self.GRAD_RING_SMALL if B <= 64 else self.GRAD_RING)
-        ring = int(os.environ.get("PDDL_GRAD_RING", ring0)) if self._two_stream_wanted(B) else 1
+        ring = opt(E, "grad_ring", ring0) if self._two_stream_wanted(B) else 1
         self.gbuf = [torch.empty(outer, **bf) for _ in range(max(2, ring))]
         self.g1bufs = [torch.empty(inner, **bf) for _ in range(ring)]
         self.g2bufs = [torch.empty(inner, **bf) for _ in range(ring)]
@@ -438,7 +441,7 @@ class HipEngine:
                 and self._bwd_fused(bi - 1, pb, s2))
 
     def _bwd_fused(self, bi, b, s2):
-        # stage 2 (256 <- 64 channels) and stage 3 (512 <- 128); PDDL_FUSE_BWD=2: stage 2 only
+        # stage 2 (256 <- 64 channels) and stage 3 (512 <- 128); PDDL_ENGINE fuse_bwd=2: stage 2 only
         return self.fuse_bwd and bi not in s2 and (b.filters == 64 or (b.filters == 128 and self._fuse_bwd3))
 
     def _use_c64(self, f, M, W, bits=True) -> bool:
@@ -585,7 +588,7 @@ class HipEngine:
 
     # ------------------------------------------------------------------ two-stream backward
     def _two_stream_wanted(self, batch) -> bool:
-        ts = os.environ.get("PDDL_TWO_STREAM", "auto")
+        ts = opt(E, "two_stream", "auto")
         return self.TWO_STREAM_OK and ((batch <= self.TWO_STREAM_MAX_BATCH) if ts == "auto" else ts == "1")
 
     def _event(self):

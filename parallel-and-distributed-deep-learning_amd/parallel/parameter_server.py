@@ -18,7 +18,7 @@ MI355X-native design:
     segment and HIP-IPC mailboxes: a worker's pack kernel writes its gradient ranges straight
     into its mailbox on the PS GPU over xGMI, the PS service thread applies fused Adam and
     peer-copies the fresh shard back (CPU roles: the same protocol in shared memory);
-    PDDL_PS_IMPL=c10d selects the portable fallback: one 2-rank process group per
+    PDDL_PS=impl=c10d selects the portable fallback: one 2-rank process group per
     (worker, PS) pair with RCCL / gloo send/recv served from Python threads;
   * a worker's push / pull round trip overlaps its next step (cfg.ps_overlap, default; the
     step then reads parameters one round trip older -- the reference's asynchronous PS has
@@ -45,6 +45,10 @@ import torch
 import torch.distributed as dist
 
 from ..models.resnet50 import ParamLayout
+from ..utils.envopts import opt
+
+
+P = "PDDL_PS"   # the PS runtime switches (utils/envopts.py KEYS)
 
 
 def add_ps_args(ap: argparse.ArgumentParser):
@@ -122,8 +126,8 @@ OP_PUSH, OP_PULL, OP_STOP = 0.0, 1.0, 2.0
 
 
 def ps_impl() -> str:
-    """Data plane: "native" (csrc/runtime/ps_service.cpp) unless PDDL_PS_IMPL=c10d."""
-    if os.environ.get("PDDL_PS_IMPL", "native") != "native":
+    """Data plane: "native" (csrc/runtime/ps_service.cpp) unless PDDL_PS=impl=c10d."""
+    if opt(P, "impl", "native") != "native":
         return "c10d"
     from ..ops.native import native_available, require_native
     return "native" if native_available() and hasattr(require_native(), "PSServer") else "c10d"
@@ -197,7 +201,7 @@ class _Heartbeat:
     barrier, worker 0's validation, a drained ticket queue); a step that runs longer than
     `stall_s` (a GPU hang, a stuck exchange) stops the stamps, so a live but stalled worker is
     declared dead and its ticket re-queued exactly like a crashed one.  `stall_s` is its own
-    threshold (PDDL_PS_STEP_STALL), separate from and larger than the coordinator's liveness
+    threshold (PDDL_PS step_stall), separate from and larger than the coordinator's liveness
     timeout `hb_timeout`: a slow but healthy step (a cold first batch from real data, a PS slowed
     by many workers) keeps beating.  A worker still stuck `stall_s + hb_timeout / 2` into a step
     ends itself: the coordinator declares it dead (and re-queues its tickets) no earlier than
@@ -379,7 +383,7 @@ class PSServer:
     def monitor(self, threads):
         """Coordinator duty on PS 0: heartbeat watch + closure re-queue of dead workers."""
         cl = self.cl
-        timeout = float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30"))
+        timeout = opt(P, "heartbeat", 30.0)
         dead = set()
         while any(t.is_alive() for t in threads):
             time.sleep(0.2)
@@ -458,7 +462,7 @@ class PSWorker:
             cl = self.cl
             dev = cl.device.index if cl.device.type == "cuda" else -1
             self.cli = require_native().PSClient(cl.job, cl.ranges, self.widx, dev,
-                                                 float(os.environ.get("PDDL_PS_TIMEOUT", "120")))
+                                                 opt(P, "timeout", 120.0))
         return self.cli
 
     def exchange_begin(self, lr: float):
@@ -592,7 +596,7 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     gpu_pg = use_gpu and impl == "c10d"
     backend = "nccl" if gpu_pg else "gloo"
     dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=int(os.environ.get("PDDL_PS_TIMEOUT", "120"))),
+                            timeout=datetime.timedelta(seconds=opt(P, "timeout", 120.0)),
                             **({"device_id": device} if gpu_pg else {}))
     cl = _Cluster(cfg, rank, world, num_ps, device, impl=impl)
     from ..parallel.strategies import build_engine
@@ -631,11 +635,11 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
     if cfg.max_steps:
         spe = min(spe, cfg.max_steps)
     fault_at = _fault_step(widx)
-    hb_timeout = float(os.environ.get("PDDL_HEARTBEAT_TIMEOUT", "30"))
-    step_stall = float(os.environ.get("PDDL_PS_STEP_STALL", str(max(300.0, 10 * hb_timeout))))
+    hb_timeout = opt(P, "heartbeat", 30.0)
+    step_stall = opt(P, "step_stall", max(300.0, 10 * hb_timeout))
     hb = _Heartbeat(store, rank, max(0.05, hb_timeout / 6), step_stall, hb_timeout)
-    epoch_timeout = float(os.environ.get("PDDL_PS_EPOCH_TIMEOUT", str(max(600.0, 10 * hb_timeout))))
-    block = max(1, int(os.environ.get("PDDL_PS_TICKET_BLOCK", "16")))
+    epoch_timeout = opt(P, "epoch_timeout", max(600.0, 10 * hb_timeout))
+    block = max(1, opt(P, "ticket_block", 16))
     it = pipe.iterate(device)
     history = []
     steps_done = 0
@@ -824,7 +828,7 @@ def run_ps_job(cfg, num_ps: Optional[int] = None, num_workers: Optional[int] = N
     for p in procs:
         p.start()
     results = []
-    deadline = time.time() + float(os.environ.get("PDDL_PS_JOB_TIMEOUT", "3600"))
+    deadline = time.time() + opt(P, "job_timeout", 3600.0)
     alive = set(range(world))
     while alive and time.time() < deadline:
         for i, p in enumerate(procs):

@@ -28,6 +28,7 @@ from ..data.datasets import Pipeline, make_source
 from ..models.resnet50 import ParamLayout
 from ..train.optim import make_optimizer
 from ..utils import profiling as prof
+from ..utils.envopts import opt
 from .collectives import BucketAllReducer
 from .faults import StepFaults
 from .launch import ClusterInfo, export_torch_env, resolve_cluster
@@ -817,7 +818,7 @@ class _LocalReplicas:
     def _eager_step(self, parts, global_batch: int, apply: bool = True):
         R = self.R
         stats = [None] * R
-        overlap = self.comm is not None and os.environ.get("PDDL_MIRROR_OVERLAP", "1") != "0"
+        overlap = self.comm is not None and opt("PDDL_MIRROR", "overlap", True)
         if overlap:
             if not hasattr(self, "_q"):
                 self._overlap_setup()
@@ -892,9 +893,9 @@ class _LocalReplicas:
         """One replica in the whole job: the gradient needs no reduction (a 1-rank all-reduce is
         the identity), so the step runs without collectives, like TF's MirroredStrategy on one
         device (no cross-device ops): eager by default, one whole-step HIP graph with --graphs.
-        PDDL_MIRROR_SEGMENTED=1 (and PDDL_COMM=graphs) keep the segmented multi-replica schedule
+        PDDL_MIRROR=segmented=1 (and PDDL_COMM=graphs) keep the segmented multi-replica schedule
         and its collectives."""
-        return (self.world_ranks == 1 and os.environ.get("PDDL_MIRROR_SEGMENTED", "0") != "1"
+        return (self.world_ranks == 1 and not opt("PDDL_MIRROR", "segmented", False)
                 and os.environ.get("PDDL_COMM") != "graphs")
 
     def _single_step(self, parts, global_batch: int):

@@ -12,6 +12,9 @@ import sys
 sys.path.insert(0, ".")
 import pddl  # noqa
 from pddl.models.resnet50 import ParamLayout
+from pddl.utils.envopts import opt
+
+E = "PDDL_ENGINE"   # the run's engine switches (the schedule follows them)
 
 
 def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fuse_stem=True):
@@ -28,14 +31,15 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         ev.append(("maxpool_fwd", "pool", 0, B * (H1 * H1 + H2 * H2) * 64 * 2))
     H = H2
     geo = []
-    c3c1_on = int(os.environ.get("PDDL_C3C1", "1"))
-    s2c = os.environ.get("PDDL_S2C", "1") != "0"
+    c3c1_on = opt(E, "c3c1", 1)
+    s2c = opt(E, "s2c", True)
     blocks = list(L.blocks)
 
     def c3c1(b, nb):   # engine._c3c1_ok
         return bool(c3c1_on) and nb is not None and b.filters == 64 and nb.filters == 64 and not b.proj \
             and not nb.proj and nb.stride == 1
     c1_done = False
+    c64_min = opt(E, "c64_min_m", 262144)
     for bi, b in enumerate(blocks):
         f, cin = b.filters, b.cin
         Ho = (H - 1) // b.stride + 1
@@ -45,7 +49,7 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
         if not c1_done:
             ev.append(("igemm", f"{b.name} c1{'+c0' if n1 > f else ''} fwd", 2 * M * cin * n1,
                        (B * H * H * cin + M * n1) * 2, (M, n1, cin)))
-        c64 = f == 64 and M >= 262144 and Ho + 2 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
+        c64 = f == 64 and M >= c64_min and Ho + 2 <= 64 and opt(E, "c64", True)
         ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 fwd", 2 * M * 9 * f * f, (M * f * 2) * 2,
                    (M, f, 9 * f)))
         c1_done = c3c1(b, nb)
@@ -73,7 +77,7 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
     ev.append(("gap_bwd", "gap", 0, 0))
     blocks = L.blocks
     s2 = {i for i in range(len(blocks) - 1) if blocks[i + 1].proj and blocks[i + 1].stride == 2}
-    c1pre_on = os.environ.get("PDDL_C1PRE", "1") != "0" and c3c1_on != 0
+    c1pre_on = opt(E, "c1pre", True) and c3c1_on != 0
 
     def fused_c3(i):
         fi = blocks[i].filters
@@ -97,10 +101,9 @@ def schedule(B, crop, fuse=True, fuse_bwd=True, fuse_bwd3=True, fuse_s2=True, fu
             ev.append(("wgrad", f"{b.name} c3 wgrad", 2 * Mc * f * 4 * f, (Mc * f + Mc * 4 * f) * 2))
             ev.append(("igemm", f"{b.name} c3 dgrad", 2 * Mc * f * 4 * f, (Mc * 4 * f + Mc * f + M * f) * 2,
                        (Mc, f, 4 * f)))
-        c64w = f == 64 and M >= 262144 and Ho + 2 <= 64 and Mc == M and os.environ.get("PDDL_C64", "1") != "0" \
-            and os.environ.get("PDDL_C64W", "1") != "0"
+        c64w = f == 64 and M >= c64_min and Ho + 2 <= 64 and Mc == M and opt(E, "c64", True) and opt(E, "c64w", True)
         ev.append(("conv3x3c64" if c64w else "wgrad", f"{b.name} c2 wgrad", 2 * Mc * 9 * f * f, (Mc + M) * f * 2))
-        c64 = f == 64 and M >= 262144 and Ho + 2 <= 64 and os.environ.get("PDDL_C64", "1") != "0"
+        c64 = f == 64 and M >= c64_min and Ho + 2 <= 64 and opt(E, "c64", True)
         ev.append(("conv3x3c64" if c64 else "igemm", f"{b.name} c2 dgrad", 2 * M * 9 * f * f, 3 * M * f * 2,
                    (M, f, 9 * f)))
         n1 = 5 * f if b.proj else f
@@ -137,9 +140,9 @@ def segment(path, B=1024, crop=224, knobs=""):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "pddl::" in r["Kernel_Name"]]
     rows = [r for r in rows if "comm_proxy" not in r["Kernel_Name"]]   # bench --comm-proxy stand-ins
-    ev = schedule(B, crop, os.environ.get("PDDL_FUSE_PROJ", "1") != "0", os.environ.get("PDDL_FUSE_BWD", "1") != "0",
-                  os.environ.get("PDDL_FUSE_BWD", "1") != "2", os.environ.get("PDDL_FUSE_BWD_S2", "1") != "0",
-                  os.environ.get("PDDL_FUSE_STEM", "1") != "0")
+    fb = opt(E, "fuse_bwd", 1)
+    ev = schedule(B, crop, opt(E, "fuse_proj", True), fb != 0, fb != 2, opt(E, "fuse_bwd_s2", True),
+                  opt(E, "fuse_stem", True))
     # a split launch (8-phase kernel for full rounds + 128x128 tail) is two dispatches of one layer
     try:
         from pddl.ops.native import require_native

@@ -12,8 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
-    os.environ.setdefault("PDDL_PS_IMPL", "native")
-    os.environ.setdefault("PDDL_PS_JOB_TIMEOUT", "150")
+    os.environ.setdefault("PDDL_PS", "impl=native,job_timeout=150")
     import pddl  # noqa: F401
     from pddl.config import make_config
     from pddl.parallel.parameter_server import run_ps_job

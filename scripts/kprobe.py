@@ -24,6 +24,7 @@ def main():
                     "(bits, add, colsum) to price each one")
     a = ap.parse_args()
     N = require_native()
+    N.allow_knob_changes(True)   # (A/B of tile knobs between launches)
     for kv in filter(None, a.set.split(",")):
         k, v = kv.split("=")
         N.set_variant(k, int(v))

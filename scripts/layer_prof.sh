@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-layer trace of a training step: bench.py under rocprofv3 --kernel-trace, summarised by
 # scripts/analyze_trace.py.   bash scripts/layer_prof.sh OUTDIR [bench args...]
-# (BATCH=256 CROP=224 for other configs; use PDDL_TWO_STREAM=0 below b1024 so the launch order
+# (BATCH=256 CROP=224 for other configs; use PDDL_ENGINE=two_stream=0 below b1024 so the launch order
 # matches the analyzer's single-stream schedule)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

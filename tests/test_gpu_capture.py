@@ -7,6 +7,8 @@ SegmentedStepGraphs (a Mirrored / MWMS replica: segments cut at the gradient buc
 two-stream backward forked across them, plus the optimizer graph) -- and compare the replayed
 trajectory with eager steps of an identically initialised engine."""
 import pytest
+
+from pddl.utils.envopts import with_opt
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -58,7 +60,7 @@ def test_whole_engine_graph_capture_at_reference_batch(monkeypatch, crop, c64):
     replayed segment by segment + the optimizer graph, each from the same initial weights."""
     from pddl.train.graph import GraphedTrainStep, SegmentedStepGraphs
     if c64:
-        monkeypatch.setenv("PDDL_C64_MIN_M", "1")
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c64_min_m", "1"))
     B, steps = 32, 4
     img, lab, flip = _inputs(steps, B, 224)
     l_ref, p_ref, eng_ref = _eager(crop, B, img, lab, flip)
@@ -127,8 +129,8 @@ def test_engine_headline_kernel_plan_within_noise_floor(monkeypatch):
     from pddl.ops.native import require_native
     from test_gpu_engine import test_engine_matches_bf16_point_reference_within_its_noise_floor as parity
     N = require_native()
-    monkeypatch.setenv("PDDL_TWO_STREAM", "0")
-    monkeypatch.setenv("PDDL_C64_MIN_M", "1")
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "two_stream", "0"))
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c64_min_m", "1"))
     N.set_variant("igemm_splitk", 0)
     try:
         # (the 8-phase 256x256 tiles need more than one round of tiles on the chip, which no

@@ -1,6 +1,8 @@
 """End-to-end parity: the HIP engine (bf16 MFMA kernels, fused epilogues, explicit backward)
 against the fp32 PyTorch reference of the Keras graph, on identical parameters and inputs."""
 import pytest
+
+from pddl.utils.envopts import with_opt
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -242,7 +244,7 @@ def test_fused_projection_matches_unfused(monkeypatch):
     """Projection blocks run conv3 + the shortcut conv as one dual-source GEMM (second source = the
     block input at the block's stride, both frozen-BN scales folded into bf16 weights), so the
     shortcut activation is never materialised.  Same parameters and batch with the fusion off
-    (PDDL_FUSE_PROJ=0: conv1 + shortcut launch, residual read by conv3): the losses and the
+    (PDDL_ENGINE fuse_proj=0: conv1 + shortcut launch, residual read by conv3): the losses and the
     flat gradients agree to the bf16 rounding of the scaled weights."""
     from pddl.models.engine import HipEngine
     from pddl.models.resnet50 import ParamLayout
@@ -251,7 +253,7 @@ def test_fused_projection_matches_unfused(monkeypatch):
     B = 8
     res = []
     for fuse in ("1", "0"):
-        monkeypatch.setenv("PDDL_FUSE_PROJ", fuse)
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "fuse_proj", fuse))
         he = HipEngine(L, B, crop=224, image_size=224)
         he.init(seed=7)
         assert he.fuse_proj == (fuse == "1")
@@ -267,7 +269,7 @@ def test_fused_projection_matches_unfused(monkeypatch):
 
 def test_fused_conv3_backward_matches_unfused(monkeypatch):
     """Stage-2 conv3 backward as one launch (bwd1x1.hip: data and weight gradient from one read
-    of the 256-channel output gradient) against the two-launch form (PDDL_FUSE_BWD=0: wgrad
+    of the 256-channel output gradient) against the two-launch form (PDDL_ENGINE fuse_bwd=0: wgrad
     kernel + igemm dgrad): same parameters and batch, losses equal and flat gradients agree to
     fp32 accumulation order."""
     from pddl.models.engine import HipEngine
@@ -276,7 +278,7 @@ def test_fused_conv3_backward_matches_unfused(monkeypatch):
     B = 8
     res = []
     for fuse in ("1", "0"):
-        monkeypatch.setenv("PDDL_FUSE_BWD", fuse)
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "fuse_bwd", fuse))
         he = HipEngine(L, B, crop=224, image_size=224)
         he.init(seed=7)
         assert he.fuse_bwd == (fuse == "1")
@@ -292,16 +294,16 @@ def test_fused_conv3_backward_matches_unfused(monkeypatch):
 
 def test_c64_kernels_in_engine_match_generic(monkeypatch):
     """The stage-2 3x3 convs on conv3x3c64.hip (forward, data gradient and weight gradient; the
-    engine enables them from b >= 84 at 224, here forced on with PDDL_C64_MIN_M) against the
+    engine enables them from b >= 84 at 224, here forced on with PDDL_ENGINE c64_min_m) against the
     generic implicit GEMM / wgrad kernels: same loss, flat gradients to fp32 accumulation order."""
     from pddl.models.engine import HipEngine
     from pddl.models.resnet50 import ParamLayout
     L = ParamLayout()
     B = 8
     res = []
-    monkeypatch.setenv("PDDL_C64_MIN_M", "1")
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c64_min_m", "1"))
     for on in ("1", "0"):
-        monkeypatch.setenv("PDDL_C64", on)
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c64", on))
         he = HipEngine(L, B, crop=224, image_size=224)
         he.init(seed=7)
         assert he.c64 == (on == "1") and he._use_c64(64, B * 56 * 56, 56) == (on == "1")
@@ -322,7 +324,7 @@ def test_c64_kernels_in_engine_match_generic(monkeypatch):
 
 
 def test_c3c1_boundary_fusion_in_engine(monkeypatch):
-    """Stage-2 block boundaries with conv3 + the next conv1 in one launch (c3c1.hip, PDDL_C3C1=1,
+    """Stage-2 block boundaries with conv3 + the next conv1 in one launch (c3c1.hip, PDDL_ENGINE c3c1=1,
     the default) against separate launches: same loss, flat gradients to fp32 order; and the
     engine with the fusion stays within the fp32 reference's bf16-point noise floor."""
     from pddl.models.engine import HipEngine
@@ -331,7 +333,7 @@ def test_c3c1_boundary_fusion_in_engine(monkeypatch):
     B = 8
     res = []
     for on in ("1", "0"):
-        monkeypatch.setenv("PDDL_C3C1", on)
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c3c1", on))
         he = HipEngine(L, B, crop=224, image_size=224)
         assert he.c3c1 == int(on)
         he.init(seed=7)
@@ -344,13 +346,13 @@ def test_c3c1_boundary_fusion_in_engine(monkeypatch):
     print(f"c3c1: loss rel {abs(l1 - l0) / abs(l0):.2e}, grad rel {((g1 - g0).norm() / g0.norm()).item():.3e}")
     assert abs(l1 - l0) < 1e-4 * abs(l0)
     assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
-    monkeypatch.setenv("PDDL_C3C1", "1")
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c3c1", "1"))
     test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
 
 
 def test_c1_dgrad_fused_into_conv3_backward(monkeypatch):
     """Stage-2 backward boundaries with the next block's conv1 data gradient computed inside the
-    fused conv3 backward (bwd1x1 pre form, PDDL_C1PRE=1, the default) against separate launches:
+    fused conv3 backward (bwd1x1 pre form, PDDL_ENGINE c1pre=1, the default) against separate launches:
     same loss, flat gradients to fp32 order; and within the fp32 reference's noise floor."""
     from pddl.models.engine import HipEngine
     from pddl.models.resnet50 import ParamLayout
@@ -358,7 +360,7 @@ def test_c1_dgrad_fused_into_conv3_backward(monkeypatch):
     B = 8
     res = []
     for on in ("1", "0"):
-        monkeypatch.setenv("PDDL_C1PRE", on)
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c1pre", on))
         he = HipEngine(L, B, crop=224, image_size=224)
         assert he.c1pre == (on == "1")
         he.init(seed=7)
@@ -371,12 +373,12 @@ def test_c1_dgrad_fused_into_conv3_backward(monkeypatch):
     print(f"c1pre: loss rel {abs(l1 - l0) / abs(l0):.2e}, grad rel {((g1 - g0).norm() / g0.norm()).item():.3e}")
     assert abs(l1 - l0) < 1e-4 * abs(l0)
     assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
-    monkeypatch.setenv("PDDL_C1PRE", "1")
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c1pre", "1"))
     test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
 
 
 def test_s2_fed_blocks_store_compact_outputs(monkeypatch):
-    """Blocks feeding a downsampling block store only their stride-2 grid (PDDL_S2C=1, the
+    """Blocks feeding a downsampling block store only their stride-2 grid (PDDL_ENGINE s2c=1, the
     default: conv3 on the compact quarter, the next block's conv1 / shortcut / weight gradient
     and ReLU mask read it as a stride-1 input) against full-resolution storage: same loss, flat
     gradients to fp32 order; and within the fp32 reference's noise floor."""
@@ -386,7 +388,7 @@ def test_s2_fed_blocks_store_compact_outputs(monkeypatch):
     B = 8
     res = []
     for on in ("1", "0"):
-        monkeypatch.setenv("PDDL_S2C", on)
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "s2c", on))
         he = HipEngine(L, B, crop=224, image_size=224)
         assert he.s2c == (on == "1")
         he.init(seed=7)
@@ -399,7 +401,7 @@ def test_s2_fed_blocks_store_compact_outputs(monkeypatch):
     print(f"s2c: loss rel {abs(l1 - l0) / abs(l0):.2e}, grad rel {((g1 - g0).norm() / g0.norm()).item():.3e}")
     assert abs(l1 - l0) < 1e-4 * abs(l0)
     assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
-    monkeypatch.setenv("PDDL_S2C", "1")
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "s2c", "1"))
     test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
 
 
@@ -407,13 +409,13 @@ def test_c64_engine_within_noise_floor(monkeypatch):
     """The engine with the stage-2 3x3 convs forced onto conv3x3c64.hip is as close to the fp32
     reference as the reference's own bf16-point floor (same criteria as the generic path:
     measured ratios 0.92-1.00 on the 8-wave row tiles vs 0.98-1.15 generic, crops 224/160/244)."""
-    monkeypatch.setenv("PDDL_C64_MIN_M", "1")
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "c64_min_m", "1"))
     test_engine_matches_bf16_point_reference_within_its_noise_floor(224, 224)
 
 
 @pytest.mark.parametrize("graphed", [False, True])
 def test_two_stream_backward_matches_one_stream(monkeypatch, graphed):
-    """Small-batch backward with the weight gradients on a side stream (PDDL_TWO_STREAM=1, the
+    """Small-batch backward with the weight gradients on a side stream (PDDL_ENGINE two_stream=1, the
     default up to 1024 images) against the single-stream schedule: same loss and gradients to
     fp32-atomic order, eager and captured in a HIP graph (the side stream forks from and joins
     the capture)."""
@@ -428,7 +430,7 @@ def test_two_stream_backward_matches_one_stream(monkeypatch, graphed):
     flips = torch.zeros(B, dtype=torch.uint8, device="cuda")
     res = []
     for two in ("1", "0"):
-        monkeypatch.setenv("PDDL_TWO_STREAM", two)
+        monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "two_stream", two))
         he = HipEngine(L, B, crop=112, image_size=112)
         assert he.two_stream == (two == "1")
         he.init(seed=7)

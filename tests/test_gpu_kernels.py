@@ -79,6 +79,27 @@ def test_igemm_forward(case, with_res):
     assert rel(out, ref) < 1e-2
 
 
+def test_kernel_knobs_freeze_after_first_launch():
+    """Tile knobs are process-global launch configuration: once a kernel has launched, set_variant
+    raises unless tuning mode is on (tests / micro-benchmarks call allow_knob_changes(True)), so
+    replica threads of one process can never see the launch plan change between their steps."""
+    x = rnd(1, 4, 4, 64)
+    w = rnd(64, 64)
+    out = torch.empty(1, 4, 4, 64, dtype=torch.bfloat16, device=dev)
+    ones, zeros = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+    N().igemm(x, None, 4, 4, 1, 1, 1, 0, 4, 4, w, 0, ones, zeros, None, None, None, out, 0, None, 0, 0, 0, 0, 0,
+              None, None)
+    N().allow_knob_changes(False)
+    try:
+        assert N().knobs_frozen()
+        with pytest.raises(RuntimeError, match="read-only"):
+            N().set_variant("igemm_pk", 0)
+    finally:
+        N().allow_knob_changes(True)
+    assert not N().knobs_frozen()
+    N().set_variant("igemm_pk", 2)   # (the default, restored in tuning mode)
+
+
 def test_igemm_split_outputs_and_f32():
     torch.manual_seed(1)
     n, h, c, f = 2, 8, 64, 64

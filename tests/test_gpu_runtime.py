@@ -3,6 +3,8 @@ driving the HIP engine end to end (1 GPU box: single-rank communicators)."""
 import os
 
 import pytest
+
+from pddl.utils.envopts import with_opt
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -106,7 +108,7 @@ def test_single_strategy_fit_with_hip_graph():
 def test_mirrored_strategy_one_gpu_uses_rccl(monkeypatch):
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
-    monkeypatch.setenv("PDDL_MIRROR_SEGMENTED", "1")   # (the multi-replica schedule on 1 GPU)
+    monkeypatch.setenv("PDDL_MIRROR", with_opt("PDDL_MIRROR", "segmented", "1"))   # (the multi-replica schedule on 1 GPU)
     cfg = _cfg("mirrored")
     st = make_strategy(cfg)
     tr = Trainer(cfg, st)
@@ -133,12 +135,12 @@ def test_mirrored_graphed_step_matches_eager(monkeypatch, segmented):
     """Mirrored with HIP graphs follows the eager Mirrored trajectory.  segmented: the
     multi-replica schedule (per-device step segments split at the gradient buckets, with the
     two-stream backward, grouped all-reduce of bucket k between segment k and k+1, captured
-    optimizer), forced on this 1-replica job with PDDL_MIRROR_SEGMENTED=1; otherwise the
+    optimizer), forced on this 1-replica job with PDDL_MIRROR segmented=1; otherwise the
     1-replica job's whole-step graph (no collective to run)."""
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
     if segmented:
-        monkeypatch.setenv("PDDL_MIRROR_SEGMENTED", "1")
+        monkeypatch.setenv("PDDL_MIRROR", with_opt("PDDL_MIRROR", "segmented", "1"))
     res = []
     for graphs in (False, True):
         cfg = _cfg("mirrored", graphs=graphs, flip=False, max_steps=3, batch_size=8)
@@ -231,7 +233,7 @@ def test_mirrored_on_init_rank_communicator(monkeypatch):
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
     monkeypatch.setenv("PDDL_RCCL_INIT", "rank")
-    monkeypatch.setenv("PDDL_MIRROR_SEGMENTED", "1")
+    monkeypatch.setenv("PDDL_MIRROR", with_opt("PDDL_MIRROR", "segmented", "1"))
     cfg = _cfg("mirrored", max_steps=4, batch_size=8)
     st = make_strategy(cfg)
     tr = Trainer(cfg, st)
@@ -250,7 +252,7 @@ def test_bench_parameter_server_rehearsal_on_one_gpu():
     event-chained PS service (Adam + snapshot copy per request, `done` published on event
     completion) and the workers' poster threads (no host sync on push)."""
     out = _bench_json(["--gpus", "3", "--strategy", "ps", "--ps", "1", "--batch", "32", "--steps", "8"],
-                      {"PDDL_REHEARSE": "1", "PDDL_PS_IMPL": "native"})
+                      {"PDDL_REHEARSE": "1", "PDDL_PS": "impl=native"})
     assert out["n_gpus"] == 3 and out["config"]["parallelism"] == "ps1+w2" and out["rehearsal"] is True
     assert out["steps_timed_epoch"] == 8 and out["value"] > 0
 

@@ -194,3 +194,35 @@ def test_preprocess_semantics():
     assert torch.allclose(x, img[:, 1:3, 2:4].permute(0, 3, 1, 2) / 255)
     x = preprocess(img, 8, True)            # RandomCrop larger than the input -> resize (Q1)
     assert x.shape == (2, 3, 8, 8)
+
+
+def test_ps_bf16_wire_loss_trajectory_tracks_fp32_wire():
+    """--ps-wire bf16 (opt-in; the reference's PS moves fp32): the PS keeps fp32 master weights
+    and Adam state, the worker pushes bf16-rounded gradients and trains on bf16-rounded pulled
+    weights (csrc/runtime/ps_service.cpp, exactly tests/test_gpu_ps.py's pack / Adam kernels).
+    Emulated here on the fp32 reference engine over 12 Adam steps on a fixed batch: the bf16-wire
+    loss trajectory (6.90 -> 1.38 nats) stays within 3 % / 0.08 nats of the fp32-wire one at every
+    step and ends within 1 % of it (measured: at most 2.0 %, 0.047 nats, in the steepest step)."""
+    from pddl.train.optim import Adam
+    torch.manual_seed(5)
+    img = torch.randint(0, 256, (4, 32, 32, 3), dtype=torch.uint8)
+    lab = torch.tensor([1, 2, 3, 4])
+    traj = {}
+    for wire in ("fp32", "bf16"):
+        L, e = _tiny_engine(4, 32)
+        opt = Adam(e, lr=1e-4)
+        master = e.params.clone()
+        losses = []
+        for _ in range(12):
+            # pull: the worker's copy of the PS weights
+            e.params.copy_(master.to(torch.bfloat16).float() if wire == "bf16" else master)
+            losses.append(e.forward_backward(img, lab, 0.25)[0].item() / 4)
+            if wire == "bf16":   # push: bf16-rounded gradient
+                e.grads.copy_(e.grads.to(torch.bfloat16).float())
+            e.params.copy_(master)   # the PS applies Adam to its fp32 master
+            opt.step()
+            master.copy_(e.params)
+        traj[wire] = losses
+    a, b = torch.tensor(traj["fp32"]), torch.tensor(traj["bf16"])
+    assert ((a - b).abs() / a.abs()).max().item() < 0.03 and (a - b).abs().max().item() < 0.08, (traj["fp32"], traj["bf16"])
+    assert abs(b[-1] - a[-1]) / a[-1] < 0.01 and b[-1] < 0.3 * b[0]

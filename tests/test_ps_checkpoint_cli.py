@@ -8,6 +8,8 @@ import time
 
 import numpy as np
 import pytest
+
+from pddl.utils.envopts import with_opt
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -25,8 +27,8 @@ def _cfg(preset, **kw):
 @pytest.mark.parametrize("impl", ["native", "c10d"])
 def test_ps_async_job_runs_and_applies_every_step(impl, monkeypatch):
     from pddl.parallel.parameter_server import run_ps_job
-    monkeypatch.setenv("PDDL_PS_IMPL", impl)
-    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "600")   # a loaded CI box must not look like a dead worker
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "impl", impl))
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "heartbeat", "600"))   # a loaded CI box must not look like a dead worker
     cfg = _cfg("ps", steps_per_epoch=6, validation_steps=1, batch_size=2, epochs=2)
     res = run_ps_job(cfg, num_ps=2, num_workers=2, return_results=True)
     ps = [r for r in res if r[0] == "ps"]
@@ -42,9 +44,9 @@ def test_ps_async_job_runs_and_applies_every_step(impl, monkeypatch):
 @pytest.mark.parametrize("impl", ["native", "c10d"])
 def test_ps_worker_failure_requeues_closure(impl, monkeypatch):
     from pddl.parallel.parameter_server import run_ps_job
-    monkeypatch.setenv("PDDL_PS_IMPL", impl)
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "impl", impl))
     monkeypatch.setenv("PDDL_FAULT", "kill_worker:1@1")
-    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "heartbeat", "3"))
     cfg = _cfg("ps", steps_per_epoch=6, batch_size=2, epochs=1)
     res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
     wk = [r for r in res if r[0] == "worker"]
@@ -60,10 +62,10 @@ def test_ps_worker_death_inside_a_ticket_block_is_not_replayed(monkeypatch):
     re-queued and the PS applies spe updates (spe + 1 if the last push was in flight), not
     spe + 3 as with per-block publishing."""
     from pddl.parallel.parameter_server import run_ps_job
-    monkeypatch.setenv("PDDL_PS_IMPL", "c10d")
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "impl", "c10d"))
     monkeypatch.setenv("PDDL_FAULT", "kill_worker:1@3")
-    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
-    monkeypatch.setenv("PDDL_PS_TICKET_BLOCK", "16")
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "heartbeat", "3"))
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "ticket_block", "16"))
     spe = 40
     cfg = _cfg("ps", steps_per_epoch=spe, batch_size=2, epochs=1, train_images=2 * spe)
     res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
@@ -77,7 +79,7 @@ def test_ps_plateau_lowers_lr_and_early_stop_ends_job(monkeypatch):
     on worker 0's val_loss and publishes the LR and the stop flag to every worker: a flat
     val_loss (lr ~ 0) lowers the LR after `patience` epochs and stops the job early."""
     from pddl.parallel.parameter_server import run_ps_job
-    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "600")
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "heartbeat", "600"))
     cfg = _cfg("ps", steps_per_epoch=2, validation_steps=1, batch_size=2, epochs=6, lr=1e-12, min_lr=1e-14,
                reduce_lr_patience=1, early_stop_patience=3)
     res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
@@ -94,7 +96,7 @@ def test_ps_final_checkpoint_holds_the_ps_state(tmp_path, monkeypatch):
     saves the PS variables, imagenet-resnet50-ps.py:145-148), not worker 0's last snapshot."""
     from pddl.parallel.parameter_server import run_ps_job
     from pddl.utils.checkpoint import read_keras_weights
-    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "600")
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "heartbeat", "600"))
     cfg = _cfg("ps", steps_per_epoch=4, batch_size=2, epochs=1, save=True, save_dir=str(tmp_path))
     res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
     ps = [r for r in res if r[0] == "ps"]
@@ -225,8 +227,8 @@ def test_ps_stalled_worker_declared_dead_and_requeued(monkeypatch):
     the heartbeat timeout (before the coordinator can declare it dead)."""
     from pddl.parallel.parameter_server import run_ps_job
     monkeypatch.setenv("PDDL_FAULT", "hang_worker:1@1")
-    monkeypatch.setenv("PDDL_HEARTBEAT_TIMEOUT", "3")
-    monkeypatch.setenv("PDDL_PS_STEP_STALL", "3")
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "heartbeat", "3"))
+    monkeypatch.setenv("PDDL_PS", with_opt("PDDL_PS", "step_stall", "3"))
     cfg = _cfg("ps", steps_per_epoch=6, batch_size=2, epochs=1)
     res = run_ps_job(cfg, num_ps=1, num_workers=2, return_results=True)
     wk = [r for r in res if r[0] == "worker"]
@@ -267,7 +269,7 @@ def test_requeue_orphans_scans_the_next_epoch():
 
 
 def test_heartbeat_keeps_beating_through_a_slow_step():
-    """The in-step stall threshold (PDDL_PS_STEP_STALL) is separate from the liveness timeout:
+    """The in-step stall threshold (PDDL_PS step_stall) is separate from the liveness timeout:
     a step longer than the heartbeat timeout but shorter than the stall threshold keeps the
     beacon stamping (a slow but healthy worker is not declared dead)."""
     import torch.distributed as dist
