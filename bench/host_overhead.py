@@ -60,13 +60,77 @@ def measure(graphs: bool, B: int, steps: int):
             "hip_graph": st.mirror.graph_mode}
 
 
+class _StubComm:
+    """Stand-in for the native RCCL communicator of a Mirrored job: the host issues exactly the
+    calls of the graphed step (one grouped all-reduce per bucket over the R comm streams), which
+    return at once -- so what is timed is the driver's own host loop, not RCCL."""
+    calls = 0
+
+    def all_reduce_on(self, bufs, op, streams, tag):
+        assert len(bufs) == len(streams)
+        _StubComm.calls += 1
+
+    def check(self):
+        pass
+
+
+def measure_replicas(R: int, B: int, steps: int):
+    """R segmented replicas of the in-process Mirrored design, all on device 0 (the host loop of
+    _LocalReplicas._graphed_step for an R-GPU node: per replica the input load, nb segment
+    replays, nb event records + comm-stream waits, nb grouped collective calls, the optimizer
+    graph), with the stub communicator.  host_ms: wall time of one step() call (the enqueue)."""
+    from pddl.config import make_config
+    from pddl.parallel.strategies import _LocalReplicas
+    cfg = make_config("mirrored", device="cuda", batch_size=B, crop=224, image_size=224, save=False, verbose=0,
+                      data="synthetic_fixed")
+    lr = _LocalReplicas(cfg, [0] * R)
+    lr.comm = _StubComm()
+    lr.graph_mode = True
+    lr.launch_streams = [torch.cuda.Stream() for _ in range(R)]   # one per replica, as on R devices
+    eng = os.environ.get("PDDL_ENGINE", "")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    images = [torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(R)]
+    labels = [torch.randint(0, 1000, (B,), dtype=torch.int64, device="cuda", generator=g) for _ in range(R)]
+    for _ in range(3):
+        lr.step(images, labels, B * R)
+    torch.cuda.synchronize()
+    host = []
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lr.step(images, labels, B * R)
+        host.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    if os.environ.get("HOST_PROFILE"):
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        for _ in range(10):
+            torch.cuda.synchronize()
+            pr.enable()
+            lr.step(images, labels, B * R)
+            pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+    host.sort()
+    nb = len(lr.buckets)
+    return {"mode": "graphed, stub communicator", "PDDL_ENGINE": eng,
+            "two_stream": lr.replicas[0][0].side is not None, "replicas": R, "batch_per_replica": B, "buckets": nb,
+            "host_ms": round(host[len(host) // 2] * 1e3, 3), "host_ms_min": round(host[0] * 1e3, 3),
+            "graph_launches_per_step": R * (nb + 1), "collective_calls_per_step": nb}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="> 0: only the R-replica host-loop rehearsal on device 0 (stub communicator)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
-    rows = [measure(False, a.batch, a.steps), measure(True, a.batch, a.steps)]
+    if a.replicas > 0:
+        rows = [measure_replicas(a.replicas, a.batch, a.steps)]
+    else:
+        rows = [measure(False, a.batch, a.steps), measure(True, a.batch, a.steps)]
     for r in rows:
         print(json.dumps(r), flush=True)
     if a.json:

@@ -721,6 +721,7 @@ void register_fusion(pybind11::module& m);
 void register_loader(pybind11::module& m);
 void register_ps(pybind11::module& m);
 void register_crash_trace(pybind11::module& m);
+void register_graph_launch(pybind11::module& m);
 
 // Kernel launches release the GIL: replica threads (Mirrored / multi-GPU workers) then enqueue
 // their launch streams concurrently instead of serializing on the interpreter lock.
@@ -733,6 +734,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_loader(m);
   register_ps(m);
   register_crash_trace(m);
+  register_graph_launch(m);
   // rows: host int64 [n, 3] of (flat offset, packed offset, length), bounds-checked here
   m.def("range_copy", [](Tensor src, Tensor dst, Tensor rows, bool scatter) {
     PCHECK(!rows.is_cuda() && rows.scalar_type() == torch::kInt64 && rows.dim() == 2 && rows.size(1) == 3,

@@ -945,34 +945,59 @@ const char* prep_f32_launch(const float* params, const PrepLayer* layers_dev, in
 }
 
 // --------------------------------------------------------------------- wgrad finalize
-__global__ void wgrad_finalize_kernel(const float* __restrict__ prm, float* __restrict__ grads,
-                                      const FinLayer* __restrict__ L, const float* __restrict__ scale,
-                                      float* __restrict__ dgamma_raw) {
-  __shared__ float red[4];
+// Per output row co of each layer in the table: dW[co] *= a[co] (the folded BN scale) and
+// dgamma_raw[co] = <W[co], dW_raw[co]>.  One WAVE per row, 4 rows per 256-thread workgroup, rows
+// streamed as 16-byte vectors two deep (a row is 64-4608 floats): the pass is bound by reading
+// W + dW and writing dW once (a one-row-per-workgroup form ran b32 at 16 us per block, 5x the
+// bytes bound).  Rows whose offset or length is not a multiple of 4 floats (the stem, k = 147)
+// take the scalar loop.
+__global__ void __launch_bounds__(256) wgrad_finalize_kernel(const float* __restrict__ prm, float* __restrict__ grads,
+                                                             const FinLayer* __restrict__ L,
+                                                             const float* __restrict__ scale,
+                                                             float* __restrict__ dgamma_raw) {
   const FinLayer l = L[blockIdx.y];
-  const int co = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int co = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (co >= l.cout) return;
-  const float* w = prm + l.w_off + (long)co * l.k;
-  float* dw = grads + l.w_off + (long)co * l.k;
+  const long base = l.w_off + (long)co * l.k;
   const float a = l.ch_off >= 0 ? scale[l.ch_off + co] : 1.f;
   float dot = 0.f;
-  for (int k = threadIdx.x; k < l.k; k += blockDim.x) {
-    const float d = dw[k];
-    dot += w[k] * d;
-    dw[k] = d * a;
+  if (((base | l.k) & 3) == 0) {
+    const float4* w = reinterpret_cast<const float4*>(prm + base);
+    float4* dw = reinterpret_cast<float4*>(grads + base);
+    const int n4 = l.k >> 2;
+    int i = lane;
+    for (; i + 64 < n4; i += 128) {
+      const float4 w0 = w[i], w1 = w[i + 64], d0 = dw[i], d1 = dw[i + 64];
+      dot += w0.x * d0.x + w0.y * d0.y + w0.z * d0.z + w0.w * d0.w;
+      dot += w1.x * d1.x + w1.y * d1.y + w1.z * d1.z + w1.w * d1.w;
+      dw[i] = make_float4(d0.x * a, d0.y * a, d0.z * a, d0.w * a);
+      dw[i + 64] = make_float4(d1.x * a, d1.y * a, d1.z * a, d1.w * a);
+    }
+    if (i < n4) {
+      const float4 w0 = w[i], d0 = dw[i];
+      dot += w0.x * d0.x + w0.y * d0.y + w0.z * d0.z + w0.w * d0.w;
+      dw[i] = make_float4(d0.x * a, d0.y * a, d0.z * a, d0.w * a);
+    }
+  } else {
+    const float* w = prm + base;
+    float* dw = grads + base;
+    for (int k = lane; k < l.k; k += 64) {
+      const float d = dw[k];
+      dot += w[k] * d;
+      dw[k] = d * a;
+    }
   }
   dot = warp_sum(dot);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dot;
-  __syncthreads();
-  if (threadIdx.x == 0 && l.dg_off >= 0) dgamma_raw[l.dg_off + co] = red[0] + red[1] + red[2] + red[3];
+  if (lane == 0 && l.dg_off >= 0) dgamma_raw[l.dg_off + co] = dot;
 }
 const char* wgrad_finalize_launch(const float* params, float* grads, const FinLayer* layers_dev, int nlayers,
                                   const float* scale, float* dgamma_raw, hipStream_t s, int max_cout) {
-  // one workgroup per output row of the widest layer in the table (the table's other layers'
-  // surplus rows exit at once): a stage-2 block's table is 256 rows wide, not 2048
-  if (max_cout < 1 || max_cout > 65535) return "wgrad_finalize: max_cout out of range";
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(max_cout, nlayers), dim3(256), 0, s, params, grads, layers_dev, scale,
-                     dgamma_raw);
+  // rows of the widest layer in the table, 4 per workgroup (the table's other layers' surplus
+  // rows exit at once): a stage-2 block's table is 256 rows wide, not 2048
+  if (max_cout < 1 || max_cout > 65535 * 4) return "wgrad_finalize: max_cout out of range";
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((max_cout + 3) / 4, nlayers), dim3(256), 0, s, params, grads, layers_dev,
+                     scale, dgamma_raw);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

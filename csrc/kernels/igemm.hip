@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(256, IGEMM_MIN_BLOCKS) igemm_kernel(IgemmParam
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         dst[(i * TN + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    return;
+    return;   // igemm_splitk_reduce_kernel combines
   }
 
   // ---------------- epilogue: fragments -> LDS (fp32) -> 16-byte row stores -------------
@@ -913,9 +913,12 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
 // CU pulls its slabs) sums the `ksplit` fp32 partial tiles its slices left in the workspace
 // (same fragment order, so each lane reads 16-byte vectors of its own accumulator registers,
 // two slices' loads in flight at a time) and runs the unchanged fused epilogue on the sum.
-// A separate launch instead of an in-launch last-arriver reduction: one boundary per layer
-// (cdna_hip_programming §5, "In-launch split-K reduction": only worth it when it beats the
-// boundary it replaces).
+// A separate launch instead of an in-launch last-arriver reduction (cdna_hip_programming §5,
+// "In-launch split-K reduction"): built and measured in round 6 -- each slice published its
+// 64 KiB partial with one agent-scope release and drew a ticket, the tile's last arriver summed
+// the slices and ran the epilogue -- the b32 step went from 3.72-3.73 to 4.31 ms: the partials
+// are 4-8 x 64 KiB per tile (10x the guide's "few tens of KB"), so one workgroup's serial
+// read of them and the per-slice L2 write-back cost far more than the boundary saved.
 template <int BM, int BN>
 __global__ void __launch_bounds__(64) igemm_splitk_reduce_kernel(IgemmParams p) {
   constexpr int NW = 4, WTM = 64, WTN = 64, TM = 4, TN = 4, WAVES_N = BN / WTN, F = TM * TN;
@@ -1434,9 +1437,9 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
     // slices -> workspace, then the combine + fused epilogue (without a workspace the same
     // tile config runs unsplit, so the partial-row layout does not change)
     p.ksplit = pl.ks;
-    igemm_launch_cfg(p, pl.cfg, stream);
     const int BM = igemm_bm(pl.cfg), BN = pl.cfg == 0 ? 64 : 128;
     const int tiles = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
+    igemm_launch_cfg(p, pl.cfg, stream);
     if (pl.cfg == 0) hipLaunchKernelGGL((igemm_splitk_reduce_kernel<256, 64>), dim3(tiles * 4), dim3(64), 0, stream, p);
     else hipLaunchKernelGGL((igemm_splitk_reduce_kernel<128, 128>), dim3(tiles * 4), dim3(64), 0, stream, p);
   } else if (pl.split < p.M) {

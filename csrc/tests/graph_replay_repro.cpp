@@ -19,6 +19,8 @@
 //      stream, destroy the previous one, replay the new one on stream 0
 //   D  as C with the capture's side streams destroyed and re-created every round (torch creates
 //      side streams from its pool; an exec keeps a stream pointer only if the runtime copies it)
+//   E  the Mirrored replica driver's churn (2-3 replicas x 6 chain-shaped execs, event forks to
+//      comm streams, everything destroyed per round), then a fresh two-stream exec
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -60,6 +62,43 @@ static hipGraphExec_t make_exec(hipStream_t origin, std::vector<hipStream_t>& si
   hipGraphExec_t ex = nullptr;
   CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
   CK(hipGraphDestroy(g));   // (torch keeps only the executable unless keep_graph)
+  for (auto& e : ev) CK(hipEventDestroy(e));
+  return ex;
+}
+
+// The engine's two-stream backward shape: ONE side stream forked `pairs` times (per layer: the
+// origin's data-gradient kernel, an event, the side stream's weight-gradient kernel after it),
+// the origin waiting on the side stream every 3 pairs (gradient-ring back-pressure) and joining
+// it at the end; two = false: every kernel on the origin (the single-stream schedule).
+// Kernels per replay: 2 * pairs + 2.
+static hipGraphExec_t make_chain_exec(hipStream_t origin, hipStream_t side, int pairs, bool two,
+                                      unsigned long long* ctr, int slot) {
+  hipGraph_t g = nullptr;
+  std::vector<hipEvent_t> ev(2 * pairs + 2);
+  for (auto& e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  CK(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
+  hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, origin, ctr, slot);
+  for (int p = 0; p < pairs; ++p) {
+    hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, origin, ctr, slot);
+    if (!two) {
+      hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, origin, ctr, slot + 1);
+      continue;
+    }
+    CK(hipEventRecord(ev[2 * p], origin));
+    CK(hipStreamWaitEvent(side, ev[2 * p], 0));
+    hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, side, ctr, slot + 1);
+    CK(hipEventRecord(ev[2 * p + 1], side));
+    if (p % 3 == 2) CK(hipStreamWaitEvent(origin, ev[2 * p + 1], 0));
+  }
+  if (two) {
+    CK(hipEventRecord(ev[2 * pairs], side));
+    CK(hipStreamWaitEvent(origin, ev[2 * pairs], 0));
+  }
+  hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, origin, ctr, slot);
+  CK(hipStreamEndCapture(origin, &g));
+  hipGraphExec_t ex = nullptr;
+  CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  CK(hipGraphDestroy(g));
   for (auto& e : ev) CK(hipEventDestroy(e));
   return ex;
 }
@@ -154,6 +193,64 @@ int main(int argc, char** argv) {
     }
     CK(hipGraphExecDestroy(prev));
     ok &= check("D", ctr, want);
+  }
+  {  // E
+    // The Mirrored replica driver's pattern (tests/test_gpu_runtime.py
+    // test_graphed_replicas_match_eager_replicas, then a whole-step capture: the in-process
+    // sequence that faults, profiles/r6_graph_repro.txt): per round R = 2 or 3 replicas, each
+    // 5 segment execs + 1 "optimizer" exec (chain shape, one-stream in 2 of 3 rounds), replayed
+    // 4 steps on per-replica created launch streams with every segment forked by an event to a
+    // per-replica comm stream and the optimizer after the comm stream; then all destroyed.
+    // Finally a fresh two-stream chain exec is captured and replayed on a created stream.
+    std::printf("E: replica-driver churn, %d rounds, then a fresh two-stream exec\n", rounds / 10);
+    std::fflush(stdout);
+    unsigned long long want = 0;
+    for (int r = 0; r < rounds / 10; ++r) {
+      const int R = 2 + r % 2;
+      const bool two = r % 3 == 2;
+      std::vector<hipStream_t> ls(R), cs(R), rs(R);
+      std::vector<std::vector<hipGraphExec_t>> ex(R);
+      std::vector<std::vector<hipEvent_t>> ev(R, std::vector<hipEvent_t>(6));
+      for (int i = 0; i < R; ++i) {
+        CK(hipStreamCreate(&ls[i]));
+        CK(hipStreamCreate(&cs[i]));
+        CK(hipStreamCreate(&rs[i]));
+        for (auto& e : ev[i]) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (int k = 0; k < 6; ++k) ex[i].push_back(make_chain_exec(cap, rs[i], k < 5 ? 12 : 1, two && k < 5, ctr, 2 * k));
+      }
+      for (int step = 0; step < 4; ++step) {
+        for (int k = 0; k < 5; ++k)
+          for (int i = 0; i < R; ++i) {
+            CK(hipGraphLaunch(ex[i][k], ls[i]));
+            CK(hipEventRecord(ev[i][k], ls[i]));
+            CK(hipStreamWaitEvent(cs[i], ev[i][k], 0));
+          }
+        for (int i = 0; i < R; ++i) {
+          CK(hipEventRecord(ev[i][5], cs[i]));
+          CK(hipStreamWaitEvent(ls[i], ev[i][5], 0));
+          CK(hipGraphLaunch(ex[i][5], ls[i]));
+        }
+      }
+      want += (unsigned long long)R * 4 * (5 * (2 * 12 + 2) + (2 * 1 + 2));
+      CK(hipDeviceSynchronize());
+      for (int i = 0; i < R; ++i) {
+        for (auto e : ex[i]) CK(hipGraphExecDestroy(e));
+        for (auto e : ev[i]) CK(hipEventDestroy(e));
+        CK(hipStreamDestroy(ls[i]));
+        CK(hipStreamDestroy(cs[i]));
+        CK(hipStreamDestroy(rs[i]));
+      }
+    }
+    hipStream_t s2, l2;
+    CK(hipStreamCreate(&s2));
+    CK(hipStreamCreate(&l2));
+    hipGraphExec_t fresh = make_chain_exec(cap, s2, 40, true, ctr, 20);
+    for (int i = 0; i < 3; ++i) CK(hipGraphLaunch(fresh, l2));
+    want += 3ull * (2 * 40 + 2);
+    CK(hipGraphExecDestroy(fresh));
+    ok &= check("E", ctr, want);
+    CK(hipStreamDestroy(s2));
+    CK(hipStreamDestroy(l2));
   }
   for (auto& s : side) CK(hipStreamDestroy(s));
   CK(hipStreamDestroy(cap));

@@ -56,6 +56,14 @@ class HipEngine:
     C3C1_OK = True          # stage-2 boundaries: conv3 + next conv1 fused (c3c1.hip)
     S2C_OK = True           # blocks feeding a downsampling block store only their stride-2 grid
     TWO_STREAM_MAX_BATCH = 1024
+    # Engines whose steps replay from HIP graphs run ONE stream (two_stream=1 forces the side
+    # stream into their graphs).  The runtime launches a single-stream graph from pre-built
+    # packets (~0.5 us per kernel; R = 8 b32 host loop 1.6 ms) but a multi-branch one node by node
+    # (~3.5 us; 6.2 ms) through its parallel-stream table -- and that path faults (a freed stream
+    # in the table, SIGSEGV at +0xaee41) on the first launch of a fresh multi-branch executable
+    # once the process has created, replayed and destroyed replica graphs: deterministic in-process
+    # repro in profiles/r6_graph_repro.txt.  Cost where the branches paid: segmented Mirrored
+    # b256 12.95 vs 12.2 ms (b32: 4.45 one stream vs 4.85-5.00 two, eager 4.36).
     GRAD_RING = 5           # two-stream: gradient buffers per kind, so the data-gradient chain can run
                             # up to four blocks ahead of the weight gradients still reading older ones
                             # (b32: 3 -> 5 buffers 4.21 -> 4.17 ms eager, 4.17 -> 4.05 ms graphed)
@@ -68,8 +76,9 @@ class HipEngine:
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None,
-                 grad_ring: Optional[int] = None):
+                 grad_ring: Optional[int] = None, graphed: bool = False):
         self._grad_ring = grad_ring   # None: GRAD_RING_SMALL at batches <= 64, else GRAD_RING
+        self.graphed = graphed        # steps replay from HIP graphs: one stream (see TWO_STREAM_MAX_BATCH)
         if bn_mode not in self.BN_MODES:
             raise ValueError(f"{type(self).__name__} runs bn_mode in {self.BN_MODES}, not {bn_mode!r} "
                              "(use make_hip_engine)")
@@ -589,7 +598,9 @@ class HipEngine:
     # ------------------------------------------------------------------ two-stream backward
     def _two_stream_wanted(self, batch) -> bool:
         ts = opt(E, "two_stream", "auto")
-        return self.TWO_STREAM_OK and ((batch <= self.TWO_STREAM_MAX_BATCH) if ts == "auto" else ts == "1")
+        if ts != "auto":
+            return self.TWO_STREAM_OK and ts == "1"
+        return self.TWO_STREAM_OK and batch <= self.TWO_STREAM_MAX_BATCH and not self.graphed
 
     def _event(self):
         """The next fork/join event of this step, from a pool the engine owns for its whole

@@ -76,7 +76,8 @@ def build_engine(cfg, device: torch.device, cap: int, graphed: Optional[bool] = 
     precision=fp32 the reference-precision engine on the fp32-MFMA HIP convolutions
     (models/engine_f32.py).  On CPU: the fp32 PyTorch reference engine (config 1 of
     BASELINE.json: CPU plumbing).  graphed (default: cfg.graphs is True): the step will replay
-    from HIP graphs, which keep the shallower gradient rings (HipEngine.GRAD_RING_SMALL)."""
+    from HIP graphs, which keep the shallower gradient rings (HipEngine.GRAD_RING) and stay on
+    one stream (HipEngine.TWO_STREAM_MAX_BATCH)."""
     L = ParamLayout(cfg.num_classes)
     if device.type == "cuda" and cfg.precision == "bf16":
         from ..models.engine import HipEngine, make_hip_engine
@@ -84,7 +85,7 @@ def build_engine(cfg, device: torch.device, cap: int, graphed: Optional[bool] = 
             graphed = cfg.graphs is True
         return make_hip_engine(L, cap, bn_mode=cfg.bn_mode, crop=cfg.crop, image_size=cfg.image_size,
                                device=device, num_classes=cfg.num_classes,
-                               grad_ring=HipEngine.GRAD_RING if graphed else None)
+                               grad_ring=HipEngine.GRAD_RING if graphed else None, graphed=graphed)
     if device.type == "cuda":
         from ..models.engine_f32 import HipF32AutogradEngine, HipF32Engine
         if cfg.bn_mode == "frozen":   # the reference's configuration: explicit fused fp32 schedule
@@ -313,45 +314,17 @@ class HorovodStrategy(_ProcessGroupMixin, Strategy):
 
     def __init__(self, cfg, comm: str = "fusion"):
         super().__init__(cfg)
-        self.comm = os.environ.get("PDDL_COMM", comm)
+        self.comm = comm
 
-    def _graphed_ranks(self) -> bool:
-        """Graphed ranks: each GPU rank replays its step from HIP graphs segmented at the
-        gradient buckets, with the bucket all-reduces on a native RCCL communicator
-        (ncclCommInitRank) between the segment replays (the Mirrored replica design,
-        _LocalReplicas with one local replica).  Selected by --graphs (cfg.graphs True) with
-        world > 1, or PDDL_COMM=graphs (also on a 1-rank communicator).
-
-        The default is the eager step with the FusionEngine (buckets all-reduced over the c10d
-        RCCL group by its worker thread while the backward runs): measured on one MI355X through
-        the Trainer at the Horovod preset (b32, crop 160) the eager rank runs 10,059 img/s, the
-        whole-step graph 9,261 and the segmented graphs 8,137 (seven graph launches plus the
-        host-ordered all-reduces per step); at b2560 the segmented path costs 86.2 vs 85.8 ms
-        (profiles/r5_strategy_bench_1gpu.txt).  Never in a rehearsal (ranks sharing one GPU:
-        RCCL refuses that) or on the fp32 engine."""
-        if not (self.device.type == "cuda" and self.cfg.precision == "bf16" and self.cfg.graphs is not False
-                and not rehearsing()):
-            return False
-        comm = os.environ.get("PDDL_COMM")
-        # one rank: no collective is needed (the whole-step graph below with --graphs);
-        # PDDL_COMM=graphs still runs the multi-rank design over a 1-rank communicator
-        if comm == "graphs":
-            return True
-        return self.world > 1 and comm is None and self.cfg.graphs is True
-
+    # (Round 6 removed the graphed-rank variant -- the step replayed from bucket-segmented HIP
+    # graphs with each bucket all-reduced on a native RCCL communicator between the segment
+    # replays: at the Horovod preset's b32 / crop 160 it ran 3.81 ms per step against 3.19 ms
+    # eager with the FusionEngine (profiles/r6_mirror_host_loop.txt), and a rank issues only
+    # its own ~220 launches, which the eager step hides behind the GPU.)
     def _build(self, trainer):
         info = resolve_cluster(port_base=self.cfg.port_base)
         self.device = self._pick_device(info.local_rank if gpu_available() else 0)
         self._init_process_group(info)
-        if self._graphed_ranks():
-            # one local replica on this rank's GPU, one RCCL communicator over every rank
-            # (ncclCommInitRank; the unique id travels over the c10d group)
-            self.mirror = _LocalReplicas(self.cfg, [self.device], global_rank_base=self.rank,
-                                         world_ranks=self.world)
-            self.engine, self.opt = self.mirror.replicas[0]
-            self.fusion, self.reducer, self._tune = None, None, None
-            self.buckets = self.engine.L.buckets(self.cfg.bucket_mb if self.cfg.bucket_mb > 0 else 32.0)
-            return
         cap = max(self.cfg.batch_size, self.cfg.val_batch_size or 0)
         self.engine, self.opt = self._make_engine_and_opt(self.device, cap)
         self.aug = Augment(self.cfg, self.device, self.cfg.seed + 1000 * self.rank)
@@ -591,8 +564,7 @@ class _LocalReplicas:
         self.augs = []
         # (several replicas / ranks replay graphed segments unless --no-graphs; one replica in the
         # whole job runs eager unless --graphs)
-        ws = world_ranks or len(self.devices)
-        graphed = cfg.graphs is True or (cfg.graphs is None and ws > 1)
+        graphed = cfg.graphs is True or (cfg.graphs is None and not self._single_replica_job())
         for i, d in enumerate(self.devices):
             if d.type == "cuda":
                 torch.cuda.set_device(d)
@@ -627,6 +599,9 @@ class _LocalReplicas:
                            and (cfg.graphs if cfg.graphs is not None else True))
         self.graphs = None
         self.buckets = None
+        # graph launch stream per replica (None: train/graph.py replay_stream of its device; the
+        # host-loop rehearsal with every replica on one device gives each its own)
+        self.launch_streams = None
 
     # ------------------------------------------------------------------ state
     def broadcast(self):
@@ -699,12 +674,20 @@ class _LocalReplicas:
         self._gb = global_batch
 
     def _graphed_step(self, parts, global_batch: int):
+        """Segment k on every device, then the grouped all-reduce of bucket k on per-device comm
+        streams while segment k + 1 computes, then the optimizer graphs after the comm streams.
+        Each phase of the R devices is ONE native call (graph_launch_group: launches, event
+        records and stream waits with the GIL released), so the host loop is the runtime's graph
+        submission plus nb collective calls; with one-stream graphs (small batches) a phase's R
+        launches run concurrently on the native launch pool (R = 8, b32:
+        profiles/r6_mirror_host_loop.txt)."""
         B = parts[0][0].shape[0]
         if self.graphs is None or self.graphs[0].B != B or self._gb != global_batch:
             out = self._eager_step(parts, global_batch)   # first step eager (lazy tables), then capture
             self._capture(parts, global_batch)
             return out
-        from ..ops.native import native
+        from ..ops.native import native, require_native
+        N = require_native()
         grads = [e.grads for e, _ in self.replicas]
         # Graphs are launched on a stream of their own, never on the legacy default stream: a
         # multi-branch graph (the two-stream backward) launched there segfaulted inside
@@ -712,23 +695,20 @@ class _LocalReplicas:
         # other graphs -- train/graph.py replay_stream
         from ..train.graph import replay_stream
         amb = [torch.cuda.current_stream(d) for d in self.devices]
-        cur = [replay_stream(d) for d in self.devices]
-        for r in range(self.R):
-            cur[r].wait_stream(amb[r])
+        cur = self.launch_streams or [replay_stream(d) for d in self.devices]
         for r, (g, d) in enumerate(zip(self.graphs, self.devices)):
             with torch.cuda.device(d), torch.cuda.stream(cur[r]):
+                cur[r].wait_stream(amb[r])
                 flip, off = self.augs[r](B)
                 g.load(parts[r][0], parts[r][1], flip, off)
-        streams = [cs.cuda_stream for cs in self.comm_streams]
+        P = self._plan(cur)
+        streams = P["comm"]
         tl = self.tl
         if tl is not None:
             tl["t0"].record(cur[0])
+        par = P["parallel"]
         for k, (s, e) in enumerate(self.buckets):
-            for r, d in enumerate(self.devices):
-                with torch.cuda.device(d), torch.cuda.stream(cur[r]):
-                    self.graphs[r].replay_segment(k)
-                    self.evs[k][r].record(cur[r])
-                    self.comm_streams[r].wait_event(self.evs[k][r])
+            N.graph_launch_group(P["dev"], P["seg"][k], P["cur"], [], [], P["ev"][k], P["comm"], par)
             if tl is not None:
                 tl["b"][k][0].record(cur[0])
                 tl["b"][k][1].record(self.comm_streams[0])
@@ -744,14 +724,42 @@ class _LocalReplicas:
                         native.cast_f32(self.lowp[r][s:e], grads[r][s:e])
             if tl is not None:
                 tl["b"][k][2].record(self.comm_streams[0])
-        for r, d in enumerate(self.devices):
-            with torch.cuda.device(d), torch.cuda.stream(cur[r]):
-                cur[r].wait_stream(self.comm_streams[r])
-                self.graphs[r].replay_optimizer()
+        for g in self.graphs:
+            g.opt.sync_hparams()
+        N.graph_launch_group(P["dev"], P["opt"], P["cur"], P["cdone"], P["comm"], [], [], par)
+        for r, g in enumerate(self.graphs):
+            g.opt._iterations += 1
             amb[r].wait_stream(cur[r])
         if tl is not None:
             tl["steps"] += 1
         return self._sum_stats([g.stats for g in self.graphs])
+
+    def _plan(self, cur):
+        """Raw handles of the graphed step's native group launches (per launch-stream set)."""
+        key = tuple(c.cuda_stream for c in cur)
+        if getattr(self, "_plan_cache", None) and self._plan_cache[0] == key:
+            return self._plan_cache[1]
+        R = self.R
+        if not hasattr(self, "_cdone"):
+            self._cdone = [torch.cuda.Event() for _ in range(R)]
+        for r in range(R):      # (a torch event exists once recorded: create every handle now)
+            with torch.cuda.device(self.devices[r]):
+                for k in range(len(self.buckets)):
+                    self.evs[k][r].record(cur[r])
+                self._cdone[r].record(self.comm_streams[r])
+        ex = [g.exec_handles() for g in self.graphs]
+        P = {"dev": [d.index for d in self.devices], "cur": list(key),
+             "comm": [cs.cuda_stream for cs in self.comm_streams],
+             "seg": [[ex[r][0][k] for r in range(R)] for k in range(len(self.buckets))],
+             "opt": [ex[r][1] for r in range(R)],
+             "ev": [[self.evs[k][r].cuda_event for r in range(R)] for k in range(len(self.buckets))],
+             "cdone": [e.cuda_event for e in self._cdone],
+             # (the launch pool runs one-stream graphs only: graph_launch.cpp; PDDL_MIRROR
+             # pool=0 keeps every launch in this thread)
+             "parallel": (opt("PDDL_MIRROR", "pool", True)
+                          and all(e.side is None for e, _ in self.replicas))}
+        self._plan_cache = (key, P)
+        return P
 
     def timeline_json(self, rank: int = 0) -> Optional[str]:
         """Chrome-trace JSON of the last graphed step (device 0): per bucket READY (its segment
@@ -893,10 +901,8 @@ class _LocalReplicas:
         """One replica in the whole job: the gradient needs no reduction (a 1-rank all-reduce is
         the identity), so the step runs without collectives, like TF's MirroredStrategy on one
         device (no cross-device ops): eager by default, one whole-step HIP graph with --graphs.
-        PDDL_MIRROR=segmented=1 (and PDDL_COMM=graphs) keep the segmented multi-replica schedule
-        and its collectives."""
-        return (self.world_ranks == 1 and not opt("PDDL_MIRROR", "segmented", False)
-                and os.environ.get("PDDL_COMM") != "graphs")
+        PDDL_MIRROR=segmented=1 keeps the segmented multi-replica schedule and its collectives."""
+        return self.world_ranks == 1 and not opt("PDDL_MIRROR", "segmented", False)
 
     def _single_step(self, parts, global_batch: int):
         """One replica in the whole job, default: the eager two-stream step (no collective to
@@ -958,6 +964,13 @@ class MirroredStrategy(Strategy):
 
     def broadcast_state(self, trainer, root=0):
         self.mirror.broadcast()
+
+    def write_timeline(self, path: str):
+        """The graphed replicas' per-bucket READY / ALLREDUCE timeline (device 0), if recorded."""
+        js = self.mirror.timeline_json(0)
+        if js is not None:
+            with open(f"{path}.rank0.json", "w") as f:
+                f.write(js)
 
 
 def make_strategy(cfg) -> Strategy:

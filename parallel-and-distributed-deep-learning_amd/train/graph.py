@@ -45,13 +45,16 @@ def replay_stream(device) -> torch.cuda.Stream:
     graphed step; alone it passed).  The same graphs launched on a created stream ran clean in
     the same sequence (profiles/r5_graph_crash.txt).
 
-    Owner (round 6): not reproduced outside torch.  The standalone HIP program
-    csrc/tests/graph_replay_repro.cpp (no torch: 2-5-branch fork / join captures, executables
-    created, run, destroyed and churned, side streams destroyed and re-created, thousands of
-    replays on the legacy default stream) ran clean against both the ROCm 7.2 runtime and the
-    runtime torch bundles (scripts/graph_repro.sh, profiles/r6_graph_repro.txt).  So the plain
-    runtime API sequence does not fault; the trigger needs torch's graph / allocator / stream
-    pool state in that long-lived process, and the created launch stream stays the fix."""
+    Owner (round 6): the runtime's multi-branch launch path, entered only by graphs with
+    parallel branches.  The standalone HIP program csrc/tests/graph_replay_repro.cpp (no torch:
+    fork / join captures, executables created, run, destroyed and churned, side streams
+    re-created, the Mirrored replica driver's churn, thousands of replays on the legacy default
+    and created streams) runs clean against both the ROCm 7.2 runtime and the runtime torch
+    bundles (scripts/graph_repro.sh, profiles/r6_graph_repro.txt); in-process, three
+    multi-replica graphed tests followed by a fresh two-stream capture fault at the same frames
+    on a CREATED stream too, with torch's replay and with the native launch alike
+    (profiles/r6_mirror_host_loop.txt).  So graphed engines run one stream (models/engine.py):
+    a single-stream executable is launched from its packets and never walks the table."""
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
     s = _REPLAY.get(idx)
@@ -263,6 +266,13 @@ class SegmentedStepGraphs(GraphedTrainStep):
         if self.segments[k] is not None:
             _launch(self.segments[k])
 
+    def exec_handles(self):
+        """([segment k's raw executable, 0 if empty], the optimizer graph's): what the Mirrored
+        driver's native group launch replays (sync_hparams / the iteration count stay with the
+        caller, as in replay_optimizer)."""
+        return ([g.raw_cuda_graph_exec() if g is not None else 0 for g in self.segments],
+                self.opt_graph.raw_cuda_graph_exec())
+
     def replay_optimizer(self):
         self.opt.sync_hparams()
         _launch(self.opt_graph)
@@ -280,15 +290,22 @@ def _capture_is_empty() -> bool:
     return n == 0
 
 
+def _replay(g, stream: torch.cuda.Stream):
+    """hipGraphLaunch of g's executable on `stream` through the native extension, GIL released
+    (csrc/runtime/graph_launch.cpp).  The captured steps draw no torch RNG, so torch's replay
+    prologue (generator offsets) has nothing to do."""
+    from ..ops.native import require_native
+    require_native().graph_launch(g.raw_cuda_graph_exec(), stream.cuda_stream)
+
+
 def _launch(g):
     """Replay on the current stream, or through replay_stream() when that is the legacy
     default stream (ordered after and before the default stream's work)."""
     amb = torch.cuda.current_stream()
     if amb.cuda_stream != 0:
-        g.replay()
+        _replay(g, amb)
         return
     rs = replay_stream(amb.device)
     rs.wait_stream(amb)
-    with torch.cuda.stream(rs):
-        g.replay()
+    _replay(g, rs)
     amb.wait_stream(rs)

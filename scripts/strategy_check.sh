@@ -1,7 +1,7 @@
 #!/bin/bash
 # Strategy-level GPU checks on one GPU: the entry-script sweep at b256 (crop presets), Mirrored
 # and single at the reference's batch 32, the Horovod preset (b32, crop 160) through the Trainer
-# eager / whole-step graph / segmented graphs over a 1-rank RCCL communicator.
+# eager / whole-step graph.
 #   bash scripts/strategy_check.sh OUTDIR
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -16,10 +16,9 @@ b mirrored_b32 --strategy mirrored --batch 32 --steps 60 --warmup 10 && \
 b mirrored_b32c244 --strategy mirrored --batch 32 --crop 244 --steps 60 --warmup 10 && \
 b single_b32g --batch 32 --steps 60 --warmup 10 --graph 1 || exit 1
 H="--data synthetic --epochs 1 --steps-per-epoch 80 --validation-steps 0 --batch-size 32 --no-save"
-for mode in eager graphs whole; do
+for mode in eager whole; do
   case $mode in
     eager) env= ; extra= ;;
-    graphs) env="PDDL_COMM=graphs"; extra= ;;
     whole) env= ; extra="--graphs" ;;
   esac
   timeout -k 10 300 env $env python -u imagenet-resnet50-hvd.py $H $extra > $OUT/hvd_$mode.log 2>&1

@@ -896,7 +896,8 @@ def test_igemm_splitk_matches_unsplit_and_fp32(case, ks):
     """Split-K (K slices -> fp32 partial tiles in the workspace -> combine kernel running the
     unchanged fused epilogue) against the unsplit kernel and the fp32 reference: forward with
     BN affine + residual + ReLU + bitmask, dgrad with residual-gradient add + ReLU mask + fused
-    column sums.  ks 0 = the heuristic (these problems have 1-16 tiles: it splits them)."""
+    column sums.  ks 0 = the heuristic (these problems have 1-16 tiles: it splits them).  Three
+    launches in a row give identical bits (the combine sums the slices in a fixed order)."""
     torch.manual_seed(31)
     kind, n, h, cin, co, r, pad = case
     M = n * h * h
@@ -916,10 +917,15 @@ def test_igemm_splitk_matches_unsplit_and_fp32(case, ks):
                     w = rnd(co, r, r, cin, scale=0.03)
                     sc, sh = torch.rand(co, device=dev) + 0.5, torch.randn(co, device=dev)
                     res = rnd(n, h, h, co)
-                out = torch.empty(n, h, h, co, dtype=torch.bfloat16, device=dev)
-                bits = torch.zeros(n, h, h, (co + 7) // 8, dtype=torch.uint8, device=dev)
-                nat.igemm(x, None, h, h, r, r, 1, pad, h, h, w.view(co, -1), 0, sc, sh, res, None, None, out, 1,
-                          None, 0, 0, 0, 0, 0, None, bits)
+                outs = []
+                for _ in range(3 if knob else 1):
+                    out = torch.empty(n, h, h, co, dtype=torch.bfloat16, device=dev)
+                    bits = torch.zeros(n, h, h, (co + 7) // 8, dtype=torch.uint8, device=dev)
+                    nat.igemm(x, None, h, h, r, r, 1, pad, h, h, w.view(co, -1), 0, sc, sh, res, None, None, out, 1,
+                              None, 0, 0, 0, 0, 0, None, bits)
+                    outs.append(out.clone())
+                for o in outs[1:]:
+                    assert torch.equal(o, outs[0])
                 results.append((out.float(), bits.clone(), None))
                 ref = (conv_ref(x, w, 1, pad) * sc + sh + res.float()).relu()
             else:
@@ -1341,3 +1347,35 @@ def test_c3c1_boundary_fusion_matches_two_launches(with_res, m):
     assert (b3 != b3_r).float().mean().item() < 1e-3
     assert rel(y1, y1_r) < 5e-3
     assert (b1 != b1_r).float().mean().item() < 1e-3
+
+
+def test_wgrad_finalize_matches_reference():
+    """wgrad_finalize (one wave per row, 16-byte vectors where rows are aligned, scalar rows
+    otherwise) against fp32 PyTorch: dW[co] *= a[co] and dgamma_raw[co] = <W[co], dW_raw[co]>,
+    over a table mixing an unaligned stem-like layer (k = 147), a short row (k = 64), a long
+    3x3 row (k = 4608), a layer without scale (ch_off -1) and one without dgamma (dg_off -1)."""
+    import struct
+    torch.manual_seed(9)
+    nat = N()
+    layers = [(256, 64, 64, 64), (40, 4608, 320, 320), (96, 576, -1, 360), (72, 100, 456, -1), (64, 147, 0, 0)]
+    off, rows = 4, []                    # (aligned rows first; the k = 147 rows end unaligned)
+    for cout, k, ch, dg in layers:
+        rows.append((off, cout, k, ch, dg))
+        off += cout * k
+    params = torch.randn(off, device=dev)
+    grads = torch.randn(off, device=dev)
+    scale = torch.rand(600, device=dev) + 0.5
+    dgr = torch.full((600,), float("nan"), device=dev)
+    table = torch.tensor(list(b"".join(struct.pack("<5i", *r) for r in rows)), dtype=torch.uint8, device=dev)
+    g0 = grads.clone()
+    nat.wgrad_finalize(params, grads, table, len(rows), scale, dgr, max(c for c, *_ in layers))
+    torch.cuda.synchronize()
+    for o, cout, k, ch, dg in rows:
+        w = params[o:o + cout * k].view(cout, k)
+        d = g0[o:o + cout * k].view(cout, k)
+        a = scale[ch:ch + cout, None] if ch >= 0 else 1.0
+        assert rel(grads[o:o + cout * k].view(cout, k), d * a) < 1e-6
+        if dg >= 0:
+            assert rel(dgr[dg:dg + cout], (w * d).sum(1)) < 1e-5
+    assert torch.equal(grads[:4], g0[:4])                 # nothing outside the table is touched
+    assert torch.isnan(dgr[456:528]).all()                # (dg_off -1: no dgamma written)

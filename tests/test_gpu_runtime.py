@@ -151,7 +151,8 @@ def test_mirrored_graphed_step_matches_eager(monkeypatch, segmented):
         assert st.mirror.graph_mode == graphs
         if graphs and segmented:
             g = st.mirror.graphs[0]
-            assert g.captured and len(g.segments) == len(st.mirror.buckets) >= 2 and st.engine.side is not None
+            assert g.captured and len(g.segments) == len(st.mirror.buckets) >= 2
+            assert st.engine.side is None         # (graphed engines run one stream: HipEngine)
             assert st.mirror.comm.watchdog_state()["issued"] >= 2 * len(st.mirror.buckets)
         elif graphs:
             assert st.mirror.graphs is None and st.mirror._whole.graph is not None
@@ -159,6 +160,63 @@ def test_mirrored_graphed_step_matches_eager(monkeypatch, segmented):
     assert i0 == i1 == 3
     assert abs(l0 - l1) <= 1e-3 * abs(l0)
     assert ((p0 - p1).norm() / p0.norm()).item() < 2e-3
+
+
+class _SumComm:
+    """In-process sum of the replicas' buckets (all on device 0) on the comm streams: the
+    stand-in for the grouped RCCL all-reduce when R replicas share one GPU."""
+    nranks = 2
+
+    def all_reduce_on(self, ts, op, streams, what):
+        ss = [torch.cuda.ExternalStream(s) for s in streams]
+        for s in ss[1:]:
+            ss[0].wait_stream(s)
+        with torch.cuda.stream(ss[0]):
+            tot = ts[0].clone()
+            for t in ts[1:]:
+                tot += t
+            for t in ts:
+                t.copy_(tot)
+        for s in ss[1:]:
+            s.wait_stream(ss[0])
+
+    def check(self):
+        pass
+
+
+@pytest.mark.parametrize("R,two", [(2, "auto"), (3, "auto"), (2, "1")])
+def test_graphed_replicas_match_eager_replicas(monkeypatch, R, two):
+    """R graphed replicas (segments, events and comm-stream waits issued by one native group
+    launch per phase) train like R eager replicas: R replicas on device 0, each with its own
+    launch stream, gradients summed per bucket on the comm streams.  two "auto": the graphed
+    engines run one stream (HipEngine); "1": the two-stream segments."""
+    from pddl.parallel.strategies import _LocalReplicas
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "two_stream", two))
+    B = 8
+    g = torch.Generator(device="cuda").manual_seed(3)
+    images = [torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(R)]
+    labels = [torch.randint(0, 1000, (B,), dtype=torch.int64, device="cuda", generator=g) for _ in range(R)]
+    out = []
+    for graphed in (False, True):
+        lr = _LocalReplicas(_cfg("mirrored", flip=False, batch_size=B, graphs=graphed, lr=1e-4), [0] * R)
+        lr.broadcast()                              # (no communicator yet: in-process copies)
+        lr.comm = _SumComm()
+        lr.graph_mode = graphed
+        lr.launch_streams = [torch.cuda.Stream() for _ in range(R)]
+        losses = [lr.step(images, labels, B * R)[0].item() for _ in range(4)]
+        torch.cuda.synchronize()
+        if graphed:
+            assert len(lr.graphs) == R and len(lr.buckets) >= 2
+            assert (lr.replicas[0][0].side is not None) == (two == "1")
+        assert all(o.iterations == 4 for _, o in lr.replicas)
+        ps = [e.params.clone() for e, _ in lr.replicas]
+        for p in ps[1:]:
+            assert ((p - ps[0]).norm() / ps[0].norm()).item() < 1e-6   # replicas stay in sync
+        out.append((losses, ps[0]))
+    # (the weight-gradient atomics make runs differ in the last bits)
+    for a, b in zip(out[0][0], out[1][0]):
+        assert abs(a - b) <= 1e-3 * abs(a), (out[0][0], out[1][0])
+    assert ((out[0][1] - out[1][1]).norm() / out[0][1].norm()).item() < 2e-3
 
 
 def _bench_json(args, env):
@@ -327,31 +385,26 @@ def test_comm_proxy_holds_its_duration_and_leaves_the_gradient():
 
 
 @pytest.mark.parametrize("wire", ["fp32", "bf16"])
-def test_horovod_rank_graphs_over_one_rank_communicator(monkeypatch, tmp_path, wire):
-    """Horovod (and 1-GPU-per-process MWMS) ranks replay their step from HIP graphs segmented at
-    the gradient buckets, with each bucket's all-reduce on a native RCCL communicator between
-    the segment replays (the Mirrored replica design).  PDDL_COMM=graphs forces it on a 1-rank
-    job (nranks = 1 communicator): 4 steps of the Horovod preset's crop 160 at the reference's
-    batch 32 follow the eager rank step, and the timeline has a READY and an ALLREDUCE per
-    bucket (imagenet-resnet50-hvd.py:25,89,101)."""
+def test_mirrored_segmented_wire_and_timeline_over_one_rank_communicator(monkeypatch, tmp_path, wire):
+    """The multi-replica schedule (PDDL_MIRROR segmented=1: bucket-segmented graphs, each
+    bucket all-reduced on the native RCCL communicator between the segment replays, fp32 or bf16
+    wire) at the reference's batch 32 (crop 160) follows the eager one-replica step, and its
+    timeline has a READY and an ALLREDUCE per bucket (imagenet-resnet50-mirror.py:21,54)."""
     import json
     from pddl.parallel.strategies import make_strategy
     from pddl.train.trainer import Trainer
     res = []
-    for comm in ("graphs", "eager"):
-        if comm == "graphs":
-            monkeypatch.setenv("PDDL_COMM", "graphs")
-        else:
-            monkeypatch.delenv("PDDL_COMM", raising=False)
+    for seg in ("1", "0"):
+        monkeypatch.setenv("PDDL_MIRROR", with_opt("PDDL_MIRROR", "segmented", seg))
         tl = str(tmp_path / "tl")
-        cfg = _cfg("horovod", flip=False, max_steps=4, batch_size=32, crop=160, lr=1e-3, lr_scale_by_size=False,
-                   warmup_epochs=0, grad_dtype=wire, timeline=tl if comm == "graphs" else None)
+        cfg = _cfg("mirrored", flip=False, max_steps=4, batch_size=32, crop=160, lr=1e-3, grad_dtype=wire,
+                   timeline=tl if seg == "1" else None)
         st = make_strategy(cfg)
         tr = Trainer(cfg, st)
         h = tr.fit(1, [], validation=False)
         res.append((h.history["loss"][0], st.engine.params.clone(), st.opt.iterations))
-        if comm == "graphs":
-            m = st.mirror
+        m = st.mirror
+        if seg == "1":
             assert m.graph_mode and m.graphs is not None and m.comm.nranks == 1
             assert (m.lowp is not None) == (wire == "bf16")
             st.write_timeline(tl)
@@ -360,7 +413,7 @@ def test_horovod_rank_graphs_over_one_rank_communicator(monkeypatch, tmp_path, w
             assert sum(e["name"] == "READY" for e in ev) == nb and sum(e["name"] == "ALLREDUCE" for e in ev) == nb
             assert all(e["dur"] >= 0 for e in ev if e["name"] == "ALLREDUCE")
         else:
-            assert getattr(st, "mirror", None) is None and st.fusion is None
+            assert m.graphs is None
     (l0, p0, i0), (l1, p1, i1) = res
     assert i0 == i1 == 4
     if wire == "fp32":
