@@ -742,10 +742,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     Tensor r = rows.contiguous();
     const int64_t* q = r.data_ptr<int64_t>();
     const int64_t flat_n = scatter ? dst.numel() : src.numel(), packed_n = scatter ? src.numel() : dst.numel();
-    for (int64_t i = 0; i < r.size(0); ++i)
+    for (int64_t i = 0; i < r.size(0); ++i) {
       PCHECK(q[3 * i] >= 0 && q[3 * i + 1] >= 0 && q[3 * i + 2] >= 0 && q[3 * i] + q[3 * i + 2] <= flat_n &&
                  q[3 * i + 1] + q[3 * i + 2] <= packed_n,
              "range out of bounds");
+      PCHECK(i == 0 || q[3 * i + 1] == q[3 * (i - 1) + 1] + q[3 * (i - 1) + 2], "ranges must be laid end to end in packed order");
+    }
     static_assert(sizeof(pddl::RangeRow) == 3 * sizeof(int64_t), "RangeRow layout");
     Tensor dev = r.to(src.device());
     ok(pddl::range_copy_launch(f32p(src), f32p(dst), reinterpret_cast<const pddl::RangeRow*>(dev.data_ptr()),
@@ -763,10 +765,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     Tensor r = rows.contiguous();
     const int64_t* q = r.data_ptr<int64_t>();
     const int64_t flat_n = scatter ? dst.numel() : src.numel(), packed_n = scatter ? src.numel() : dst.numel();
-    for (int64_t i = 0; i < r.size(0); ++i)
+    for (int64_t i = 0; i < r.size(0); ++i) {
       PCHECK(q[3 * i] >= 0 && q[3 * i + 1] >= 0 && q[3 * i + 2] >= 0 && q[3 * i] + q[3 * i + 2] <= flat_n &&
                  q[3 * i + 1] + q[3 * i + 2] <= packed_n,
              "range out of bounds");
+      PCHECK(i == 0 || q[3 * i + 1] == q[3 * (i - 1) + 1] + q[3 * (i - 1) + 2], "ranges must be laid end to end in packed order");
+    }
     Tensor dev = r.to(src.device());
     ok(pddl::range_copy_cvt_launch(src.data_ptr(), dst.data_ptr(), reinterpret_cast<const pddl::RangeRow*>(dev.data_ptr()),
                                    (int)r.size(0), scatter ? 1 : 0, cur_stream()),

@@ -947,9 +947,9 @@ const char* prep_f32_launch(const float* params, const PrepLayer* layers_dev, in
 // --------------------------------------------------------------------- wgrad finalize
 // Per output row co of each layer in the table: dW[co] *= a[co] (the folded BN scale) and
 // dgamma_raw[co] = <W[co], dW_raw[co]>.  One WAVE per row, 4 rows per 256-thread workgroup, rows
-// streamed as 16-byte vectors two deep (a row is 64-4608 floats): the pass is bound by reading
-// W + dW and writing dW once (a one-row-per-workgroup form ran b32 at 16 us per block, 5x the
-// bytes bound).  Rows whose offset or length is not a multiple of 4 floats (the stem, k = 147)
+// streamed as 16-byte vectors (a row is 64-4608 floats): the pass is bound by reading
+// W + dW and writing dW once, four 16-byte pairs per lane in flight (a one-row-per-workgroup
+// form ran b32 at 16 us per block, 5x the bytes bound).  Rows whose offset or length is not a multiple of 4 floats (the stem, k = 147)
 // take the scalar loop.
 __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const float* __restrict__ prm, float* __restrict__ grads,
                                                              const FinLayer* __restrict__ L,
@@ -967,14 +967,17 @@ __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const float* __rest
     float4* dw = reinterpret_cast<float4*>(grads + base);
     const int n4 = l.k >> 2;
     int i = lane;
-    for (; i + 64 < n4; i += 128) {
-      const float4 w0 = w[i], w1 = w[i + 64], d0 = dw[i], d1 = dw[i + 64];
-      dot += w0.x * d0.x + w0.y * d0.y + w0.z * d0.z + w0.w * d0.w;
-      dot += w1.x * d1.x + w1.y * d1.y + w1.z * d1.z + w1.w * d1.w;
-      dw[i] = make_float4(d0.x * a, d0.y * a, d0.z * a, d0.w * a);
-      dw[i + 64] = make_float4(d1.x * a, d1.y * a, d1.z * a, d1.w * a);
+    for (; i + 192 < n4; i += 256) {   // four 16-byte pairs per lane in flight
+      float4 wv[4], dv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { wv[u] = w[i + 64 * u]; dv[u] = dw[i + 64 * u]; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        dot += wv[u].x * dv[u].x + wv[u].y * dv[u].y + wv[u].z * dv[u].z + wv[u].w * dv[u].w;
+        dw[i + 64 * u] = make_float4(dv[u].x * a, dv[u].y * a, dv[u].z * a, dv[u].w * a);
+      }
     }
-    if (i < n4) {
+    for (; i < n4; i += 64) {
       const float4 w0 = w[i], d0 = dw[i];
       dot += w0.x * d0.x + w0.y * d0.y + w0.z * d0.z + w0.w * d0.w;
       dw[i] = make_float4(d0.x * a, d0.y * a, d0.z * a, d0.w * a);

@@ -1299,7 +1299,7 @@ static int igemm_splitk_slices(int M, int Nn, int K, int cfg) {
   if (2 * T > C && !(T < target && KT >= 32)) return 1;
   long ks = (target + T - 1) / T;
   if (ks > KT / 4) ks = KT / 4;
-  if (ks > 8) ks = 8;
+  if (ks > 8) ks = 8;   // (a cap of 4 measured +0.5 %, 2 +7 % on the b32 step, round 6)
   return ks >= 2 ? (int)ks : 1;
 }
 

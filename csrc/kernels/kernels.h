@@ -330,7 +330,7 @@ const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint
                                 float* grads, long M, hipStream_t s);
 
 // ---- range gather / scatter (pack.hip) ----
-struct RangeRow { long flat, packed, len; };
+struct RangeRow { long flat, packed, len; };   // rows laid end to end: packed[i + 1] = packed[i] + len[i]
 // scatter = 0: dst[packed + i] = src[flat + i]; 1: dst[flat + i] = src[packed + i].
 const char* range_copy_launch(const float* src, float* dst, const RangeRow* rows_dev, int nrows, int scatter,
                               hipStream_t s);

@@ -49,6 +49,7 @@ from ..utils.envopts import opt
 
 
 P = "PDDL_PS"   # the PS runtime switches (utils/envopts.py KEYS)
+_WARM_STEPS = 2   # steps of each epoch outside the throughput window (train/callbacks.py ThroughputMeter)
 
 
 def add_ps_args(ap: argparse.ArgumentParser):
@@ -664,6 +665,10 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         st.begin_epoch()
         t_epoch = time.perf_counter()
         t_drained = None
+        # steady-state rate window, as the other strategies' ThroughputMeter: from this worker's
+        # WARM-th step of the epoch (lazy tables, first-touch allocations and the PS's first
+        # round trips before it) to its last
+        ep_steps, t_warm, n_warm = 0, None, 0
         while True:
             # tickets are claimed in blocks: the control plane costs a few round trips per
             # block, none per step (no host / device synchronisation inside a block either)
@@ -697,6 +702,11 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
                 images, labels = next(it)
                 st.train_step(images, labels, lr)
                 steps_done += 1
+                ep_steps += 1
+                if ep_steps == _WARM_STEPS:
+                    if device.type == "cuda":
+                        torch.cuda.synchronize(device)
+                    t_warm, n_warm = time.perf_counter(), st.n_img
                 # progress is published per step, not per block: a worker that dies inside a
                 # block leaves only its unfinished tickets to the re-queue (each finished step
                 # already pushed its gradient; re-running it would apply that update twice)
@@ -714,6 +724,9 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
         hb.wait()
         # epoch end: worker 0 (coordinator-side logic) validates and runs the callbacks
         loss_sum, correct, n_img = st.end_epoch()       # (the epoch's one device -> host read)
+        if t_warm is not None and n_img > n_warm:
+            store.add(f"acc/{epoch}/ips_milli", int((n_img - n_warm) / (time.perf_counter() - t_warm) * 1e3))
+            store.add(f"acc/{epoch}/ips_workers", 1)
         store.add(f"acc/{epoch}/loss", int(loss_sum * 1e6))
         store.add(f"acc/{epoch}/correct", int(correct))
         store.add(f"acc/{epoch}/n", int(n_img))
@@ -722,9 +735,15 @@ def _ps_main(rank: int, world: int, num_ps: int, cfg, port: int, result_q=None):
             _wait_count(store, f"epoch_end/{epoch}", lambda: cl.num_workers - store.add("dead_workers", 0))
             dt = time.perf_counter() - t_epoch      # every worker's training steps, before validation
             n = max(1, store.add(f"acc/{epoch}/n", 0))
+            # throughput: the sum of the workers' steady-state rates (async workers) when every
+            # live worker measured one, else the whole epoch's images over its wall time
+            ips = n / max(dt, 1e-9)
+            live = cl.num_workers - store.add("dead_workers", 0)
+            if store.add(f"acc/{epoch}/ips_workers", 0) >= live:
+                ips = store.add(f"acc/{epoch}/ips_milli", 0) / 1e3
             logs = {"loss": store.add(f"acc/{epoch}/loss", 0) / 1e6 / n,
                     "accuracy": store.add(f"acc/{epoch}/correct", 0) / n, "steps": store.add(f"done/{epoch}", 0),
-                    "images_per_sec": n / max(dt, 1e-9)}
+                    "images_per_sec": ips, "epoch_images_per_sec": n / max(dt, 1e-9)}
             if cfg.validation_steps:
                 logs.update(_validate(cfg, eng, device))
             for cb in cbs:
@@ -881,8 +900,11 @@ class ParameterServerStrategy:
         if cl is None or cl.is_ps:
             raise RuntimeError("ParameterServerStrategy.setup runs in a worker role of run_ps_job")
         self.device = cl.device
+        # (eager by default, like a Horovod rank: one process per GPU keeps its launches ahead of
+        # the GPU, and the eager step keeps the weight-gradient side stream that graphed engines
+        # give up -- models/engine.py; --graphs replays forward + backward as one HIP graph)
         eng = build_engine(cfg, cl.device, max(cfg.batch_size, cfg.val_batch_size or 0),
-                           graphed=cfg.graphs is not False)
+                           graphed=cfg.graphs is True)
         eng.init(seed=cfg.seed)
         if cfg.weights and cfg.weights != "none":
             from ..utils.checkpoint import load_pretrained
@@ -893,7 +915,7 @@ class ParameterServerStrategy:
         self.widx = cl.rank - cl.num_ps
         self.aug = Augment(cfg, cl.device, cfg.seed + 7919 * self.widx)
         self.graphed = None
-        if cl.device.type == "cuda" and hasattr(eng, "wbf") and cfg.graphs is not False:
+        if cl.device.type == "cuda" and hasattr(eng, "wbf") and cfg.graphs is True:
             from ..train.graph import GraphedTrainStep   # forward + backward as one HIP graph
             self.graphed = GraphedTrainStep(eng, None, cfg.batch_size, (cfg.image_size, cfg.image_size),
                                             1.0 / cfg.batch_size, with_optimizer=False)
