@@ -204,9 +204,15 @@ void bn_apply(Tensor z, Tensor a, Tensor b, OptT r, OptT a2, OptT b2, bool relu,
   if (bits.has_value())
     PCHECK(bits->scalar_type() == torch::kUInt8 && bits->is_contiguous() && bits->numel() * 8 >= z.numel(),
            "bn_apply bits");
-  ok(pddl::bn_apply_launch(bfp(z), f32p(a), f32p(b), obfp(r), of32p(a2), of32p(b2), relu ? 1 : 0, bfpm(y),
-                           bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr, M, C, cur_stream()),
-     "bn_apply");
+  uint8_t* bp = bits.has_value() ? bits->data_ptr<uint8_t>() : nullptr;
+  if (z.scalar_type() == torch::kFloat32)   // (the fp32 train-BN engine)
+    ok(pddl::bn_apply_launch(f32p(z), f32p(a), f32p(b), r.has_value() ? f32p(*r) : nullptr, of32p(a2), of32p(b2),
+                             relu ? 1 : 0, f32p(y), bp, M, C, cur_stream()),
+       "bn_apply");
+  else
+    ok(pddl::bn_apply_launch(bfp(z), f32p(a), f32p(b), obfp(r), of32p(a2), of32p(b2), relu ? 1 : 0, bfpm(y), bp, M,
+                             C, cur_stream()),
+       "bn_apply");
 }
 void bn_bwd_reduce(Tensor g, Tensor z, OptT z2, Tensor mean, OptT mean2, Tensor sg, Tensor sgx, OptT sg2,
                    OptT sgx2) {
@@ -217,10 +223,16 @@ void bn_bwd_reduce(Tensor g, Tensor z, OptT z2, Tensor mean, OptT mean2, Tensor 
     PCHECK(z2->is_contiguous() && z2->numel() == z.numel() && mean2.has_value() && sg2.has_value() &&
                sgx2.has_value() && mean2->numel() >= C && sg2->numel() >= C && sgx2->numel() >= C,
            "bn_bwd_reduce z2");
-  ok(pddl::bn_bwd_reduce_launch(bfp(g), bfp(z), obfp(z2), f32p(mean), of32p(mean2), rows_of(z), (int)C, f32p(sg),
-                                f32p(sgx), sg2.has_value() ? f32p(*sg2) : nullptr,
-                                sgx2.has_value() ? f32p(*sgx2) : nullptr, cur_stream()),
-     "bn_bwd_reduce");
+  float* o2 = sg2.has_value() ? f32p(*sg2) : nullptr;
+  float* ox2 = sgx2.has_value() ? f32p(*sgx2) : nullptr;
+  if (z.scalar_type() == torch::kFloat32)
+    ok(pddl::bn_bwd_reduce_launch(f32p(g), f32p(z), z2.has_value() ? f32p(*z2) : nullptr, f32p(mean), of32p(mean2),
+                                  rows_of(z), (int)C, f32p(sg), f32p(sgx), o2, ox2, cur_stream()),
+       "bn_bwd_reduce");
+  else
+    ok(pddl::bn_bwd_reduce_launch(bfp(g), bfp(z), obfp(z2), f32p(mean), of32p(mean2), rows_of(z), (int)C, f32p(sg),
+                                  f32p(sgx), o2, ox2, cur_stream()),
+       "bn_bwd_reduce");
 }
 pddl::BnBwdLayer bn_layer(const std::vector<double>& v) {
   PCHECK(v.size() == 6, "BN layer: (C, ch, gamma_off, beta_off, bias_off, count)");
@@ -246,10 +258,16 @@ void bn_bwd_apply(Tensor g, Tensor z, OptT z2, std::vector<double> l, std::vecto
   PCHECK(mean.numel() >= L1.ch + L1.C && mean.numel() >= L2.ch + L2.C && inv.numel() == mean.numel() &&
              sg.numel() >= mean.numel() && sgx.numel() >= mean.numel(),
          "bn_bwd_apply: per-channel arrays too short for the layer offsets");
-  ok(pddl::bn_bwd_apply_launch(bfp(g), bfp(z), obfp(z2), L1, L2, f32p(params), f32p(mean), f32p(inv), f32p(sg),
-                               f32p(sgx), f32p(coef), (int)ldc, bfpm(dz), dz2.has_value() ? bfpm(*dz2) : nullptr,
-                               f32p(grads), rows_of(z), cur_stream()),
-     "bn_bwd_apply");
+  if (z.scalar_type() == torch::kFloat32)
+    ok(pddl::bn_bwd_apply_launch(f32p(g), f32p(z), z2.has_value() ? f32p(*z2) : nullptr, L1, L2, f32p(params),
+                                 f32p(mean), f32p(inv), f32p(sg), f32p(sgx), f32p(coef), (int)ldc, f32p(dz),
+                                 dz2.has_value() ? f32p(*dz2) : nullptr, f32p(grads), rows_of(z), cur_stream()),
+       "bn_bwd_apply");
+  else
+    ok(pddl::bn_bwd_apply_launch(bfp(g), bfp(z), obfp(z2), L1, L2, f32p(params), f32p(mean), f32p(inv), f32p(sg),
+                                 f32p(sgx), f32p(coef), (int)ldc, bfpm(dz), dz2.has_value() ? bfpm(*dz2) : nullptr,
+                                 f32p(grads), rows_of(z), cur_stream()),
+       "bn_bwd_apply");
 }
 
 void wgrad(Tensor x, int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Ho,

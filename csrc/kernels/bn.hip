@@ -14,12 +14,47 @@
 //             bn_bwd_apply         -> dz = gamma/sigma * (g - Sg/M - (z-mean)/sigma^2 * Sgx/M),
 //                                     dgamma = Sgx/sigma, dbeta = Sg, dbias = 0
 //
-// Every elementwise pass moves 16 bytes (8 channels) per lane and keeps one channel group per
-// lane (grid stride a multiple of C/8), so its per-channel coefficients load once.
+// Every elementwise pass moves 8 channels per lane (16 bytes bf16, 32 bytes fp32: the kernels are
+// templated on the activation type, the fp32 ones serve the reference-precision train-BN engine)
+// and keeps one channel group per lane (grid stride a multiple of C/8), so its per-channel
+// coefficients load once.
 #include "common.h"
 #include "kernels.h"
 
 namespace pddl {
+
+// 8 consecutive channels of one row: bf16 activations (one 16-byte load) or fp32 ones (the
+// reference-precision engine, models/engine_f32.py: two 16-byte loads).  store() returns the
+// ReLU bitmask of the stored values (bit e: value e > 0).
+template <class T> struct Vec8;
+template <> struct Vec8<bf16_t> {
+  uint4 q;
+  __device__ __forceinline__ void load(const bf16_t* p, long t) { q = reinterpret_cast<const uint4*>(p)[t]; }
+  __device__ __forceinline__ void get(float* v) const { unpack8(q, v); }
+  __device__ static __forceinline__ uint32_t store(bf16_t* p, long t, const float* v) {
+    const uint4 k = pack8(v);
+    reinterpret_cast<uint4*>(p)[t] = k;
+    return pos_bits8(k);
+  }
+};
+template <> struct Vec8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p, long t) {
+    a = reinterpret_cast<const float4*>(p)[2 * t];
+    b = reinterpret_cast<const float4*>(p)[2 * t + 1];
+  }
+  __device__ __forceinline__ void get(float* v) const {
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ static __forceinline__ uint32_t store(float* p, long t, const float* v) {
+    reinterpret_cast<float4*>(p)[2 * t] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[2 * t + 1] = make_float4(v[4], v[5], v[6], v[7]);
+    uint32_t m = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m |= (v[e] > 0.f ? 1u : 0u) << e;
+    return m;
+  }
+};
 
 // ~8 blocks of 256 lanes per CU; lanes loop so their per-channel setup is amortized
 // Grid caps of the streaming BN kernels (bench/bn.py sweep at b256, profiles/r1_bn_kernels_b256.json):
@@ -73,10 +108,10 @@ const char* bn_stats_launch(const float* acc, const BnStatLayer* layers_dev, int
 
 // ------------------------------------------------------------------------------ apply
 // y = act(z*a + b (+ r | + r*a2 + b2)); bits (nullable) = ReLU bitmask of the stored y.
-__global__ void bn_apply_kernel(const bf16_t* __restrict__ z, const float* __restrict__ a, const float* __restrict__ b,
-                                const bf16_t* __restrict__ r, const float* __restrict__ a2,
-                                const float* __restrict__ b2, int relu, bf16_t* __restrict__ y,
-                                uint8_t* __restrict__ bits, long M, int C) {
+template <class T>
+__global__ void bn_apply_kernel(const T* __restrict__ z, const float* __restrict__ a, const float* __restrict__ b,
+                                const T* __restrict__ r, const float* __restrict__ a2, const float* __restrict__ b2,
+                                int relu, T* __restrict__ y, uint8_t* __restrict__ bits, long M, int C) {
   // the grid stride is a multiple of C/8 (a power of two <= 256): every lane keeps one
   // channel group, so its per-channel coefficients are loaded once
   const int cg = C >> 3;
@@ -94,23 +129,25 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ z, const float* __res
   const long stride = (long)gridDim.x * blockDim.x;
   for (long t = t0; t < total; t += 2 * stride) {
     const bool two = t + stride < total;
-    const uint4 zq0 = reinterpret_cast<const uint4*>(z)[t];
-    const uint4 zq1 = two ? reinterpret_cast<const uint4*>(z)[t + stride] : zq0;
-    uint4 rq0 = zq0, rq1 = zq0;
+    Vec8<T> zq0, zq1, rq0, rq1;
+    zq0.load(z, t);
+    zq1 = zq0;
+    if (two) zq1.load(z, t + stride);
     if (r) {
-      rq0 = reinterpret_cast<const uint4*>(r)[t];
-      rq1 = two ? reinterpret_cast<const uint4*>(r)[t + stride] : rq0;
+      rq0.load(r, t);
+      rq1 = rq0;
+      if (two) rq1.load(r, t + stride);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && !two) break;
       float v[8];
-      unpack8(u ? zq1 : zq0, v);
+      (u ? zq1 : zq0).get(v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = v[e] * sa[e] + sb[e];
       if (r) {
         float rv[8];
-        unpack8(u ? rq1 : rq0, rv);
+        (u ? rq1 : rq0).get(rv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += rv[e] * ra[e] + rb[e];
       }
@@ -118,21 +155,30 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ z, const float* __res
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       }
-      const uint4 pk = pack8(v);
       const long tu = t + u * stride;
-      reinterpret_cast<uint4*>(y)[tu] = pk;
-      if (bits) bits[tu] = (uint8_t)pos_bits8(pk);
+      const uint32_t m = Vec8<T>::store(y, tu, v);
+      if (bits) bits[tu] = (uint8_t)m;
     }
   }
 }
 
-const char* bn_apply_launch(const uint16_t* z, const float* a, const float* b, const uint16_t* r, const float* a2,
-                            const float* b2, int relu, uint16_t* y, uint8_t* bits, long M, int C, hipStream_t s) {
+template <class T>
+static const char* bn_apply_any(const T* z, const float* a, const float* b, const T* r, const float* a2,
+                                const float* b2, int relu, T* y, uint8_t* bits, long M, int C, hipStream_t s) {
   if (C % 8 || 256 % (C / 8)) return "bn_apply: C/8 must divide 256";
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_grid(M * (C / 8))), dim3(256), 0, s, z, a, b, r, a2, b2, relu, y, bits,
-                     M, C);
+  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(bn_grid(M * (C / 8))), dim3(256), 0, s, z, a, b, r, a2, b2, relu, y,
+                     bits, M, C);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+const char* bn_apply_launch(const uint16_t* z, const float* a, const float* b, const uint16_t* r, const float* a2,
+                            const float* b2, int relu, uint16_t* y, uint8_t* bits, long M, int C, hipStream_t s) {
+  return bn_apply_any<bf16_t>(reinterpret_cast<const bf16_t*>(z), a, b, reinterpret_cast<const bf16_t*>(r), a2, b2,
+                              relu, reinterpret_cast<bf16_t*>(y), bits, M, C, s);
+}
+const char* bn_apply_launch(const float* z, const float* a, const float* b, const float* r, const float* a2,
+                            const float* b2, int relu, float* y, uint8_t* bits, long M, int C, hipStream_t s) {
+  return bn_apply_any<float>(z, a, b, r, a2, b2, relu, y, bits, M, C, s);
 }
 
 // ----------------------------------------------------------------------- bwd reduce
@@ -140,8 +186,9 @@ const char* bn_apply_launch(const uint16_t* z, const float* a, const float* b, c
 // A block takes a contiguous row range; lane (row-slot, column-group) keeps 8 channels in
 // registers, the row slots are folded through LDS and one fp32 atomic per channel and block
 // lands in the per-step workspace.
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ z,
-                                                            const bf16_t* __restrict__ z2,
+template <class T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ g, const T* __restrict__ z,
+                                                            const T* __restrict__ z2,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ mean2, long M, int C,
                                                             float* __restrict__ sg, float* __restrict__ sgx,
@@ -162,20 +209,20 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
     for (long row = r0 + slot; row < r1; row += 2 * RPI) {   // two rows in flight per lane
       const bool two = row + RPI < r1;
       const long o = row * G + cgi, o1 = two ? o + (long)RPI * G : o;
-      const uint4 gq0 = reinterpret_cast<const uint4*>(g)[o], gq1 = reinterpret_cast<const uint4*>(g)[o1];
-      const uint4 zq0 = reinterpret_cast<const uint4*>(z)[o], zq1 = reinterpret_cast<const uint4*>(z)[o1];
-      uint4 wq0 = zq0, wq1 = zq1;
-      if (z2) { wq0 = reinterpret_cast<const uint4*>(z2)[o]; wq1 = reinterpret_cast<const uint4*>(z2)[o1]; }
+      Vec8<T> gq0, gq1, zq0, zq1, wq0, wq1;
+      gq0.load(g, o); gq1.load(g, o1);
+      zq0.load(z, o); zq1.load(z, o1);
+      if (z2) { wq0.load(z2, o); wq1.load(z2, o1); }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (u == 1 && !two) break;
         float gv[8], zv[8];
-        unpack8(u ? gq1 : gq0, gv);
-        unpack8(u ? zq1 : zq0, zv);
+        (u ? gq1 : gq0).get(gv);
+        (u ? zq1 : zq0).get(zv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) { s0[e] += gv[e]; s1[e] += gv[e] * (zv[e] - mu[e]); }
         if (z2) {
-          unpack8(u ? wq1 : wq0, zv);
+          (u ? wq1 : wq0).get(zv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) s2[e] += gv[e] * (zv[e] - mu2[e]);
         }
@@ -207,9 +254,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
   }
 }
 
-const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const float* mean,
-                                 const float* mean2, long M, int C, float* sg, float* sgx, float* sg2,
-                                 float* sgx2, hipStream_t s) {
+template <class T>
+static const char* bn_bwd_reduce_any(const T* g, const T* z, const T* z2, const float* mean, const float* mean2,
+                                     long M, int C, float* sg, float* sgx, float* sg2, float* sgx2, hipStream_t s) {
   if (C % 8 || C > 2048) return "bn_bwd_reduce: C must be a multiple of 8 and <= 2048";
   const int G = C / 8, rpi = 256 / G;
   // >= 8 row iterations per lane
@@ -219,10 +266,21 @@ const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uin
   // reduce at 3.2 TB/s, 256 blocks at 6.0); the largest layers take 512.
   const long cap = g_bn_red_blocks > 0 ? g_bn_red_blocks : (M * C > (1L << 27) ? 512 : 256);
   nb = nb < 1 ? 1 : (nb > cap ? cap : nb);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((int)nb), dim3(256), 0, s, g, z, z2, mean, mean2, M, C, sg, sgx,
-                     sg2, sgx2);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3((int)nb), dim3(256), 0, s, g, z, z2, mean, mean2, M, C, sg,
+                     sgx, sg2, sgx2);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const float* mean,
+                                 const float* mean2, long M, int C, float* sg, float* sgx, float* sg2,
+                                 float* sgx2, hipStream_t s) {
+  return bn_bwd_reduce_any<bf16_t>(reinterpret_cast<const bf16_t*>(g), reinterpret_cast<const bf16_t*>(z),
+                                   reinterpret_cast<const bf16_t*>(z2), mean, mean2, M, C, sg, sgx, sg2, sgx2, s);
+}
+const char* bn_bwd_reduce_launch(const float* g, const float* z, const float* z2, const float* mean,
+                                 const float* mean2, long M, int C, float* sg, float* sgx, float* sg2,
+                                 float* sgx2, hipStream_t s) {
+  return bn_bwd_reduce_any<float>(g, z, z2, mean, mean2, M, C, sg, sgx, sg2, sgx2, s);
 }
 
 // ------------------------------------------------------------------------ bwd apply
@@ -255,10 +313,11 @@ __device__ __forceinline__ void load8(const float* p, float* v) {
 // dz = A*g + B*z + C (and dz2 from z2 with the second layer's coefficients; same g).
 // dz / dz2 may alias g (each lane reads its g before writing).  The grid stride is a
 // multiple of C/8, so a lane's 24 (or 48) coefficients are loaded once.
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* g, const bf16_t* __restrict__ z,
-                                                           const bf16_t* __restrict__ z2,
+template <class T>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* g, const T* __restrict__ z,
+                                                           const T* __restrict__ z2,
                                                            const float* __restrict__ c1, const float* __restrict__ c2,
-                                                           int ldc, bf16_t* dz, bf16_t* dz2, long M, int C) {
+                                                           int ldc, T* dz, T* dz2, long M, int C) {
   const int cg = C >> 3;
   const long total = M * cg;
   const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -269,40 +328,43 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* g, cons
   const long stride = (long)gridDim.x * blockDim.x;
   for (long t = t0; t < total; t += 2 * stride) {   // two items in flight per lane (see bn_apply)
     const bool two = t + stride < total;
-    const uint4 gq0 = reinterpret_cast<const uint4*>(g)[t];
-    const uint4 zq0 = reinterpret_cast<const uint4*>(z)[t];
-    const uint4 gq1 = two ? reinterpret_cast<const uint4*>(g)[t + stride] : gq0;
-    const uint4 zq1 = two ? reinterpret_cast<const uint4*>(z)[t + stride] : zq0;
-    uint4 wq0 = zq0, wq1 = zq0;
+    Vec8<T> gq0, zq0, gq1, zq1, wq0, wq1;
+    gq0.load(g, t);
+    zq0.load(z, t);
+    gq1 = gq0;
+    zq1 = zq0;
+    if (two) { gq1.load(g, t + stride); zq1.load(z, t + stride); }
     if (z2) {
-      wq0 = reinterpret_cast<const uint4*>(z2)[t];
-      wq1 = two ? reinterpret_cast<const uint4*>(z2)[t + stride] : wq0;
+      wq0.load(z2, t);
+      wq1 = wq0;
+      if (two) wq1.load(z2, t + stride);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && !two) break;
       float gv[8], zv[8], o[8];
-      unpack8(u ? gq1 : gq0, gv);
-      unpack8(u ? zq1 : zq0, zv);
+      (u ? gq1 : gq0).get(gv);
+      (u ? zq1 : zq0).get(zv);
       const long tu = t + u * stride;
       if (z2) {
         float wv[8], o2[8];
-        unpack8(u ? wq1 : wq0, wv);
+        (u ? wq1 : wq0).get(wv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) o2[e] = A2[e] * gv[e] + B2[e] * wv[e] + C2[e];
-        reinterpret_cast<uint4*>(dz2)[tu] = pack8(o2);
+        Vec8<T>::store(dz2, tu, o2);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = A[e] * gv[e] + B[e] * zv[e] + Cc[e];
-      reinterpret_cast<uint4*>(dz)[tu] = pack8(o);
+      Vec8<T>::store(dz, tu, o);
     }
   }
 }
 
-const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const BnBwdLayer& l,
-                                const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
-                                const float* sg, const float* sgx, float* coef, int ldc, uint16_t* dz, uint16_t* dz2,
-                                float* grads, long M, hipStream_t s) {
+template <class T>
+static const char* bn_bwd_apply_any(const T* g, const T* z, const T* z2, const BnBwdLayer& l, const BnBwdLayer& l2,
+                                    const float* params, const float* mean, const float* inv, const float* sg,
+                                    const float* sgx, float* coef, int ldc, T* dz, T* dz2, float* grads, long M,
+                                    hipStream_t s) {
   if (l.C % 8 || 256 % (l.C / 8)) return "bn_bwd_apply: C/8 must divide 256";
   if (z2 && (l2.C != l.C || !dz2)) return "bn_bwd_apply: second source must match";
   const int cb = (l.C + 255) / 256;
@@ -310,10 +372,24 @@ const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint
   if (z2)
     hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3(cb), dim3(256), 0, s, l2, params, mean, inv, sg, sgx, coef, ldc,
                        grads);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(M * (l.C / 8))), dim3(256), 0, s, g, z, z2, coef + l.ch,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_grid(M * (l.C / 8))), dim3(256), 0, s, g, z, z2, coef + l.ch,
                      coef + l2.ch, ldc, dz, dz2, M, l.C);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const BnBwdLayer& l,
+                                const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
+                                const float* sg, const float* sgx, float* coef, int ldc, uint16_t* dz, uint16_t* dz2,
+                                float* grads, long M, hipStream_t s) {
+  return bn_bwd_apply_any<bf16_t>(reinterpret_cast<const bf16_t*>(g), reinterpret_cast<const bf16_t*>(z),
+                                  reinterpret_cast<const bf16_t*>(z2), l, l2, params, mean, inv, sg, sgx, coef, ldc,
+                                  reinterpret_cast<bf16_t*>(dz), reinterpret_cast<bf16_t*>(dz2), grads, M, s);
+}
+const char* bn_bwd_apply_launch(const float* g, const float* z, const float* z2, const BnBwdLayer& l,
+                                const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
+                                const float* sg, const float* sgx, float* coef, int ldc, float* dz, float* dz2,
+                                float* grads, long M, hipStream_t s) {
+  return bn_bwd_apply_any<float>(g, z, z2, l, l2, params, mean, inv, sg, sgx, coef, ldc, dz, dz2, grads, M, s);
 }
 
 }  // namespace pddl

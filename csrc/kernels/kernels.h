@@ -310,13 +310,18 @@ struct BnStatLayer {
 const char* bn_stats_launch(const float* acc, const BnStatLayer* layers_dev, int nlayers, int max_c, int training,
                             float* params, float* mean, float* inv, float* scale, float* shift, float eps,
                             float momentum, hipStream_t s);
-// y = act(z*a + b (+ r*a2 + b2 | + r)) over [M][C] bf16; bits (nullable) = ReLU bitmask of y.
+// y = act(z*a + b (+ r*a2 + b2 | + r)) over [M][C] bf16 or fp32; bits (nullable) = ReLU bitmask of y.
 const char* bn_apply_launch(const uint16_t* z, const float* a, const float* b, const uint16_t* r, const float* a2,
                             const float* b2, int relu, uint16_t* y, uint8_t* bits, long M, int C, hipStream_t s);
+const char* bn_apply_launch(const float* z, const float* a, const float* b, const float* r, const float* a2,
+                            const float* b2, int relu, float* y, uint8_t* bits, long M, int C, hipStream_t s);   // fp32
 // sg[c] += sum g, sgx[c] += sum g*(z-mean[c]) (sg2/sgx2 for z2/mean2, nullable).
 const char* bn_bwd_reduce_launch(const uint16_t* g, const uint16_t* z, const uint16_t* z2, const float* mean,
                                  const float* mean2, long M, int C, float* sg, float* sgx, float* sg2, float* sgx2,
                                  hipStream_t s);
+const char* bn_bwd_reduce_launch(const float* g, const float* z, const float* z2, const float* mean,
+                                 const float* mean2, long M, int C, float* sg, float* sgx, float* sg2, float* sgx2,
+                                 hipStream_t s);   // fp32
 struct BnBwdLayer {
   int C, ch;                             // channels, per-channel array offset
   int gamma_off, beta_off, bias_off;     // flat offsets (params for gamma, grads for all)
@@ -328,6 +333,10 @@ const char* bn_bwd_apply_launch(const uint16_t* g, const uint16_t* z, const uint
                                 const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
                                 const float* sg, const float* sgx, float* coef, int ldc, uint16_t* dz, uint16_t* dz2,
                                 float* grads, long M, hipStream_t s);
+const char* bn_bwd_apply_launch(const float* g, const float* z, const float* z2, const BnBwdLayer& l,
+                                const BnBwdLayer& l2, const float* params, const float* mean, const float* inv,
+                                const float* sg, const float* sgx, float* coef, int ldc, float* dz, float* dz2,
+                                float* grads, long M, hipStream_t s);   // fp32
 
 // ---- range gather / scatter (pack.hip) ----
 struct RangeRow { long flat, packed, len; };   // rows laid end to end: packed[i + 1] = packed[i] + len[i]

@@ -12,8 +12,10 @@ schedule (models/engine.py) in fp32 end to end -- no autograd, no PyTorch kernel
              projection block's two dgrad sources are two launches (the second adds the
              first); then the bf16 engine's wgrad_finalize / colsum_reduce / bn_grad kernels
              (dW *= BN scale, dgamma / dbeta / dbias).
-HipF32AutogradEngine: the PyTorch-autograd form over the fp32 conv op (ops/conv_f32.py), for
---bn-mode train in fp32.
+HipF32EngineBNTrain (`--bn-mode train`): the same explicit schedule with batch-statistics BN
+(bn.hip's kernels in fp32) -- no PyTorch op in the step either.
+(tests/f32_autograd.py keeps a PyTorch-autograd form over the fp32 conv op as an independent
+test oracle.)
 """
 from __future__ import annotations
 
@@ -21,75 +23,11 @@ import struct
 from typing import Callable, Dict, Optional
 
 import torch
-import torch.nn.functional as F
 
-from ..ops.conv_f32 import conv2d_f32
 from ..ops.native import require_native
 from ..utils import profiling as prof
 from .engine import _BNG_FMT, _CRED_FMT, _FIN_FMT, _PREP_FMT, STEM_K
-from .reference import ReferenceResNet50, TorchEngine, preprocess
-from .resnet50 import BN_EPS, ParamLayout
-
-
-class HipF32ResNet50(ReferenceResNet50):
-    """ReferenceResNet50 with fp32 HIP convolutions (the explicit stem pad becomes the
-    kernel's zero padding: same values, no padded copy of the input)."""
-
-    def __init__(self, layout: ParamLayout, bn_mode: str = "frozen"):
-        super().__init__(layout, bn_mode, bf16_points=False)
-
-    def _conv(self, params, x, c, pad_explicit=False):
-        w = self._w(params, c.name, "kernel")          # OHWI
-        b = self._w(params, c.name, "bias")
-        return conv2d_f32(x, w, b, c.stride, 0 if pad_explicit else c.pad)
-
-    def features(self, params, x, training=True):
-        # the stem's explicit (3, 3, 3, 3) pad folded into the conv's padding
-        L = self.L
-        s = L.stem
-        x = F.relu(self._bn(params, conv2d_f32(x, self._w(params, s.name, "kernel"), self._w(params, s.name, "bias"),
-                                               s.stride, 3), s, training))
-        x = F.pad(x, (1, 1, 1, 1))
-        x = F.max_pool2d(x, 3, 2)
-        for b in L.blocks:
-            c = b.convs
-            sc = self._bn(params, self._conv(params, x, c["0"]), c["0"], training) if b.proj else x
-            y = F.relu(self._bn(params, self._conv(params, x, c["1"]), c["1"], training))
-            y = F.relu(self._bn(params, self._conv(params, y, c["2"]), c["2"], training))
-            y = self._bn(params, self._conv(params, y, c["3"]), c["3"], training)
-            x = F.relu(y + sc)
-        return x.mean(dim=(2, 3))
-
-    def logits(self, params, x, training=True):
-        f = self.features(params, x, training)
-        w = self._w(params, "dense", "kernel")        # [classes, 2048]
-        out = conv2d_f32(f.view(f.shape[0], -1, 1, 1), w.view(w.shape[0], 1, 1, -1), self._w(params, "dense", "bias"))
-        return out.reshape(f.shape[0], -1)
-
-
-class HipF32AutogradEngine(TorchEngine):
-    """TorchEngine interface (flat fp32 params / grads, forward_backward, evaluate) over
-    HipF32ResNet50 on the GPU: the autograd form, kept for --bn-mode train in fp32 (batch
-    statistics); the frozen-BN reference configuration runs HipF32Engine below."""
-
-    def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, device="cuda", bn_mode="frozen",
-                 num_classes: int = 1000):
-        super().__init__(layout, batch, crop=crop, device=device, bn_mode=bn_mode, num_classes=num_classes)
-        self.model = HipF32ResNet50(layout, bn_mode)
-
-    def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0), bucket_cb=None, buckets=None):
-        with torch.backends.cudnn.flags(enabled=False):
-            return super().forward_backward(images, labels, gscale, flip, crop_offset, bucket_cb, buckets)
-
-    @torch.no_grad()
-    def evaluate(self, images, labels):
-        with torch.backends.cudnn.flags(enabled=False):
-            x = preprocess(images.to(self.device), self.crop, False)
-            self.model.stats = self.params
-            logits = self.model.logits(self.params, x, training=False)
-            lab = labels.to(self.device)
-            loss_sum = F.cross_entropy(logits, lab, reduction="sum")
-            return torch.stack([loss_sum, (logits.argmax(1) == lab).sum().float()])
+from .resnet50 import BN_EPS, BN_MOMENTUM, ParamLayout
 
 
 EPI_PLAIN, EPI_FWD, EPI_DGRAD = 0, 1, 2
@@ -107,8 +45,8 @@ class HipF32Engine:
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: Optional[int] = None,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000):
         if bn_mode not in self.BN_MODES:
-            raise ValueError("HipF32Engine runs frozen BN (the reference's training=False); "
-                             "use HipF32AutogradEngine for bn_mode='train'")
+            raise ValueError(f"{type(self).__name__} runs bn_mode {self.BN_MODES[0]!r} "
+                             "(HipF32Engine: frozen, the reference's training=False; HipF32EngineBNTrain: train)")
         self.N = require_native()
         self.L = L = layout
         self.device = dev = torch.device(device)
@@ -454,4 +392,277 @@ class HipF32Engine:
         self._forward(images, B, False, None, (0, 0))
         self.N.softmax_xent_f32(self.logits[:B], lab, self.num_classes, 0.0, self.dlogits[:B], self.stats[0:1],
                                 self.stats[1:2])
+        return self.stats
+
+
+_STAT_FMT = "<8if i"   # BnStatLayer (csrc/kernels/kernels.h)
+
+
+class HipF32EngineBNTrain(HipF32Engine):
+    """fp32 engine with train-mode BatchNormalization (Keras `training=True`: batch mean / biased
+    variance normalise, Bessel-corrected variance into the moving statistics, momentum 0.99,
+    epsilon 1.001e-5) -- the explicit schedule of HipF32Engine with nothing folded into the
+    convolutions and the bf16 train engine's BN kernels (csrc/kernels/bn.hip, templated on the
+    activation type) in fp32.  No PyTorch op in the step:
+
+      forward, per conv  : conv_f32 -> z = conv + bias (fp32)
+                           -> bn_bwd_reduce(z, z, mean 0) = per-channel (sum z, sum z^2)
+                           -> bn_stats (mean, 1/sigma, BN scale / shift, moving statistics)
+                           -> bn_apply: y = relu(bn(z) [+ x | + bn0(z0)])
+      backward, per conv : (the next conv's dgrad applies the ReLU mask of y and adds the
+                           residual gradient) -> bn_bwd_reduce (sum g, sum g*(z - mean))
+                           -> bn_bwd_apply (dz; dgamma, dbeta, dbias = 0) -> wgrad_f32(x, dz)
+                           and the conv_f32 dgrad of dz; a projection block's BN3 and BN0 share
+                           one reduce and one apply (same gradient).
+    The reference itself freezes BN (imagenet-resnet50.py:57): this is the `--bn-mode train`
+    variant at the reference's precision (tests/test_gpu_f32.py bounds it against the PyTorch
+    reference model in float64)."""
+    BN_MODES = ("train",)
+
+    def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: Optional[int] = None,
+                 device="cuda", bn_mode: str = "train", num_classes: int = 1000):
+        super().__init__(layout, batch, crop=crop, image_size=image_size, device=device, bn_mode=bn_mode,
+                         num_classes=num_classes)
+        assert struct.calcsize(_STAT_FMT) == self.N.BNSTAT_LAYER_BYTES
+        f32 = dict(dtype=torch.float32, device=self.device)
+        n = self.nch
+        self.bn_mean, self.bn_inv = torch.zeros(n, **f32), torch.ones(n, **f32)
+        self.bn_scale, self.bn_shift = torch.ones(n, **f32), torch.zeros(n, **f32)
+        self.bws = torch.zeros(4 * n, **f32)          # zeroed every step: acc S | acc Q | sum g | sum g(z-mean)
+        self.acc = self.bws[:2 * n]
+        self.bsg, self.bsgx = self.bws[2 * n:3 * n], self.bws[3 * n:]
+        self.bcoef = torch.zeros(3 * n, **f32)
+        self.zero_c = torch.zeros(2048, **f32)
+        L = self.L
+        self._bng_dense = self._dev_table([struct.pack(_BNG_FMT, self.num_classes, self.ch["dense"],
+                                                       L.off("dense", "bias"), -1, -1, -1, -1, self.ch["dense"], -1)])
+        self._stat_tabs: Dict[tuple, torch.Tensor] = {}
+        self._eval_tab = self._stat_table(L.convs, 1.0, training=False)
+
+    # ------------------------------------------------------------------ tables
+    def _tables(self):
+        super()._tables()
+        # nothing folded: the conv epilogue adds only the bias (scale 1), the dgrad weights are
+        # W^T unscaled; the batch statistics drive bn_apply / bn_bwd_apply instead
+        L, rows = self.L, []
+        for c in L.convs:
+            stem = c is L.stem
+            rows.append(struct.pack(_PREP_FMT, L.off(c.name, "kernel"), c.cout, c.k, c.k, c.cin,
+                                    STEM_K if stem else c.k * c.k * c.cin, 0, -1 if stem else self.wd[c.name],
+                                    c.cout, L.off(c.name, "bias"), -1, -1, -1, -1, self.ch[c.name], 1 if stem else 0))
+        rows.append(struct.pack(_PREP_FMT, L.off("dense", "kernel"), self.num_classes, 1, 1, 2048, 2048, 0,
+                                self.wd["dense"], self.num_classes, L.off("dense", "bias"), -1, -1, -1, -1,
+                                self.ch["dense"], 0))
+        self._prep_tab, self._prep_n = self._dev_table(rows), len(rows)
+
+    def _stat_table(self, convs, count: float, training: bool = True):
+        n, L = self.nch, self.L
+        rows = [struct.pack(_STAT_FMT, c.cout, self.ch[c.name], n + self.ch[c.name], self.ch[c.name],
+                            L.off(c.bn, "gamma"), L.off(c.bn, "beta"), L.off(c.bn, "moving_mean"),
+                            L.off(c.bn, "moving_variance"), float(count), 0) for c in convs]
+        return self._dev_table(rows)
+
+    def _stats(self, c, M):
+        key = (c.name, M)
+        t = self._stat_tabs.get(key)
+        if t is None:
+            t = self._stat_tabs[key] = self._stat_table([c], float(M))
+        return t
+
+    def _alloc(self, B):
+        super()._alloc(B)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.zs = torch.empty(B, self.H1, self.H1, 64, **f32)
+        self.z: Dict[str, Dict[str, torch.Tensor]] = {}
+        for b in self.L.blocks:
+            H, Ho = self.geo[b.name]
+            f = b.filters
+            z = {"1": torch.empty(B, Ho, Ho, f, **f32), "2": torch.empty(B, Ho, Ho, f, **f32),
+                 "3": torch.empty(B, Ho, Ho, 4 * f, **f32)}
+            if b.proj:
+                z["0"] = torch.empty(B, Ho, Ho, 4 * f, **f32)
+            self.z[b.name] = z
+        self.gbuf3 = torch.empty_like(self.gbuf[0])
+
+    # ------------------------------------------------------------------ forward
+    def _chs(self, arr, c):
+        o = self.ch[c.name]
+        return arr[o:o + c.cout]
+
+    def _z(self, c, x, R, stride, pad, Ho, w, z, training):
+        """z = conv(x) + bias; when training, its batch statistics -> BN scale / shift."""
+        ch = self.ch[c.name]
+        self._conv(x, R, stride, pad, Ho, w, z, self.scale[ch:], self.shift[ch:], None, 0)
+        if training:
+            M = z.numel() // c.cout
+            self.N.bn_bwd_reduce(z, z, None, self.zero_c[:c.cout], None, self.acc[ch:ch + c.cout],
+                                 self.acc[self.nch + ch:self.nch + ch + c.cout], None, None)
+            self.N.bn_stats(self.acc, self._stats(c, M), 1, c.cout, True, self.params, self.bn_mean, self.bn_inv,
+                            self.bn_scale, self.bn_shift, BN_EPS, BN_MOMENTUM)
+
+    def _forward(self, images, B, training, flip, crop_offset):
+        N, L = self.N, self.L
+        if not training:   # the moving statistics for every layer at once
+            N.bn_stats(self.acc, self._eval_tab, len(L.convs), 2048, False, self.params, self.bn_mean, self.bn_inv,
+                       self.bn_scale, self.bn_shift, BN_EPS, BN_MOMENTUM)
+        mode, oy, ox = self._stem_mode(training, crop_offset)
+        x2 = self.x2[:B]
+        N.stem_s2d(images, flip if training else None, mode, self.crop, self.crop, oy, ox, x2, None)
+        s = L.stem
+        zs, c1 = self.zs[:B], self.c1[:B]
+        self._z(s, x2, 4, 1, 0, self.H1, self.wf32[:64 * STEM_K].view(64, STEM_K), zs, training)
+        N.bn_apply(zs, self._chs(self.bn_scale, s), self._chs(self.bn_shift, s), None, None, None, True, c1, None)
+        pool = self.pool[:B]
+        N.maxpool_fwd_f32(c1, pool, self.pidx[:B])
+        x = pool
+        for b in L.blocks:
+            a = {k: v[:B] for k, v in self.acts[b.name].items()}
+            z = {k: v[:B] for k, v in self.z[b.name].items()}
+            Ho = self.geo[b.name][1]
+            f = b.filters
+            c = b.convs
+            self._z(c["1"], x, 1, b.stride, 0, Ho, self._w(c["1"].name, f, b.cin), z["1"], training)
+            if b.proj:
+                self._z(c["0"], x, 1, b.stride, 0, Ho, self._w(c["0"].name, 4 * f, b.cin), z["0"], training)
+            N.bn_apply(z["1"], self._chs(self.bn_scale, c["1"]), self._chs(self.bn_shift, c["1"]), None, None, None,
+                       True, a["y1"], None)
+            self._z(c["2"], a["y1"], 3, 1, 1, Ho, self._w(c["2"].name, f, 9 * f), z["2"], training)
+            N.bn_apply(z["2"], self._chs(self.bn_scale, c["2"]), self._chs(self.bn_shift, c["2"]), None, None, None,
+                       True, a["y2"], None)
+            self._z(c["3"], a["y2"], 1, 1, 0, Ho, self._w(c["3"].name, 4 * f, f), z["3"], training)
+            if b.proj:
+                N.bn_apply(z["3"], self._chs(self.bn_scale, c["3"]), self._chs(self.bn_shift, c["3"]), z["0"],
+                           self._chs(self.bn_scale, c["0"]), self._chs(self.bn_shift, c["0"]), True, a["out"], None)
+            else:
+                N.bn_apply(z["3"], self._chs(self.bn_scale, c["3"]), self._chs(self.bn_shift, c["3"]), x, None, None,
+                           True, a["out"], None)
+            x = a["out"]
+        pooled = self.pooled[:B]
+        N.gap_fwd_f32(x, pooled)
+        chd = self.ch["dense"]
+        self._conv(pooled.view(B, 1, 1, 2048), 1, 1, 0, 1, self._w("dense", self.num_classes, 2048),
+                   self.logits[:B].view(B, 1, 1, self.num_classes), self.scale[chd:], self.shift[chd:], None, 0)
+        return x
+
+    # ------------------------------------------------------------------ backward
+    def _bn_layer(self, c, M):
+        L = self.L
+        return [float(c.cout), float(self.ch[c.name]), float(L.off(c.bn, "gamma")), float(L.off(c.bn, "beta")),
+                float(L.off(c.name, "bias")), float(M)]
+
+    def _bn_bwd(self, g, z, c, M, out, z2=None, c2=None, out2=None):
+        """dz (into `out`, may alias g) from g = dL/dy of conv `c`'s BN; with z2 / c2 the second BN
+        fed by the same gradient (a projection block's shortcut)."""
+        N = self.N
+        if z2 is None:
+            N.bn_bwd_reduce(g, z, None, self._chs(self.bn_mean, c), None, self._chs(self.bsg, c),
+                            self._chs(self.bsgx, c), None, None)
+            N.bn_bwd_apply(g, z, None, self._bn_layer(c, M), [], self.params, self.bn_mean, self.bn_inv, self.bsg,
+                           self.bsgx, out, None, self.grads, self.bcoef)
+        else:
+            N.bn_bwd_reduce(g, z, z2, self._chs(self.bn_mean, c), self._chs(self.bn_mean, c2), self._chs(self.bsg, c),
+                            self._chs(self.bsgx, c), self._chs(self.bsg, c2), self._chs(self.bsgx, c2))
+            N.bn_bwd_apply(g, z, z2, self._bn_layer(c, M), self._bn_layer(c2, M), self.params, self.bn_mean,
+                           self.bn_inv, self.bsg, self.bsgx, out, out2, self.grads, self.bcoef)
+
+    def forward_backward(self, images, labels, gscale, flip=None, crop_offset=(0, 0),
+                         bucket_cb: Optional[Callable[[int], None]] = None, buckets=None):
+        N, L = self.N, self.L
+        B = images.shape[0]
+        assert B <= self.cap, "batch larger than the engine's buffers"
+        self.ws.zero_()
+        self.bws.zero_()
+        lab = self._labels(labels, B)
+        prof.push("step/forward")
+        x5 = self._forward(images, B, True, flip, crop_offset)
+        prof.pop()
+        prof.push("step/backward")
+        ncls = self.num_classes
+        dl = self.dlogits[:B]
+        N.softmax_xent_f32(self.logits[:B], lab, ncls, float(gscale), dl, self.stats[0:1], self.stats[1:2])
+        bks = buckets if buckets is not None else []
+        nb = [0]
+
+        def done_upto(off):
+            while bucket_cb is not None and nb[0] < len(bks) - 1 and bks[nb[0]][1] <= off:
+                bucket_cb(nb[0])
+                nb[0] += 1
+
+        # ---- head: Dense wgrad, bias gradient (column sums), dgrad into the pooled features
+        pooled = self.pooled[:B]
+        chd = self.ch["dense"]
+        N.wgrad_f32(pooled.view(B, 1, 1, 2048), 1, 1, 1, 0, dl.view(B, 1, 1, ncls), self._gv("dense", ncls, 2048))
+        N.colsum_f32(dl, ncls, self.colsum[chd:])
+        N.bn_grad(self.params, self.grads, self._bng_dense, 1, self.colsum, self.dgr, self.scale, BN_EPS)
+        dpooled = self.dpooled[:B]
+        self._conv(dl.view(B, 1, 1, ncls), 1, 1, 0, 1, self._wd("dense", 2048, ncls), dpooled.view(B, 1, 1, 2048),
+                   epi=EPI_PLAIN)
+        e = L.entry("dense", "kernel")
+        done_upto(e.offset + e.size)
+        cur = 0
+        H5, bl = self.H5, L.blocks
+        gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
+        N.gap_bwd_f32(dpooled, x5, gout, None)
+        for bi in range(len(bl) - 1, -1, -1):
+            b = bl[bi]
+            a = {k: v[:B] for k, v in self.acts[b.name].items()}
+            z = {k: v[:B] for k, v in self.z[b.name].items()}
+            H, Ho = self.geo[b.name]
+            M = B * Ho * Ho
+            f, cin = b.filters, b.cin
+            x_in = self.acts[bl[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
+            c1c, c2c, c3c = b.convs["1"], b.convs["2"], b.convs["3"]
+            gsrc = self.s2full[bi] if bi in self.s2 else self.gbuf[cur]
+            gout = gsrc[: M * 4 * f].view(B, Ho, Ho, 4 * f)
+            dz3 = self.gbuf3[: M * 4 * f].view(B, Ho, Ho, 4 * f)
+            if b.proj:   # BN3 and the shortcut's BN0 share gout; dz0 overwrites gout in place
+                self._bn_bwd(gout, z["3"], c3c, M, dz3, z["0"], b.convs["0"], gout)
+            else:
+                self._bn_bwd(gout, z["3"], c3c, M, dz3)
+            g2 = self.g2buf[: M * f].view(B, Ho, Ho, f)
+            g1 = self.g1buf[: M * f].view(B, Ho, Ho, f)
+            N.wgrad_f32(a["y2"], 1, 1, 1, 0, dz3, self._gv(c3c.name, 4 * f, f))
+            self._conv(dz3, 1, 1, 0, Ho, self._wd(c3c.name, f, 4 * f), g2, epi=EPI_DGRAD, mask=a["y2"])
+            self._bn_bwd(g2, z["2"], c2c, M, g2)
+            N.wgrad_f32(a["y1"], 3, 3, 1, 1, g2, self._gv(c2c.name, f, 9 * f))
+            self._conv(g2, 3, 1, 1, Ho, self._wd(c2c.name, f, 9 * f), g1, epi=EPI_DGRAD, mask=a["y1"])
+            self._bn_bwd(g1, z["1"], c1c, M, g1)
+            nxt = 1 - cur
+            if b.proj:
+                c0n = b.convs["0"].name
+                N.wgrad_f32(x_in, 1, 1, b.stride, 0, g1, self._gv(c1c.name, f, cin))
+                N.wgrad_f32(x_in, 1, 1, b.stride, 0, gout, self._gv(c0n, 4 * f, cin))
+                tmp = self.tmp[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
+                self._conv(g1, 1, 1, 0, Ho, self._wd(c1c.name, cin, f), tmp, epi=EPI_PLAIN)
+                if b.stride == 2:
+                    gx = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin)   # grid positions only
+                    self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
+                               mask=x_in, up2=1)
+                else:
+                    gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                    self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
+                               mask=x_in)
+                last = L.entry(c0n, "kernel")
+            else:
+                N.wgrad_f32(x_in, 1, 1, 1, 0, g1, self._gv(c1c.name, f, cin))
+                gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                self._conv(g1, 1, 1, 0, H, self._wd(c1c.name, cin, f), gx, epi=EPI_DGRAD, add=gout, mask=x_in)
+                last = L.entry(c1c.name, "kernel")
+            done_upto(last.offset + last.size)
+            cur = nxt
+        # ---- stem: max-pool backward with conv1's ReLU mask, the stem BN, s2d-domain wgrad
+        H1, H2 = self.H1, self.H2
+        gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
+        gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
+        s = L.stem
+        N.maxpool_bwd_f32(gpool, self.pidx[:B], self.c1[:B], gc1)
+        self._bn_bwd(gc1, self.zs[:B], s, B * H1 * H1, gc1)
+        N.wgrad_f32(self.x2[:B], 4, 4, 1, 0, gc1, self.stem_dw2)
+        N.stem_wgrad_fold(self.stem_dw2, self._gv(s.name, 64, 147), 64)
+        done_upto(L.kernels_end)
+        prof.pop()
+        if bucket_cb is not None:
+            while nb[0] < len(bks):
+                bucket_cb(nb[0])
+                nb[0] += 1
         return self.stats

@@ -87,12 +87,10 @@ def build_engine(cfg, device: torch.device, cap: int, graphed: Optional[bool] = 
                                device=device, num_classes=cfg.num_classes,
                                grad_ring=HipEngine.GRAD_RING if graphed else None, graphed=graphed)
     if device.type == "cuda":
-        from ..models.engine_f32 import HipF32AutogradEngine, HipF32Engine
-        if cfg.bn_mode == "frozen":   # the reference's configuration: explicit fused fp32 schedule
-            return HipF32Engine(L, cap, crop=cfg.crop, image_size=cfg.image_size, device=device,
-                                num_classes=cfg.num_classes)
-        return HipF32AutogradEngine(L, cap, crop=cfg.crop, device=device, bn_mode=cfg.bn_mode,
-                                    num_classes=cfg.num_classes)
+        from ..models.engine_f32 import HipF32Engine, HipF32EngineBNTrain
+        # frozen: the reference's configuration; train: batch statistics (both explicit fp32 schedules)
+        cls = HipF32Engine if cfg.bn_mode == "frozen" else HipF32EngineBNTrain
+        return cls(L, cap, crop=cfg.crop, image_size=cfg.image_size, device=device, num_classes=cfg.num_classes)
     from ..models.reference import TorchEngine
     return TorchEngine(L, cap, crop=cfg.crop, device=device, bn_mode=cfg.bn_mode, num_classes=cfg.num_classes)
 
