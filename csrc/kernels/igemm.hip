@@ -1171,7 +1171,10 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgemmParams p) {
 }
 
 int g_igemm_variant = 0;   // 0 = heuristic; 1, 2 = forced pipeline depth (4-wave tiles)
-int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed)
+int g_igemm_deep = 2;      // depth the heuristic uses for K >= 256 (3-stage measured slower: removed;
+                           // round 6 again for the split-K layers at b32 as a counted-vmcnt 3-stage
+                           // tile with asm fragment reads: split slices 3.92-3.95 ms, unsplit
+                           // 4.04 ms vs 3.73-3.74 -- its 96 KiB of LDS leaves one block per CU)
 int g_igemm_pf = 1;        // epilogue-operand prefetch (PF variant) for 1x1 layers with a residual / add
 int g_igemm8 = 2;          // 8-phase 256x256 kernel (igemm8_kernel) for Nn >= 256, K >= 256, Nn < 4K:
                            // 0 off, 1 on, 2 on with the wave-row stagger (default: b1024 end to end
