@@ -14,16 +14,11 @@
 // multi-branch graphs (the two-stream backward) on one device segfaulted inside the runtime
 // (3 replicas on one GPU, round 6); those phases run in the calling thread.
 #include <hip/hip_runtime.h>
-#include <immintrin.h>
 
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
-#include <functional>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
+
+#include "launch_pool.h"
 
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -32,69 +27,8 @@ namespace py = pybind11;
 
 namespace {
 
-// Persistent worker threads (never joined: detached, blocked on a condition variable at exit).
-// Worker i runs task i of each generation; a worker spins ~200 us for the next generation
-// before it sleeps, so the back-to-back phases of one step see no futex wake-up latency.
-class LaunchPool {
- public:
-  void run(size_t n, const std::function<void(size_t)>& f) {
-    std::lock_guard<std::mutex> one(run_mu_);   // (one group launch at a time)
-    while (workers_ < n) {
-      const size_t i = workers_++;
-      std::thread([this, i] { loop(i); }).detach();
-    }
-    fn_ = &f;
-    n_ = n;
-    pending_.store((int)workers_, std::memory_order_relaxed);   // every worker checks in
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      gen_.fetch_add(1, std::memory_order_release);
-    }
-    cv_.notify_all();
-    if (!spin([&] { return pending_.load(std::memory_order_acquire) == 0; })) {
-      std::unique_lock<std::mutex> lk(mu_);
-      done_cv_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
-    }
-  }
-
- private:
-  template <class P>
-  static bool spin(P&& ready) {
-    const auto t0 = std::chrono::steady_clock::now();
-    while (!ready()) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) return false;
-      _mm_pause();
-    }
-    return true;
-  }
-
-  void loop(size_t i) {
-    uint64_t seen = 0;
-    for (;;) {
-      if (!spin([&] { return gen_.load(std::memory_order_acquire) != seen; })) {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
-      }
-      seen = gen_.load(std::memory_order_acquire);
-      if (i < n_) (*fn_)(i);
-      if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-        std::lock_guard<std::mutex> lk(mu_);
-        done_cv_.notify_one();
-      }
-    }
-  }
-
-  std::mutex run_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  std::atomic<uint64_t> gen_{0};
-  std::atomic<int> pending_{0};
-  size_t workers_ = 0;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  size_t n_ = 0;
-};
-
-LaunchPool& pool() {
-  static LaunchPool* p = new LaunchPool();   // (leaked: its threads outlive static destruction)
+pddl::LaunchPool& pool() {
+  static pddl::LaunchPool* p = new pddl::LaunchPool();   // (leaked: its threads outlive static destruction)
   return *p;
 }
 

@@ -694,19 +694,22 @@ class _LocalReplicas:
         from ..train.graph import replay_stream
         amb = [torch.cuda.current_stream(d) for d in self.devices]
         cur = self.launch_streams or [replay_stream(d) for d in self.devices]
+        # inputs staged on the ambient streams (where the batch was produced); the first group
+        # launch makes each launch stream wait for them, the optimizer's hands the step back
         for r, (g, d) in enumerate(zip(self.graphs, self.devices)):
-            with torch.cuda.device(d), torch.cuda.stream(cur[r]):
-                cur[r].wait_stream(amb[r])
+            with torch.cuda.device(d):
                 flip, off = self.augs[r](B)
                 g.load(parts[r][0], parts[r][1], flip, off)
-        P = self._plan(cur)
+        P = self._plan(cur, amb)
         streams = P["comm"]
         tl = self.tl
-        if tl is not None:
-            tl["t0"].record(cur[0])
         par = P["parallel"]
         for k, (s, e) in enumerate(self.buckets):
-            N.graph_launch_group(P["dev"], P["seg"][k], P["cur"], [], [], P["ev"][k], P["comm"], par)
+            first = k == 0
+            N.graph_launch_group(P["dev"], P["seg"][k], P["cur"], P["in_ev"] if first else [],
+                                 P["amb"] if first else [], P["ev"][k], P["comm"], par)
+            if first and tl is not None:
+                tl["t0"].record(cur[0])
             if tl is not None:
                 tl["b"][k][0].record(cur[0])
                 tl["b"][k][1].record(self.comm_streams[0])
@@ -724,29 +727,34 @@ class _LocalReplicas:
                 tl["b"][k][2].record(self.comm_streams[0])
         for g in self.graphs:
             g.opt.sync_hparams()
-        N.graph_launch_group(P["dev"], P["opt"], P["cur"], P["cdone"], P["comm"], [], [], par)
-        for r, g in enumerate(self.graphs):
+        N.graph_launch_group(P["dev"], P["opt"], P["cur"], P["cdone"], P["comm"], P["out_ev"], P["amb"], par)
+        for g in self.graphs:
             g.opt._iterations += 1
-            amb[r].wait_stream(cur[r])
         if tl is not None:
             tl["steps"] += 1
         return self._sum_stats([g.stats for g in self.graphs])
 
-    def _plan(self, cur):
-        """Raw handles of the graphed step's native group launches (per launch-stream set)."""
-        key = tuple(c.cuda_stream for c in cur)
+    def _plan(self, cur, amb):
+        """Raw handles of the graphed step's native group launches (per launch / ambient stream set)."""
+        key = tuple(c.cuda_stream for c in cur) + tuple(a.cuda_stream for a in amb)
         if getattr(self, "_plan_cache", None) and self._plan_cache[0] == key:
             return self._plan_cache[1]
         R = self.R
         if not hasattr(self, "_cdone"):
             self._cdone = [torch.cuda.Event() for _ in range(R)]
+            self._in_ev = [torch.cuda.Event() for _ in range(R)]
+            self._out_ev = [torch.cuda.Event() for _ in range(R)]
         for r in range(R):      # (a torch event exists once recorded: create every handle now)
             with torch.cuda.device(self.devices[r]):
                 for k in range(len(self.buckets)):
                     self.evs[k][r].record(cur[r])
                 self._cdone[r].record(self.comm_streams[r])
+                self._in_ev[r].record(amb[r])
+                self._out_ev[r].record(cur[r])
         ex = [g.exec_handles() for g in self.graphs]
-        P = {"dev": [d.index for d in self.devices], "cur": list(key),
+        P = {"dev": [d.index for d in self.devices], "cur": [c.cuda_stream for c in cur],
+             "amb": [a.cuda_stream for a in amb],
+             "in_ev": [e.cuda_event for e in self._in_ev], "out_ev": [e.cuda_event for e in self._out_ev],
              "comm": [cs.cuda_stream for cs in self.comm_streams],
              "seg": [[ex[r][0][k] for r in range(R)] for k in range(len(self.buckets))],
              "opt": [ex[r][1] for r in range(R)],

@@ -19,7 +19,8 @@
 #     network completing collectives at random delays and a hung collective for the stall
 #     inspector; csrc/tests/ps_protocol_test.cpp runs the PS service loop against 4 worker
 #     threads over one control segment (runtime/ps_protocol.h), whose plain mailbox / receive
-#     buffer traffic is ordered only by the protocol's release / acquire sequence numbers.
+#     buffer traffic is ordered only by the protocol's release / acquire sequence numbers;
+#     csrc/tests/launch_pool_test.cpp runs the graph group-launch pool (runtime/launch_pool.h).
 #     TSan uses ROCm's clang runtime: GCC 11's libtsan does not intercept
 #     pthread_cond_clockwait (std::condition_variable::wait_for) and reports a false "double lock".
 #
@@ -39,7 +40,7 @@ g++ -std=c++17 -O1 -g -fsanitize=thread -I csrc -I /opt/conda/include \
     csrc/tests/io_core_test.cpp "$OUT/lib/libjpeg.so.9" -Wl,-rpath,"$PWD/$OUT/lib" -lpthread -o "$OUT/io_core_tsan"
 TSAN_OPTIONS=halt_on_error=1 "$OUT/io_core_tsan"
 CLANG=${CLANG:-/opt/rocm/llvm/bin/clang++}
-for t in fusion_core comm_watch ps_protocol; do
+for t in fusion_core comm_watch ps_protocol launch_pool; do
   echo "== TSan: $t"
   "$CLANG" -std=c++17 -O1 -g -fsanitize=thread -I csrc "csrc/tests/${t}_test.cpp" -lpthread -o "$OUT/${t}_tsan"
   TSAN_OPTIONS=halt_on_error=1 "$OUT/${t}_tsan"

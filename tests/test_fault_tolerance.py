@@ -100,3 +100,18 @@ def test_native_comm_watchdog_core(tmp_path):
                    check=True, timeout=300)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "comm_watch_test: ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/llvm/bin/clang++"), reason="no clang (TSan runtime)")
+def test_native_launch_pool_under_tsan(tmp_path):
+    """runtime/launch_pool.h (the Mirrored graphed step's per-device launch threads) under
+    ThreadSanitizer: runs of changing width (late-joining workers never replay a finished run),
+    plain per-task writes read by the caller after run(), concurrent callers."""
+    exe = tmp_path / "lp"
+    subprocess.run(["/opt/rocm/llvm/bin/clang++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-I",
+                    os.path.join(ROOT, "csrc"), os.path.join(ROOT, "csrc", "tests", "launch_pool_test.cpp"),
+                    "-lpthread", "-o", str(exe)], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0 and "launch_pool_test: ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
