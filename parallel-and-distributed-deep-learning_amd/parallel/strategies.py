@@ -656,6 +656,7 @@ class _LocalReplicas:
                 self.graphs.append(g)
         self.comm_streams = [torch.cuda.Stream(device=d) for d in self.devices]
         self.evs = [[torch.cuda.Event() for _ in self.devices] for _ in self.buckets]
+        self._plan_cache = None   # (raw handles of the previous capture's graphs and events)
         # bf16 wire (cfg.grad_dtype, Horovod's fp16 compression analogue): each bucket is rounded
         # into a bf16 copy on the comm stream, all-reduced, and widened back into the fp32 grads
         self.lowp = None

@@ -213,6 +213,18 @@ def test_graphed_replicas_match_eager_replicas(monkeypatch, R, two):
         for p in ps[1:]:
             assert ((p - ps[0]).norm() / ps[0].norm()).item() < 1e-6   # replicas stay in sync
         out.append((losses, ps[0]))
+        if graphed and two == "auto":
+            # a batch-size change (the epoch's last partial batch) re-captures: the group launches
+            # must replay the new graphs, never the freed ones (the launch plan is rebuilt).
+            # (one-stream graphs only: re-capturing multi-branch ones is the runtime-fault trigger)
+            half = [im[: B // 2] for im in images], [lb[: B // 2] for lb in labels]
+            for _ in range(2):
+                assert torch.isfinite(lr.step(half[0], half[1], B // 2 * R)).all()
+            assert lr.graphs[0].B == B // 2
+            for _ in range(2):
+                assert torch.isfinite(lr.step(images, labels, B * R)).all()
+            torch.cuda.synchronize()
+            assert lr.graphs[0].B == B and all(o.iterations == 8 for _, o in lr.replicas)
     # (the weight-gradient atomics make runs differ in the last bits)
     for a, b in zip(out[0][0], out[1][0]):
         assert abs(a - b) <= 1e-3 * abs(a), (out[0][0], out[1][0])
