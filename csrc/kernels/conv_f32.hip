@@ -733,7 +733,10 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
 // (the atomic epilogue shrinks) lose -- {4, 2} 65.11, {4, 1} 69.63, {2, 3} 65.73; more win:
 // {8, 3} 63.27, {16, 3} 63.02, {4, 6} 63.14, {16, 6} 62.09, {24, 8} 62.24, {32, 12} 62.20.  The
 // kernels are MFMA-bound and the surplus workgroups keep every CU fed to the end of the launch.
-int g_wgrad_f32_wpc[2] = {16, 6};
+// Round 6, weight gradients on the side stream of the two-stream backward (models/engine_f32.py):
+// {16, 6} 58.34-58.50, {8, 4} 58.39-58.48, {4, 3} 58.95-58.99, {16, 3} 58.14-58.29 ms -- the
+// 128-wide ones now share the CUs with the data-gradient chain.
+int g_wgrad_f32_wpc[2] = {16, 3};
 const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream) {
   if (const char* e = check_f32(p)) return e;
   p.mg_howo = fdiv_magic(p.Ho * p.Wo);

@@ -2,7 +2,9 @@
 with no mixed-precision policy, imagenet-resnet50.py:56-62).
 
 HipF32Engine (frozen BN, the reference's `training=False`, Q3): the bf16 engine's explicit
-schedule (models/engine.py) in fp32 end to end -- no autograd, no PyTorch kernel in the step:
+schedule (models/engine.py) in fp32 end to end -- no autograd, no PyTorch kernel in the step;
+up to batch 1024 the weight gradients (and each block's finalize) run on a side stream while the
+data-gradient chain continues, over 5-deep gradient rings (b256: 61.9 -> 58.1-58.3 ms):
   forward  : stem_s2d (fp32 space-to-depth image) -> conv_f32 (4x4 window stem) -> maxpool_f32
              -> 16 bottleneck blocks of conv_f32 launches whose epilogues fold frozen BN + bias
              + residual + ReLU -> gap_f32 -> conv_f32 (Dense, bias epilogue)
@@ -26,6 +28,7 @@ import torch
 
 from ..ops.native import require_native
 from ..utils import profiling as prof
+from ..utils.envopts import opt
 from .engine import _BNG_FMT, _CRED_FMT, _FIN_FMT, _PREP_FMT, STEM_K
 from .resnet50 import BN_EPS, BN_MOMENTUM, ParamLayout
 
@@ -167,8 +170,17 @@ class HipF32Engine:
             outer = max(outer, B * H * H * b.cin, B * Ho * Ho * 4 * f)
             H = Ho
         self.H5 = H
-        self.gbuf = [torch.empty(outer, **f32), torch.empty(outer, **f32)]
-        self.g1buf, self.g2buf = torch.empty(inner, **f32), torch.empty(inner, **f32)
+        # two-stream backward (weight gradients on a side stream, HipF32Engine._side_run): the
+        # gradient buffers are rings deep enough for the data-gradient chain to run a few
+        # blocks ahead of the weight gradients still reading older ones
+        self.two_stream = self._two_stream_wanted(B)
+        D = opt("PDDL_ENGINE", "grad_ring", self.RING) if self.two_stream else 1
+        self.gbuf = [torch.empty(outer, **f32) for _ in range(max(2, D))]
+        self.g1bufs = [torch.empty(inner, **f32) for _ in range(D)]
+        self.g2bufs = [torch.empty(inner, **f32) for _ in range(D)]
+        self.g1buf, self.g2buf = self.g1bufs[0], self.g2bufs[0]
+        self.side = torch.cuda.Stream(dev) if self.two_stream and dev.type == "cuda" else None
+        self._evpool, self._evi = [], 0
         self.tmp = torch.empty(tmp, **f32)
         # blocks feeding a stride-2 projection block: their output gradient is written on the
         # stride-2 grid only (dgrad up2 scatter) into a buffer zeroed once here
@@ -209,6 +221,58 @@ class HipF32Engine:
         res = (offs, self._dev_table(rows), off, len(rows))
         self._cred[B] = res
         return res
+
+    # ------------------------------------------------------------------ two-stream backward
+    TWO_STREAM_MAX_BATCH = 1024
+    RING = 5   # (fp32 b256: ring 2 / 3 / 5 / 8 -> 59.9 / 59.3 / 58.4 / 58.5 ms; one stream 61.9)
+
+    def _two_stream_wanted(self, batch) -> bool:
+        ts = opt("PDDL_ENGINE", "two_stream", "auto")
+        if ts != "auto":
+            return ts == "1"
+        return batch <= self.TWO_STREAM_MAX_BATCH
+
+    def _event(self):
+        """The i-th fork / join event of every step reuses one pooled event (a wait binds to the
+        record made before it), so a step creates no HIP events."""
+        i = self._evi
+        self._evi += 1
+        if i == len(self._evpool):
+            self._evpool.append(torch.cuda.Event())
+        return self._evpool[i]
+
+    def _side_run(self, fn, *args, reads=()):
+        """fn(*args) on the side stream after everything enqueued on the compute stream so far;
+        `reads`: the gradient buffers it reads, which the compute stream must not overwrite
+        before it is done (_before_write)."""
+        if self.side is None:
+            fn(*args)
+            return
+        ev = self._event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            fn(*args)
+        done = self._event()
+        done.record(self.side)
+        for r in reads:
+            self._pending[r] = done
+        self._last_side = done
+
+    def _before_write(self, *bufs):
+        if self.side is None:
+            return
+        main = torch.cuda.current_stream(self.device)
+        for b in bufs:
+            ev = self._pending.pop(b, None)
+            if ev is not None:
+                main.wait_event(ev)
+
+    def _join_side(self):
+        if self.side is not None and self._last_side is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._last_side)
+            self._pending.clear()
+            self._last_side = None
 
     # ------------------------------------------------------------------ params
     def init(self, seed=0):
@@ -298,6 +362,7 @@ class HipF32Engine:
                 nb[0] += 1
 
         # ---- head
+        self._pending, self._last_side, self._evi = {}, None, 0
         pooled = self.pooled[:B]
         chd = self.ch["dense"]
         N.wgrad_f32(pooled.view(B, 1, 1, 2048), 1, 1, 1, 0, dl.view(B, 1, 1, ncls), self._gv("dense", ncls, 2048))
@@ -307,13 +372,18 @@ class HipF32Engine:
                    epi=EPI_PLAIN)
         e = L.entry("dense", "kernel")
         done_upto(e.offset + e.size)
-        cur = 0
         H5, bl = self.H5, L.blocks
         coffs, ctab, _, cn = self._colred(B)
         cp = self.colpart
+        D = len(self.g1bufs)
+        nbuf = len(self.gbuf)
 
         def part(layer):
             return cp[coffs[layer]:]
+        # weight gradients (+ each block's finalize) on the side stream, data gradients on the
+        # compute stream; ("g", i) / ("g1", j) / ("g2", j) / ("s2", bi): gradient buffers a side
+        # launch reads, which the compute stream waits for before overwriting
+        cur = 0
         gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
         N.gap_bwd_f32(dpooled, x5, gout, part(bl[-1].convs["3"].name))
         for bi in range(len(bl) - 1, -1, -1):
@@ -323,56 +393,68 @@ class HipF32Engine:
             f, cin = b.filters, b.cin
             x_in = self.acts[bl[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
             c1n, c2n, c3n = b.convs["1"].name, b.convs["2"].name, b.convs["3"].name
+            gkey = ("s2", bi) if bi in self.s2 else ("g", cur)
             gsrc = self.s2full[bi] if bi in self.s2 else self.gbuf[cur]
             gout = gsrc[: B * Ho * Ho * 4 * f].view(B, Ho, Ho, 4 * f)
-            g2 = self.g2buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
-            g1 = self.g1buf[: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            j = bi % D
+            g2 = self.g2bufs[j][: B * Ho * Ho * f].view(B, Ho, Ho, f)
+            g1 = self.g1bufs[j][: B * Ho * Ho * f].view(B, Ho, Ho, f)
             # conv3 (1x1) and conv2 (3x3): raw dW, then dgrad with the ReLU mask of their input
-            N.wgrad_f32(a["y2"], 1, 1, 1, 0, gout, self._gv(c3n, 4 * f, f))
+            self._side_run(N.wgrad_f32, a["y2"], 1, 1, 1, 0, gout, self._gv(c3n, 4 * f, f), reads=(gkey,))
+            self._before_write(("g2", j))
             self._conv(gout, 1, 1, 0, Ho, self._wd(c3n, f, 4 * f), g2, epi=EPI_DGRAD, mask=a["y2"],
                        colsum=part(c2n))
-            N.wgrad_f32(a["y1"], 3, 3, 1, 1, g2, self._gv(c2n, f, 9 * f))
+            self._side_run(N.wgrad_f32, a["y1"], 3, 3, 1, 1, g2, self._gv(c2n, f, 9 * f), reads=(("g2", j),))
+            self._before_write(("g1", j))
             self._conv(g2, 3, 1, 1, Ho, self._wd(c2n, f, 9 * f), g1, epi=EPI_DGRAD, mask=a["y1"],
                        colsum=part(c1n))
             # conv1 (+ conv0): input gradient of the block
-            nxt = 1 - cur
+            nxt = (cur + 1) % nbuf
             cs_in = part(bl[bi - 1].convs["3"].name) if bi > 0 else None
             if b.proj:
                 c0n = b.convs["0"].name
-                N.wgrad_f32(x_in, 1, 1, b.stride, 0, g1, self._gv(c1n, f, cin))
-                N.wgrad_f32(x_in, 1, 1, b.stride, 0, gout, self._gv(c0n, 4 * f, cin))
-                N.wgrad_finalize(self.params, self.grads, self._fin[b.name], 4, self.scale, self.dgr)
+                self._side_run(N.wgrad_f32, x_in, 1, 1, b.stride, 0, g1, self._gv(c1n, f, cin), reads=(("g1", j),))
+                self._side_run(N.wgrad_f32, x_in, 1, 1, b.stride, 0, gout, self._gv(c0n, 4 * f, cin), reads=(gkey,))
+                self._side_run(N.wgrad_finalize, self.params, self.grads, self._fin[b.name], 4, self.scale, self.dgr)
                 # dx = (W1'.g1 + W0'.gout) * mask: the first source into `tmp`, added by the second
                 tmp = self.tmp[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
                 self._conv(g1, 1, 1, 0, Ho, self._wd(c1n, cin, f), tmp, epi=EPI_PLAIN)
                 if b.stride == 2:
                     gx = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin)   # grid positions only
+                    self._before_write(("s2", bi - 1))
                     self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
                                mask=x_in, up2=1, colsum=cs_in)
                 else:
                     gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                    self._before_write(("g", nxt))
                     self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
                                mask=x_in, colsum=cs_in)
                 last = L.entry(c0n, "kernel")
             else:
-                N.wgrad_f32(x_in, 1, 1, 1, 0, g1, self._gv(c1n, f, cin))
-                N.wgrad_finalize(self.params, self.grads, self._fin[b.name], 3, self.scale, self.dgr)
+                self._side_run(N.wgrad_f32, x_in, 1, 1, 1, 0, g1, self._gv(c1n, f, cin), reads=(("g1", j),))
+                self._side_run(N.wgrad_finalize, self.params, self.grads, self._fin[b.name], 3, self.scale, self.dgr)
                 gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                self._before_write(("g", nxt))
                 self._conv(g1, 1, 1, 0, H, self._wd(c1n, cin, f), gx, epi=EPI_DGRAD, add=gout, mask=x_in,
                            colsum=cs_in)
                 last = L.entry(c1n, "kernel")
+            if bucket_cb is not None:
+                self._join_side()   # (a bucket's weight gradients come from the side stream)
             done_upto(last.offset + last.size)
             cur = nxt
         # ---- stem: max-pool backward (with conv1's ReLU mask), s2d-domain wgrad folded to 7x7x3
         H1, H2 = self.H1, self.H2
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
-        gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
+        gi = (cur + 1) % nbuf
+        gc1 = self.gbuf[gi][: B * H1 * H1 * 64].view(B, H1, H1, 64)
         s = L.stem
+        self._before_write(("g", gi))
         N.maxpool_bwd_f32(gpool, self.pidx[:B], self.c1[:B], gc1)
         N.colsum_f32(gc1.view(-1, 64), 64, self.colsum[self.ch[s.name]:])
-        N.wgrad_f32(self.x2[:B], 4, 4, 1, 0, gc1, self.stem_dw2)
-        N.stem_wgrad_fold(self.stem_dw2, self._gv(s.name, 64, 147), 64)
-        N.wgrad_finalize(self.params, self.grads, self._fin["stem"], 1, self.scale, self.dgr)
+        self._side_run(N.wgrad_f32, self.x2[:B], 4, 4, 1, 0, gc1, self.stem_dw2, reads=(("g", gi),))
+        self._side_run(N.stem_wgrad_fold, self.stem_dw2, self._gv(s.name, 64, 147), 64)
+        self._side_run(N.wgrad_finalize, self.params, self.grads, self._fin["stem"], 1, self.scale, self.dgr)
+        self._join_side()
         done_upto(L.kernels_end)
         N.colsum_reduce(cp, ctab, cn, self.colsum)
         N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
@@ -418,6 +500,9 @@ class HipF32EngineBNTrain(HipF32Engine):
     variant at the reference's precision (tests/test_gpu_f32.py bounds it against the PyTorch
     reference model in float64)."""
     BN_MODES = ("train",)
+
+    def _two_stream_wanted(self, batch) -> bool:
+        return False   # (its own backward schedule runs on one stream)
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: Optional[int] = None,
                  device="cuda", bn_mode: str = "train", num_classes: int = 1000):
