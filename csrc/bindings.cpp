@@ -63,9 +63,9 @@ void splitk_use(OptT ws) {
                              "split-K workspace: contiguous fp32 GPU tensor");
   tls_splitk = ws.has_value() ? *ws : Tensor();
 }
-int64_t splitk_default_floats(int64_t device) {   // the heuristic's bound: < 2 x (2 x #CUs) tiles of 16384 floats
+int64_t splitk_default_floats(int64_t device) {   // the heuristic's bound: tiles x slices < (fill + 2) x #CUs tiles of 16384 floats
   c10::hip::HIPGuardMasqueradingAsCUDA g((int)device);
-  return 4L * pddl::num_cus() * 16384;
+  return (long)(pddl::g_igemm_sk_fill + 2) * pddl::num_cus() * 16384;
 }
 
 // Generic implicit-GEMM (conv forward / dgrad / fp32 dense).
@@ -875,6 +875,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "wgrad1") pddl::g_wgrad1 = v;
     else if (which == "igemm_n64") pddl::g_igemm_n64 = v;
     else if (which == "igemm_splitk") pddl::g_igemm_splitk = v;
+    else if (which == "igemm_sk_fill") { TORCH_CHECK(v >= 1 && v <= 8, "igemm_sk_fill: 1-8"); pddl::g_igemm_sk_fill = v; }
+    else if (which == "igemm_sk_cap") { TORCH_CHECK(v >= 2 && v <= 16, "igemm_sk_cap: 2-16"); pddl::g_igemm_sk_cap = v; }
+    else if (which == "igemm_sk_elig") { TORCH_CHECK(v >= 1 && v <= 8, "igemm_sk_elig: 1-8"); pddl::g_igemm_sk_elig = v; }
     else if (which == "igemm_pk_all") pddl::g_igemm_pk_all = v;
     else if (which == "igemm_pk_dual") pddl::g_igemm_pk_dual = v;
     else if (which == "igemm_pk") { TORCH_CHECK(v == 0 || (v >= 2 && v <= 4), "igemm_pk: 0 or ring depth 2-4"); pddl::g_igemm_pk = v; }

@@ -908,11 +908,15 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring's trailing (zero) steps land before exit
 }
 
-// Split-K combine: one single-wave workgroup per 64x64 wave sub-tile (4 per output tile, so a
-// small-M layer's few tiles still spread over the chip: the combine is bound by how fast ONE
-// CU pulls its slabs) sums the `ksplit` fp32 partial tiles its slices left in the workspace
-// (same fragment order, so each lane reads 16-byte vectors of its own accumulator registers,
-// two slices' loads in flight at a time) and runs the unchanged fused epilogue on the sum.
+// Split-K combine: one 4-wave workgroup per 64x64 wave sub-tile (4 per output tile, so a
+// small-M layer's few tiles still spread over the chip), each wave owning one 16-column
+// fragment group: it sums that group's 4 fragments over the `ksplit` fp32 partial tiles its
+// slices left in the workspace (same fragment order: 16-byte vectors of the slices' own
+// accumulator registers, four slices' loads in flight) and runs the fused epilogue on its 64 x 16
+// columns.  (Round 6: the single-wave form -- one wave pulling all 16 fragments of every slice,
+// two slices in flight -- was bound by that one wave's memory-level parallelism: 493 us of the
+// 3.75 ms b32 step.  Here no LDS reduction is needed: the fragment groups are disjoint, and the
+// fused column sums still land as one partial row per 64-row wave tile.)
 // A separate launch instead of an in-launch last-arriver reduction (cdna_hip_programming §5,
 // "In-launch split-K reduction"): built and measured in round 6 -- each slice published its
 // 64 KiB partial with one agent-scope release and drew a ticket, the tile's last arriver summed
@@ -920,46 +924,46 @@ __global__ void __launch_bounds__(256, NB == 2 ? 2 : 1) igemm_pk_kernel(IgemmPar
 // are 4-8 x 64 KiB per tile (10x the guide's "few tens of KB"), so one workgroup's serial
 // read of them and the per-slice L2 write-back cost far more than the boundary saved.
 template <int BM, int BN>
-__global__ void __launch_bounds__(64) igemm_splitk_reduce_kernel(IgemmParams p) {
+__global__ void __launch_bounds__(256) igemm_splitk_reduce_kernel(IgemmParams p) {
   constexpr int NW = 4, WTM = 64, WTN = 64, TM = 4, TN = 4, WAVES_N = BN / WTN, F = TM * TN;
-  __shared__ __attribute__((aligned(16))) char smem[32 * (WTN + 4) * 4];
-  const int lane = threadIdx.x;
-  const int wave = blockIdx.x % NW;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  constexpr int EPI_LD = 16 + 4;
+  __shared__ __attribute__((aligned(16))) float smem[4][32 * EPI_LD];
+  const int lane = threadIdx.x & 63;
+  const int jw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // this wave's fragment column group
+  const int sub = blockIdx.x % NW;
+  const int wm = sub / WAVES_N, wn = sub % WAVES_N;
   const int nt = (p.Nn + BN - 1) / BN;
   const int tile = blockIdx.x / NW, tn = tile % nt, tm = tile / nt;
-  v4f acc[TM][TN];
+  v4f acc[TM][1];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  const float4* src = reinterpret_cast<const float4*>(p.slab) + ((long)tile * p.ksplit * NW + wave) * F * 64 + lane;
+  for (int i = 0; i < TM; ++i) acc[i][0] = v4f{0.f, 0.f, 0.f, 0.f};
+  // fragment f = i * TN + jw of slice sl
+  const float4* src = reinterpret_cast<const float4*>(p.slab) + ((long)tile * p.ksplit * NW + sub) * F * 64 + jw * 64 + lane;
   const long sstride = (long)NW * F * 64;
-  auto add = [&](const float4 (&v)[F]) {
+  auto add = [&](const float4 (&v)[TM]) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const float4 q = v[i * TN + j];
-        acc[i][j][0] += q.x; acc[i][j][1] += q.y; acc[i][j][2] += q.z; acc[i][j][3] += q.w;
-      }
+    for (int i = 0; i < TM; ++i) {
+      acc[i][0][0] += v[i].x; acc[i][0][1] += v[i].y; acc[i][0][2] += v[i].z; acc[i][0][3] += v[i].w;
+    }
   };
   int sl = 0;
-  for (; sl + 1 < p.ksplit; sl += 2) {
-    float4 v0[F], v1[F];
+  for (; sl + 3 < p.ksplit; sl += 4) {
+    float4 v[4][TM];
 #pragma unroll
-    for (int f = 0; f < F; ++f) { v0[f] = src[sl * sstride + f * 64]; v1[f] = src[(sl + 1) * sstride + f * 64]; }
-    add(v0);
-    add(v1);
-  }
-  if (sl < p.ksplit) {
-    float4 v0[F];
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-    for (int f = 0; f < F; ++f) v0[f] = src[sl * sstride + f * 64];
-    add(v0);
+      for (int i = 0; i < TM; ++i) v[u][i] = src[(sl + u) * sstride + i * TN * 64];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add(v[u]);
   }
-  igemm_epilogue<TM, TN, false>(p, acc, p.m_begin + tm * BM + wm * WTM, tn * BN + wn * WTN,
-                                p.prow_begin + tm * (BM / WTM) + wm, reinterpret_cast<float*>(smem), lane);
+  for (; sl < p.ksplit; ++sl) {
+    float4 v[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) v[i] = src[sl * sstride + i * TN * 64];
+    add(v);
+  }
+  igemm_epilogue<TM, 1, false>(p, acc, p.m_begin + tm * BM + wm * WTM, tn * BN + wn * WTN + jw * 16,
+                               p.prow_begin + tm * (BM / WTM) + wm, smem[jw], lane);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1272,6 +1276,9 @@ int num_cus() {
 struct IgemmPlan { int cfg, split, ks; };
 
 int g_igemm_splitk = 1;
+// Split-K plan knobs (igemm_sk_fill / _cap / _elig): slice workgroups aimed at fill x #CUs, at
+// most cap slices, and only problems with elig x tiles <= #CUs (plus the long-K exception).
+int g_igemm_sk_fill = 2, g_igemm_sk_cap = 8, g_igemm_sk_elig = 2;
 int g_igemm_pk = 2;        // persistent ring kernel (igemm_pk_kernel) for the short-K 1x1 layers:
                            // 0 off, else the ring depth NB (2: two 68 KiB blocks per CU; 3, 4: one
                            // 128 KiB+ block per CU, measured 5-7 % slower end to end)
@@ -1297,12 +1304,12 @@ static int igemm_splitk_slices(int M, int Nn, int K, int cfg) {
   // is long enough that the slab round trip is a few % of the layer (b256 crop 160: the stage-5
   // 3x3 runs 200 tiles = 200 lone 4-wave blocks on 256 CUs at 340 TF/s unsplit).
   const long C = num_cus();
-  const long target = 2L * C;
+  const long target = (long)g_igemm_sk_fill * C;
   if (KT < 8) return 1;
-  if (2 * T > C && !(T < target && KT >= 32)) return 1;
+  if ((long)g_igemm_sk_elig * T > C && !(T < target && KT >= 32)) return 1;
   long ks = (target + T - 1) / T;
   if (ks > KT / 4) ks = KT / 4;
-  if (ks > 8) ks = 8;   // (a cap of 4 measured +0.5 %, 2 +7 % on the b32 step, round 6)
+  if (ks > g_igemm_sk_cap) ks = g_igemm_sk_cap;   // (a cap of 4 measured +0.5 %, 2 +7 % on the b32 step, round 6)
   return ks >= 2 ? (int)ks : 1;
 }
 
@@ -1443,8 +1450,8 @@ const char* igemm_launch(const IgemmParams& p_in, hipStream_t stream) {
     const int BM = igemm_bm(pl.cfg), BN = pl.cfg == 0 ? 64 : 128;
     const int tiles = ((p.M + BM - 1) / BM) * ((p.Nn + BN - 1) / BN);
     igemm_launch_cfg(p, pl.cfg, stream);
-    if (pl.cfg == 0) hipLaunchKernelGGL((igemm_splitk_reduce_kernel<256, 64>), dim3(tiles * 4), dim3(64), 0, stream, p);
-    else hipLaunchKernelGGL((igemm_splitk_reduce_kernel<128, 128>), dim3(tiles * 4), dim3(64), 0, stream, p);
+    if (pl.cfg == 0) hipLaunchKernelGGL((igemm_splitk_reduce_kernel<256, 64>), dim3(tiles * 4), dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((igemm_splitk_reduce_kernel<128, 128>), dim3(tiles * 4), dim3(256), 0, stream, p);
   } else if (pl.split < p.M) {
     IgemmParams head = p, tail = p;
     head.M = pl.split;

@@ -57,6 +57,7 @@ long igemm_splitk_floats(int M, int Nn, int K);     // split-K workspace a probl
 extern int g_igemm8, g_igemm8_min_tiles, g_igemm8_min_n, g_igemm_ns1_kt, g_wgrad8, g_wgrad1;
 int num_cus();   // compute units of the current device (cached)
 extern int g_wgrad_f32_wpc[2];
+extern int g_igemm_sk_fill, g_igemm_sk_cap, g_igemm_sk_elig;   // split-K plan knobs (igemm.hip)
 extern int g_igemm_splitk, g_wgrad8_min_rows, g_igemm_pk, g_igemm_pk_all, g_igemm_pk_dual;   // split-K: 0 off, 1 heuristic (default), >= 2 forced slices (where legal)
 extern int g_stem_variant, g_igemm_n64, g_igemm_variant, g_igemm_deep, g_igemm_pf, g_bn_red_blocks, g_bn_apply_blocks, g_pool_blocks, g_colred_chunks;   // tuning knobs (A/B timing)
 
