@@ -76,9 +76,14 @@ class HipEngine:
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: int = 224,
                  device="cuda", bn_mode: str = "frozen", num_classes: int = 1000, bitmask: Optional[bool] = None,
-                 grad_ring: Optional[int] = None, graphed: bool = False):
+                 grad_ring: Optional[int] = None, graphed=False):
         self._grad_ring = grad_ring   # None: GRAD_RING_SMALL at batches <= 64, else GRAD_RING
-        self.graphed = graphed        # steps replay from HIP graphs: one stream (see TWO_STREAM_MAX_BATCH)
+        # graphed: steps replay from HIP graphs -- True: one stream (see TWO_STREAM_MAX_BATCH);
+        # "segmented": bucket-segmented graphs (train/graph.py SegmentedStepGraphs) with the weight
+        # gradients deferred into a single-stream SIDE graph per segment (see _side_run)
+        self.graphed = bool(graphed)
+        self.defer_side = graphed == "segmented" and bool(opt(E, "seg_side", True)) and self.TWO_STREAM_OK
+        self._defer = None            # capture-time list of deferred side-stream closures
         if bn_mode not in self.BN_MODES:
             raise ValueError(f"{type(self).__name__} runs bn_mode in {self.BN_MODES}, not {bn_mode!r} "
                              "(use make_hip_engine)")
@@ -320,6 +325,11 @@ class HipEngine:
         # (set before _alloc_acts runs; the subclasses' engines keep one stream)
         ring0 = self._grad_ring or (self.GRAD_RING_SMALL if B <= 64 else self.GRAD_RING)
         ring = opt(E, "grad_ring", ring0) if self._two_stream_wanted(B) else 1
+        # deferred side graphs read a segment's data gradients while the next segment runs: no
+        # gradient buffer is reused within a step (one per block, + head and stem)
+        deep = self.defer_side and self._two_stream_wanted(B)
+        if deep:
+            ring = len(L.blocks) + 2
         self.gbuf = [torch.empty(outer, **bf) for _ in range(max(2, ring))]
         self.g1bufs = [torch.empty(inner, **bf) for _ in range(ring)]
         self.g2bufs = [torch.empty(inner, **bf) for _ in range(ring)]
@@ -333,6 +343,7 @@ class HipEngine:
             gc = max(gc, B * Hc * Hc * 4 * b.filters)
             g2c = max(g2c, B * Hc * Hc * b.filters)
         self.gcbuf = torch.empty(gc, **bf)
+        self.gcbufs = {bi: torch.empty(gc, **bf) for bi in self._s2_fed()} if deep else None
         # full-resolution output gradient of those blocks, zeroed ONCE: the downsampling block's
         # dgrad writes only the stride-2 grid positions (up2 = 2), the off-grid zeros persist
         self.s2full = {}
@@ -343,6 +354,7 @@ class HipEngine:
         self.s2g2full = {bi: torch.zeros(B * self.geo[L.blocks[bi].name][1] ** 2 * L.blocks[bi].filters, **bf)
                          for bi in self._s2_fed()}   # (same for their conv2-output gradient)
         self.g2cbuf = torch.empty(g2c, **bf)
+        self.g2cbufs = {bi: torch.empty(g2c, **bf) for bi in self._s2_fed()} if deep else None
         self.pooled = torch.empty(B, 2048, **bf)
         self.logits = torch.empty(B, self.num_classes, dtype=torch.float32, device=dev)
         self.dlogits = torch.zeros(B, self.ncls_pad, **bf)
@@ -600,7 +612,7 @@ class HipEngine:
         ts = opt(E, "two_stream", "auto")
         if ts != "auto":
             return self.TWO_STREAM_OK and ts == "1"
-        return self.TWO_STREAM_OK and batch <= self.TWO_STREAM_MAX_BATCH and not self.graphed
+        return self.TWO_STREAM_OK and batch <= self.TWO_STREAM_MAX_BATCH and (not self.graphed or self.defer_side)
 
     def _event(self):
         """The next fork/join event of this step, from a pool the engine owns for its whole
@@ -616,7 +628,17 @@ class HipEngine:
     def _side_run(self, fn, *args, reads=()):
         """Launch a weight-gradient kernel on the side stream, ordered after everything enqueued
         on the compute stream so far; `reads` names the gradient buffers it reads, which the
-        compute stream must not overwrite before it is done (see _before_write)."""
+        compute stream must not overwrite before it is done (see _before_write).
+
+        Deferred (a segmented capture, begin_defer): the call is queued instead, and the capture
+        records the queue of each segment as a single-stream side graph that the replay runs
+        after that segment's main graph, concurrently with the next segment.  No fork / join
+        events inside any graph (the runtime launches single-stream graphs from pre-built packets;
+        its multi-branch launch path faults: train/graph.py replay_stream), and no buffer hazards:
+        the deferred engine's gradient buffers are never reused within a step (_alloc_acts)."""
+        if self._defer is not None:
+            self._defer.append((fn, args))
+            return
         if self.side is None:
             fn(*args)
             return
@@ -635,7 +657,7 @@ class HipEngine:
     def _before_write(self, *bufs):
         """The compute stream is about to overwrite these gradient buffers: wait for the side
         stream's last reader of each."""
-        if self.side is None:
+        if self.side is None or self._defer is not None:
             return
         main = torch.cuda.current_stream(self.device)
         for b in bufs:
@@ -648,7 +670,7 @@ class HipEngine:
         side stream first waits for the compute stream and the callback runs with the SIDE stream
         current -- whatever it enqueues or records (an all-reduce, an optimizer update) is
         ordered after both, and the compute stream never blocks on the side stream."""
-        if self.side is None:
+        if self.side is None or self._defer is not None:
             cb(i)
             return
         if getattr(cb, "needs_join", False):   # (e.g. a graph capture cut at the bucket boundary)
@@ -663,6 +685,19 @@ class HipEngine:
         done = self._event()
         done.record(self.side)
         self._last_side = done
+
+    def begin_defer(self):
+        """Queue side-stream work from now on (segmented capture; take_deferred drains it)."""
+        assert self.side is not None and self.defer_side
+        self._defer = []
+
+    def take_deferred(self):
+        q, self._defer = self._defer, []
+        return q
+
+    def end_defer(self):
+        left, self._defer = self._defer, None
+        assert not left, "deferred side work left uncaptured"
 
     def _join_side(self):
         if self.side is None or self._last_side is None:
@@ -752,8 +787,8 @@ class HipEngine:
                 # gout is zero off the stride-2 grid (the next block reads only even rows /
                 # columns); its compact copy `gc` came from that block's dgrad epilogue
                 Hc = Ho // 2 + Ho % 2
-                gc = self.gcbuf[: B * Hc * Hc * 4 * f].view(B, Hc, Hc, 4 * f)
-                g2c = self.g2cbuf[: B * Hc * Hc * f].view(B, Hc, Hc, f)
+                gc = (self.gcbufs[bi] if self.gcbufs else self.gcbuf)[: B * Hc * Hc * 4 * f].view(B, Hc, Hc, 4 * f)
+                g2c = (self.g2cbufs[bi] if self.g2cbufs else self.g2cbuf)[: B * Hc * Hc * f].view(B, Hc, Hc, f)
                 if self._bwd_fused_s2(bi, b, s2):   # one read of gc: data + weight gradient
                     self._before_write(g2_n, "g2c")
                     N.bwd1x1(gc, y2, self._wdv(c3n, f, 4 * f), y2m, g2, part(c2n), self._gview(c3n, 4 * f, f), g2c)
@@ -804,7 +839,7 @@ class HipEngine:
                   self._fin_rows_n[b.name])
                 gxc, up2 = None, 1 if b.stride == 2 else 0
                 if bi - 1 in s2:   # compact copy for the previous block's stride-2-grid passes
-                    gxc = self.gcbuf[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
+                    gxc = (self.gcbufs[bi - 1] if self.gcbufs else self.gcbuf)[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
                     # grid positions only, into the pre-zeroed full-resolution buffer (saves the
                     # 3/4 zero-fill writes: conv3_block1 c1 dgrad 942 -> 681 us at b1024)
                     gx = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin)
@@ -849,7 +884,10 @@ class HipEngine:
         self._join_side()
         done_upto(L.kernels_end)
         N.colsum_reduce(cp, ctab, cn, self.colsum)
-        N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
+        # (deferred: after the finalizes that wrote dgr, in the last side graph, which waits for
+        # the main graph holding colsum_reduce)
+        (W if self._defer is not None else (lambda f, *a: f(*a)))(
+            N.bn_grad, self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
         prof.pop()
         if bucket_cb is not None:
             while nb[0] < len(bks):

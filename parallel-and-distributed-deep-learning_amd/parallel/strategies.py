@@ -71,13 +71,14 @@ def gpu_available() -> bool:
     return torch.cuda.is_available() and torch.cuda.device_count() > 0
 
 
-def build_engine(cfg, device: torch.device, cap: int, graphed: Optional[bool] = None):
+def build_engine(cfg, device: torch.device, cap: int, graphed=None):
     """On a GPU: the bf16 HIP engine (bf16 MFMA kernels; frozen or train-mode BN), or for
     precision=fp32 the reference-precision engine on the fp32-MFMA HIP convolutions
     (models/engine_f32.py).  On CPU: the fp32 PyTorch reference engine (config 1 of
     BASELINE.json: CPU plumbing).  graphed (default: cfg.graphs is True): the step will replay
     from HIP graphs, which keep the shallower gradient rings (HipEngine.GRAD_RING) and stay on
-    one stream (HipEngine.TWO_STREAM_MAX_BATCH)."""
+    one stream (HipEngine.TWO_STREAM_MAX_BATCH); "segmented": bucket-segmented graphs whose
+    weight gradients replay as a side graph per segment (HipEngine._side_run)."""
     L = ParamLayout(cfg.num_classes)
     if device.type == "cuda" and cfg.precision == "bf16":
         from ..models.engine import HipEngine, make_hip_engine
@@ -562,7 +563,11 @@ class _LocalReplicas:
         self.augs = []
         # (several replicas / ranks replay graphed segments unless --no-graphs; one replica in the
         # whole job runs eager unless --graphs)
-        graphed = cfg.graphs is True or (cfg.graphs is None and not self._single_replica_job())
+        single = self._single_replica_job()
+        graphed = cfg.graphs is True or (cfg.graphs is None and not single)
+        # (segmented replica graphs defer their weight gradients into side graphs; a one-replica
+        # job's --graphs whole-step graph stays one stream: GraphedTrainStep captures no side graphs)
+        graphed = ("segmented" if not single else True) if graphed else False
         for i, d in enumerate(self.devices):
             if d.type == "cuda":
                 torch.cuda.set_device(d)
@@ -656,6 +661,10 @@ class _LocalReplicas:
                 self.graphs.append(g)
         self.comm_streams = [torch.cuda.Stream(device=d) for d in self.devices]
         self.evs = [[torch.cuda.Event() for _ in self.devices] for _ in self.buckets]
+        # deferred replicas: segment k's side graph runs on the engine's side stream after segment
+        # k; bucket k's all-reduce waits for it (sevs[k])
+        self.deferred = all(g.deferred for g in self.graphs)
+        self.sevs = [[torch.cuda.Event() for _ in self.devices] for _ in self.buckets] if self.deferred else None
         self._plan_cache = None   # (raw handles of the previous capture's graphs and events)
         # bf16 wire (cfg.grad_dtype, Horovod's fp16 compression analogue): each bucket is rounded
         # into a bf16 copy on the comm stream, all-reduced, and widened back into the fp32 grads
@@ -705,14 +714,19 @@ class _LocalReplicas:
         streams = P["comm"]
         tl = self.tl
         par = P["parallel"]
+        dfr = self.deferred
         for k, (s, e) in enumerate(self.buckets):
             first = k == 0
+            # segment k (main graph); with deferred replicas its end forks to the side stream,
+            # whose graph k then forks to the comm stream
             N.graph_launch_group(P["dev"], P["seg"][k], P["cur"], P["in_ev"] if first else [],
-                                 P["amb"] if first else [], P["ev"][k], P["comm"], par)
+                                 P["amb"] if first else [], P["ev"][k], P["sides"] if dfr else P["comm"], par)
+            if dfr:
+                N.graph_launch_group(P["dev"], P["side"][k], P["sides"], [], [], P["sev"][k], P["comm"], par)
             if first and tl is not None:
                 tl["t0"].record(cur[0])
             if tl is not None:
-                tl["b"][k][0].record(cur[0])
+                tl["b"][k][0].record(self.replicas[0][0].side if dfr else cur[0])
                 tl["b"][k][1].record(self.comm_streams[0])
             if self.lowp is None:
                 self.comm.all_reduce_on([gr[s:e] for gr in grads], "sum", streams, f"bucket {k} all_reduce")
@@ -749,6 +763,8 @@ class _LocalReplicas:
             with torch.cuda.device(self.devices[r]):
                 for k in range(len(self.buckets)):
                     self.evs[k][r].record(cur[r])
+                    if self.deferred:
+                        self.sevs[k][r].record(self.replicas[r][0].side)
                 self._cdone[r].record(self.comm_streams[r])
                 self._in_ev[r].record(amb[r])
                 self._out_ev[r].record(cur[r])
@@ -761,10 +777,14 @@ class _LocalReplicas:
              "opt": [ex[r][1] for r in range(R)],
              "ev": [[self.evs[k][r].cuda_event for r in range(R)] for k in range(len(self.buckets))],
              "cdone": [e.cuda_event for e in self._cdone],
-             # (the launch pool runs one-stream graphs only: graph_launch.cpp; PDDL_MIRROR
-             # pool=0 keeps every launch in this thread)
+             # (the launch pool runs one-stream graphs only: graph_launch.cpp -- deferred replicas'
+             # main and side graphs are; PDDL_MIRROR pool=0 keeps every launch in this thread)
              "parallel": (opt("PDDL_MIRROR", "pool", True)
-                          and all(e.side is None for e, _ in self.replicas))}
+                          and (self.deferred or all(e.side is None for e, _ in self.replicas)))}
+        if self.deferred:
+            P["sides"] = [e.side.cuda_stream for e, _ in self.replicas]
+            P["side"] = [[ex[r][2][k] for r in range(R)] for k in range(len(self.buckets))]
+            P["sev"] = [[self.sevs[k][r].cuda_event for r in range(R)] for k in range(len(self.buckets))]
         self._plan_cache = (key, P)
         return P
 

@@ -168,6 +168,7 @@ class SegmentedStepGraphs(GraphedTrainStep):
         super().__init__(engine, optimizer, batch, image_hw, gscale, image_dtype, with_optimizer=False)
         self.buckets = list(buckets)
         self.segments = []
+        self.side_segments = []          # deferred engines: segment k's weight-gradient graph (or None)
         self.opt_graph: Optional[torch.cuda.CUDAGraph] = None
         self.two_stream = two_stream
         self.keep_graph = keep_graph     # (diagnostics: keep the hipGraph_t for node queries)
@@ -190,6 +191,11 @@ class SegmentedStepGraphs(GraphedTrainStep):
         # two_stream=False forces the single-stream schedule.
         if getattr(eng, "side", None) is not None and self.two_stream is False:
             eng.side = None
+        # A deferring engine (HipEngine graphed="segmented") queues its side-stream work during the
+        # capture; each cut records the queue as a single-stream side graph on the engine's side
+        # stream: the replay launches segment k, then side k (after segment k, concurrently with
+        # segment k + 1), and bucket k's all-reduce after side k.
+        self.deferred = getattr(eng, "side", None) is not None and getattr(eng, "defer_side", False)
         opt.sync_hparams()
         torch.cuda.synchronize(dev)
         # as torch.cuda.graph does: collect garbage now, and none while capturing
@@ -208,6 +214,9 @@ class SegmentedStepGraphs(GraphedTrainStep):
         segs = []         # segs[i]: the graph ending with bucket i, None when bucket i completed
         live = []         # at the same point as bucket i-1 (nothing captured in between)
         pool = []
+        sides = []        # deferred engines: sides[i] the side graph of segment i (None: no side work)
+        deferred = self.deferred
+        mark = torch.zeros(1, device=dev) if deferred else None
 
         def begin():
             g = _new_graph(keep_graph=self.keep_graph)
@@ -215,17 +224,33 @@ class SegmentedStepGraphs(GraphedTrainStep):
             live.append(g)
 
         def cut(i):
+            q = eng.take_deferred() if deferred else []
             if _capture_is_empty():
-                segs.append(None)          # (an empty capture cannot end: it stays open for i+1)
-                if i == nb - 1:
+                if not q and i < nb - 1:
+                    segs.append(None)      # (an empty capture cannot end: it stays open for i+1)
+                    sides.append(None)
+                    return
+                if not deferred:
                     raise RuntimeError("segmented capture: the last bucket captured no work")
-                return
+                mark.zero_()               # (one tiny node, so the segment can end and order its side graph)
             live[-1].capture_end()
             if not pool:                   # (pool() exists once a capture has ended)
                 pool.append(live[-1].pool())
             segs.append(live[-1])
             if self.probe is not None:
                 self.probe(len(segs) - 1, segs[-1])
+            if deferred:
+                sg = None
+                if q:
+                    sg = _new_graph(keep_graph=self.keep_graph)
+                    with torch.cuda.stream(eng.side):
+                        sg.capture_begin(pool=pool[0], capture_error_mode=CAPTURE_MODE)
+                        try:
+                            for fn, args in q:
+                                fn(*args)
+                        finally:
+                            sg.capture_end()
+                sides.append(sg)
             if i < nb - 1:
                 begin()
         cut.needs_join = True   # (a two-stream engine joins its side stream before each cut)
@@ -233,8 +258,12 @@ class SegmentedStepGraphs(GraphedTrainStep):
         with torch.cuda.device(dev):
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(torch.cuda.current_stream(dev))
+            if deferred:
+                eng.side.wait_stream(s)
             with torch.cuda.stream(s):
                 begin()
+                if deferred:
+                    eng.begin_defer()
                 try:
                     self.stats = eng.forward_backward(self.images, self.labels, self.gscale, flip=self.flip,
                                                       crop_offset=self.crop, bucket_cb=cut, buckets=self.buckets)
@@ -251,12 +280,17 @@ class SegmentedStepGraphs(GraphedTrainStep):
                             live[-1].capture_end()
                         except Exception:
                             pass
+                    if deferred:
+                        eng._defer = None      # (back to launching: the capture is abandoned)
                     raise
+                if deferred:
+                    eng.end_defer()
             torch.cuda.current_stream(dev).wait_stream(s)
         if len(segs) != nb:
             raise RuntimeError(f"segmented capture produced {len(segs)} segments for {nb} buckets")
         opt._iterations = it        # capture ran no kernels: training state did not advance
         self.segments = segs
+        self.side_segments = sides if deferred else [None] * nb
         self.opt_graph = og
 
     def load(self, images, labels, flip=None, crop_offset=(0, 0)):
@@ -265,13 +299,20 @@ class SegmentedStepGraphs(GraphedTrainStep):
     def replay_segment(self, k: int):
         if self.segments[k] is not None:
             _launch(self.segments[k])
+        if self.side_segments[k] is not None:   # (after segment k, on the engine's side stream)
+            amb = torch.cuda.current_stream()
+            side = self.engine.side
+            side.wait_stream(amb)
+            _replay(self.side_segments[k], side)
+            amb.wait_stream(side)
 
     def exec_handles(self):
         """([segment k's raw executable, 0 if empty], the optimizer graph's): what the Mirrored
         driver's native group launch replays (sync_hparams / the iteration count stay with the
         caller, as in replay_optimizer)."""
         return ([g.raw_cuda_graph_exec() if g is not None else 0 for g in self.segments],
-                self.opt_graph.raw_cuda_graph_exec())
+                self.opt_graph.raw_cuda_graph_exec(),
+                [g.raw_cuda_graph_exec() if g is not None else 0 for g in self.side_segments])
 
     def replay_optimizer(self):
         self.opt.sync_hparams()

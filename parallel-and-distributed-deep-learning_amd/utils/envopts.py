@@ -28,6 +28,7 @@ KEYS: Dict[str, Dict[str, str]] = {
         "bitmask": "1: ReLU masks as 1-bit masks (0: re-read the bf16 activation)",
         "grad_ring": "gradient buffers per kind of the two-stream backward (default 16 at b <= 64, else 5)",
         "two_stream": "auto: weight gradients on a side stream up to batch 1024; 1 / 0 force",
+        "seg_side": "segmented graphs (Mirrored replicas): weight gradients in a side graph per segment (1, default) or one stream (0)",
     },
     "PDDL_PS": {
         "impl": "native: shm + HIP-IPC data plane (csrc/runtime/ps_service.cpp); c10d: process-group fallback",

@@ -22,11 +22,11 @@ def _inputs(steps, B, hw, seed=21):
     return img, lab, flip
 
 
-def _engine(crop, B):
+def _engine(crop, B, graphed=False):
     from pddl.models.engine import HipEngine
     from pddl.models.resnet50 import ParamLayout
     from pddl.train.optim import make_optimizer
-    eng = HipEngine(ParamLayout(), B, crop=crop, image_size=224)
+    eng = HipEngine(ParamLayout(), B, crop=crop, image_size=224, graphed=graphed)
     eng.init(seed=13)
     return eng, make_optimizer("adam", eng, lr=1e-3)
 
@@ -98,25 +98,35 @@ def test_whole_engine_graph_capture_at_reference_batch(monkeypatch, crop, c64):
 
 
 def test_segmented_single_stream_matches_two_stream():
-    """The segmented replica graphs with the side stream (default) and with the single-stream
-    schedule (two_stream=False) replay the same gradient."""
+    """The segmented replica graphs with the side stream forked inside each segment, with the
+    single-stream schedule (two_stream=False) and with the weight gradients deferred into one
+    single-stream side graph per segment (the Mirrored replicas' default, HipEngine
+    graphed="segmented") replay the same gradient -- incl. the BN / bias gradients the last side
+    graph's bn_grad writes."""
     from pddl.train.graph import SegmentedStepGraphs
     B = 32
     img, lab, flip = _inputs(1, B, 224, seed=4)
     out = []
-    for two in (None, False):
-        eng, opt = _engine(224, B)
+    for mode in ("forked", "one", "deferred"):
+        eng, opt = _engine(224, B, graphed="segmented" if mode == "deferred" else False)
         bks = eng.L.buckets(25.0)
         eng.forward_backward(img[0], lab[0], 1.0 / B, flip=flip[0], buckets=bks)
-        sg = SegmentedStepGraphs(eng, opt, B, (224, 224), 1.0 / B, bks, two_stream=two)
+        sg = SegmentedStepGraphs(eng, opt, B, (224, 224), 1.0 / B, bks, two_stream=False if mode == "one" else None)
         sg.capture()
-        assert (eng.side is not None) == (two is None)
+        assert (eng.side is not None) == (mode != "one")
+        assert sg.deferred == (mode == "deferred")
+        if sg.deferred:
+            assert len(sg.side_segments) == len(bks) and any(x is not None for x in sg.side_segments)
+            assert eng._defer is None
         sg.load(img[0], lab[0], flip[0], (0, 0))
         for k in range(len(bks)):
             sg.replay_segment(k)
         torch.cuda.synchronize()
         out.append(eng.grads.clone())
-    r = ((out[0] - out[1]).norm() / out[1].norm()).item()
+    for o in out[:2]:
+        r = ((o - out[1]).norm() / out[1].norm()).item()
+        assert r < 1e-4, r
+    r = ((out[2] - out[1]).norm() / out[1].norm()).item()
     assert r < 1e-4, r
 
 

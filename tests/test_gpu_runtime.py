@@ -152,7 +152,8 @@ def test_mirrored_graphed_step_matches_eager(monkeypatch, segmented):
         if graphs and segmented:
             g = st.mirror.graphs[0]
             assert g.captured and len(g.segments) == len(st.mirror.buckets) >= 2
-            assert st.engine.side is None         # (graphed engines run one stream: HipEngine)
+            # (the weight gradients replay as a side graph per segment: HipEngine._side_run)
+            assert g.deferred and any(x is not None for x in g.side_segments)
             assert st.mirror.comm.watchdog_state()["issued"] >= 2 * len(st.mirror.buckets)
         elif graphs:
             assert st.mirror.graphs is None and st.mirror._whole.graph is not None
@@ -184,14 +185,15 @@ class _SumComm:
         pass
 
 
-@pytest.mark.parametrize("R,two", [(2, "auto"), (3, "auto"), (2, "1")])
-def test_graphed_replicas_match_eager_replicas(monkeypatch, R, two):
+@pytest.mark.parametrize("R,side", [(2, "1"), (3, "1"), (2, "0")])
+def test_graphed_replicas_match_eager_replicas(monkeypatch, R, side):
     """R graphed replicas (segments, events and comm-stream waits issued by one native group
     launch per phase) train like R eager replicas: R replicas on device 0, each with its own
-    launch stream, gradients summed per bucket on the comm streams.  two "auto": the graphed
-    engines run one stream (HipEngine); "1": the two-stream segments."""
+    launch stream, gradients summed per bucket on the comm streams.  side "1" (default): each
+    segment's weight gradients replay as a single-stream side graph after it, concurrently with
+    the next segment (HipEngine._side_run deferred); "0": one stream."""
     from pddl.parallel.strategies import _LocalReplicas
-    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "two_stream", two))
+    monkeypatch.setenv("PDDL_ENGINE", with_opt("PDDL_ENGINE", "seg_side", side))
     B = 8
     g = torch.Generator(device="cuda").manual_seed(3)
     images = [torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device="cuda", generator=g) for _ in range(R)]
@@ -207,16 +209,17 @@ def test_graphed_replicas_match_eager_replicas(monkeypatch, R, two):
         torch.cuda.synchronize()
         if graphed:
             assert len(lr.graphs) == R and len(lr.buckets) >= 2
-            assert (lr.replicas[0][0].side is not None) == (two == "1")
+            assert lr.deferred == (side == "1")
+            assert all(any(x is not None for x in g.side_segments) == (side == "1") for g in lr.graphs)
         assert all(o.iterations == 4 for _, o in lr.replicas)
         ps = [e.params.clone() for e, _ in lr.replicas]
         for p in ps[1:]:
             assert ((p - ps[0]).norm() / ps[0].norm()).item() < 1e-6   # replicas stay in sync
         out.append((losses, ps[0]))
-        if graphed and two == "auto":
+        if graphed:
             # a batch-size change (the epoch's last partial batch) re-captures: the group launches
             # must replay the new graphs, never the freed ones (the launch plan is rebuilt).
-            # (one-stream graphs only: re-capturing multi-branch ones is the runtime-fault trigger)
+            # (every graph is single-stream: re-capturing multi-branch ones is the runtime-fault trigger)
             half = [im[: B // 2] for im in images], [lb[: B // 2] for lb in labels]
             for _ in range(2):
                 assert torch.isfinite(lr.step(half[0], half[1], B // 2 * R)).all()
