@@ -63,7 +63,11 @@ class HipEngine:
     # in the table, SIGSEGV at +0xaee41) on the first launch of a fresh multi-branch executable
     # once the process has created, replayed and destroyed replica graphs: deterministic in-process
     # repro in profiles/r6_graph_repro.txt.  Cost where the branches paid: segmented Mirrored
-    # b256 12.95 vs 12.2 ms (b32: 4.45 one stream vs 4.85-5.00 two, eager 4.36).
+    # b256 12.95 vs 12.2 ms (b32: 4.45 one stream vs 4.85-5.00 two, eager 4.36).  The segmented
+    # replica graphs (graphed="segmented") get the overlap back without branches: each segment's
+    # weight gradients become a single-stream SIDE graph replayed on the side stream after the
+    # segment, concurrently with the next one (b32 -15.5 % -> -4 % of eager, b256 -3 %:
+    # profiles/r6_mirror_seg_side.txt).
     GRAD_RING = 5           # two-stream: gradient buffers per kind, so the data-gradient chain can run
                             # up to four blocks ahead of the weight gradients still reading older ones
                             # (b32: 3 -> 5 buffers 4.21 -> 4.17 ms eager, 4.17 -> 4.05 ms graphed)
