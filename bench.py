@@ -352,7 +352,8 @@ def run(args):
         "horovod": "horovod-style 1 proc/GPU, native FusionEngine: RCCL bucketed all-reduce overlapped with backward",
         "single": "single process, whole step replayed as one HIP graph",
         "mirrored": (f"mirrored: 1 process x {args.gpus} GPUs, ncclCommInitAll, grouped bucket all-reduce"
-                     + (" between per-device HIP-graph segments" if getattr(st, "mirror", None) is not None
+                     + (" between per-device HIP-graph segments (weight gradients as per-segment side graphs)"
+                        if getattr(st, "mirror", None) is not None
                         and st.mirror.graph_mode else "")
                      if not (getattr(st, "mirror", None) is not None and st.mirror.graph_mode
                              and st.mirror._single_replica_job())
