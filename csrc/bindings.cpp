@@ -674,11 +674,12 @@ void softmax_xent(Tensor logits, Tensor labels, int64_t ncls, double gscale, Ten
      "softmax_xent");
 }
 void prep(Tensor params, Tensor table, int64_t nlayers, int64_t max_elems, Tensor wbf, Tensor scale, Tensor shift,
-          double eps) {
+          double eps, int64_t parts) {
   PCHECK(table.is_cuda() && table.scalar_type() == torch::kUInt8, "prep table");
   PCHECK(table.numel() == nlayers * (int64_t)sizeof(pddl::PrepLayer), "prep table size");
+  PCHECK(parts >= 1 && parts <= 3, "prep: parts 1 (forward), 2 (dgrad) or 3 (both)");
   ok(pddl::prep_launch(f32p(params), reinterpret_cast<const pddl::PrepLayer*>(table.data_ptr()), (int)nlayers,
-                       (int)max_elems, bfpm(wbf), f32p(scale), f32p(shift), (float)eps, cur_stream()),
+                       (int)max_elems, bfpm(wbf), f32p(scale), f32p(shift), (float)eps, cur_stream(), (int)parts),
      "prep");
 }
 void prep_fuse(Tensor params, Tensor table, int64_t nlayers, int64_t max_elems, Tensor wbf, Tensor scale, Tensor shift,
@@ -916,7 +917,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("maxpool_bwd_partial_rows", &pddl::maxpool_bwd_partial_rows);
   m.attr("COLRED_LAYER_BYTES") = (int)sizeof(pddl::ColRedLayer);
-  m.def("prep", &prep, REL);
+  m.def("prep", &prep, REL, py::arg("params"), py::arg("table"), py::arg("nlayers"), py::arg("max_elems"),
+        py::arg("wbf"), py::arg("scale"), py::arg("shift"), py::arg("eps"), py::arg("parts") = 3);
   m.def("prep_fuse", &prep_fuse, REL);
   m.def("wgrad_finalize", &wgrad_finalize, REL, py::arg("params"), py::arg("grads"), py::arg("table"),
         py::arg("nlayers"), py::arg("scale"), py::arg("dgamma_raw"), py::arg("max_cout") = 2048);

@@ -927,12 +927,16 @@ const char* prep_fuse_launch(const float* params, const FuseLayer* layers_dev, i
 }
 
 const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems, uint16_t* wbf,
-                        float* scale, float* shift, float eps, hipStream_t s) {
+                        float* scale, float* shift, float eps, hipStream_t s, int parts) {
+  // parts: bit 0 the forward weights + folded affine, bit 1 the dgrad weights (independent
+  // passes over the master: the engine may run the second on its side stream, under the forward)
   int gx = (max_elems / 4 + 255) / 256;
   if (gx > 512) gx = 512;
-  hipLaunchKernelGGL(prep_kernel<uint16_t>, dim3(gx, nlayers), dim3(256), 0, s, params, layers_dev, wbf, scale, shift,
-                     eps);
-  hipLaunchKernelGGL(prep_dgrad_kernel<uint16_t>, dim3(576, nlayers), dim3(256), 0, s, params, layers_dev, wbf, eps);
+  if (parts & 1)
+    hipLaunchKernelGGL(prep_kernel<uint16_t>, dim3(gx, nlayers), dim3(256), 0, s, params, layers_dev, wbf, scale, shift,
+                       eps);
+  if (parts & 2)
+    hipLaunchKernelGGL(prep_dgrad_kernel<uint16_t>, dim3(576, nlayers), dim3(256), 0, s, params, layers_dev, wbf, eps);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? nullptr : hipGetErrorString(e);
 }

@@ -276,7 +276,7 @@ const char* prep_fuse_launch(const float* params, const FuseLayer* layers_dev, i
 const char* prep_f32_launch(const float* params, const PrepLayer* layers_dev, int nlayers, float* wf32, float* scale,
                             float* shift, float eps, hipStream_t s);   // fp32 stem s2d + dgrad weights
 const char* prep_launch(const float* params, const PrepLayer* layers_dev, int nlayers, int max_elems,
-                        uint16_t* wbf, float* scale, float* shift, float eps, hipStream_t s);
+                        uint16_t* wbf, float* scale, float* shift, float eps, hipStream_t s, int parts = 3);
 
 // dW finalize: dgamma_raw[c] = sum_k W[c,k] * dWraw[c,k]; dW[c,k] *= a[c] (in place).
 struct FinLayer {

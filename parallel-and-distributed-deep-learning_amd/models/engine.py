@@ -175,6 +175,7 @@ class HipEngine:
         self.side = torch.cuda.Stream(dev) if self.two_stream and dev.type == "cuda" else None
         self._pending, self._last_side = {}, None
         self._evpool, self._evi = [], 0   # fork/join events (see _event)
+        self._prep_evs, self._dgrad_ready = None, None   # (after_update's dgrad-weight fork)
 
     # ------------------------------------------------------------------ tables
     def _build_weight_tables(self):
@@ -440,9 +441,26 @@ class HipEngine:
         self.after_update()
 
     def after_update(self):
-        """Refresh bf16 forward / dgrad weights and folded BN affine from the fp32 master."""
-        self.N.prep(self.params, self._prep_tab, self._prep_n, self._prep_max, self.wbf, self.scale, self.shift,
-                    BN_EPS)
+        """Refresh bf16 forward / dgrad weights and folded BN affine from the fp32 master.  With a
+        side stream (eager steps), the dgrad weights are prepared there, under the next forward;
+        the backward waits for them before its first data gradient (b32: 43 us off the step)."""
+        side = self.side
+        if side is None or self._defer is not None or torch.cuda.is_current_stream_capturing():
+            self.N.prep(self.params, self._prep_tab, self._prep_n, self._prep_max, self.wbf, self.scale, self.shift,
+                        BN_EPS)
+        else:
+            self.N.prep(self.params, self._prep_tab, self._prep_n, self._prep_max, self.wbf, self.scale, self.shift,
+                        BN_EPS, parts=1)
+            if self._prep_evs is None:
+                self._prep_evs = (torch.cuda.Event(), torch.cuda.Event())
+            fork, done = self._prep_evs
+            fork.record(torch.cuda.current_stream(self.device))
+            side.wait_event(fork)
+            with torch.cuda.stream(side):
+                self.N.prep(self.params, self._prep_tab, self._prep_n, self._prep_max, self.wbf, self.scale,
+                            self.shift, BN_EPS, parts=2)
+            done.record(side)
+            self._dgrad_ready = done
         if self.fuse_proj and self._fuse_n:
             self.N.prep_fuse(self.params, self._fuse_tab, self._fuse_n, self._fuse_max, self.wbf, self.scale,
                              self.shift, BN_EPS)
@@ -727,6 +745,10 @@ class HipEngine:
         logits = self.logits[:B]
         dl = self.dlogits[:B]
         N.softmax_xent(logits, lab, self.num_classes, float(gscale), dl, self.stats[0:1], self.stats[1:2])
+        if self._dgrad_ready is not None:   # the dgrad weights after_update prepared on the side stream
+            if not torch.cuda.is_current_stream_capturing():   # (a capture starts synchronized)
+                torch.cuda.current_stream(self.device).wait_event(self._dgrad_ready)
+            self._dgrad_ready = None
 
         # bucket readiness tracking (kernels region is filled in layout order)
         bks = buckets if buckets is not None else []
