@@ -907,9 +907,11 @@ class HipEngine:
             W(N.stem_wgrad_fold, self.stem_dw2, self._gview(s.name, 64, 147), 64)
         W(N.wgrad_finalize, self.params, self.grads, self._fin_tabs["stem"], 1, self.scale, self.dgr,
           self._fin_rows_n["stem"])
+        # (the column-sum fold reads only what the compute stream wrote: it runs under the side
+        # stream's last weight gradients, before the join)
+        N.colsum_reduce(cp, ctab, cn, self.colsum)
         self._join_side()
         done_upto(L.kernels_end)
-        N.colsum_reduce(cp, ctab, cn, self.colsum)
         # (deferred: after the finalizes that wrote dgr, in the last side graph, which waits for
         # the main graph holding colsum_reduce)
         (W if self._defer is not None else (lambda f, *a: f(*a)))(

@@ -454,9 +454,9 @@ class HipF32Engine:
         self._side_run(N.wgrad_f32, self.x2[:B], 4, 4, 1, 0, gc1, self.stem_dw2, reads=(("g", gi),))
         self._side_run(N.stem_wgrad_fold, self.stem_dw2, self._gv(s.name, 64, 147), 64)
         self._side_run(N.wgrad_finalize, self.params, self.grads, self._fin["stem"], 1, self.scale, self.dgr)
+        N.colsum_reduce(cp, ctab, cn, self.colsum)   # (compute-stream data only: under the side stream's tail)
         self._join_side()
         done_upto(L.kernels_end)
-        N.colsum_reduce(cp, ctab, cn, self.colsum)
         N.bn_grad(self.params, self.grads, self._bng_tab, self._bng_n, self.colsum, self.dgr, self.scale, BN_EPS)
         prof.pop()
         if bucket_cb is not None:
