@@ -494,15 +494,12 @@ class HipF32EngineBNTrain(HipF32Engine):
       backward, per conv : (the next conv's dgrad applies the ReLU mask of y and adds the
                            residual gradient) -> bn_bwd_reduce (sum g, sum g*(z - mean))
                            -> bn_bwd_apply (dz; dgamma, dbeta, dbias = 0) -> wgrad_f32(x, dz)
-                           and the conv_f32 dgrad of dz; a projection block's BN3 and BN0 share
-                           one reduce and one apply (same gradient).
+                           (on the side stream, as in HipF32Engine) and the conv_f32 dgrad of dz;
+                           a projection block's BN3 and BN0 share one reduce and one apply.
     The reference itself freezes BN (imagenet-resnet50.py:57): this is the `--bn-mode train`
     variant at the reference's precision (tests/test_gpu_f32.py bounds it against the PyTorch
     reference model in float64)."""
     BN_MODES = ("train",)
-
-    def _two_stream_wanted(self, batch) -> bool:
-        return False   # (its own backward schedule runs on one stream)
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: Optional[int] = None,
                  device="cuda", bn_mode: str = "train", num_classes: int = 1000):
@@ -567,7 +564,9 @@ class HipF32EngineBNTrain(HipF32Engine):
             if b.proj:
                 z["0"] = torch.empty(B, Ho, Ho, 4 * f, **f32)
             self.z[b.name] = z
-        self.gbuf3 = torch.empty_like(self.gbuf[0])
+        # dz3 of each block: a ring like the other gradient buffers (the side stream's conv3
+        # weight gradient reads it while the compute stream runs ahead)
+        self.gbuf3s = [torch.empty_like(self.gbuf[0]) for _ in range(len(self.g1bufs))]
 
     # ------------------------------------------------------------------ forward
     def _chs(self, arr, c):
@@ -674,6 +673,7 @@ class HipF32EngineBNTrain(HipF32Engine):
                 nb[0] += 1
 
         # ---- head: Dense wgrad, bias gradient (column sums), dgrad into the pooled features
+        self._pending, self._last_side, self._evi = {}, None, 0
         pooled = self.pooled[:B]
         chd = self.ch["dense"]
         N.wgrad_f32(pooled.view(B, 1, 1, 2048), 1, 1, 1, 0, dl.view(B, 1, 1, ncls), self._gv("dense", ncls, 2048))
@@ -686,8 +686,13 @@ class HipF32EngineBNTrain(HipF32Engine):
         done_upto(e.offset + e.size)
         cur = 0
         H5, bl = self.H5, L.blocks
+        D, nbuf = len(self.g1bufs), len(self.gbuf)
+        W = self._side_run
         gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
         N.gap_bwd_f32(dpooled, x5, gout, None)
+        # weight gradients on the side stream (HipF32Engine._side_run), BN backward and data
+        # gradients on the compute stream; ("g", i) / ("s2", bi) / ("z3", j) / ("g2", j) / ("g1", j):
+        # gradient buffers a side launch reads, waited for before the compute stream rewrites them
         for bi in range(len(bl) - 1, -1, -1):
             b = bl[bi]
             a = {k: v[:B] for k, v in self.acts[b.name].items()}
@@ -697,53 +702,66 @@ class HipF32EngineBNTrain(HipF32Engine):
             f, cin = b.filters, b.cin
             x_in = self.acts[bl[bi - 1].name]["out"][:B] if bi > 0 else self.pool[:B]
             c1c, c2c, c3c = b.convs["1"], b.convs["2"], b.convs["3"]
+            gkey = ("s2", bi) if bi in self.s2 else ("g", cur)
             gsrc = self.s2full[bi] if bi in self.s2 else self.gbuf[cur]
             gout = gsrc[: M * 4 * f].view(B, Ho, Ho, 4 * f)
-            dz3 = self.gbuf3[: M * 4 * f].view(B, Ho, Ho, 4 * f)
+            j = bi % D
+            dz3 = self.gbuf3s[j][: M * 4 * f].view(B, Ho, Ho, 4 * f)
+            self._before_write(("z3", j))
             if b.proj:   # BN3 and the shortcut's BN0 share gout; dz0 overwrites gout in place
                 self._bn_bwd(gout, z["3"], c3c, M, dz3, z["0"], b.convs["0"], gout)
             else:
                 self._bn_bwd(gout, z["3"], c3c, M, dz3)
-            g2 = self.g2buf[: M * f].view(B, Ho, Ho, f)
-            g1 = self.g1buf[: M * f].view(B, Ho, Ho, f)
-            N.wgrad_f32(a["y2"], 1, 1, 1, 0, dz3, self._gv(c3c.name, 4 * f, f))
+            g2 = self.g2bufs[j][: M * f].view(B, Ho, Ho, f)
+            g1 = self.g1bufs[j][: M * f].view(B, Ho, Ho, f)
+            W(N.wgrad_f32, a["y2"], 1, 1, 1, 0, dz3, self._gv(c3c.name, 4 * f, f), reads=(("z3", j),))
+            self._before_write(("g2", j))
             self._conv(dz3, 1, 1, 0, Ho, self._wd(c3c.name, f, 4 * f), g2, epi=EPI_DGRAD, mask=a["y2"])
             self._bn_bwd(g2, z["2"], c2c, M, g2)
-            N.wgrad_f32(a["y1"], 3, 3, 1, 1, g2, self._gv(c2c.name, f, 9 * f))
+            W(N.wgrad_f32, a["y1"], 3, 3, 1, 1, g2, self._gv(c2c.name, f, 9 * f), reads=(("g2", j),))
+            self._before_write(("g1", j))
             self._conv(g2, 3, 1, 1, Ho, self._wd(c2c.name, f, 9 * f), g1, epi=EPI_DGRAD, mask=a["y1"])
             self._bn_bwd(g1, z["1"], c1c, M, g1)
-            nxt = 1 - cur
+            nxt = (cur + 1) % nbuf
             if b.proj:
                 c0n = b.convs["0"].name
-                N.wgrad_f32(x_in, 1, 1, b.stride, 0, g1, self._gv(c1c.name, f, cin))
-                N.wgrad_f32(x_in, 1, 1, b.stride, 0, gout, self._gv(c0n, 4 * f, cin))
+                W(N.wgrad_f32, x_in, 1, 1, b.stride, 0, g1, self._gv(c1c.name, f, cin), reads=(("g1", j),))
+                W(N.wgrad_f32, x_in, 1, 1, b.stride, 0, gout, self._gv(c0n, 4 * f, cin), reads=(gkey,))
                 tmp = self.tmp[: B * Ho * Ho * cin].view(B, Ho, Ho, cin)
                 self._conv(g1, 1, 1, 0, Ho, self._wd(c1c.name, cin, f), tmp, epi=EPI_PLAIN)
                 if b.stride == 2:
                     gx = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin)   # grid positions only
+                    self._before_write(("s2", bi - 1))
                     self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
                                mask=x_in, up2=1)
                 else:
                     gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                    self._before_write(("g", nxt))
                     self._conv(gout, 1, 1, 0, Ho, self._wd(c0n, cin, 4 * f), gx, epi=EPI_DGRAD, add=tmp,
                                mask=x_in)
                 last = L.entry(c0n, "kernel")
             else:
-                N.wgrad_f32(x_in, 1, 1, 1, 0, g1, self._gv(c1c.name, f, cin))
+                W(N.wgrad_f32, x_in, 1, 1, 1, 0, g1, self._gv(c1c.name, f, cin), reads=(("g1", j),))
                 gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+                self._before_write(("g", nxt))
                 self._conv(g1, 1, 1, 0, H, self._wd(c1c.name, cin, f), gx, epi=EPI_DGRAD, add=gout, mask=x_in)
                 last = L.entry(c1c.name, "kernel")
+            if bucket_cb is not None:
+                self._join_side()   # (a bucket's weight gradients come from the side stream)
             done_upto(last.offset + last.size)
             cur = nxt
         # ---- stem: max-pool backward with conv1's ReLU mask, the stem BN, s2d-domain wgrad
         H1, H2 = self.H1, self.H2
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
-        gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
+        gi = (cur + 1) % nbuf
+        gc1 = self.gbuf[gi][: B * H1 * H1 * 64].view(B, H1, H1, 64)
         s = L.stem
+        self._before_write(("g", gi))
         N.maxpool_bwd_f32(gpool, self.pidx[:B], self.c1[:B], gc1)
         self._bn_bwd(gc1, self.zs[:B], s, B * H1 * H1, gc1)
-        N.wgrad_f32(self.x2[:B], 4, 4, 1, 0, gc1, self.stem_dw2)
-        N.stem_wgrad_fold(self.stem_dw2, self._gv(s.name, 64, 147), 64)
+        W(N.wgrad_f32, self.x2[:B], 4, 4, 1, 0, gc1, self.stem_dw2, reads=(("g", gi),))
+        W(N.stem_wgrad_fold, self.stem_dw2, self._gv(s.name, 64, 147), 64)
+        self._join_side()
         done_upto(L.kernels_end)
         prof.pop()
         if bucket_cb is not None:
