@@ -51,6 +51,7 @@ class HipEngine:
     FUSE_BWD_OK = True      # stage-2/3 conv3 backward: dgrad + wgrad in one launch (bwd1x1.hip)
     FUSE_STEM_OK = True     # stem conv + BN + ReLU + max-pool forward in one launch (stem.hip)
     TWO_STREAM_OK = True
+    DEFER_OK = True         # segmented graphs may defer the side work into side graphs (_side_run)
     C64_OK = True           # stage-2 3x3 convs on the row-tile kernels (conv3x3c64.hip)
     C64_MIN_M = 262144      # ... from 4 x 256 CUs x 256-pixel tiles up (b >= 84 at 56 x 56)
     C3C1_OK = True          # stage-2 boundaries: conv3 + next conv1 fused (c3c1.hip)
@@ -86,7 +87,8 @@ class HipEngine:
         # "segmented": bucket-segmented graphs (train/graph.py SegmentedStepGraphs) with the weight
         # gradients deferred into a single-stream SIDE graph per segment (see _side_run)
         self.graphed = bool(graphed)
-        self.defer_side = graphed == "segmented" and bool(opt(E, "seg_side", True)) and self.TWO_STREAM_OK
+        self.defer_side = (graphed == "segmented" and bool(opt(E, "seg_side", True)) and self.TWO_STREAM_OK
+                           and self.DEFER_OK)
         self._defer = None            # capture-time list of deferred side-stream closures
         if bn_mode not in self.BN_MODES:
             raise ValueError(f"{type(self).__name__} runs bn_mode in {self.BN_MODES}, not {bn_mode!r} "

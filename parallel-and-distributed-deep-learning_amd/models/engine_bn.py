@@ -38,7 +38,9 @@ class HipEngineBNTrain(HipEngine):
     FUSE_BWD_OK = False    # (its conv3 dgrad carries the fused BN-backward sums)
     FUSE_PROJ_OK = False   # (batch statistics: the shortcut's BN cannot be folded into weights)
     FUSE_STEM_OK = False   # (conv1's batch statistics need its raw output)
-    TWO_STREAM_OK = False  # (its own backward schedule runs on one stream)
+    # weight gradients on the side stream up to TWO_STREAM_MAX_BATCH (eager steps; its graphed
+    # steps keep one stream: no deferred side graphs for this schedule)
+    DEFER_OK = False
     C64_OK = False         # (train-mode BN needs the batch statistics from the conv epilogue)
     C3C1_OK = False
     S2C_OK = False
@@ -161,7 +163,8 @@ class HipEngineBNTrain(HipEngine):
             if b.proj:
                 z["0"] = torch.empty(B, Ho, Ho, 4 * f, **bf)
             self.z[b.name] = z
-        self.gbuf3 = torch.empty_like(self.gbuf[0])
+        # dz3 of each block, a ring like the other gradient buffers (two-stream backward)
+        self.gbuf3s = [torch.empty_like(self.gbuf[0]) for _ in range(len(self.g1bufs))]
         self._stat_cache = {}
         self.partial = torch.empty(self._launch_tables(B)["_max_part"], dtype=torch.float32, device=dev)
 
@@ -300,12 +303,17 @@ class HipEngineBNTrain(HipEngine):
         logits = self.logits[:B]
         dl = self.dlogits[:B]
         N.softmax_xent(logits, lab, self.num_classes, float(gscale), dl, self.stats[0:1], self.stats[1:2])
+        if self._dgrad_ready is not None:   # the dgrad weights after_update prepared on the side stream
+            torch.cuda.current_stream(self.device).wait_event(self._dgrad_ready)
+            self._dgrad_ready = None
+        self._pending, self._last_side = {}, None
+        self._evi = 0
         bks = buckets if buckets is not None else []
         nb = [0]
 
         def done_upto(off):
             while bucket_cb is not None and nb[0] < len(bks) - 1 and bks[nb[0]][1] <= off:
-                bucket_cb(nb[0])
+                self._bucket_ready(bucket_cb, nb[0])
                 nb[0] += 1
 
         # ---- head (as the frozen engine)
@@ -324,9 +332,14 @@ class HipEngineBNTrain(HipEngine):
         cur = 0
         H5 = self.H5
         blocks = L.blocks
+        D, nbuf = len(self.g1bufs), len(self.gbuf)
+        W = self._side_run
         gout = self.gbuf[cur][: B * H5 * H5 * 2048].view(B, H5, H5, 2048)
         N.gap_bwd(dpooled, x5, gout, None)
         s2 = self._s2_fed()
+        # weight gradients on the side stream (HipEngine._side_run), BN backward and data gradients
+        # on the compute stream; ("g", i) / ("s2", bi) / ("z3", j) / ("g2", j) / ("g1", j): gradient
+        # buffers a side launch reads, waited for before the compute stream rewrites them
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
             a = self.acts[b.name]
@@ -341,34 +354,47 @@ class HipEngineBNTrain(HipEngine):
                 mask_in = self.bits[blocks[bi - 1].name]["out"][:B] if bi > 0 else self.pool_bits[:B]
                 y1m, y2m = self.bits[b.name]["y1"][:B], self.bits[b.name]["y2"][:B]
             y1, y2 = a["y1"][:B], a["y2"][:B]
+            gkey = ("s2", bi) if bi in s2 else ("g", cur)
             gout = (self.s2full[bi] if bi in s2 else self.gbuf[cur])[: M * 4 * f].view(B, Ho, Ho, 4 * f)
-            dz3 = self.gbuf3[: M * 4 * f].view(B, Ho, Ho, 4 * f)
+            j = bi % D
+            dz3 = self.gbuf3s[j][: M * 4 * f].view(B, Ho, Ho, 4 * f)
             c1c, c2c, c3c = b.convs["1"], b.convs["2"], b.convs["3"]
+            self._before_write(("z3", j))
             if b.proj:   # BN3 and the shortcut BN0 share gout; dz0 overwrites gout in place
                 self._bn_bwd(gout, z["3"], c3c, M, dz3, z["0"], b.convs["0"], gout)
             else:
                 self._bn_bwd(gout, z["3"], c3c, M, dz3)
             # conv3
-            N.wgrad(y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, dz3, None, 0, self._gview(c3c.name, 4 * f, f), f, 0)
-            g2 = self.g2buf[: M * f].view(B, Ho, Ho, f)
+            W(N.wgrad, y2, Ho, Ho, 1, 1, 1, 0, Ho, Ho, dz3, None, 0, self._gview(c3c.name, 4 * f, f), f, 0,
+              reads=(("z3", j),))
+            g2 = self.g2bufs[j][: M * f].view(B, Ho, Ho, f)
+            self._before_write(("g2", j))
             self._dgrad_bn_bwd(dz3, Ho, 1, 0, self._wdv(c3c.name, f, 4 * f), y2m, g2, z["2"], c2c, M)
             # conv2 (3x3)
-            N.wgrad(y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2c.name, f, 9 * f), 9 * f, 0)
-            g1 = self.g1buf[: M * f].view(B, Ho, Ho, f)
+            W(N.wgrad, y1, Ho, Ho, 3, 3, 1, 1, Ho, Ho, g2, None, 0, self._gview(c2c.name, f, 9 * f), 9 * f, 0,
+              reads=(("g2", j),))
+            g1 = self.g1bufs[j][: M * f].view(B, Ho, Ho, f)
+            self._before_write(("g1", j))
             self._dgrad_bn_bwd(g2, Ho, 3, 1, self._wdv(c2c.name, f, 9 * f), y1m, g1, z["1"], c1c, M)
             # conv1 (+ conv0)
-            nxt = 1 - cur
+            nxt = (cur + 1) % nbuf
             gx = self.gbuf[nxt][: B * H * H * cin].view(B, H, H, cin)
+            gx_key = ("g", nxt)
             if b.proj:
-                N.wgrad(x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1c.name, 5 * f, cin), cin, 0)
+                W(N.wgrad, x_in, H, H, 1, 1, b.stride, 0, Ho, Ho, g1, gout, f, self._gview(c1c.name, 5 * f, cin), cin, 0,
+                  reads=(("g1", j), gkey))
                 up2 = 1 if b.stride == 2 else 0
                 if bi - 1 in s2:   # grid positions only, into the pre-zeroed full-resolution buffer
                     gx, up2 = self.s2full[bi - 1][: B * H * H * cin].view(B, H, H, cin), 2
+                    gx_key = ("s2", bi - 1)
+                self._before_write(gx_key)
                 N.igemm(g1, gout, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1c.name, cin, 5 * f), 1, None, None, None,
                         mask_in, None, gx, 0, None, 0, 0, up2, H, H, None, None)
                 last = L.entry(b.convs["0"].name, "kernel")
             else:
-                N.wgrad(x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1c.name, f, cin), cin, 0)
+                W(N.wgrad, x_in, H, H, 1, 1, 1, 0, Ho, Ho, g1, None, 0, self._gview(c1c.name, f, cin), cin, 0,
+                  reads=(("g1", j),))
+                self._before_write(gx_key)
                 N.igemm(g1, None, Ho, Ho, 1, 1, 1, 0, Ho, Ho, self._wdv(c1c.name, cin, f), 1, None, None, None,
                         mask_in, gout, gx, 0, None, 0, 0, 0, 0, 0, None, None)
                 last = L.entry(c1c.name, "kernel")
@@ -377,16 +403,20 @@ class HipEngineBNTrain(HipEngine):
         # ---- stem
         H1, H2, Hs = self.H1, self.H2, self.Hs
         gpool = self.gbuf[cur][: B * H2 * H2 * 64].view(B, H2, H2, 64)
-        gc1 = self.gbuf[1 - cur][: B * H1 * H1 * 64].view(B, H1, H1, 64)
+        gi = (cur + 1) % nbuf
+        gc1 = self.gbuf[gi][: B * H1 * H1 * 64].view(B, H1, H1, 64)
         s = L.stem
+        self._before_write(("g", gi))
         N.maxpool_bwd(gpool, self.pidx[:B], None, gc1, None)
         self._bn_bwd(gc1, self.zs[:B], s, B * H1 * H1, gc1)
-        N.wgrad(self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0)
-        N.stem_wgrad_fold(self.stem_dw2, self._gview(s.name, 64, 147), 64)
+        W(N.wgrad, self.stem_x2[:B], Hs, Hs, 4, 4, 1, 0, H1, H1, gc1, None, 0, self.stem_dw2, STEM_K, 0,
+          reads=(("g", gi),))
+        W(N.stem_wgrad_fold, self.stem_dw2, self._gview(s.name, 64, 147), 64)
+        self._join_side()
         done_upto(L.kernels_end)
         prof.pop()
         if bucket_cb is not None:
             while nb[0] < len(bks):
-                bucket_cb(nb[0])
+                self._bucket_ready(bucket_cb, nb[0])
                 nb[0] += 1
         return self.stats
