@@ -78,7 +78,8 @@ def parse(argv=None):
     # (profiles/r3_batch_plateau.txt); after the fused kernels b2048 26.16-26.17k vs b2560
     # 26.57-26.58k on one box (profiles/r3_b2560_ab.txt: the ~4.4 ms per-step fixed cost
     # amortised further).  b2675+ would exceed 2^31 elements in conv1's output.
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 2560; fp32 256; CPU 32)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (default 2560; train-mode BN 1024; fp32 256; CPU 32)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--crop", type=int, default=None, help="network input (default = image size)")
     ap.add_argument("--optimizer", default="adam", choices=["adam", "sgd"])
@@ -106,7 +107,10 @@ def parse(argv=None):
                          "rank dumps its stacks and the job exits non-zero")
     args = ap.parse_args(argv)
     if args.batch is None:
-        args.batch = 32 if args.device == "cpu" else (256 if args.precision == "fp32" else 2560)
+        # (train-mode BN keeps every pre-BN activation: at 2560 they pass the kernels' 2^31-element
+        # tensor bound, so its default is the largest power-of-two batch under it)
+        args.batch = 32 if args.device == "cpu" else (256 if args.precision == "fp32" else
+                                                      1024 if args.bn_mode == "train" else 2560)
     if args.crop is None:
         args.crop = args.image_size
     if args.timeout is None:
