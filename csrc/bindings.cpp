@@ -338,6 +338,14 @@ int64_t bwd1x1_partial_rows(int64_t M, int64_t CO, int64_t CI) {
 }
 
 // fp32 convolution (reference precision): y[N,Ho,Wo,Cout] = conv(x[N,H,W,C], w[Cout, R*S*C]) (+ bias)
+// the calling engine's split-K workspace (splitk_use) for the fp32 conv launcher's small-M slices
+static void f32_splitk(pddl::ConvF32Params& p, const Tensor& x) {
+  if (tls_splitk.defined() && tls_splitk.device() == x.device()) {
+    p.slab = tls_splitk.data_ptr<float>();
+    p.slab_floats = tls_splitk.numel();
+  }
+}
+
 void conv_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tensor w, OptT bias, Tensor y) {
   pddl::ConvF32Params p{};
   PCHECK(x.is_contiguous() && x.dim() == 4 && w.is_contiguous() && y.is_contiguous() && y.dim() == 4,
@@ -351,6 +359,7 @@ void conv_f32(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, Tenso
   PCHECK(y.size(3) == p.Cout && p.K == p.R * p.S * p.C, "conv_f32: weight shape");
   if (bias.has_value()) { PCHECK(bias->numel() == p.Cout, "conv_f32: bias"); p.bias = f32p(*bias); }
   p.y = f32p(y);
+  f32_splitk(p, x);
   ok(pddl::conv_f32_launch(p, cur_stream()), "conv_f32");
 }
 
@@ -406,6 +415,7 @@ void conv_f32_epi(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, i
     p.colsum = f32p(*colsum);
   }
   p.y = f32p(y);
+  f32_splitk(p, x);
   ok(pddl::conv_f32_launch(p, cur_stream()), "conv_f32_epi");
 }
 
@@ -885,6 +895,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "wgrad8_min_rows") { TORCH_CHECK(v >= 64, "wgrad8_min_rows"); pddl::g_wgrad8_min_rows = v; }
     else if (which == "stem") pddl::g_stem_variant = v;
     else if (which == "conv_f32") pddl::g_conv_f32_variant = v;
+    else if (which == "conv_f32_splitk") pddl::g_conv_f32_splitk = v;
     else if (which == "wgrad_f32_wpc64") { TORCH_CHECK(v >= 1 && v <= 32, "wgrad_f32_wpc64"); pddl::g_wgrad_f32_wpc[0] = v; }
     else if (which == "wgrad_f32_wpc128") { TORCH_CHECK(v >= 1 && v <= 32, "wgrad_f32_wpc128"); pddl::g_wgrad_f32_wpc[1] = v; }
     else if (which == "c64_grid") pddl::g_c64_grid = v;

@@ -363,6 +363,10 @@ __device__ __forceinline__ float4 f32_read16(const char* p) {
 }  // namespace
 
 template <int BN>
+__device__ __forceinline__ void f32_big_epilogue(const ConvF32Params& p, v4f (&acc)[4][BN / 32], int m0, int n0,
+                                                 int tm, char* smem);
+
+template <int BN>
 __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
   constexpr int A_CH = G_BM * 16, B_CH = BN * 16;   // bytes of one 16-byte chunk column
   constexpr int B_BASE = 4 * A_CH, STAGE = 4 * (A_CH + B_CH);
@@ -375,8 +379,10 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int mt = (p.M + G_BM - 1) / G_BM, nt = (p.Cout + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, mt * nt);
-  const int tn = wg % nt, tm = wg / nt;
+  const int ks = p.ksplit > 1 ? p.ksplit : 1;   // split-K: slice `slice` of the tile's K steps
+  const int wg = xcd_remap(blockIdx.x, mt * nt * ks);
+  const int tile = wg % (mt * nt), slice = wg / (mt * nt);
+  const int tn = tile % nt, tm = tile / nt;
   const int m0 = tm * G_BM, n0 = tn * BN;
   const int HoWo = p.Ho * p.Wo;
   // descriptors: A from the first image of the tile (lane offsets span a few images at any batch)
@@ -410,7 +416,16 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
     const int nn = n0 + rh * 64 + lane;
     b_off[rh] = nn < p.Cout ? (uint32_t)((nn * p.K + 4 * wave) * 4) : OOB_OFF;
   }
-  int ld_r = 0, ld_s = 0, ld_c0 = 0, ld_k = 0;
+  const int KT_all = p.K / 16;
+  const int t_begin = (int)((long)KT_all * slice / ks), t_end = (int)((long)KT_all * (slice + 1) / ks);
+  // (16-float steps never straddle a tap: C % 16 == 0)
+  int ld_k = t_begin * 16, ld_r, ld_s, ld_c0;
+  {
+    const int tap = ld_k / p.C;
+    ld_c0 = ld_k - tap * p.C;
+    ld_r = tap / p.S;
+    ld_s = tap - ld_r * p.S;
+  }
   auto load_step = [&](int buf) {
     char* base = smem + buf * STAGE;
     const int tap = ld_r * p.S + ld_s;
@@ -434,7 +449,7 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  const int KT = p.K / 16;
+  const int KT = t_end - t_begin;
   load_step(0);
   if (KT > 1) load_step(1);
   const int fr = lane & 15, g = lane >> 4;
@@ -466,8 +481,29 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (ks > 1) {   // split-K slice: the fp32 partial tile in fragment order, combined by conv_f32_splitk_kernel
+    float4* dst = reinterpret_cast<float4*>(p.slab) + (long)(tile * ks + slice) * (4 * TJ) * 256 + tid;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) dst[(i * TJ + j) * 256] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    return;
+  }
   __syncthreads();   // every fragment read done: the epilogue reuses the pipeline's LDS
+  f32_big_epilogue<BN>(p, acc, m0, n0, tm, smem);
+}
 
+// Fused epilogue of the 128 x BN fp32 tiles (conv_f32_big_kernel, conv_f32_splitk_kernel): the
+// accumulator fragments through LDS into 16-byte row stores.
+template <int BN>
+__device__ __forceinline__ void f32_big_epilogue(const ConvF32Params& p, v4f (&acc)[4][BN / 32], int m0, int n0,
+                                                 int tm, char* smem) {
+  constexpr int TJ = BN / 32, CLD = BN + 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, g = lane >> 4;
+  const int HoWo = p.Ho * p.Wo;
   // epilogue: thread -> one 4-column group (CG groups across the tile) and every RPI-th row
   constexpr int CG = BN / 4, RPI = 256 / CG;
   float* Cs = reinterpret_cast<float*>(smem);
@@ -572,7 +608,49 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
     __syncthreads();   // (the next half overwrites Cs)
   }
 }
-int g_conv_f32_variant = 1;   // 0: 64 x 64 register-staged kernels only; 1: the LDS-DMA kernels where they
+
+// Split-K combine of the fp32 tiles: one workgroup per 128 x BN tile, each thread sums its own
+// fragments over the slices (16-byte loads, four slices in flight) and runs the fused epilogue.
+template <int BN>
+__global__ void __launch_bounds__(256) conv_f32_splitk_kernel(ConvF32Params p) {
+  constexpr int TJ = BN / 32, F = 4 * TJ;
+  __shared__ __attribute__((aligned(16))) char smem[64 * (BN + 4) * 4];
+  const int nt = (p.Cout + BN - 1) / BN;
+  const int tile = blockIdx.x, tn = tile % nt, tm = tile / nt;
+  const int tid = threadIdx.x;
+  v4f acc[4][TJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const float4* src = reinterpret_cast<const float4*>(p.slab) + (long)tile * p.ksplit * F * 256 + tid;
+  auto add = [&](const float4* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const float4 q = v[i * TJ + j];
+        acc[i][j][0] += q.x; acc[i][j][1] += q.y; acc[i][j][2] += q.z; acc[i][j][3] += q.w;
+      }
+  };
+  int sl = 0;
+  for (; sl + 1 < p.ksplit; sl += 2) {
+    float4 v0[F], v1[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) { v0[f] = src[((long)sl * F + f) * 256]; v1[f] = src[((long)(sl + 1) * F + f) * 256]; }
+    add(v0);
+    add(v1);
+  }
+  if (sl < p.ksplit) {
+    float4 v0[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) v0[f] = src[((long)sl * F + f) * 256];
+    add(v0);
+  }
+  f32_big_epilogue<BN>(p, acc, tm * G_BM, tn * BN, tm, smem);
+}
+int g_conv_f32_variant = 1;
+int g_conv_f32_splitk = 1;    // split-K of the underfilled fp32 conv / dgrad problems (knob conv_f32_splitk)   // 0: 64 x 64 register-staged kernels only; 1: the LDS-DMA kernels where they
                               // apply (C % 16 == 0: 128 x 64 conv tiles; the 128 x 128 weight-gradient
                               // tiles where both GEMM sides are >= 128 wide); 2: 128 x 128 conv tiles and
                               // the 128 x 128 weight gradient wherever they apply
@@ -711,12 +789,30 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
     // 128 x 64 tiles unless forced: 4 workgroups per CU (36 KB of LDS, 76 VGPRs) against the wide
     // tile's 3, equal or faster on every ResNet-50 layer (bench/f32.py, profiles/r4_fp32.txt)
     const bool wide = g_conv_f32_variant == 2;
-    if (wide) {
-      const int grid = mt * ((p.Cout + 127) / 128);
-      hipLaunchKernelGGL(conv_f32_big_kernel<128>, dim3(grid), dim3(256), 0, stream, p);
+    const int BN = wide ? 128 : 64;
+    const int T = mt * ((p.Cout + BN - 1) / BN);
+    // split-K where the tiles leave CUs idle (small batches: b32 stage 5 is 104 tiles of a
+    // 288-step K loop on 256 CUs): slices aimed at 4 workgroups per CU, >= 8 K steps each, <= 8
+    const long C = num_cus(), KT = p.K / 16;
+    long ks = 1;
+    if (g_conv_f32_splitk && T < C) {
+      ks = (4 * C + T - 1) / T;
+      if (ks > 8) ks = 8;
+      if (ks > KT / 8) ks = KT / 8;
+    }
+    if (ks >= 2 && p.slab && p.slab_floats >= (long)T * ks * G_BM * BN) {
+      p.ksplit = (int)ks;
+      if (wide) {
+        hipLaunchKernelGGL(conv_f32_big_kernel<128>, dim3(T * ks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(conv_f32_splitk_kernel<128>, dim3(T), dim3(256), 0, stream, p);
+      } else {
+        hipLaunchKernelGGL(conv_f32_big_kernel<64>, dim3(T * ks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(conv_f32_splitk_kernel<64>, dim3(T), dim3(256), 0, stream, p);
+      }
     } else {
-      const int grid = mt * ((p.Cout + 63) / 64);
-      hipLaunchKernelGGL(conv_f32_big_kernel<64>, dim3(grid), dim3(256), 0, stream, p);
+      p.ksplit = 1;
+      if (wide) hipLaunchKernelGGL(conv_f32_big_kernel<128>, dim3(T), dim3(256), 0, stream, p);
+      else hipLaunchKernelGGL(conv_f32_big_kernel<64>, dim3(T), dim3(256), 0, stream, p);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? nullptr : hipGetErrorString(e);

@@ -182,6 +182,9 @@ class HipF32Engine:
         self.side = torch.cuda.Stream(dev) if self.two_stream and dev.type == "cuda" else None
         self._evpool, self._evi = [], 0
         self.tmp = torch.empty(tmp, **f32)
+        # split-K workspace of the underfilled conv / dgrad problems (conv_f32.hip: small batches),
+        # this engine's own (N.splitk_use makes it current for the launching thread)
+        self.splitk_ws = torch.empty(self.N.splitk_default_floats(dev.index or 0), **f32) if dev.type == "cuda" else None
         # blocks feeding a stride-2 projection block: their output gradient is written on the
         # stride-2 grid only (dgrad up2 scatter) into a buffer zeroed once here
         bl = L.blocks
@@ -302,6 +305,7 @@ class HipF32Engine:
                    self.scale[ch:], self.shift[ch:], res, relu)
 
     def _forward(self, images, B, training, flip, crop_offset):
+        self.N.splitk_use(self.splitk_ws)   # this engine's split-K workspace, for this thread's launches
         N, L = self.N, self.L
         mode, oy, ox = self._stem_mode(training, crop_offset)
         x2 = self.x2[:B]
@@ -585,6 +589,7 @@ class HipF32EngineBNTrain(HipF32Engine):
                             self.bn_scale, self.bn_shift, BN_EPS, BN_MOMENTUM)
 
     def _forward(self, images, B, training, flip, crop_offset):
+        self.N.splitk_use(self.splitk_ws)   # this engine's split-K workspace, for this thread's launches
         N, L = self.N, self.L
         if not training:   # the moving statistics for every layer at once
             N.bn_stats(self.acc, self._eval_tab, len(L.convs), 2048, False, self.params, self.bn_mean, self.bn_inv,
