@@ -444,7 +444,7 @@ def test_conv_f32_splitk_matches_unsplit_and_fp64(case, v):
     g = torch.randn(n, ho, ho, co, device=dev)
     ws = torch.empty(N().splitk_default_floats(0), device=dev)
     outs = []
-    for sk in (1, 0):
+    for sk in (4, 0):
         N().set_variant("conv_f32_splitk", sk)
         N().set_variant("conv_f32", v)
         N().splitk_use(ws)
@@ -457,7 +457,7 @@ def test_conv_f32_splitk_matches_unsplit_and_fp64(case, v):
             torch.cuda.synchronize()
             outs.append((y, yd, cs.sum(0)))
         finally:
-            N().set_variant("conv_f32_splitk", 1)
+            N().set_variant("conv_f32_splitk", 4)
             N().set_variant("conv_f32", 1)
             N().splitk_use(None)
     conv = F.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), stride=st,
