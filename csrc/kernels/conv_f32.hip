@@ -364,7 +364,7 @@ __device__ __forceinline__ float4 f32_read16(const char* p) {
 
 template <int BN>
 __device__ __forceinline__ void f32_big_epilogue(const ConvF32Params& p, v4f (&acc)[4][BN / 32], int m0, int n0,
-                                                 int tm, char* smem);
+                                                 int tm, char* smem, int half = -1);
 
 template <int BN>
 __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
@@ -497,11 +497,13 @@ __global__ void __launch_bounds__(256, 2) conv_f32_big_kernel(ConvF32Params p) {
 // accumulator fragments through LDS into 16-byte row stores.
 template <int BN>
 __device__ __forceinline__ void f32_big_epilogue(const ConvF32Params& p, v4f (&acc)[4][BN / 32], int m0, int n0,
-                                                 int tm, char* smem) {
+                                                 int tm, char* smem, int half) {
+  // half < 0: the whole 128-row tile, wave (wm, wn) holding rows wm * 64 + [0, 64); half 0 / 1:
+  // only that 64-row half, its fragments in waves 0 / 1 (as wn), waves 2 / 3 holding none
   constexpr int TJ = BN / 32, CLD = BN + 4;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = half < 0 ? wave >> 1 : (wave < 2 ? half : -1), wn = wave & 1;
   const int fr = lane & 15, g = lane >> 4;
   const int HoWo = p.Ho * p.Wo;
   // epilogue: thread -> one 4-column group (CG groups across the tile) and every RPI-th row
@@ -517,7 +519,8 @@ __device__ __forceinline__ void f32_big_epilogue(const ConvF32Params& p, v4f (&a
       else if (p.epi == F32_EPI_PLAIN && p.bias) sh[e] = p.bias[col + e];
     }
   }
-  for (int h = 0; h < 2; ++h) {
+  const int h_lo = half < 0 ? 0 : half, h_hi = half < 0 ? 2 : half + 1;
+  for (int h = h_lo; h < h_hi; ++h) {
     if (wm == h) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -609,21 +612,24 @@ __device__ __forceinline__ void f32_big_epilogue(const ConvF32Params& p, v4f (&a
   }
 }
 
-// Split-K combine of the fp32 tiles: one workgroup per 128 x BN tile, each thread sums its own
-// fragments over the slices (16-byte loads, four slices in flight) and runs the fused epilogue.
+// Split-K combine of the fp32 tiles: one workgroup per 64-row half of a 128 x BN tile (the
+// combines run ~100 tiles at small batches: one workgroup per tile measured bound by its two-half
+// epilogue), waves 0 / 1 summing the fragments of the half's two slice waves over the slices
+// (16-byte loads, two slices in flight), then the fused epilogue of that half.
 template <int BN>
 __global__ void __launch_bounds__(256) conv_f32_splitk_kernel(ConvF32Params p) {
   constexpr int TJ = BN / 32, F = 4 * TJ;
   __shared__ __attribute__((aligned(16))) char smem[64 * (BN + 4) * 4];
   const int nt = (p.Cout + BN - 1) / BN;
-  const int tile = blockIdx.x, tn = tile % nt, tm = tile / nt;
+  const int tile = blockIdx.x >> 1, half = blockIdx.x & 1, tn = tile % nt, tm = tile / nt;
   const int tid = threadIdx.x;
   v4f acc[4][TJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  const float4* src = reinterpret_cast<const float4*>(p.slab) + (long)tile * p.ksplit * F * 256 + tid;
+  // (slice wave 2 * half + w wrote rows half * 64 + [0, 64) of the tile; w = this wave, 0 or 1)
+  const float4* src = reinterpret_cast<const float4*>(p.slab) + (long)tile * p.ksplit * F * 256 + half * 128 + tid;
   auto add = [&](const float4* v) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -633,7 +639,7 @@ __global__ void __launch_bounds__(256) conv_f32_splitk_kernel(ConvF32Params p) {
         acc[i][j][0] += q.x; acc[i][j][1] += q.y; acc[i][j][2] += q.z; acc[i][j][3] += q.w;
       }
   };
-  int sl = 0;
+  int sl = tid < 128 ? 0 : p.ksplit;   // (waves 2 / 3 hold no fragments)
   for (; sl + 1 < p.ksplit; sl += 2) {
     float4 v0[F], v1[F];
 #pragma unroll
@@ -647,7 +653,7 @@ __global__ void __launch_bounds__(256) conv_f32_splitk_kernel(ConvF32Params p) {
     for (int f = 0; f < F; ++f) v0[f] = src[((long)sl * F + f) * 256];
     add(v0);
   }
-  f32_big_epilogue<BN>(p, acc, tm * G_BM, tn * BN, tm, smem);
+  f32_big_epilogue<BN>(p, acc, tm * G_BM, tn * BN, tm, smem, half);
 }
 int g_conv_f32_variant = 1;
 int g_conv_f32_splitk = 4;    // split-K of the underfilled fp32 conv / dgrad problems: slice workgroups aimed
@@ -805,10 +811,10 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
       p.ksplit = (int)ks;
       if (wide) {
         hipLaunchKernelGGL(conv_f32_big_kernel<128>, dim3(T * ks), dim3(256), 0, stream, p);
-        hipLaunchKernelGGL(conv_f32_splitk_kernel<128>, dim3(T), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(conv_f32_splitk_kernel<128>, dim3(2 * T), dim3(256), 0, stream, p);
       } else {
         hipLaunchKernelGGL(conv_f32_big_kernel<64>, dim3(T * ks), dim3(256), 0, stream, p);
-        hipLaunchKernelGGL(conv_f32_splitk_kernel<64>, dim3(T), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(conv_f32_splitk_kernel<64>, dim3(2 * T), dim3(256), 0, stream, p);
       }
     } else {
       p.ksplit = 1;
