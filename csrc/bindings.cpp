@@ -896,6 +896,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else if (which == "stem") pddl::g_stem_variant = v;
     else if (which == "conv_f32") pddl::g_conv_f32_variant = v;
     else if (which == "conv_f32_splitk") pddl::g_conv_f32_splitk = v;
+    else if (which == "conv_f32_sk_elig") { TORCH_CHECK(v >= 1 && v <= 8, "conv_f32_sk_elig: 1-8"); pddl::g_conv_f32_sk_elig = v; }
     else if (which == "wgrad_f32_wpc64") { TORCH_CHECK(v >= 1 && v <= 32, "wgrad_f32_wpc64"); pddl::g_wgrad_f32_wpc[0] = v; }
     else if (which == "wgrad_f32_wpc128") { TORCH_CHECK(v >= 1 && v <= 32, "wgrad_f32_wpc128"); pddl::g_wgrad_f32_wpc[1] = v; }
     else if (which == "c64_grid") pddl::g_c64_grid = v;

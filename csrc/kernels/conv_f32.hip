@@ -656,6 +656,7 @@ __global__ void __launch_bounds__(256) conv_f32_splitk_kernel(ConvF32Params p) {
   f32_big_epilogue<BN>(p, acc, tm * G_BM, tn * BN, tm, smem, half);
 }
 int g_conv_f32_variant = 1;
+int g_conv_f32_sk_elig = 1;   // ... for problems of fewer than this many tiles per CU (knob conv_f32_sk_elig)
 int g_conv_f32_splitk = 4;    // split-K of the underfilled fp32 conv / dgrad problems: slice workgroups aimed
                               // at this many per CU (knob conv_f32_splitk, 0 off)   // 0: 64 x 64 register-staged kernels only; 1: the LDS-DMA kernels where they
                               // apply (C % 16 == 0: 128 x 64 conv tiles; the 128 x 128 weight-gradient
@@ -802,7 +803,7 @@ const char* conv_f32_launch(ConvF32Params p, hipStream_t stream) {
     // 288-step K loop on 256 CUs): slices aimed at 4 workgroups per CU, >= 8 K steps each, <= 8
     const long C = num_cus(), KT = p.K / 16;
     long ks = 1;
-    if (g_conv_f32_splitk > 0 && T < C) {
+    if (g_conv_f32_splitk > 0 && T < (long)g_conv_f32_sk_elig * C) {
       ks = ((long)g_conv_f32_splitk * C + T - 1) / T;
       if (ks > 8) ks = 8;
       if (ks > KT / 8) ks = KT / 8;

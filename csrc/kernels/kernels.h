@@ -129,7 +129,7 @@ struct ConvF32Params {
 };
 enum { F32_EPI_PLAIN = 0, F32_EPI_FWD = 1, F32_EPI_DGRAD = 2 };
 const char* conv_f32_launch(ConvF32Params p, hipStream_t stream);
-extern int g_conv_f32_variant, g_conv_f32_splitk;   // 0: 64 x 64 register-staged fp32 kernels; 1: LDS-DMA 128 x {64, 128} by model (default); 2: 128 x 128; 3: 128 x 64
+extern int g_conv_f32_variant, g_conv_f32_splitk, g_conv_f32_sk_elig;   // 0: 64 x 64 register-staged fp32 kernels; 1: LDS-DMA 128 x {64, 128} by model (default); 2: 128 x 128; 3: 128 x 64
 const char* wgrad_f32_launch(ConvF32Params p, hipStream_t stream);
 // fp32 elementwise kernels of the fp32 engine (f32.hip)
 const char* maxpool_fwd_f32_launch(const float* x, float* y, uint8_t* idx, int B, int H, int W, int C, int Ho, int Wo,
