@@ -16,7 +16,8 @@ def load(path):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                         r.get("Stream_Id") or r.get("Queue_Id") or "?"))
     rows.sort()
     return rows
 
@@ -62,6 +63,15 @@ def main():
     busy = sum(o[1] for o in out) / n
     print(f"steps {n}: span {span:.3f} ms, busy {busy:.3f} ms, idle {span - busy:.3f} ms, "
           f"kernels/step {sum(o[2] for o in out) / n:.1f}")
+    # per stream (rocprofv3 Stream_Id, else Queue_Id): busy time of each stream's own kernels
+    per_s = defaultdict(float)
+    for s in steps:
+        by = defaultdict(list)
+        for r in s:
+            by[r[3]].append((r[0], r[1]))
+        for k, iv in by.items():
+            per_s[k] += union(iv) / 1e6 / len(steps)
+    print("  per stream busy: " + ", ".join(f"{k}: {v:.3f} ms" for k, v in sorted(per_s.items(), key=lambda kv: -kv[1])))
     for name, t in sorted(per.items(), key=lambda kv: -kv[1])[:top]:
         print(f"  {t:9.1f} us  {name[:110]}")
 
