@@ -47,6 +47,10 @@ class HipEngineBNTrain(HipEngine):
 
     def __init__(self, layout: ParamLayout, batch: int, **kw):
         kw.setdefault("bn_mode", "train")
+        # deeper gradient rings up to b256 (b256 ring 3 / 5 / 8 / 12 / 16: 20.70 / 20.64 / 20.52 /
+        # 20.45 / 20.45 ms, round 6); larger batches keep GRAD_RING (12 x 1.6 GB of ring at b1024)
+        if kw.get("grad_ring") is None and batch <= 256:
+            kw["grad_ring"] = 12
         # (needed by _alloc_acts, which the base constructor calls)
         self.L = layout
         self._launch_nn = self._fwd_launches()

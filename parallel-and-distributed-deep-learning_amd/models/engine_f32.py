@@ -504,6 +504,7 @@ class HipF32EngineBNTrain(HipF32Engine):
     variant at the reference's precision (tests/test_gpu_f32.py bounds it against the PyTorch
     reference model in float64)."""
     BN_MODES = ("train",)
+    RING = 12   # (fp32 b256: ring 3 / 5 / 8 / 12 / 16 -> 73.4 / 73.1 / 72.3-72.6 / 71.9 / 71.8 ms)
 
     def __init__(self, layout: ParamLayout, batch: int, crop: int = 224, image_size: Optional[int] = None,
                  device="cuda", bn_mode: str = "train", num_classes: int = 1000):
