@@ -43,6 +43,7 @@ KEYS: Dict[str, Dict[str, str]] = {
         "segmented": "1: a one-replica job runs the multi-replica schedule (segmented graphs + all-reduce)",
         "overlap": "1: eager replicas all-reduce each bucket while backward continues (0: after it)",
         "pool": "1: graphed one-stream replicas launch each phase on the native launch pool (0: one thread)",
+        "tail_cuts": "auto (batch >= 128) / 1 / 0: graphed replicas also cut a segment at every block of the last kernel bucket",
     },
 }
 

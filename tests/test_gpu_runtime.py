@@ -316,7 +316,8 @@ def test_mirrored_on_init_rank_communicator(monkeypatch):
     assert h.history["loss"][0] == h.history["loss"][0]
     torch.cuda.synchronize()
     ws = comm.watchdog_state()
-    assert ws["armed"] and ws["issued"] >= 4 * len(st.mirror.buckets) and not ws["stalled"], ws
+    # (step 1 runs eager, then 3 graphed steps: one collective per segment bucket each)
+    assert ws["armed"] and ws["issued"] >= 3 * len(st.mirror.buckets) and not ws["stalled"], ws
 
 
 def test_bench_parameter_server_rehearsal_on_one_gpu():

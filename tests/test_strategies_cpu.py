@@ -156,3 +156,21 @@ def test_horovod_bf16_wire_close_to_fp32():
     assert upd > 0
     assert ((bf16[0][1] - fp32[0][1]).norm() / upd).item() < 0.05
     assert torch.equal(bf16[0][1], bf16[1][1])        # both ranks applied the same reduced gradient
+
+
+def test_segmented_tail_cuts_split_the_last_kernel_bucket_at_block_boundaries():
+    """Graphed replicas' tail cuts (strategies._LocalReplicas._split_tail): the last kernel bucket is
+    split at every block boundary inside it, the ranges stay contiguous and cover the same span,
+    and the per-channel tail bucket stays last."""
+    from pddl.models.resnet50 import ParamLayout
+    from pddl.parallel.strategies import _LocalReplicas
+    L = ParamLayout()
+    bks = L.buckets(32.0)
+    out = _LocalReplicas._split_tail(bks, L)
+    assert out[:len(bks) - 2] == bks[:-2] and out[-1] == bks[-1]
+    assert len(out) > len(bks)
+    assert all(a[1] == b[0] for a, b in zip(out, out[1:-1]))
+    assert out[len(bks) - 2][0] == bks[-2][0] and out[-2][1] == bks[-2][1]
+    ends = {L.entry(b.convs["0" if b.proj else "1"].name, "kernel").offset
+            + L.entry(b.convs["0" if b.proj else "1"].name, "kernel").size for b in L.blocks}
+    assert all(e in ends for _, e in out[len(bks) - 2:-2])
