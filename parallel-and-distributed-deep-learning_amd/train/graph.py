@@ -307,9 +307,9 @@ class SegmentedStepGraphs(GraphedTrainStep):
             amb.wait_stream(side)
 
     def exec_handles(self):
-        """([segment k's raw executable, 0 if empty], the optimizer graph's): what the Mirrored
-        driver's native group launch replays (sync_hparams / the iteration count stay with the
-        caller, as in replay_optimizer)."""
+        """([segment k's raw executable, 0 if empty], the optimizer graph's, [segment k's side
+        graph, 0 if none]): what the Mirrored driver's native group launches replay (sync_hparams /
+        the iteration count stay with the caller, as in replay_optimizer)."""
         return ([g.raw_cuda_graph_exec() if g is not None else 0 for g in self.segments],
                 self.opt_graph.raw_cuda_graph_exec(),
                 [g.raw_cuda_graph_exec() if g is not None else 0 for g in self.side_segments])
